@@ -1,0 +1,359 @@
+"""constdb_amd — MI355X-native batched CRDT merge engine for ConstDB's replica-sync path.
+
+Thin ctypes mirror of the C ABI in ``include/cdb_merge.h`` (libcdbmerge.so: HIP kernels
+for gfx950 + host C++). The product path is the HIP library: there is no CPU fallback —
+merging without a visible gfx950 device raises ``NoDevice``.
+
+Reference interface mirrored (fxsjy/ConstDB):
+  * ``decode_snapshot``  ~ ``SnapshotLoader::next`` loop      (src/snapshot.rs:120-220)
+  * ``DB.merge_snapshots`` ~ ``Puller::merge_replicates_in_main`` applying
+    ``DB::merge_entry`` / ``DB::delete`` / ``DB::expire_at``    (src/replica/pull.rs:116-159)
+  * errors ~ ``CstError`` (src/lib.rs:146-175)
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libcdbmerge.so")
+
+# ----------------------------------------------------------------- errors (lib.rs:146-175)
+OK = 0
+INVALID_SNAPSHOT = 1
+INVALID_SNAPSHOT_CHECKSUM = 2
+INVALID_TYPE = 3
+IO_ERROR = 4
+DICT_MERGE_UNIMPLEMENTED = 5
+BAD_ARGUMENT = 6
+DEVICE_ERROR = 7
+OUT_OF_MEMORY = 8
+NO_DEVICE = 9
+
+DECODE_REFERENCE_CHECKSUM = 1
+MERGE_STRICT_DICT_PANIC = 1
+MERGE_GC_DELETES = 2
+MERGE_GC_MEMBERS = 4
+
+
+class CstError(Exception):
+    status = -1
+
+
+class InvalidSnapshot(CstError):
+    status = INVALID_SNAPSHOT
+
+    def __init__(self, offset: int):
+        super().__init__(f"invalid data in snapshot at offset {offset}")
+        self.offset = offset
+
+
+class InvalidSnapshotChecksum(CstError):
+    status = INVALID_SNAPSHOT_CHECKSUM
+
+
+class InvalidType(CstError):
+    status = INVALID_TYPE
+
+
+class IoError(CstError):
+    status = IO_ERROR
+
+
+class DictMergeUnimplemented(CstError):
+    status = DICT_MERGE_UNIMPLEMENTED
+
+
+class NoDevice(CstError):
+    status = NO_DEVICE
+
+
+class DeviceError(CstError):
+    status = DEVICE_ERROR
+
+
+_ERRORS = {INVALID_SNAPSHOT_CHECKSUM: InvalidSnapshotChecksum, INVALID_TYPE: InvalidType,
+           IO_ERROR: IoError, DICT_MERGE_UNIMPLEMENTED: DictMergeUnimplemented, NO_DEVICE: NoDevice,
+           DEVICE_ERROR: DeviceError, OUT_OF_MEMORY: DeviceError, BAD_ARGUMENT: ValueError}
+
+
+def _raise(st: int, msg: str = "", offset: int = 0):
+    if st == INVALID_SNAPSHOT:
+        raise InvalidSnapshot(offset)
+    cls = _ERRORS.get(st, CstError)
+    raise cls(msg or f"cdb status {st}")
+
+
+# ----------------------------------------------------------------- ctypes structs
+class BatchInfo(ctypes.Structure):
+    _fields_ = [("n_data", ctypes.c_uint64), ("n_expires", ctypes.c_uint64), ("n_deletes", ctypes.c_uint64),
+                ("n_nodes", ctypes.c_uint64), ("n_members", ctypes.c_uint64), ("node_id", ctypes.c_uint64),
+                ("uuid_he_sent", ctypes.c_uint64), ("n_replica_add", ctypes.c_uint32),
+                ("n_replica_del", ctypes.c_uint32), ("version", ctypes.c_char * 16)]
+
+
+class MergeOpts(ctypes.Structure):
+    _fields_ = [("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("gc_watermark", ctypes.c_uint64)]
+
+
+class MergeStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "key_rows_in", "node_rows_in", "member_rows_in", "key_rows_out", "node_rows_out", "member_rows_out",
+        "type_conflicts", "dict_merges", "deletes_gced", "members_gced", "duplicate_rows", "orphan_children",
+        "hot_buckets")] + [(n, ctypes.c_double) for n in ("device_ms", "partition_ms", "bucket_ms", "finish_ms")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class DevRows(ctypes.Structure):
+    _fields_ = [("col", ctypes.c_void_p * 8), ("n", ctypes.c_uint64)]
+
+
+class DevInput(ctypes.Structure):
+    _fields_ = [("keys", DevRows), ("nodes", DevRows), ("members", DevRows), ("n_pos", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class DevOutput(ctypes.Structure):
+    _fields_ = [("keys", DevRows), ("nodes", DevRows), ("members", DevRows), ("compact", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class GenConfig(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("universe", ctypes.c_uint64)] + [(n, ctypes.c_uint32) for n in (
+        "n_replicas", "key_permille", "mix_bytes", "mix_counter", "mix_set", "mix_dict", "conflict_ppm",
+        "tie_permille", "max_nodes", "mean_members", "member_universe", "del_permille", "side_permille",
+        "value_min", "value_max", "shard", "n_shards", "replica_lo", "replica_hi")]
+
+
+# exported C-ABI function names (tests check the .so exports every one of them)
+ABI_FUNCTIONS = (
+    "cdb_ctx_create", "cdb_ctx_destroy", "cdb_last_error", "cdb_decode_snapshot", "cdb_batch_info_get",
+    "cdb_batch_column", "cdb_batch_free", "cdb_merge", "cdb_merged_canonical_dump", "cdb_merged_free", "cdb_free",
+    "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_gen_default", "cdb_gen_snapshot",
+    "cdb_gen_device")
+
+_lib = None
+
+
+def lib_path() -> str:
+    return _LIB_PATH
+
+
+def lib():
+    """Loads libcdbmerge.so. Raises OSError when it was not built (see __graft_entry__.build)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise OSError(f"{_LIB_PATH} missing: build it with `python constdb_amd/build.py`")
+    L = ctypes.CDLL(_LIB_PATH)
+    vp, c_st = ctypes.c_void_p, ctypes.c_int
+    P = ctypes.POINTER
+    sig = {
+        "cdb_ctx_create": (c_st, [P(vp), ctypes.c_int]),
+        "cdb_ctx_destroy": (None, [vp]),
+        "cdb_last_error": (ctypes.c_char_p, [vp]),
+        "cdb_decode_snapshot": (c_st, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, P(vp),
+                                       P(ctypes.c_size_t)]),
+        "cdb_batch_info_get": (c_st, [vp, P(BatchInfo)]),
+        "cdb_batch_column": (c_st, [vp, ctypes.c_int, ctypes.c_int, P(P(ctypes.c_uint64)), P(ctypes.c_uint64)]),
+        "cdb_batch_free": (None, [vp]),
+        "cdb_merge": (c_st, [vp, P(vp), ctypes.c_uint32, P(MergeOpts), P(vp), P(MergeStats)]),
+        "cdb_merged_canonical_dump": (c_st, [vp, vp, P(vp), P(ctypes.c_size_t)]),
+        "cdb_merged_free": (None, [vp]),
+        "cdb_free": (None, [vp]),
+        "cdb_dev_rows_alloc": (c_st, [vp, P(DevRows), ctypes.c_uint64, ctypes.c_int]),
+        "cdb_dev_rows_release": (None, [vp, P(DevRows)]),
+        "cdb_merge_device": (c_st, [vp, P(DevInput), P(MergeOpts), P(DevOutput), P(MergeStats), vp]),
+        "cdb_gen_default": (None, [P(GenConfig)]),
+        "cdb_gen_snapshot": (c_st, [P(GenConfig), ctypes.c_uint32, P(vp), P(ctypes.c_size_t)]),
+        "cdb_gen_device": (c_st, [vp, P(GenConfig), P(DevInput)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+# ----------------------------------------------------------------- context
+class Context:
+    """A device context (cdb_ctx). Needs a visible gfx950 GPU; raises NoDevice otherwise."""
+
+    def __init__(self, device: int = 0):
+        self._ctx = ctypes.c_void_p()
+        st = lib().cdb_ctx_create(ctypes.byref(self._ctx), device)
+        if st != OK:
+            _raise(st, "no HIP device" if st == NO_DEVICE else "cdb_ctx_create failed")
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._ctx
+
+    def last_error(self) -> str:
+        return (lib().cdb_last_error(self._ctx) or b"").decode()
+
+    def check(self, st: int):
+        if st != OK:
+            _raise(st, self.last_error())
+
+    def close(self):
+        if self._ctx:
+            lib().cdb_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ----------------------------------------------------------------- decode
+class Batch:
+    """A decoded snapshot (cdb_batch): columnar rows + byte arena, host resident."""
+
+    def __init__(self, handle, checksum_ok: bool = True):
+        self._h = handle
+        self.checksum_ok = checksum_ok
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self) -> BatchInfo:
+        bi = BatchInfo()
+        lib().cdb_batch_info_get(self._h, ctypes.byref(bi))
+        return bi
+
+    def column(self, family: int, col: int):
+        """(numpy-free) list of the u64 values of one decoded column."""
+        ptr = ctypes.POINTER(ctypes.c_uint64)()
+        n = ctypes.c_uint64()
+        st = lib().cdb_batch_column(self._h, family, col, ctypes.byref(ptr), ctypes.byref(n))
+        if st != OK:
+            _raise(st)
+        return [ptr[i] for i in range(n.value)]
+
+    def column_array(self, family: int, col: int):
+        import numpy as np
+        ptr = ctypes.POINTER(ctypes.c_uint64)()
+        n = ctypes.c_uint64()
+        st = lib().cdb_batch_column(self._h, family, col, ctypes.byref(ptr), ctypes.byref(n))
+        if st != OK:
+            _raise(st)
+        if n.value == 0:
+            return np.zeros(0, dtype=np.uint64)
+        return np.ctypeslib.as_array(ptr, shape=(n.value,)).copy()
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().cdb_batch_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+def decode_snapshot(data: bytes, reference_checksum: bool = False, allow_bad_checksum: bool = False) -> Batch:
+    """Decodes one snapshot (writer layout, server.rs:183-215). Mirrors the loader's errors:
+    InvalidSnapshot(offset) / InvalidSnapshotChecksum / InvalidType / IoError."""
+    h = ctypes.c_void_p()
+    off = ctypes.c_size_t()
+    flags = DECODE_REFERENCE_CHECKSUM if reference_checksum else 0
+    st = lib().cdb_decode_snapshot(None, bytes(data), len(data), flags, ctypes.byref(h), ctypes.byref(off))
+    if st == INVALID_SNAPSHOT_CHECKSUM and allow_bad_checksum and h:
+        return Batch(h, checksum_ok=False)
+    if st != OK:
+        if h:
+            lib().cdb_batch_free(h)
+        _raise(st, offset=off.value)
+    return Batch(h)
+
+
+# ----------------------------------------------------------------- merge
+class Merged:
+    """A merge result (cdb_merged)."""
+
+    def __init__(self, ctx: Context, handle, stats: MergeStats, inputs: Sequence[Batch]):
+        self._ctx = ctx
+        self._h = handle
+        self.stats = stats
+        self._inputs = list(inputs)   # keep the byte arenas alive
+
+    def canonical_dump(self) -> bytes:
+        out = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        self._ctx.check(lib().cdb_merged_canonical_dump(self._ctx.handle, self._h, ctypes.byref(out),
+                                                        ctypes.byref(n)))
+        try:
+            return ctypes.string_at(out.value, n.value) if n.value else b""
+        finally:
+            lib().cdb_free(out)
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().cdb_merged_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+class DB:
+    """Batched stand-in for the reference DB's replica-sync entry point.
+
+    ``merge_snapshots([local, remote1, ...])`` has the effect of folding each snapshot, in
+    order, through DB::merge_entry / DB::delete / DB::expire_at (replica/pull.rs:120-158),
+    optionally followed by DB::gc(watermark) (db.rs:82-119)."""
+
+    def __init__(self, ctx: Optional[Context] = None, device: int = 0):
+        self.ctx = ctx or Context(device)
+
+    def merge_batches(self, batches: Sequence[Batch], strict_dict_panic: bool = False,
+                      gc_watermark: Optional[int] = None, gc_members: bool = False) -> Merged:
+        n = len(batches)
+        arr = (ctypes.c_void_p * max(n, 1))(*[b.handle for b in batches])
+        opts = MergeOpts()
+        opts.flags = (MERGE_STRICT_DICT_PANIC if strict_dict_panic else 0)
+        if gc_watermark is not None:
+            opts.flags |= MERGE_GC_DELETES | (MERGE_GC_MEMBERS if gc_members else 0)
+            opts.gc_watermark = gc_watermark
+        st = MergeStats()
+        h = ctypes.c_void_p()
+        rc = lib().cdb_merge(self.ctx.handle, arr, n, ctypes.byref(opts), ctypes.byref(h), ctypes.byref(st))
+        if rc not in (OK, DICT_MERGE_UNIMPLEMENTED):
+            _raise(rc, self.ctx.last_error())
+        m = Merged(self.ctx, h, st, batches)
+        if rc == DICT_MERGE_UNIMPLEMENTED:
+            raise DictMergeUnimplemented(self.ctx.last_error())
+        return m
+
+    def merge_snapshots(self, snapshots: Sequence[bytes], **kw) -> Merged:
+        return self.merge_batches([decode_snapshot(s) for s in snapshots], **kw)
+
+
+# ----------------------------------------------------------------- synthetic inputs
+def gen_config(**overrides) -> GenConfig:
+    c = GenConfig()
+    lib().cdb_gen_default(ctypes.byref(c))
+    for k, v in overrides.items():
+        setattr(c, k, v)
+    return c
+
+
+def gen_snapshot(cfg: GenConfig, replica: int) -> bytes:
+    out = ctypes.c_void_p()
+    n = ctypes.c_size_t()
+    st = lib().cdb_gen_snapshot(ctypes.byref(cfg), replica, ctypes.byref(out), ctypes.byref(n))
+    if st != OK:
+        _raise(st)
+    try:
+        return ctypes.string_at(out.value, n.value)
+    finally:
+        lib().cdb_free(out)

@@ -1,0 +1,51 @@
+// Host-side columnar batch: one decoded snapshot (SoA rows + the byte arena they refer to).
+#pragma once
+#include <stdint.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+namespace cdb {
+
+struct ByteRef {  // a byte range inside Batch::raw
+  uint64_t off, len;
+};
+
+struct ReplicaAdd { uint64_t add_time, node_id; std::string alias, addr; uint64_t uuid; };
+struct ReplicaDel { std::string addr; uint64_t t; };
+
+struct Batch {
+  std::vector<uint8_t> raw;  // the snapshot bytes: arena for keys, values, members
+
+  // Key rows in stream order: DATAS entries, then EXPIRES, then DELETES (db.rs:122-136).
+  // The GPU sees kh kf ct ut dt aux meta; key_ref/val_ref stay on the host.
+  std::vector<uint64_t> kh, kf, ct, ut, dt, aux, meta;
+  std::vector<ByteRef> key_ref, val_ref;
+  uint64_t n_data = 0, n_expires = 0, n_deletes = 0;
+
+  // Counter children (type_counter.rs:21): pkh pkf node v t meta.
+  std::vector<uint64_t> n_pkh, n_pkf, n_node, n_v, n_t, n_meta;
+
+  // Set/Dict member tags after load-time reconstruction: pkh pkf mh mf t meta (+ refs).
+  std::vector<uint64_t> m_pkh, m_pkf, m_h, m_f, m_t, m_meta;
+  std::vector<ByteRef> m_ref, m_vref;
+
+  // Node header and replica metadata (snapshot.rs:140-179).
+  std::string version;
+  uint64_t node_id = 0, uuid_he_sent = 0;
+  std::string alias, addr;
+  std::vector<ReplicaAdd> replica_add;
+  std::vector<ReplicaDel> replica_del;
+
+  uint64_t n_keys() const { return kh.size(); }
+  uint64_t n_nodes() const { return n_pkh.size(); }
+  uint64_t n_members() const { return m_pkh.size(); }
+};
+
+// Decoder (decode.cpp). Returns a cdb_status value.
+int decode_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off);
+
+}  // namespace cdb

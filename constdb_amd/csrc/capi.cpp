@@ -1,0 +1,302 @@
+// Host-level C-ABI: decoded batches, the high-level merge (upload, device pipeline,
+// download) and the canonical dump of a merge result.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "batch.h"
+#include "engine.h"
+
+namespace cdb {
+cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts,
+                             cdb_dev_output* out, cdb_merge_stats* stats, hipStream_t s);
+}
+
+struct cdb_batch {
+  std::shared_ptr<cdb::Batch> b;
+};
+
+struct cdb_merged {
+  std::vector<std::shared_ptr<cdb::Batch>> inputs;  // pos -> decoded batch (byte arenas)
+  std::vector<uint64_t> k[cdb::kKeyOutCols], nd[cdb::kNodeCols], mb[cdb::kMemberCols];
+};
+
+using namespace cdb;
+
+namespace {
+
+struct DevBlock {  // one allocation holding ncol columns of `rows` rows
+  uint64_t* p = nullptr;
+  ~DevBlock() {
+    if (p) hipFree(p);
+  }
+};
+
+cdb_status upload(cdb_ctx* ctx, DevBlock& blk, int ncol, uint64_t rows, const std::vector<const uint64_t*>& src_cols,
+                  cdb_dev_rows* r) {
+  const uint64_t n = std::max<uint64_t>(rows, 1);
+  cdb_status st = hip_check(ctx, hipMalloc(&blk.p, ncol * n * 8), "hipMalloc(input)");
+  if (st != CDB_OK) return st;
+  std::memset(r, 0, sizeof *r);
+  for (int c = 0; c < ncol; ++c) {
+    r->col[c] = blk.p + c * n;
+    if (rows && c < (int)src_cols.size() && src_cols[c]) {
+      st = hip_check(ctx, hipMemcpyAsync(r->col[c], src_cols[c], rows * 8, hipMemcpyHostToDevice, ctx->stream), "h2d");
+      if (st != CDB_OK) return st;
+    }
+  }
+  r->n = rows;
+  return CDB_OK;
+}
+
+std::string hex(const uint8_t* p, uint64_t n) {
+  static const char* d = "0123456789abcdef";
+  std::string o(n * 2, '0');
+  for (uint64_t i = 0; i < n; ++i) {
+    o[2 * i] = d[p[i] >> 4];
+    o[2 * i + 1] = d[p[i] & 15];
+  }
+  return o;
+}
+
+}  // namespace
+
+extern "C" {
+
+cdb_status cdb_decode_snapshot(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags, cdb_batch** out,
+                               size_t* err_offset) {
+  (void)ctx;
+  if (!out || (!buf && len)) return CDB_BAD_ARGUMENT;
+  *out = nullptr;
+  auto b = std::make_shared<Batch>();
+  size_t eo = 0;
+  const int rc = decode_snapshot(buf, len, flags, b.get(), &eo);
+  if (err_offset) *err_offset = eo;
+  if (rc == CDB_OK || rc == CDB_INVALID_SNAPSHOT_CHECKSUM) {
+    *out = new cdb_batch{b};
+  }
+  return (cdb_status)rc;
+}
+
+cdb_status cdb_batch_info_get(const cdb_batch* cb, cdb_batch_info* info) {
+  if (!cb || !info) return CDB_BAD_ARGUMENT;
+  const Batch& b = *cb->b;
+  std::memset(info, 0, sizeof *info);
+  info->n_data = b.n_data;
+  info->n_expires = b.n_expires;
+  info->n_deletes = b.n_deletes;
+  info->n_nodes = b.n_nodes();
+  info->n_members = b.n_members();
+  info->node_id = b.node_id;
+  info->uuid_he_sent = b.uuid_he_sent;
+  info->n_replica_add = (uint32_t)b.replica_add.size();
+  info->n_replica_del = (uint32_t)b.replica_del.size();
+  std::snprintf(info->version, sizeof info->version, "%s", b.version.c_str());
+  return CDB_OK;
+}
+
+cdb_status cdb_batch_column(const cdb_batch* cb, int family, int col, const uint64_t** data, uint64_t* n) {
+  if (!cb || !data || !n) return CDB_BAD_ARGUMENT;
+  const Batch& b = *cb->b;
+  const std::vector<uint64_t>* k[] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
+  const std::vector<uint64_t>* nd[] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
+  const std::vector<uint64_t>* mb[] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
+  const std::vector<uint64_t>* v = nullptr;
+  if (family == 0 && col >= 0 && col < kKeyCols) v = k[col];
+  else if (family == 1 && col >= 0 && col < kNodeCols) v = nd[col];
+  else if (family == 2 && col >= 0 && col < kMemberCols) v = mb[col];
+  if (!v) return CDB_BAD_ARGUMENT;
+  *data = v->data();
+  *n = v->size();
+  return CDB_OK;
+}
+
+void cdb_batch_free(cdb_batch* b) { delete b; }
+
+cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, const cdb_merge_opts* opts, cdb_merged** out,
+                     cdb_merge_stats* stats) {
+  if (!ctx || !out || (n && !inputs)) return CDB_BAD_ARGUMENT;
+  *out = nullptr;
+  if (n > (uint32_t)kMaxPos) return fail(ctx, CDB_BAD_ARGUMENT, "at most 63 batches per merge");
+  hipSetDevice(ctx->device);
+  // concatenate the batches in fold order, stamping pos = array index into meta
+  uint64_t K = 0, N = 0, M = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    K += inputs[i]->b->n_keys();
+    N += inputs[i]->b->n_nodes();
+    M += inputs[i]->b->n_members();
+  }
+  std::vector<uint64_t> hk[kKeyCols], hn[kNodeCols], hm[kMemberCols];
+  for (auto& v : hk) v.reserve(K);
+  for (auto& v : hn) v.reserve(N);
+  for (auto& v : hm) v.reserve(M);
+  auto restamp = [](uint64_t m, uint32_t pos) { return meta_pack(meta_tag(m), pos, meta_src(m)); };
+  for (uint32_t i = 0; i < n; ++i) {
+    const Batch& b = *inputs[i]->b;
+    hk[K_KH].insert(hk[K_KH].end(), b.kh.begin(), b.kh.end());
+    hk[K_KF].insert(hk[K_KF].end(), b.kf.begin(), b.kf.end());
+    hk[K_CT].insert(hk[K_CT].end(), b.ct.begin(), b.ct.end());
+    hk[K_UT].insert(hk[K_UT].end(), b.ut.begin(), b.ut.end());
+    hk[K_DT].insert(hk[K_DT].end(), b.dt.begin(), b.dt.end());
+    hk[K_AUX].insert(hk[K_AUX].end(), b.aux.begin(), b.aux.end());
+    for (uint64_t m : b.meta) hk[K_META].push_back(restamp(m, i));
+    hn[C_PKH].insert(hn[C_PKH].end(), b.n_pkh.begin(), b.n_pkh.end());
+    hn[C_PKF].insert(hn[C_PKF].end(), b.n_pkf.begin(), b.n_pkf.end());
+    hn[C_ID1].insert(hn[C_ID1].end(), b.n_node.begin(), b.n_node.end());
+    hn[C_ID2].insert(hn[C_ID2].end(), b.n_v.begin(), b.n_v.end());
+    hn[C_T].insert(hn[C_T].end(), b.n_t.begin(), b.n_t.end());
+    for (uint64_t m : b.n_meta) hn[C_META].push_back(restamp(m, i));
+    hm[C_PKH].insert(hm[C_PKH].end(), b.m_pkh.begin(), b.m_pkh.end());
+    hm[C_PKF].insert(hm[C_PKF].end(), b.m_pkf.begin(), b.m_pkf.end());
+    hm[C_ID1].insert(hm[C_ID1].end(), b.m_h.begin(), b.m_h.end());
+    hm[C_ID2].insert(hm[C_ID2].end(), b.m_f.begin(), b.m_f.end());
+    hm[C_T].insert(hm[C_T].end(), b.m_t.begin(), b.m_t.end());
+    for (uint64_t m : b.m_meta) hm[C_META].push_back(restamp(m, i));
+  }
+  auto ptrs = [](std::vector<uint64_t>* v, int nc) {
+    std::vector<const uint64_t*> p(nc);
+    for (int c = 0; c < nc; ++c) p[c] = v[c].data();
+    return p;
+  };
+  DevBlock bk, bn, bm, ok, on, om;
+  cdb_dev_input din;
+  std::memset(&din, 0, sizeof din);
+  cdb_dev_output dout;
+  std::memset(&dout, 0, sizeof dout);
+  din.n_pos = n;
+  cdb_status st;
+  if ((st = upload(ctx, bk, kKeyCols, K, ptrs(hk, kKeyCols), &din.keys)) != CDB_OK) return st;
+  if ((st = upload(ctx, bn, kNodeCols, N, ptrs(hn, kNodeCols), &din.nodes)) != CDB_OK) return st;
+  if ((st = upload(ctx, bm, kMemberCols, M, ptrs(hm, kMemberCols), &din.members)) != CDB_OK) return st;
+  if ((st = upload(ctx, ok, kKeyOutCols, K, {}, &dout.keys)) != CDB_OK) return st;
+  if ((st = upload(ctx, on, kNodeCols, N, {}, &dout.nodes)) != CDB_OK) return st;
+  if ((st = upload(ctx, om, kMemberCols, M, {}, &dout.members)) != CDB_OK) return st;
+  dout.compact = 1;
+  cdb_merge_stats local;
+  st = merge_device_impl(ctx, &din, opts, &dout, stats ? stats : &local, ctx->stream);
+  if (st != CDB_OK && st != CDB_DICT_MERGE_UNIMPLEMENTED) return st;
+  const cdb_status merge_st = st;
+  auto* m = new cdb_merged();
+  for (uint32_t i = 0; i < n; ++i) m->inputs.push_back(inputs[i]->b);
+  auto down = [&](std::vector<uint64_t>* dst, int nc, const cdb_dev_rows& r) -> cdb_status {
+    for (int c = 0; c < nc; ++c) {
+      dst[c].resize(r.n);
+      if (r.n) {
+        cdb_status s2 = hip_check(ctx, hipMemcpy(dst[c].data(), r.col[c], r.n * 8, hipMemcpyDeviceToHost), "d2h");
+        if (s2 != CDB_OK) return s2;
+      }
+    }
+    return CDB_OK;
+  };
+  if ((st = down(m->k, kKeyOutCols, dout.keys)) != CDB_OK || (st = down(m->nd, kNodeCols, dout.nodes)) != CDB_OK ||
+      (st = down(m->mb, kMemberCols, dout.members)) != CDB_OK) {
+    delete m;
+    return st;
+  }
+  *out = m;
+  return merge_st;
+}
+
+cdb_status cdb_merged_canonical_dump(cdb_ctx* ctx, cdb_merged* m, char** out, size_t* len) {
+  (void)ctx;
+  if (!m || !out || !len) return CDB_BAD_ARGUMENT;
+  const uint64_t nk = m->k[O_KH].size();
+  struct KeyView { const uint8_t* p; uint64_t n; uint64_t row; };
+  auto key_of = [&](uint64_t r) {
+    const uint64_t mt = m->k[O_META][r];
+    const Batch& b = *m->inputs[meta_pos(mt)];
+    const ByteRef kr = b.key_ref[meta_src(mt)];
+    return KeyView{b.raw.data() + kr.off, kr.len, r};
+  };
+  auto less = [](const KeyView& a, const KeyView& b) {
+    const int c = std::memcmp(a.p, b.p, std::min(a.n, b.n));
+    return c != 0 ? c < 0 : a.n < b.n;
+  };
+  std::vector<KeyView> data, exps, dels;
+  for (uint64_t r = 0; r < nk; ++r) {
+    const uint32_t T = meta_tag(m->k[O_META][r]);
+    (T == TAG_EXPIRE ? exps : T == TAG_DELETE ? dels : data).push_back(key_of(r));
+  }
+  std::sort(data.begin(), data.end(), less);
+  std::sort(exps.begin(), exps.end(), less);
+  std::sort(dels.begin(), dels.end(), less);
+  std::string o;
+  char buf[160];
+  for (const KeyView& kv : data) {
+    const uint64_t r = kv.row;
+    const uint32_t T = meta_tag(m->k[O_META][r]);
+    std::snprintf(buf, sizeof buf, " %u %llu %llu %llu\n", T, (unsigned long long)m->k[O_CT][r],
+                  (unsigned long long)m->k[O_UT][r], (unsigned long long)m->k[O_DT][r]);
+    o += "K " + hex(kv.p, kv.n) + buf;
+    const uint64_t cref = m->k[O_CREF][r];
+    const uint64_t cb = cref >> 24, cc = cref & 0xFFFFFF;
+    if (T == TAG_BYTES) {
+      const uint64_t w = m->k[O_WIN][r];
+      const Batch& b = *m->inputs[meta_pos(w)];
+      const ByteRef v = b.val_ref[meta_src(w)];
+      o += " V " + hex(b.raw.data() + v.off, v.len) + "\n";
+    } else if (T == TAG_COUNTER) {
+      std::snprintf(buf, sizeof buf, " S %lld\n", (long long)m->k[O_WIN][r]);
+      o += buf;
+      std::vector<uint64_t> rows;
+      for (uint64_t j = cb; j < cb + cc; ++j) rows.push_back(j);
+      std::sort(rows.begin(), rows.end(), [&](uint64_t a, uint64_t b) { return m->nd[C_ID1][a] < m->nd[C_ID1][b]; });
+      for (uint64_t j : rows) {
+        std::snprintf(buf, sizeof buf, " N %llu %lld %llu\n", (unsigned long long)m->nd[C_ID1][j],
+                      (long long)m->nd[C_ID2][j], (unsigned long long)m->nd[C_T][j]);
+        o += buf;
+      }
+    } else {
+      struct MV { const uint8_t* p; uint64_t n; uint64_t row; };
+      std::vector<MV> ms;
+      for (uint64_t j = cb; j < cb + cc; ++j) {
+        const uint64_t mt = m->mb[C_META][j];
+        const Batch& b = *m->inputs[meta_pos(mt)];
+        const ByteRef mr = b.m_ref[meta_src(mt)];
+        ms.push_back(MV{b.raw.data() + mr.off, mr.len, j});
+      }
+      std::sort(ms.begin(), ms.end(), [](const MV& a, const MV& b) {
+        const int c = std::memcmp(a.p, b.p, std::min(a.n, b.n));
+        return c != 0 ? c < 0 : a.n < b.n;
+      });
+      for (const MV& mv : ms) {
+        const uint64_t mt = m->mb[C_META][mv.row];
+        std::snprintf(buf, sizeof buf, " %llu", (unsigned long long)m->mb[C_T][mv.row]);
+        if (meta_tag(mt) == KIND_ADD) {
+          o += " A " + hex(mv.p, mv.n) + buf;
+          if (T == TAG_DICT) {
+            const Batch& b = *m->inputs[meta_pos(mt)];
+            const ByteRef vr = b.m_vref[meta_src(mt)];
+            o += " " + hex(b.raw.data() + vr.off, vr.len);
+          }
+          o += "\n";
+        } else {
+          o += " D " + hex(mv.p, mv.n) + buf + "\n";
+        }
+      }
+    }
+  }
+  for (int side = 0; side < 2; ++side) {
+    for (const KeyView& kv : side == 0 ? exps : dels) {
+      std::snprintf(buf, sizeof buf, " %llu\n", (unsigned long long)m->k[O_CT][kv.row]);
+      o += std::string(side == 0 ? "X " : "R ") + hex(kv.p, kv.n) + buf;
+    }
+  }
+  *out = (char*)std::malloc(o.size() + 1);
+  if (!*out) return CDB_OUT_OF_MEMORY;
+  std::memcpy(*out, o.data(), o.size());
+  (*out)[o.size()] = 0;
+  *len = o.size();
+  return CDB_OK;
+}
+
+void cdb_merged_free(cdb_merged* m) { delete m; }
+void cdb_free(void* p) { std::free(p); }
+
+}  // extern "C"

@@ -1,0 +1,385 @@
+// Snapshot decoder: ConstDB wire format -> columnar Batch.
+//
+// Follows the reference loader (snapshot.rs:120-295) and the object loaders
+// (object.rs:110-129, type_counter.rs:111-126, crdt/lwwhash.rs:207-226,341-358) but reads
+// from one in-memory buffer in a single pass (the reference issues one awaited
+// read_exact per varint flag byte and CRCs byte-slices as it goes) and emits SoA rows.
+#include <algorithm>
+#include <cstring>
+
+#include "../../include/cdb_merge.h"
+#include "batch.h"
+
+namespace cdb {
+namespace {
+
+// CRC-64/Jones (crc64 2.0.0, Cargo.lock:197-200): reflected poly 0x95AC9329AC4BC9B5,
+// init 0, no xorout. Slice-by-8 table for the decoder's one CRC pass over the stream.
+struct Crc64 {
+  uint64_t t[8][256];
+  Crc64() {
+    for (int i = 0; i < 256; ++i) {
+      uint64_t c = (uint64_t)i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x95AC9329AC4BC9B5ull : c >> 1;
+      t[0][i] = c;
+    }
+    for (int i = 0; i < 256; ++i)
+      for (int s = 1; s < 8; ++s) t[s][i] = t[0][t[s - 1][i] & 0xFF] ^ (t[s - 1][i] >> 8);
+  }
+  uint64_t update(uint64_t crc, const uint8_t* p, size_t n) const {
+    while (n >= 8) {
+      uint64_t w;
+      std::memcpy(&w, p, 8);
+      crc ^= w;
+      crc = t[7][crc & 0xFF] ^ t[6][(crc >> 8) & 0xFF] ^ t[5][(crc >> 16) & 0xFF] ^
+            t[4][(crc >> 24) & 0xFF] ^ t[3][(crc >> 32) & 0xFF] ^ t[2][(crc >> 40) & 0xFF] ^
+            t[1][(crc >> 48) & 0xFF] ^ t[0][crc >> 56];
+      p += 8;
+      n -= 8;
+    }
+    while (n--) crc = t[0][(crc ^ *p++) & 0xFF] ^ (crc >> 8);
+    return crc;
+  }
+};
+const Crc64& crc_tables() {
+  static const Crc64 c;
+  return c;
+}
+
+struct Cursor {
+  const uint8_t* p;
+  size_t n, off = 0;
+  int err = CDB_OK;
+
+  bool need(size_t k) {
+    if (k > n - off) { err = CDB_IO_ERROR; return false; }  // read_exact -> UnexpectedEof
+    return true;
+  }
+  bool u8(uint8_t* b) {
+    if (!need(1)) return false;
+    *b = p[off++];
+    return true;
+  }
+  // read_integer (snapshot.rs:243-264): 2-bit tag in the flag byte's top bits.
+  bool integer(int64_t* out) {
+    uint8_t f;
+    if (!u8(&f)) return false;
+    switch (f >> 6) {
+      case 0: *out = f & 0x3F; return true;
+      case 1:
+        if (!need(1)) return false;
+        *out = ((int64_t)(f & 0x3F) << 8) | p[off];
+        off += 1;
+        return true;
+      case 2:
+        if (!need(3)) return false;
+        *out = ((int64_t)(f & 0x3F) << 24) | ((int64_t)p[off] << 16) | ((int64_t)p[off + 1] << 8) | p[off + 2];
+        off += 3;
+        return true;
+      default: {
+        if (!need(8)) return false;
+        uint64_t v = 0;
+        for (int i = 0; i < 8; ++i) v = (v << 8) | p[off + i];
+        off += 8;
+        *out = (int64_t)v;
+        return true;
+      }
+    }
+  }
+  bool u64(uint64_t* out) {  // `as u64` of the i64
+    int64_t v;
+    if (!integer(&v)) return false;
+    *out = (uint64_t)v;
+    return true;
+  }
+  bool length(uint64_t* out) {  // `as usize`: a negative length can never be read
+    int64_t v;
+    if (!integer(&v)) return false;
+    if (v < 0) { err = CDB_IO_ERROR; return false; }
+    *out = (uint64_t)v;
+    return true;
+  }
+  bool span(ByteRef* r) {  // length-prefixed bytes
+    uint64_t l;
+    if (!length(&l) || !need(l)) return false;
+    r->off = off;
+    r->len = l;
+    off += l;
+    return true;
+  }
+};
+
+bool valid_utf8(const uint8_t* s, size_t n) {
+  size_t i = 0;
+  while (i < n) {
+    const uint8_t c = s[i];
+    size_t k;
+    uint32_t cp;
+    if (c < 0x80) { i += 1; continue; }
+    if ((c >> 5) == 6) { k = 1; cp = c & 0x1F; }
+    else if ((c >> 4) == 14) { k = 2; cp = c & 0x0F; }
+    else if ((c >> 3) == 30) { k = 3; cp = c & 0x07; }
+    else return false;
+    if (i + k >= n) return false;
+    for (size_t j = 1; j <= k; ++j) {
+      if ((s[i + j] & 0xC0) != 0x80) return false;
+      cp = (cp << 6) | (s[i + j] & 0x3F);
+    }
+    if ((k == 1 && cp < 0x80) || (k == 2 && cp < 0x800) || (k == 3 && cp < 0x10000) || cp > 0x10FFFF ||
+        (cp >= 0xD800 && cp <= 0xDFFF))
+      return false;
+    i += k + 1;
+  }
+  return true;
+}
+
+struct Decoder {
+  Cursor c;
+  Batch* b;
+  const uint8_t* base;
+
+  bool str(std::string* s) {
+    ByteRef r;
+    if (!c.span(&r)) return false;
+    if (!valid_utf8(base + r.off, r.len)) {  // snapshot.rs:143-149 unwraps -> panic
+      c.err = CDB_INVALID_SNAPSHOT;
+      return false;
+    }
+    s->assign((const char*)base + r.off, r.len);
+    return true;
+  }
+
+  // Counter::load_snapshot (type_counter.rs:111-126): data.insert per node (the last of a
+  // duplicated node id wins) while `total` sums every value read (wrapping i64).
+  bool counter(uint64_t kh, uint64_t kf, uint64_t* total) {
+    uint64_t cnt;
+    if (!c.length(&cnt)) return false;
+    struct N { uint64_t node, v, t; };
+    std::vector<N> ns;
+    ns.reserve(cnt < (1u << 20) ? cnt : (1u << 20));
+    uint64_t sum = 0;
+    for (uint64_t i = 0; i < cnt; ++i) {
+      N x;
+      int64_t v;
+      if (!c.u64(&x.node) || !c.integer(&v) || !c.u64(&x.t)) return false;
+      x.v = (uint64_t)v;
+      sum += x.v;
+      ns.push_back(x);
+    }
+    // A node id repeated inside one counter (never written by type_counter.rs:101-109):
+    // HashMap::insert keeps the last (node, v, t); `total` still counted every value.
+    std::vector<uint8_t> keep(ns.size(), 1);
+    if (ns.size() > 1) {
+      std::vector<uint32_t> ord(ns.size());
+      for (uint32_t i = 0; i < ord.size(); ++i) ord[i] = i;
+      std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b2) {
+        return ns[a].node != ns[b2].node ? ns[a].node < ns[b2].node : a < b2;
+      });
+      for (size_t j = 0; j + 1 < ord.size(); ++j)
+        if (ns[ord[j]].node == ns[ord[j + 1]].node) keep[ord[j]] = 0;
+    }
+    for (size_t i = 0; i < ns.size(); ++i) {
+      if (!keep[i]) continue;
+      const uint64_t src = b->n_pkh.size();
+      b->n_pkh.push_back(kh);
+      b->n_pkf.push_back(kf);
+      b->n_node.push_back(ns[i].node);
+      b->n_v.push_back(ns[i].v);
+      b->n_t.push_back(ns[i].t);
+      b->n_meta.push_back(meta_pack(0, 0, src));
+    }
+    *total = sum;
+    return true;
+  }
+
+  // Set/Dict::load_snapshot (lwwhash.rs:207-226, 341-358): every add through set(), then
+  // every del through rem(). Emits the resulting single tag per member.
+  bool lwwhash(uint64_t kh, uint64_t kf, bool is_dict) {
+    struct Op { Hash128 id; ByteRef m, v; uint64_t t; bool add; };
+    std::vector<Op> ops;
+    uint64_t na;
+    if (!c.length(&na)) return false;
+    ops.reserve(na);
+    for (uint64_t i = 0; i < na; ++i) {
+      Op o;
+      if (!c.span(&o.m) || !c.u64(&o.t)) return false;
+      o.v = {0, 0};
+      if (is_dict && !c.span(&o.v)) return false;
+      o.add = true;
+      o.id = hash_bytes(base + o.m.off, o.m.len, kDomainMember);
+      ops.push_back(o);
+    }
+    uint64_t nd;
+    if (!c.length(&nd)) return false;
+    for (uint64_t i = 0; i < nd; ++i) {
+      Op o;
+      if (!c.span(&o.m) || !c.u64(&o.t)) return false;
+      o.v = {0, 0};
+      o.add = false;
+      o.id = hash_bytes(base + o.m.off, o.m.len, kDomainMember);
+      ops.push_back(o);
+    }
+    // Duplicate members within one object (never written by lwwhash.rs:189-205/325-339,
+    // whose add/del maps hold a member at most once in total): replay set/rem exactly.
+    std::vector<uint32_t> order(ops.size());
+    for (uint32_t i = 0; i < ops.size(); ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+      if (ops[x].id.h != ops[y].id.h) return ops[x].id.h < ops[y].id.h;
+      if (ops[x].id.f != ops[y].id.f) return ops[x].id.f < ops[y].id.f;
+      return x < y;
+    });
+    std::vector<uint8_t> keep(ops.size(), 1);
+    for (size_t s = 0; s < order.size();) {
+      size_t e = s + 1;
+      while (e < order.size() && ops[order[e]].id.h == ops[order[s]].id.h && ops[order[e]].id.f == ops[order[s]].id.f) ++e;
+      if (e - s > 1) {
+        // state machine of lwwhash.rs:87-128 over the ops of this member in stream order
+        int st = -1;  // index of the op holding the current tag, -1 = none
+        for (size_t j = s; j < e; ++j) {
+          const Op& o = ops[order[j]];
+          if (st >= 0 && ops[st].t > o.t) continue;  // tag newer than o -> rejected
+          st = (int)order[j];
+        }
+        for (size_t j = s; j < e; ++j) keep[order[j]] = (int)order[j] == st;
+      }
+      s = e;
+    }
+    for (size_t i = 0; i < ops.size(); ++i) {
+      if (!keep[i]) continue;
+      const Op& o = ops[i];
+      const uint64_t src = b->m_pkh.size();
+      b->m_pkh.push_back(kh);
+      b->m_pkf.push_back(kf);
+      b->m_h.push_back(o.id.h);
+      b->m_f.push_back(o.id.f);
+      b->m_t.push_back(o.t);
+      b->m_meta.push_back(meta_pack(o.add ? KIND_ADD : KIND_DEL, 0, src));
+      b->m_ref.push_back(o.m);
+      b->m_vref.push_back(o.v);
+    }
+    return true;
+  }
+
+  bool data_entry() {  // read_entry (snapshot.rs:280-287) + Object::load_snapshot
+    ByteRef k;
+    if (!c.span(&k)) return false;
+    uint64_t ct, ut, dt;
+    if (!c.u64(&ct) || !c.u64(&ut) || !c.u64(&dt)) return false;
+    uint8_t tag;
+    if (!c.u8(&tag)) return false;
+    const Hash128 h = hash_bytes(base + k.off, k.len, kDomainKey);
+    uint64_t aux = 0;
+    ByteRef v{0, 0};
+    switch (tag) {
+      case TAG_COUNTER:
+        if (!counter(h.h, h.f, &aux)) return false;
+        break;
+      case TAG_BYTES:
+        if (!c.span(&v)) return false;
+        break;
+      case TAG_SET:
+      case TAG_DICT:
+        if (!lwwhash(h.h, h.f, tag == TAG_DICT)) return false;
+        break;
+      default:
+        c.err = CDB_INVALID_TYPE;  // object.rs:121
+        return false;
+    }
+    push_key(h, ct, ut, dt, aux, tag, k, v);
+    return true;
+  }
+
+  void push_key(const Hash128& h, uint64_t ct, uint64_t ut, uint64_t dt, uint64_t aux, uint8_t tag,
+                ByteRef k, ByteRef v) {
+    const uint64_t src = b->kh.size();
+    b->kh.push_back(h.h);
+    b->kf.push_back(h.f);
+    b->ct.push_back(ct);
+    b->ut.push_back(ut);
+    b->dt.push_back(dt);
+    b->aux.push_back(aux);
+    b->meta.push_back(meta_pack(tag, 0, src));
+    b->key_ref.push_back(k);
+    b->val_ref.push_back(v);
+  }
+
+  bool side_entry(uint8_t tag) {  // read_key_int (snapshot.rs:289-295)
+    ByteRef k;
+    uint64_t t;
+    if (!c.span(&k) || !c.u64(&t)) return false;
+    const Hash128 h = hash_bytes(base + k.off, k.len, kDomainKey);
+    push_key(h, t, 0, 0, 0, tag, k, ByteRef{0, 0});
+    return true;
+  }
+
+  int run(uint32_t flags, size_t* err_off) {
+    auto fail = [&]() {
+      *err_off = c.off;
+      return c.err == CDB_OK ? CDB_INVALID_SNAPSHOT : c.err;
+    };
+    // Begin + Version (snapshot.rs:123-139); the magic is not checked by the reference.
+    if (!c.need(11)) return fail();
+    char vbuf[32];
+    snprintf(vbuf, sizeof vbuf, "%u.%u.%u.%u", base[7], base[8], base[9], base[10]);
+    b->version = vbuf;
+    c.off = 11;
+    // Node (snapshot.rs:140-153)
+    if (!c.u64(&b->node_id) || !str(&b->alias) || !str(&b->addr) || !c.u64(&b->uuid_he_sent)) return fail();
+    for (;;) {
+      uint8_t flag;
+      if (!c.u8(&flag)) return fail();  // convert_stat (snapshot.rs:222-241)
+      if (flag == 3) {                  // SNAPSHOT_FLAG_REPLICA_ADD
+        ReplicaAdd r;
+        if (!c.u64(&r.add_time) || !c.u64(&r.node_id) || !str(&r.alias) || !str(&r.addr) || !c.u64(&r.uuid))
+          return fail();
+        b->replica_add.push_back(std::move(r));
+      } else if (flag == 4) {  // SNAPSHOT_FLAG_REPLICA_REM
+        ReplicaDel r;
+        if (!str(&r.addr) || !c.u64(&r.t)) return fail();
+        b->replica_del.push_back(std::move(r));
+      } else if (flag == 5 || flag == 6 || flag == 7) {  // DATAS / EXPIRES / DELETES
+        uint64_t cnt;
+        if (!c.length(&cnt)) return fail();
+        for (uint64_t i = 0; i < cnt; ++i) {
+          bool ok = flag == 5 ? data_entry() : side_entry(flag == 6 ? TAG_EXPIRE : TAG_DELETE);
+          if (!ok) return fail();
+        }
+        if (flag == 5) b->n_data += cnt;
+        else if (flag == 6) b->n_expires += cnt;
+        else b->n_deletes += cnt;
+      } else if (flag == 8) {  // SNAPSHOT_FLAG_CHECKSUM
+        const uint64_t crc = crc_tables().update(0, base, c.off);
+        if (flags & CDB_DECODE_REFERENCE_CHECKSUM) {
+          // snapshot.rs:207-213: read the checksum as a varint, CRC those bytes too
+          const size_t at = c.off;
+          int64_t got;
+          if (!c.integer(&got)) return fail();
+          const uint64_t crc2 = crc_tables().update(crc, base + at, c.off - at);
+          if ((uint64_t)got != crc2) { *err_off = c.off; return CDB_INVALID_SNAPSHOT_CHECKSUM; }
+          return CDB_OK;
+        }
+        if (!c.need(8)) return fail();
+        uint64_t got = 0;
+        for (int i = 7; i >= 0; --i) got = (got << 8) | base[c.off + i];
+        c.off += 8;
+        if (got != crc) { *err_off = c.off; return CDB_INVALID_SNAPSHOT_CHECKSUM; }
+        return CDB_OK;
+      } else {
+        c.err = CDB_INVALID_SNAPSHOT;
+        c.off -= 1;
+        return fail();
+      }
+    }
+  }
+};
+
+}  // namespace
+
+int decode_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off) {
+  out->raw.assign(buf, buf + len);
+  Decoder d{Cursor{out->raw.data(), out->raw.size()}, out, out->raw.data()};
+  *err_off = 0;
+  return d.run(flags, err_off);
+}
+
+}  // namespace cdb

@@ -1,0 +1,35 @@
+// Internal engine interface shared by the HIP driver (engine.hip) and the host C-ABI
+// glue (capi.cpp). Not part of the public ABI (include/cdb_merge.h is).
+#pragma once
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/cdb_merge.h"
+
+struct cdb_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_part = nullptr, ev_bucket = nullptr;
+  std::string last_error;
+  struct Buf { void* p = nullptr; size_t bytes = 0; };
+  Buf ws[32];  // named workspace slots, grown on demand, reused across calls
+};
+
+namespace cdb {
+
+enum WsSlot {
+  WS_KA = 0, WS_KB, WS_NA, WS_NB, WS_MA, WS_MB,         // partition ping-pong per family
+  WS_DIR,                                               // bucket directories + hist/cursor
+  WS_MISC,                                              // stats, last_bad, hot list
+  WS_HOT,                                               // hot-bucket scratch slab
+  WS_SCAN,                                              // scan partials
+  WS_COUNT
+};
+
+cdb_status fail(cdb_ctx* ctx, cdb_status st, const std::string& msg);
+cdb_status hip_check(cdb_ctx* ctx, hipError_t e, const char* what);
+void* ws_get(cdb_ctx* ctx, int slot, size_t bytes, cdb_status* st);
+
+}  // namespace cdb

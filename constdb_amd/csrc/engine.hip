@@ -1,0 +1,436 @@
+// HIP driver of the merge pipeline (gfx950): partition -> fused bucket merge ->
+// over-capacity buckets -> dense compaction. Also the device-level C-ABI entry points.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "bucket.hip.h"
+#include "engine.h"
+#include "partition.hip.h"
+
+namespace cdb {
+
+cdb_status fail(cdb_ctx* ctx, cdb_status st, const std::string& msg) {
+  if (ctx) ctx->last_error = msg;
+  return st;
+}
+
+cdb_status hip_check(cdb_ctx* ctx, hipError_t e, const char* what) {
+  if (e == hipSuccess) return CDB_OK;
+  return fail(ctx, e == hipErrorOutOfMemory ? CDB_OUT_OF_MEMORY : CDB_DEVICE_ERROR,
+              std::string(what) + ": " + hipGetErrorString(e));
+}
+
+void* ws_get(cdb_ctx* ctx, int slot, size_t bytes, cdb_status* st) {
+  cdb_ctx::Buf& b = ctx->ws[slot];
+  if (b.bytes >= bytes && b.p) return b.p;
+  if (b.p) {
+    hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 20);
+  want = (want + 4095) & ~size_t(4095);
+  hipError_t e = hipMalloc(&b.p, want);
+  if (e != hipSuccess) {
+    *st = hip_check(ctx, e, "hipMalloc(workspace)");
+    b.p = nullptr;
+    return nullptr;
+  }
+  b.bytes = want;
+  return b.p;
+}
+
+namespace {
+
+#define CDB_TRY(...)                  \
+  do {                                \
+    cdb_status _s = (__VA_ARGS__);    \
+    if (_s != CDB_OK) return _s;      \
+  } while (0)
+#define CDB_HIP(x, what) CDB_TRY(hip_check(ctx, (x), what))
+
+__global__ void set_dir_kernel(uint32_t* base, uint32_t* cnt, uint32_t n) {
+  base[0] = 0;
+  cnt[0] = n;
+}
+
+__global__ void gc_lastbad_kernel(const uint64_t* __restrict__ ct, const uint64_t* __restrict__ meta, uint64_t n,
+                                  uint64_t wm, unsigned long long* out) {
+  uint64_t best = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t m = meta[i];
+    if (meta_tag(m) == TAG_DELETE && ct[i] > wm) best = max(best, meta_order(m) + 1);
+  }
+  for (int o = 32; o > 0; o >>= 1) best = max(best, (uint64_t)__shfl_xor((unsigned long long)best, o, 64));
+  if ((threadIdx.x & 63) == 0 && best) atomicMax(out, (unsigned long long)best);
+}
+
+struct CompactArgs {
+  const uint64_t* ks[kKeyOutCols];
+  uint64_t* kd[kKeyOutCols];
+  const uint64_t* ns[kNodeCols];
+  uint64_t* nd[kNodeCols];
+  const uint64_t* ms[kMemberCols];
+  uint64_t* md[kMemberCols];
+  const uint32_t *kbase, *nbase, *mbase, *kout, *nout, *mout, *kdoff, *ndoff, *mdoff;
+};
+
+// Sparse-by-bucket outputs -> dense arrays; child ranges become absolute row indices.
+__global__ void __launch_bounds__(256) compact_kernel(CompactArgs A, uint32_t nbuckets) {
+  const uint32_t b = blockIdx.x;
+  if (b >= nbuckets) return;
+  const uint32_t kn = A.kout[b], ks = A.kbase[b], kd = A.kdoff[b];
+  for (int c = 0; c < kKeyOutCols; ++c) {
+    for (uint32_t i = threadIdx.x; i < kn; i += blockDim.x) {
+      uint64_t v = A.ks[c][ks + i];
+      if (c == O_CREF) {
+        const uint64_t cnt = v & 0xFFFFFF;
+        const uint32_t T = meta_tag(A.ks[O_META][ks + i]);
+        const uint64_t begin = cnt ? (v >> 24) + (T == TAG_COUNTER ? A.ndoff[b] : A.mdoff[b]) : 0;
+        v = cref_pack(begin, cnt);
+      }
+      A.kd[c][kd + i] = v;
+    }
+  }
+  const uint32_t nn = A.nout[b], ns = A.nbase[b], ndo = A.ndoff[b];
+  for (int c = 0; c < kNodeCols; ++c)
+    for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) A.nd[c][ndo + i] = A.ns[c][ns + i];
+  const uint32_t mn = A.mout[b], ms = A.mbase[b], mdo = A.mdoff[b];
+  for (int c = 0; c < kMemberCols; ++c)
+    for (uint32_t i = threadIdx.x; i < mn; i += blockDim.x) A.md[c][mdo + i] = A.ms[c][ms + i];
+}
+
+template <typename T, typename OutT>
+cdb_status exclusive_scan(cdb_ctx* ctx, const T* in, uint64_t n, OutT* out, OutT* out2, uint64_t* d_total,
+                          hipStream_t s) {
+  const uint64_t tiles = std::max<uint64_t>(1, (n + kScanTile - 1) / kScanTile);
+  cdb_status st = CDB_OK;
+  uint64_t* sums = (uint64_t*)ws_get(ctx, WS_SCAN, tiles * sizeof(uint64_t), &st);
+  if (!sums) return st;
+  scan_reduce_kernel<T><<<tiles, kScanThreads, 0, s>>>(in, n, sums);
+  scan_sums_kernel<<<1, kScanThreads, 0, s>>>(sums, tiles, d_total);
+  scan_apply_kernel<T, OutT><<<tiles, kScanThreads, 0, s>>>(in, n, sums, out, out2);
+  return hip_check(ctx, hipGetLastError(), "scan");
+}
+
+struct Dir {  // per-family bucket directory
+  uint32_t *hist, *base, *cursor, *out, *doff;
+};
+
+// Splits `n` rows of an NC-column family into 2^B buckets by the top bits of column 0.
+// Returns in `res` the columns holding the bucketed rows (one of in / A / B).
+template <int NC>
+cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, int B, uint64_t* const* A,
+                            uint64_t* const* Bf, const Dir& d, uint64_t** res, uint64_t** spare,
+                            hipStream_t s) {
+  if (B == 0 || n == 0) {
+    set_dir_kernel<<<1, 1, 0, s>>>(d.base, d.hist, (uint32_t)n);
+    if (B > 0) {  // n == 0 with buckets: every bucket empty
+      CDB_HIP(hipMemsetAsync(d.base, 0, sizeof(uint32_t) << B, s), "memset");
+      CDB_HIP(hipMemsetAsync(d.hist, 0, sizeof(uint32_t) << B, s), "memset");
+    }
+    for (int c = 0; c < NC; ++c) {
+      res[c] = in[c];
+      spare[c] = A[c];
+    }
+    return hip_check(ctx, hipGetLastError(), "set_dir");
+  }
+  const int levels = (B + 8) / 9;
+  int bits[8];
+  for (int l = 0; l < levels; ++l) bits[l] = B / levels + (l < B % levels ? 1 : 0);
+  const uint64_t tiles = (n + kPartTile - 1) / kPartTile;
+  uint64_t* const* cur = in;
+  int btot = 0;
+  for (int l = 0; l < levels; ++l) {
+    btot += bits[l];
+    uint64_t* const* dst = (l % 2 == 0) ? A : Bf;
+    const uint64_t nb = 1ull << btot;
+    CDB_HIP(hipMemsetAsync(d.hist, 0, nb * sizeof(uint32_t), s), "memset hist");
+    part_hist_kernel<<<tiles, kPartThreads, 0, s>>>(cur[0], n, btot, bits[l], d.hist);
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, d.hist, nb, d.base, d.cursor, nullptr, s));
+    ColSet<NC> ci, co;
+    for (int c = 0; c < NC; ++c) {
+      ci.c[c] = cur[c];
+      co.c[c] = dst[c];
+    }
+    part_scatter_kernel<NC><<<tiles, kPartThreads, 0, s>>>(ci, co, n, btot, bits[l], d.cursor);
+    CDB_HIP(hipGetLastError(), "partition");
+    cur = dst;
+  }
+  uint64_t* const* other = (cur == A) ? Bf : A;
+  for (int c = 0; c < NC; ++c) {
+    res[c] = cur[c];
+    spare[c] = other[c];
+  }
+  return CDB_OK;
+}
+
+int choose_bucket_bits(uint64_t K, uint64_t N, uint64_t M) {
+  // ~384 rows of each family per bucket on average: the LDS path holds 1024.
+  const uint64_t need = std::max<uint64_t>({(K + 383) / 384, (N + 383) / 384, (M + 383) / 384, 1});
+  int B = 0;
+  while ((1ull << B) < need) ++B;
+  return std::min(B, 24);
+}
+
+}  // namespace
+
+cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts,
+                             cdb_dev_output* out, cdb_merge_stats* stats, hipStream_t s) {
+  const uint64_t K = in->keys.n, N = in->nodes.n, M = in->members.n;
+  if (in->n_pos > (uint32_t)kMaxPos) return fail(ctx, CDB_BAD_ARGUMENT, "at most 63 fold positions per merge");
+  if (K >= (1ull << 32) || N >= (1ull << 32) || M >= (1ull << 32))
+    return fail(ctx, CDB_BAD_ARGUMENT, "row counts must be < 2^32 per family per device");
+  const uint32_t flags = opts ? opts->flags : 0;
+  const uint64_t wm = opts ? opts->gc_watermark : 0;
+  const int B = choose_bucket_bits(K, N, M);
+  const uint64_t nb = 1ull << B;
+  cdb_status st = CDB_OK;
+
+  // ---- workspace
+  auto cols = [&](int slot, int ncol, uint64_t rows, uint64_t** p) -> cdb_status {
+    const uint64_t r = std::max<uint64_t>(rows, 1);
+    uint64_t* base = (uint64_t*)ws_get(ctx, slot, ncol * r * sizeof(uint64_t), &st);
+    if (!base) return st;
+    for (int c = 0; c < ncol; ++c) p[c] = base + c * r;
+    return CDB_OK;
+  };
+  uint64_t *KA[8], *KB[8], *NA[6], *NB[6], *MA[6], *MBf[6];
+  CDB_TRY(cols(WS_KA, 8, K, KA));
+  CDB_TRY(cols(WS_KB, 8, K, KB));
+  CDB_TRY(cols(WS_NA, 6, N, NA));
+  CDB_TRY(cols(WS_NB, 6, N, NB));
+  CDB_TRY(cols(WS_MA, 6, M, MA));
+  CDB_TRY(cols(WS_MB, 6, M, MBf));
+  const uint64_t dn = nb + 1;
+  uint32_t* dir = (uint32_t*)ws_get(ctx, WS_DIR, 15 * dn * sizeof(uint32_t), &st);
+  if (!dir) return st;
+  Dir dk{dir, dir + dn, dir + 2 * dn, dir + 3 * dn, dir + 4 * dn};
+  Dir dnd{dir + 5 * dn, dir + 6 * dn, dir + 7 * dn, dir + 8 * dn, dir + 9 * dn};
+  Dir dm{dir + 10 * dn, dir + 11 * dn, dir + 12 * dn, dir + 13 * dn, dir + 14 * dn};
+  // misc: stats[8] u64 | last_bad u64 | totals[3] u64 | hot_count u32 (+pad) | hot_list[nb] u32
+  uint8_t* misc = (uint8_t*)ws_get(ctx, WS_MISC, 128 + nb * sizeof(uint32_t), &st);
+  if (!misc) return st;
+  unsigned long long* d_stats = (unsigned long long*)misc;
+  unsigned long long* d_last_bad = (unsigned long long*)(misc + 64);
+  uint64_t* d_totals = (uint64_t*)(misc + 72);
+  uint32_t* d_hot_count = (uint32_t*)(misc + 96);
+  uint32_t* d_hot_list = (uint32_t*)(misc + 128);
+  CDB_HIP(hipMemsetAsync(misc, 0, 128, s), "memset misc");
+
+  CDB_HIP(hipEventRecord(ctx->ev0, s), "event");
+  // ---- 1. bucket partition of each family by (parent) key hash
+  uint64_t *kb[8], *ksp[8], *ndb[6], *nsp[6], *mbb[6], *msp[6];
+  uint64_t* kin[8];
+  uint64_t* nin[6];
+  uint64_t* min_[6];
+  for (int c = 0; c < 8; ++c) kin[c] = in->keys.col[c];
+  for (int c = 0; c < 6; ++c) {
+    nin[c] = in->nodes.col[c];
+    min_[c] = in->members.col[c];
+  }
+  CDB_TRY(partition_family<kKeyCols>(ctx, kin, K, B, KA, KB, dk, kb, ksp, s));
+  // keys need 8 output columns: the spare buffer always has 8
+  CDB_TRY(partition_family<kNodeCols>(ctx, nin, N, B, NA, NB, dnd, ndb, nsp, s));
+  CDB_TRY(partition_family<kMemberCols>(ctx, min_, M, B, MA, MBf, dm, mbb, msp, s));
+  {  // sparse key outputs (8 columns) go to whichever ping-pong buffer is free
+    uint64_t* const* free_k = (kb[0] == KA[0]) ? KB : KA;
+    for (int c = 0; c < 8; ++c) ksp[c] = free_k[c];
+  }
+
+  CDB_HIP(hipEventRecord(ctx->ev_part, s), "event");
+  // ---- 2. GC watermark scan (DB::gc's LIFO stop point)
+  if ((flags & CDB_MERGE_GC_DELETES) && K) {
+    gc_lastbad_kernel<<<1024, 256, 0, s>>>(in->keys.col[K_CT], in->keys.col[K_META], K, wm, d_last_bad);
+    CDB_HIP(hipGetLastError(), "gc_lastbad");
+  }
+
+  // ---- 3. fused bucket merge
+  BucketArgs A;
+  std::memset(&A, 0, sizeof A);
+  for (int c = 0; c < kKeyCols; ++c) A.k[c] = kb[c];
+  for (int c = 0; c < kNodeCols; ++c) {
+    A.nd[c] = ndb[c];
+    A.mb[c] = mbb[c];
+    A.no[c] = nsp[c];
+    A.mo[c] = msp[c];
+  }
+  for (int c = 0; c < kKeyOutCols; ++c) A.ko[c] = ksp[c];
+  A.kbase = dk.base; A.kcnt = dk.hist;
+  A.nbase = dnd.base; A.ncnt = dnd.hist;
+  A.mbase = dm.base; A.mcnt = dm.hist;
+  A.bbits = B;
+  A.kout = dk.out; A.nout = dnd.out; A.mout = dm.out;
+  A.flags = (flags & CDB_MERGE_STRICT_DICT_PANIC ? F_DICT_STRICT : 0) |
+            (flags & CDB_MERGE_GC_DELETES ? F_GC_DELETES : 0) | (flags & CDB_MERGE_GC_MEMBERS ? F_GC_MEMBERS : 0);
+  A.gc_wm = wm;
+  A.last_bad = (const uint64_t*)d_last_bad;
+  A.stats = d_stats;
+  A.hot_list = d_hot_list;
+  A.hot_count = d_hot_count;
+  bucket_kernel<<<nb, kBktThreads, 0, s>>>(A, (uint32_t)nb);
+  CDB_HIP(hipGetLastError(), "bucket_kernel");
+  CDB_HIP(hipEventRecord(ctx->ev_bucket, s), "event");
+
+  // ---- 4. over-capacity buckets (same algorithm, global scratch)
+  uint32_t hot = 0;
+  CDB_HIP(hipMemcpyAsync(&hot, d_hot_count, sizeof hot, hipMemcpyDeviceToHost, s), "d2h");
+  CDB_HIP(hipStreamSynchronize(s), "sync");
+  if (hot) {
+    std::vector<uint32_t> ids(hot), kc(hot), nc(hot), mc(hot);
+    CDB_HIP(hipMemcpy(ids.data(), d_hot_list, hot * sizeof(uint32_t), hipMemcpyDeviceToHost), "d2h");
+    std::sort(ids.begin(), ids.end());
+    std::vector<uint64_t> off(hot);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < hot; ++i) {
+      CDB_HIP(hipMemcpy(&kc[i], dk.hist + ids[i], 4, hipMemcpyDeviceToHost), "d2h");
+      CDB_HIP(hipMemcpy(&nc[i], dnd.hist + ids[i], 4, hipMemcpyDeviceToHost), "d2h");
+      CDB_HIP(hipMemcpy(&mc[i], dm.hist + ids[i], 4, hipMemcpyDeviceToHost), "d2h");
+      off[i] = total;
+      total += hot_scratch_words(kc[i], std::max(nc[i], mc[i]));
+      total = (total + 15) & ~uint64_t(15);
+    }
+    uint8_t* slab = (uint8_t*)ws_get(ctx, WS_HOT, total * 8 + hot * 12 + 64, &st);
+    if (!slab) return st;
+    uint64_t* d_off = (uint64_t*)(slab + total * 8);
+    uint32_t* d_ids = (uint32_t*)(d_off + hot);
+    CDB_HIP(hipMemcpyAsync(d_off, off.data(), hot * 8, hipMemcpyHostToDevice, s), "h2d");
+    CDB_HIP(hipMemcpyAsync(d_ids, ids.data(), hot * 4, hipMemcpyHostToDevice, s), "h2d");
+    A.hot_in = d_ids;
+    A.hot_scratch = (uint64_t*)slab;
+    A.hot_scratch_off = d_off;
+    bucket_hot_kernel<<<hot, kBktThreads, 0, s>>>(A);
+    CDB_HIP(hipGetLastError(), "bucket_hot_kernel");
+  }
+
+  // ---- 5. dense compaction into the caller's output columns
+  CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dk.out, nb, dk.doff, (uint32_t*)nullptr, d_totals + 0, s));
+  CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dnd.out, nb, dnd.doff, (uint32_t*)nullptr, d_totals + 1, s));
+  CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dm.out, nb, dm.doff, (uint32_t*)nullptr, d_totals + 2, s));
+  CompactArgs C;
+  for (int c = 0; c < kKeyOutCols; ++c) {
+    C.ks[c] = ksp[c];
+    C.kd[c] = out->keys.col[c];
+  }
+  for (int c = 0; c < kNodeCols; ++c) {
+    C.ns[c] = nsp[c];
+    C.nd[c] = out->nodes.col[c];
+    C.ms[c] = msp[c];
+    C.md[c] = out->members.col[c];
+  }
+  C.kbase = dk.base; C.nbase = dnd.base; C.mbase = dm.base;
+  C.kout = dk.out; C.nout = dnd.out; C.mout = dm.out;
+  C.kdoff = dk.doff; C.ndoff = dnd.doff; C.mdoff = dm.doff;
+  compact_kernel<<<nb, 256, 0, s>>>(C, (uint32_t)nb);
+  CDB_HIP(hipGetLastError(), "compact_kernel");
+  CDB_HIP(hipEventRecord(ctx->ev1, s), "event");
+
+  uint64_t totals[3];
+  unsigned long long hs[ST_COUNT];
+  CDB_HIP(hipMemcpyAsync(totals, d_totals, sizeof totals, hipMemcpyDeviceToHost, s), "d2h");
+  CDB_HIP(hipMemcpyAsync(hs, d_stats, sizeof hs, hipMemcpyDeviceToHost, s), "d2h");
+  CDB_HIP(hipStreamSynchronize(s), "sync");
+  out->keys.n = totals[0];
+  out->nodes.n = totals[1];
+  out->members.n = totals[2];
+  if (stats) {
+    std::memset(stats, 0, sizeof *stats);
+    stats->key_rows_in = K;
+    stats->node_rows_in = N;
+    stats->member_rows_in = M;
+    stats->key_rows_out = totals[0];
+    stats->node_rows_out = totals[1];
+    stats->member_rows_out = totals[2];
+    stats->type_conflicts = hs[ST_TYPE_CONFLICTS];
+    stats->dict_merges = hs[ST_DICT_MERGES];
+    stats->deletes_gced = hs[ST_DELETES_GCED];
+    stats->members_gced = hs[ST_MEMBERS_GCED];
+    stats->duplicate_rows = hs[ST_DUP_ROWS];
+    stats->orphan_children = hs[ST_ORPHANS];
+    stats->hot_buckets = hot;
+    float ms = 0;
+    hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
+    stats->device_ms = ms;
+    hipEventElapsedTime(&ms, ctx->ev0, ctx->ev_part);
+    stats->partition_ms = ms;
+    hipEventElapsedTime(&ms, ctx->ev_part, ctx->ev_bucket);
+    stats->bucket_ms = ms;
+    hipEventElapsedTime(&ms, ctx->ev_bucket, ctx->ev1);
+    stats->finish_ms = ms;
+  }
+  if ((flags & CDB_MERGE_STRICT_DICT_PANIC) && hs[ST_DICT_MERGES])
+    return fail(ctx, CDB_DICT_MERGE_UNIMPLEMENTED, "Dict::merge reached (lwwhash.rs:180 unimplemented!())");
+  return CDB_OK;
+}
+
+}  // namespace cdb
+
+using namespace cdb;
+
+extern "C" {
+
+cdb_status cdb_ctx_create(cdb_ctx** out, int device) {
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return CDB_NO_DEVICE;
+  cdb_ctx* ctx = new cdb_ctx();
+  ctx->device = device;
+  cdb_status st = hip_check(ctx, hipSetDevice(device), "hipSetDevice");
+  if (st == CDB_OK) st = hip_check(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "stream");
+  if (st == CDB_OK) st = hip_check(ctx, hipEventCreate(&ctx->ev0), "event");
+  if (st == CDB_OK) st = hip_check(ctx, hipEventCreate(&ctx->ev1), "event");
+  if (st == CDB_OK) st = hip_check(ctx, hipEventCreate(&ctx->ev_part), "event");
+  if (st == CDB_OK) st = hip_check(ctx, hipEventCreate(&ctx->ev_bucket), "event");
+  if (st != CDB_OK) {
+    cdb_ctx_destroy(ctx);
+    return st;
+  }
+  *out = ctx;
+  return CDB_OK;
+}
+
+void cdb_ctx_destroy(cdb_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  for (auto& b : ctx->ws)
+    if (b.p) hipFree(b.p);
+  if (ctx->ev0) hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) hipEventDestroy(ctx->ev1);
+  if (ctx->ev_part) hipEventDestroy(ctx->ev_part);
+  if (ctx->ev_bucket) hipEventDestroy(ctx->ev_bucket);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* cdb_last_error(const cdb_ctx* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+
+cdb_status cdb_dev_rows_alloc(cdb_ctx* ctx, cdb_dev_rows* r, uint64_t rows, int ncols) {
+  std::memset(r, 0, sizeof *r);
+  if (ncols < 1 || ncols > 8) return fail(ctx, CDB_BAD_ARGUMENT, "ncols");
+  hipSetDevice(ctx->device);
+  const uint64_t n = std::max<uint64_t>(rows, 1);
+  uint64_t* p = nullptr;
+  cdb_status st = hip_check(ctx, hipMalloc(&p, ncols * n * sizeof(uint64_t)), "hipMalloc(rows)");
+  if (st != CDB_OK) return st;
+  for (int c = 0; c < ncols; ++c) r->col[c] = p + c * n;
+  r->n = rows;
+  return CDB_OK;
+}
+
+void cdb_dev_rows_release(cdb_ctx* ctx, cdb_dev_rows* r) {
+  if (ctx) hipSetDevice(ctx->device);
+  if (r && r->col[0]) hipFree(r->col[0]);
+  if (r) std::memset(r, 0, sizeof *r);
+}
+
+cdb_status cdb_merge_device(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts, cdb_dev_output* out,
+                            cdb_merge_stats* stats, void* stream) {
+  if (!ctx || !in || !out) return CDB_BAD_ARGUMENT;
+  hipSetDevice(ctx->device);
+  return merge_device_impl(ctx, in, opts, out, stats, stream ? (hipStream_t)stream : ctx->stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,200 @@
+// Host side of the synthetic generator: writes replica snapshots in the reference's wire
+// format (server.rs:183-215, db.rs:122-136, object.rs:85-108, type_counter.rs:101-109,
+// crdt/lwwhash.rs:189-205/325-339; Bytes values length-prefixed as the loader expects,
+// object.rs:114-117).
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/cdb_merge.h"
+#include "gen_model.h"
+
+namespace cdb {
+
+struct SnapWriter {  // SnapshotWriter (snapshot.rs:9-69) without the CRC (done at the end)
+  std::vector<uint8_t> b;
+  void bytes(const void* p, size_t n) {
+    const uint8_t* q = (const uint8_t*)p;
+    b.insert(b.end(), q, q + n);
+  }
+  void byte(uint8_t x) { b.push_back(x); }
+  void integer(int64_t i) {  // write_integer (snapshot.rs:25-37)
+    if (i < (1 << 6)) {
+      byte((uint8_t)i);
+    } else if (i < (1 << 14)) {
+      const uint16_t v = (uint16_t)((uint16_t)i | (1 << 14));
+      byte(v >> 8);
+      byte(v & 0xFF);
+    } else if (i < (1 << 30)) {
+      const uint32_t v = (uint32_t)i | (1u << 31);
+      for (int s = 24; s >= 0; s -= 8) byte((v >> s) & 0xFF);
+    } else {
+      byte(3 << 6);
+      for (int s = 56; s >= 0; s -= 8) byte(((uint64_t)i >> s) & 0xFF);
+    }
+  }
+  void str(const void* p, size_t n) {
+    integer((int64_t)n);
+    bytes(p, n);
+  }
+};
+
+uint64_t crc64_jones(const uint8_t* p, size_t n) {
+  static uint64_t t[256];
+  static bool init = false;
+  if (!init) {
+    for (int i = 0; i < 256; ++i) {
+      uint64_t c = (uint64_t)i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x95AC9329AC4BC9B5ull : c >> 1;
+      t[i] = c;
+    }
+    init = true;
+  }
+  uint64_t crc = 0;
+  for (size_t i = 0; i < n; ++i) crc = t[(crc ^ p[i]) & 0xFF] ^ (crc >> 8);
+  return crc;
+}
+
+GenModel model_of(const cdb_gen_config& c) {
+  GenModel g;
+  g.seed = c.seed;
+  g.universe = c.universe;
+  g.n_replicas = c.n_replicas;
+  g.key_permille = c.key_permille;
+  g.mix[0] = c.mix_bytes;
+  g.mix[1] = c.mix_counter;
+  g.mix[2] = c.mix_set;
+  g.mix[3] = c.mix_dict;
+  g.conflict_ppm = c.conflict_ppm;
+  g.tie_permille = c.tie_permille;
+  g.max_nodes = c.max_nodes;
+  g.mean_members = c.mean_members;
+  g.member_universe = c.member_universe;
+  g.del_permille = c.del_permille;
+  g.side_permille = c.side_permille;
+  g.value_min = c.value_min;
+  g.value_max = c.value_max;
+  g.shard = c.shard;
+  g.n_shards = c.n_shards;
+  return g;
+}
+
+}  // namespace cdb
+
+using namespace cdb;
+
+extern "C" {
+
+void cdb_gen_default(cdb_gen_config* c) {
+  std::memset(c, 0, sizeof *c);
+  c->seed = 1;
+  c->universe = 1000;
+  c->n_replicas = 2;
+  c->key_permille = 500;
+  c->mix_bytes = 60;       // C4 type mix
+  c->mix_counter = 30;
+  c->mix_set = 5;
+  c->mix_dict = 5;
+  c->conflict_ppm = 1000;  // 0.1 % cross-replica type conflicts
+  c->tie_permille = 20;    // ~2 % forced time ties
+  c->max_nodes = 8;
+  c->mean_members = 4;
+  c->member_universe = 16;
+  c->del_permille = 200;
+  c->side_permille = 20;
+  c->value_min = 8;
+  c->value_max = 32;
+  c->shard = 0;
+  c->n_shards = 1;
+  c->replica_lo = 0;
+  c->replica_hi = 2;
+}
+
+cdb_status cdb_gen_snapshot(const cdb_gen_config* cfg, uint32_t r, uint8_t** out, size_t* len) {
+  if (!cfg || !out || !len) return CDB_BAD_ARGUMENT;
+  const GenModel g = model_of(*cfg);
+  SnapWriter data, exp, del;
+  uint64_t nd = 0, ne = 0, ndel = 0;
+  uint8_t kb[24], mbuf[24];
+  for (uint64_t i = 0; i < g.universe; ++i) {
+    const Hash128 h = gen_key_hash(i);
+    if (!gen_in_shard(g, h.h)) continue;
+    const int kl = key_bytes(i, kb);
+    if (gen_present(g, i, r)) {
+      const GenKey k = gen_key(g, i, r);
+      ++nd;
+      data.str(kb, kl);
+      data.integer((int64_t)k.ct);
+      data.integer((int64_t)k.ut);
+      data.integer((int64_t)k.dt);
+      data.byte(k.tag);
+      if (k.tag == TAG_BYTES) {
+        data.integer(k.value_len);
+        for (uint32_t b = 0; b < k.value_len; ++b) data.byte(gen_byte(g, i, r, 0, b));
+      } else if (k.tag == TAG_COUNTER) {
+        data.integer(k.n_nodes);
+        for (uint32_t j = 0; j < k.n_nodes; ++j) {
+          data.integer((int64_t)gen_node_id(g, k, j));
+          data.integer((int64_t)gen_node_v(g, i, r, j));
+          data.integer((int64_t)gen_node_t(g, i, r, j));
+        }
+      } else {
+        uint32_t nadd = 0;
+        for (uint32_t j = 0; j < k.n_members; ++j) nadd += !gen_member_is_del(g, i, r, j);
+        for (int pass = 0; pass < 2; ++pass) {  // add map, then del map
+          data.integer(pass == 0 ? nadd : k.n_members - nadd);
+          for (uint32_t j = 0; j < k.n_members; ++j) {
+            if (gen_member_is_del(g, i, r, j) != (pass == 1)) continue;
+            const int ml = member_bytes(gen_member_index(g, k, j), mbuf);
+            data.str(mbuf, ml);
+            data.integer((int64_t)gen_member_t(g, i, r, j));
+            if (pass == 0 && k.tag == TAG_DICT) {
+              const uint32_t vl = gen_dict_value_len(g, i, r, j);
+              data.integer(vl);
+              for (uint32_t b = 0; b < vl; ++b) data.byte(gen_byte(g, i, r, 1 + j, b));
+            }
+          }
+        }
+      }
+    }
+    if (gen_has_expire(g, i, r)) {
+      ++ne;
+      exp.str(kb, kl);
+      exp.integer((int64_t)gen_time(g, i, r, 3));
+    }
+    if (gen_has_delete(g, i, r)) {
+      ++ndel;
+      del.str(kb, kl);
+      del.integer((int64_t)gen_time(g, i, r, 4));
+    }
+  }
+  SnapWriter w;
+  w.bytes("CONSTDB", 7);
+  const uint8_t ver[4] = {0, 1, 1, 1};
+  w.bytes(ver, 4);
+  const std::string alias = "n" + std::to_string(r + 1), addr = "127.0.0.1:" + std::to_string(9001 + r);
+  w.integer(r + 1);
+  w.str(alias.data(), alias.size());
+  w.str(addr.data(), addr.size());
+  w.integer((int64_t)((kT0Ms + 2000000) << 22));
+  w.byte(5);
+  w.integer((int64_t)nd);
+  w.bytes(data.b.data(), data.b.size());
+  w.byte(6);
+  w.integer((int64_t)ne);
+  w.bytes(exp.b.data(), exp.b.size());
+  w.byte(7);
+  w.integer((int64_t)ndel);
+  w.bytes(del.b.data(), del.b.size());
+  w.byte(8);
+  const uint64_t crc = crc64_jones(w.b.data(), w.b.size());
+  for (int i = 0; i < 8; ++i) w.byte((crc >> (8 * i)) & 0xFF);
+  *out = (uint8_t*)std::malloc(w.b.size());
+  if (!*out) return CDB_OUT_OF_MEMORY;
+  std::memcpy(*out, w.b.data(), w.b.size());
+  *len = w.b.size();
+  return CDB_OK;
+}
+
+}  // extern "C"

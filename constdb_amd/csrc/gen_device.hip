@@ -1,0 +1,181 @@
+// Device-side synthetic generator: the GenModel rows of replicas [lo, hi) written straight
+// into HBM (bench inputs; never part of a timed region). Row identities (src) are model
+// coordinates so results can be cross-checked against host-generated snapshots:
+//   data row src = i, expires src = U + i, deletes src = 2U + i,
+//   node src = i * max_nodes + node slot, member src = i * member_universe + member index.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+
+#include "engine.h"
+#include "gen_model.h"
+#include "partition.hip.h"
+
+namespace cdb {
+GenModel model_of(const cdb_gen_config& c);
+
+namespace {
+
+struct GenArgs {
+  GenModel g;
+  uint32_t lo, hi;
+  uint32_t *ck, *cn, *cm;  // per key index counts
+  uint64_t* k[kKeyCols];
+  uint64_t* nd[kNodeCols];
+  uint64_t* mb[kMemberCols];
+};
+
+__global__ void gen_count_kernel(GenArgs a) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.g.universe;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t nk = 0, nn = 0, nm = 0;
+    const Hash128 h = gen_key_hash(i);
+    if (gen_in_shard(a.g, h.h)) {
+      for (uint32_t r = a.lo; r < a.hi; ++r) {
+        if (gen_present(a.g, i, r)) {
+          const GenKey k = gen_key(a.g, i, r);
+          ++nk;
+          if (k.tag == TAG_COUNTER) nn += k.n_nodes;
+          else if (k.tag == TAG_SET || k.tag == TAG_DICT) nm += k.n_members;
+        }
+        nk += gen_has_expire(a.g, i, r);
+        nk += gen_has_delete(a.g, i, r);
+      }
+    }
+    a.ck[i] = nk;
+    a.cn[i] = nn;
+    a.cm[i] = nm;
+  }
+}
+
+__global__ void gen_fill_kernel(GenArgs a, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ on,
+                                const uint32_t* __restrict__ om) {
+  const uint64_t U = a.g.universe;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < U; i += (uint64_t)gridDim.x * blockDim.x) {
+    const Hash128 h = gen_key_hash(i);
+    if (!gen_in_shard(a.g, h.h)) continue;
+    uint64_t pk = ok[i], pn = on[i], pm = om[i];
+    auto key_row = [&](uint64_t ct, uint64_t ut, uint64_t dt, uint64_t aux, uint64_t meta) {
+      a.k[K_KH][pk] = h.h;
+      a.k[K_KF][pk] = h.f;
+      a.k[K_CT][pk] = ct;
+      a.k[K_UT][pk] = ut;
+      a.k[K_DT][pk] = dt;
+      a.k[K_AUX][pk] = aux;
+      a.k[K_META][pk] = meta;
+      ++pk;
+    };
+    for (uint32_t r = a.lo; r < a.hi; ++r) {
+      if (gen_present(a.g, i, r)) {
+        const GenKey k = gen_key(a.g, i, r);
+        uint64_t aux = 0;
+        if (k.tag == TAG_COUNTER) {
+          for (uint32_t j = 0; j < k.n_nodes; ++j) {
+            const uint64_t v = gen_node_v(a.g, i, r, j);
+            aux += v;
+            a.nd[C_PKH][pn] = h.h;
+            a.nd[C_PKF][pn] = h.f;
+            a.nd[C_ID1][pn] = gen_node_id(a.g, k, j);
+            a.nd[C_ID2][pn] = v;
+            a.nd[C_T][pn] = gen_node_t(a.g, i, r, j);
+            a.nd[C_META][pn] = meta_pack(0, r, i * a.g.max_nodes + j);
+            ++pn;
+          }
+        } else if (k.tag == TAG_SET || k.tag == TAG_DICT) {
+          for (uint32_t j = 0; j < k.n_members; ++j) {
+            const uint64_t mi = gen_member_index(a.g, k, j);
+            const Hash128 mh = gen_member_hash(mi);
+            a.mb[C_PKH][pm] = h.h;
+            a.mb[C_PKF][pm] = h.f;
+            a.mb[C_ID1][pm] = mh.h;
+            a.mb[C_ID2][pm] = mh.f;
+            a.mb[C_T][pm] = gen_member_t(a.g, i, r, j);
+            a.mb[C_META][pm] =
+                meta_pack(gen_member_is_del(a.g, i, r, j) ? KIND_DEL : KIND_ADD, r, i * a.g.member_universe + mi);
+            ++pm;
+          }
+        }
+        key_row(k.ct, k.ut, k.dt, aux, meta_pack(k.tag, r, i));
+      }
+      if (gen_has_expire(a.g, i, r)) key_row(gen_time(a.g, i, r, 3), 0, 0, 0, meta_pack(TAG_EXPIRE, r, U + i));
+      if (gen_has_delete(a.g, i, r)) key_row(gen_time(a.g, i, r, 4), 0, 0, 0, meta_pack(TAG_DELETE, r, 2 * U + i));
+    }
+  }
+}
+
+}  // namespace
+}  // namespace cdb
+
+using namespace cdb;
+
+extern "C" cdb_status cdb_gen_device(cdb_ctx* ctx, const cdb_gen_config* cfg, cdb_dev_input* in) {
+  if (!ctx || !cfg || !in) return CDB_BAD_ARGUMENT;
+  if (cfg->replica_hi > (uint32_t)kMaxPos || cfg->replica_lo >= cfg->replica_hi)
+    return fail(ctx, CDB_BAD_ARGUMENT, "replica range");
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->stream;
+  GenArgs a;
+  std::memset(&a, 0, sizeof a);
+  a.g = model_of(*cfg);
+  a.lo = cfg->replica_lo;
+  a.hi = cfg->replica_hi;
+  const uint64_t U = a.g.universe;
+  uint32_t* cnt = nullptr;
+  cdb_status st = hip_check(ctx, hipMalloc(&cnt, 6 * std::max<uint64_t>(U, 1) * sizeof(uint32_t)), "hipMalloc(gen)");
+  if (st != CDB_OK) return st;
+  a.ck = cnt;
+  a.cn = cnt + U;
+  a.cm = cnt + 2 * U;
+  uint32_t *ok = cnt + 3 * U, *on = cnt + 4 * U, *om = cnt + 5 * U;
+  uint64_t* tot = nullptr;
+  st = hip_check(ctx, hipMalloc(&tot, 3 * sizeof(uint64_t)), "hipMalloc");
+  if (st != CDB_OK) { hipFree(cnt); return st; }
+  const int grid = 4096, block = 256;
+  gen_count_kernel<<<grid, block, 0, s>>>(a);
+  // exclusive scans of the per-key counts
+  auto scan = [&](const uint32_t* c, uint32_t* o, uint64_t* t) -> cdb_status {
+    const uint64_t tiles = std::max<uint64_t>(1, (U + kScanTile - 1) / kScanTile);
+    uint64_t* sums = nullptr;
+    cdb_status s2 = hip_check(ctx, hipMalloc(&sums, tiles * 8), "hipMalloc");
+    if (s2 != CDB_OK) return s2;
+    scan_reduce_kernel<uint32_t><<<tiles, kScanThreads, 0, s>>>(c, U, sums);
+    scan_sums_kernel<<<1, kScanThreads, 0, s>>>(sums, tiles, t);
+    scan_apply_kernel<uint32_t, uint32_t><<<tiles, kScanThreads, 0, s>>>(c, U, sums, o, (uint32_t*)nullptr);
+    s2 = hip_check(ctx, hipStreamSynchronize(s), "gen scan");
+    hipFree(sums);
+    return s2;
+  };
+  if ((st = scan(a.ck, ok, tot)) != CDB_OK || (st = scan(a.cn, on, tot + 1)) != CDB_OK ||
+      (st = scan(a.cm, om, tot + 2)) != CDB_OK) {
+    hipFree(cnt);
+    hipFree(tot);
+    return st;
+  }
+  uint64_t t[3];
+  hipMemcpy(t, tot, sizeof t, hipMemcpyDeviceToHost);
+  if (t[0] >= (1ull << 32) || t[1] >= (1ull << 32) || t[2] >= (1ull << 32)) {
+    hipFree(cnt);
+    hipFree(tot);
+    return fail(ctx, CDB_BAD_ARGUMENT, "generated rows exceed 2^32 per family");
+  }
+  std::memset(in, 0, sizeof *in);
+  if ((st = cdb_dev_rows_alloc(ctx, &in->keys, t[0], kKeyCols)) != CDB_OK ||
+      (st = cdb_dev_rows_alloc(ctx, &in->nodes, t[1], kNodeCols)) != CDB_OK ||
+      (st = cdb_dev_rows_alloc(ctx, &in->members, t[2], kMemberCols)) != CDB_OK) {
+    hipFree(cnt);
+    hipFree(tot);
+    return st;
+  }
+  for (int c = 0; c < kKeyCols; ++c) a.k[c] = in->keys.col[c];
+  for (int c = 0; c < kNodeCols; ++c) {
+    a.nd[c] = in->nodes.col[c];
+    a.mb[c] = in->members.col[c];
+  }
+  gen_fill_kernel<<<grid, block, 0, s>>>(a, ok, on, om);
+  st = hip_check(ctx, hipStreamSynchronize(s), "gen fill");
+  hipFree(cnt);
+  hipFree(tot);
+  in->n_pos = cfg->replica_hi;
+  return st;
+}

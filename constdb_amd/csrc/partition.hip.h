@@ -1,0 +1,240 @@
+// Bucket partition (MSD multisplit) and device-wide scans for gfx950.
+//
+// A row family (key rows, node rows, member rows — each a set of u64 SoA columns) is
+// split into 2^B buckets by the top B bits of column 0 (the key hash kh, or the parent
+// key hash pkh for children), so a key and all its children share a bucket. B is split
+// into levels of <= 9 bits: each level is one streaming pass (histogram pass over col 0,
+// then a scatter pass that stages every column through LDS so that writes leave the CU
+// as contiguous per-digit runs). Rows inside a bucket end up in arbitrary order; the
+// bucket kernel sorts them by full identity, so results stay deterministic.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace cdb {
+namespace {  // internal linkage: included by several translation units
+
+constexpr int kPartThreads = 512;
+constexpr int kPartTile = 4096;       // rows per workgroup tile
+constexpr int kPartRowsPerThread = kPartTile / kPartThreads;
+constexpr int kPartLocalMax = 2048;   // local (tile) bucket slots held in LDS
+
+template <int NC>
+struct ColSet {
+  uint64_t* c[NC];
+};
+
+__device__ __forceinline__ uint64_t bucket_bits_of(uint64_t h, int bits) {
+  return bits ? (h >> (64 - bits)) : 0;
+}
+
+// ---------------------------------------------------------------- histogram
+// hist[gb] += number of rows whose top `btot` bits of col0 are gb. Rows arrive grouped by
+// their top `btot - db` bits (the previous level's output), so a tile spans few prefixes.
+__global__ void __launch_bounds__(kPartThreads) part_hist_kernel(const uint64_t* __restrict__ col0, uint64_t n,
+                                                                 int btot, int db, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t cnt[kPartLocalMax];
+  const uint64_t tile0 = (uint64_t)blockIdx.x * kPartTile;
+  if (tile0 >= n) return;
+  const uint64_t tile1 = min(n, tile0 + kPartTile);
+  const int pbits = btot - db;
+  const uint64_t plo = bucket_bits_of(col0[tile0], pbits);
+  const uint64_t phi = bucket_bits_of(col0[tile1 - 1], pbits);
+  const uint64_t glo = plo << db;
+  const uint64_t span = (phi - plo + 1) << db;
+  const bool local = span <= (uint64_t)kPartLocalMax;
+  for (int i = threadIdx.x; i < kPartLocalMax; i += kPartThreads) cnt[i] = 0;
+  __syncthreads();
+  for (uint64_t r = tile0 + threadIdx.x; r < tile1; r += kPartThreads) {
+    const uint64_t gb = bucket_bits_of(col0[r], btot);
+    if (local) atomicAdd(&cnt[gb - glo], 1u);
+    else atomicAdd(&hist[gb], 1u);
+  }
+  __syncthreads();
+  if (local)
+    for (int i = threadIdx.x; i < (int)span; i += kPartThreads)
+      if (cnt[i]) atomicAdd(&hist[glo + i], cnt[i]);
+}
+
+// ---------------------------------------------------------------- scatter
+// Moves every column of every row to out[cursor[gb]++] (per-tile ranges reserved with one
+// global atomic per touched bucket). Columns are staged through LDS in bucket order so
+// that each wave's stores are contiguous runs.
+template <int NC>
+__global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> in, ColSet<NC> out, uint64_t n,
+                                                                    int btot, int db,
+                                                                    uint32_t* __restrict__ cursor) {
+  __shared__ uint32_t cnt[kPartLocalMax];   // per local bucket: count, then scan
+  __shared__ uint32_t gbase[kPartLocalMax]; // reserved global start per local bucket
+  __shared__ uint16_t slot_lb[kPartTile];   // local bucket of each staged slot
+  __shared__ uint64_t stage[kPartTile];
+  const uint64_t tile0 = (uint64_t)blockIdx.x * kPartTile;
+  if (tile0 >= n) return;
+  const uint64_t tile1 = min(n, tile0 + kPartTile);
+  const int rows = (int)(tile1 - tile0);
+  const int pbits = btot - db;
+  const uint64_t plo = bucket_bits_of(in.c[0][tile0], pbits);
+  const uint64_t phi = bucket_bits_of(in.c[0][tile1 - 1], pbits);
+  const uint64_t glo = plo << db;
+  const uint64_t span = (phi - plo + 1) << db;
+
+  if (span > (uint64_t)kPartLocalMax) {  // wide tile: per-row global reservation
+    for (int r = threadIdx.x; r < rows; r += kPartThreads) {
+      const uint64_t gb = bucket_bits_of(in.c[0][tile0 + r], btot);
+      const uint32_t d = atomicAdd(&cursor[gb], 1u);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) out.c[c][d] = in.c[c][tile0 + r];
+    }
+    return;
+  }
+  for (int i = threadIdx.x; i < kPartLocalMax; i += kPartThreads) cnt[i] = 0;
+  __syncthreads();
+  uint16_t lb[kPartRowsPerThread];
+  uint32_t rk[kPartRowsPerThread];
+#pragma unroll
+  for (int k = 0; k < kPartRowsPerThread; ++k) {
+    const int r = threadIdx.x + k * kPartThreads;
+    if (r < rows) {
+      lb[k] = (uint16_t)(bucket_bits_of(in.c[0][tile0 + r], btot) - glo);
+      rk[k] = atomicAdd(&cnt[lb[k]], 1u);
+    }
+  }
+  __syncthreads();
+  // reserve global ranges, then turn cnt into an exclusive scan (single wave scan)
+  for (int i = threadIdx.x; i < (int)span; i += kPartThreads)
+    if (cnt[i]) gbase[i] = atomicAdd(&cursor[glo + i], cnt[i]);
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int per = ((int)span + 63) / 64;
+    uint32_t s = 0;
+    for (int j = 0; j < per; ++j) {
+      const int i = lane * per + j;
+      if (i < (int)span) s += cnt[i];
+    }
+    uint32_t incl = s;  // wave-wide inclusive scan of per-lane sums
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    uint32_t run = incl - s;
+    for (int j = 0; j < per; ++j) {
+      const int i = lane * per + j;
+      if (i < (int)span) {
+        const uint32_t c = cnt[i];
+        cnt[i] = run;
+        run += c;
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t slot[kPartRowsPerThread];
+#pragma unroll
+  for (int k = 0; k < kPartRowsPerThread; ++k) {
+    const int r = threadIdx.x + k * kPartThreads;
+    if (r < rows) {
+      slot[k] = cnt[lb[k]] + rk[k];
+      slot_lb[slot[k]] = lb[k];
+    }
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int c = 0; c < NC; ++c) {
+#pragma unroll
+    for (int k = 0; k < kPartRowsPerThread; ++k) {
+      const int r = threadIdx.x + k * kPartThreads;
+      if (r < rows) stage[slot[k]] = in.c[c][tile0 + r];
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < rows; j += kPartThreads) {
+      const int b = slot_lb[j];
+      out.c[c][gbase[b] + (j - cnt[b])] = stage[j];
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- scans
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 8;  // items per thread
+constexpr int kScanTile = kScanThreads * kScanItems;
+
+__device__ __forceinline__ uint64_t block_exclusive_scan_u64(uint64_t v, uint64_t* total) {
+  __shared__ uint64_t warp_sums[kScanThreads / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint64_t incl = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) warp_sums[w] = incl;
+  __syncthreads();
+  uint64_t off = 0, tot = 0;
+  for (int i = 0; i < kScanThreads / 64; ++i) {
+    if (i < w) off += warp_sums[i];
+    tot += warp_sums[i];
+  }
+  __syncthreads();
+  *total = tot;
+  return off + incl - v;
+}
+
+// pass 1: per-tile sums
+template <typename T>
+__global__ void __launch_bounds__(kScanThreads) scan_reduce_kernel(const T* __restrict__ in, uint64_t n,
+                                                                   uint64_t* __restrict__ sums) {
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  uint64_t s = 0;
+  for (int k = 0; k < kScanItems; ++k) {
+    const uint64_t i = base + (uint64_t)threadIdx.x * kScanItems + k;
+    if (i < n) s += in[i];
+  }
+  uint64_t tot;
+  block_exclusive_scan_u64(s, &tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// pass 2: exclusive scan of the tile sums (one workgroup, sequential over chunks)
+__global__ void __launch_bounds__(kScanThreads) scan_sums_kernel(uint64_t* __restrict__ sums, uint64_t m,
+                                                                 uint64_t* __restrict__ grand_total) {
+  uint64_t carry = 0;
+  for (uint64_t b = 0; b < m; b += kScanThreads) {
+    const uint64_t i = b + threadIdx.x;
+    const uint64_t v = i < m ? sums[i] : 0;
+    uint64_t tot;
+    const uint64_t ex = block_exclusive_scan_u64(v, &tot);
+    if (i < m) sums[i] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0 && grand_total) *grand_total = carry;
+}
+
+// pass 3: out[i] = exclusive prefix (as OutT); optionally copies it to out2 as well
+template <typename T, typename OutT>
+__global__ void __launch_bounds__(kScanThreads) scan_apply_kernel(const T* __restrict__ in, uint64_t n,
+                                                                  const uint64_t* __restrict__ sums,
+                                                                  OutT* __restrict__ out, OutT* __restrict__ out2) {
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile;
+  T v[kScanItems];
+  uint64_t s = 0;
+  for (int k = 0; k < kScanItems; ++k) {
+    const uint64_t i = base + (uint64_t)threadIdx.x * kScanItems + k;
+    v[k] = i < n ? in[i] : 0;
+    s += v[k];
+  }
+  uint64_t tot;
+  uint64_t run = sums[blockIdx.x] + block_exclusive_scan_u64(s, &tot);
+  for (int k = 0; k < kScanItems; ++k) {
+    const uint64_t i = base + (uint64_t)threadIdx.x * kScanItems + k;
+    if (i < n) {
+      out[i] = (OutT)run;
+      if (out2) out2[i] = (OutT)run;
+    }
+    run += v[k];
+  }
+}
+
+}  // namespace
+}  // namespace cdb

@@ -1,0 +1,203 @@
+/*
+ * cdb_merge.h — C ABI of the MI355X-native ConstDB snapshot-merge engine (libcdbmerge.so).
+ *
+ * Drop-in boundary for the reference's replica-sync hot path (fxsjy/ConstDB, Rust):
+ *   - decode:  SnapshotLoader::next            src/snapshot.rs:120-220
+ *              Object::load_snapshot            src/object.rs:110-129
+ *              Counter/Set/Dict::load_snapshot  src/type_counter.rs:111, src/crdt/lwwhash.rs:207,341
+ *   - merge:   the per-entry loop of Puller::merge_replicates_in_main
+ *              src/replica/pull.rs:120-158, i.e. DB::merge_entry (src/db.rs:31-43),
+ *              Object::merge (src/object.rs:63-83), Counter::merge (src/type_counter.rs:59-91),
+ *              Set::merge / Dict::merge (src/crdt/lwwhash.rs:319-323 / 176-181),
+ *              DB::delete / DB::expire_at (src/db.rs:68-76), DB::gc (src/db.rs:82-119).
+ * Instead of one FFI call per entry (which would defeat a GPU), a whole snapshot is
+ * decoded into a columnar batch and R batches are merged in one call. Binding examples
+ * for a Rust host (the reference's language) are in INTEGRATION.md.
+ *
+ * Plain C types only: pointers, sizes, fixed-width integers. No torch types.
+ * Threading: a cdb_ctx is used from one thread at a time (like the reference's single
+ * main task, src/server.rs:95,128-130); no callbacks into the host.
+ * Ownership: input buffers are caller-owned and read-only; everything returned by a
+ * cdb_* call is library-owned and released with the matching *_free.
+ */
+#ifndef CDB_MERGE_H
+#define CDB_MERGE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes map 1:1 onto the decode-path CstError variants (src/lib.rs:146-175). */
+typedef enum cdb_status {
+  CDB_OK = 0,
+  CDB_INVALID_SNAPSHOT = 1,          /* CstError::InvalidSnapshot(offset)      lib.rs:157 */
+  CDB_INVALID_SNAPSHOT_CHECKSUM = 2, /* CstError::InvalidSnapshotChecksum      lib.rs:173 */
+  CDB_INVALID_TYPE = 3,              /* CstError::InvalidType (unknown tag)    lib.rs:151, object.rs:121 */
+  CDB_IO_ERROR = 4,                  /* CstError::IoError (truncated stream)   lib.rs:161 */
+  CDB_DICT_MERGE_UNIMPLEMENTED = 5,  /* Dict::merge's unimplemented!() panic,  lwwhash.rs:180 (strict mode) */
+  CDB_BAD_ARGUMENT = 6,
+  CDB_DEVICE_ERROR = 7,              /* a HIP call failed */
+  CDB_OUT_OF_MEMORY = 8,
+  CDB_NO_DEVICE = 9                  /* no gfx950 device visible: the engine never falls back to the CPU */
+} cdb_status;
+
+typedef struct cdb_ctx cdb_ctx;       /* device, streams, workspace */
+typedef struct cdb_batch cdb_batch;   /* one decoded snapshot (columnar, host + device) */
+typedef struct cdb_merged cdb_merged; /* a merge result (device-resident, host-readable) */
+
+/* ------------------------------------------------------------------ context */
+/* Creates a context on HIP device `device`. Fails with CDB_NO_DEVICE when no device. */
+cdb_status cdb_ctx_create(cdb_ctx** out, int device);
+void cdb_ctx_destroy(cdb_ctx* ctx);
+/* Human-readable last error of this context (static storage, valid until the next call). */
+const char* cdb_last_error(const cdb_ctx* ctx);
+
+/* ------------------------------------------------------------------ decode
+ * Replaces SnapshotLoader::next (snapshot.rs:120-220) + the load_snapshot functions.
+ * Decodes the WRITER layout of server.rs:183-215 (CRC-64/Jones over every byte up to and
+ * including flag 0x08, then 8 raw little-endian CRC bytes). Bytes values use the
+ * loader's `len, bytes` layout (object.rs:114-117; the writer at object.rs:94-97 omits
+ * the length, which the reference itself cannot read back).
+ * On CDB_INVALID_SNAPSHOT_CHECKSUM the batch is still returned in *out (the reference
+ * merges every entry before it reaches the checksum, replica/pull.rs:64-79), so the
+ * caller decides; for every other error *out is NULL and *err_offset = byte offset. */
+enum {
+  CDB_DECODE_REFERENCE_CHECKSUM = 1u << 0 /* reproduce snapshot.rs:207-213 exactly: read the
+                                             checksum as a varint and CRC it too (rejects
+                                             practically every well-formed dump) */
+};
+cdb_status cdb_decode_snapshot(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags,
+                               cdb_batch** out, size_t* err_offset);
+
+typedef struct cdb_batch_info {
+  uint64_t n_data;        /* SnapshotEntry::Data entries   (snapshot.rs:309) */
+  uint64_t n_expires;     /* SnapshotEntry::Expires        (snapshot.rs:310) */
+  uint64_t n_deletes;     /* SnapshotEntry::Deletes        (snapshot.rs:311) */
+  uint64_t n_nodes;       /* counter children (node, v, t) (type_counter.rs:21) */
+  uint64_t n_members;     /* set/dict member tags after load-time reconstruction (lwwhash.rs:207-226,341-358) */
+  uint64_t node_id;       /* SnapshotEntry::Node           (snapshot.rs:306) */
+  uint64_t uuid_he_sent;
+  uint32_t n_replica_add; /* SnapshotEntry::ReplicaAdd     (snapshot.rs:307) */
+  uint32_t n_replica_del; /* SnapshotEntry::ReplicaDel     (snapshot.rs:308) */
+  char version[16];       /* SnapshotEntry::Version, "a.b.c.d" */
+} cdb_batch_info;
+cdb_status cdb_batch_info_get(const cdb_batch* b, cdb_batch_info* info);
+/* Read-only view of one decoded column (host memory, valid while the batch lives).
+ * family 0 = key rows (kh kf ct ut dt aux meta), 1 = counter nodes (pkh pkf node v t meta),
+ * 2 = set/dict members (pkh pkf mh mf t meta). */
+cdb_status cdb_batch_column(const cdb_batch* b, int family, int col, const uint64_t** data, uint64_t* n);
+void cdb_batch_free(cdb_batch* b);
+
+/* ------------------------------------------------------------------ merge
+ * Replaces the per-entry loop of replica/pull.rs:120-158: folds `n` decoded snapshots in
+ * array order (pos 0 = the local DB state, then remotes in apply order) exactly as R
+ * sequential applications of DB::merge_entry / DB::delete / DB::expire_at would.
+ * Deterministic: the result does not depend on row order inside a batch. */
+enum {
+  CDB_MERGE_STRICT_DICT_PANIC = 1u << 0, /* report Dict-on-Dict merges (where the reference
+                                            panics, lwwhash.rs:180) as CDB_DICT_MERGE_UNIMPLEMENTED;
+                                            default: apply the pre-panic loop (code intent) */
+  CDB_MERGE_GC_DELETES = 1u << 1,        /* run DB::gc(gc_watermark) after the merge (db.rs:82-119;
+                                            garbage list = Deletes entries in fold order) */
+  CDB_MERGE_GC_MEMBERS = 1u << 2         /* BUILD EXTENSION: drop del-only set/dict members
+                                            whose tag time < gc_watermark (the field path of
+                                            db.rs:96-115, which the reference never enqueues) */
+};
+typedef struct cdb_merge_opts {
+  uint32_t flags;
+  uint32_t reserved;
+  uint64_t gc_watermark; /* ReplicaManager::min_uuid (replica/replica.rs:87-89) */
+} cdb_merge_opts;
+
+typedef struct cdb_merge_stats {
+  uint64_t key_rows_in, node_rows_in, member_rows_in;
+  uint64_t key_rows_out, node_rows_out, member_rows_out;
+  uint64_t type_conflicts;   /* db.rs:38-40 error! log events (local kept) */
+  uint64_t dict_merges;      /* Dict-on-Dict merges (the reference panics at lwwhash.rs:180) */
+  uint64_t deletes_gced;
+  uint64_t members_gced;
+  uint64_t duplicate_rows;   /* same key twice in one snapshot (never written by db.rs:122-136) */
+  uint64_t orphan_children;  /* child rows whose key row is missing (malformed input) */
+  uint64_t hot_buckets;      /* buckets handled by the over-capacity path */
+  double   device_ms;        /* device time of the whole merge pipeline (HIP events) */
+  double   partition_ms;     /* bucket partition of the three row families */
+  double   bucket_ms;        /* fused bucket-merge kernel (the dominant kernel) */
+  double   finish_ms;        /* over-capacity buckets + dense compaction */
+} cdb_merge_stats;
+
+cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n,
+                     const cdb_merge_opts* opts, cdb_merged** out, cdb_merge_stats* stats);
+
+/* Canonical dump of a merge result: keys sorted by bytes, members by bytes, counter nodes
+ * by id, then expires and deletes (the text format of oracle/constdb_oracle.py's
+ * canonical_dump). *out is released with cdb_free. */
+cdb_status cdb_merged_canonical_dump(cdb_ctx* ctx, cdb_merged* m, char** out, size_t* len);
+void cdb_merged_free(cdb_merged* m);
+void cdb_free(void* p);
+
+/* ------------------------------------------------------------------ device level
+ * The same merge over columnar rows already resident in HBM (what bench.py times, and
+ * what a multi-GPU driver calls after its RCCL all-to-all). Every column is a u64 device
+ * array; layouts are documented in DESIGN.md §Data layout and constdb_amd/csrc/common.h.
+ * Rows may come in any order and from up to 63 fold positions (pos in the meta word). */
+typedef struct cdb_dev_rows {
+  uint64_t* col[8]; /* keys: kh kf ct ut dt aux meta | nodes: pkh pkf node v t meta |
+                       members: pkh pkf mh mf t meta */
+  uint64_t n;
+} cdb_dev_rows;
+typedef struct cdb_dev_input {
+  cdb_dev_rows keys, nodes, members;
+  uint32_t n_pos;
+  uint32_t reserved;
+} cdb_dev_input;
+/* Outputs are written sparse-by-bucket: bucket b's rows start at the bucket's input
+ * offset; dense compaction into *_dense happens when cdb_dev_output.compact != 0. */
+typedef struct cdb_dev_output {
+  cdb_dev_rows keys;    /* kh kf ct ut dt meta win cref */
+  cdb_dev_rows nodes;   /* pkh pkf node v t meta */
+  cdb_dev_rows members; /* pkh pkf mh mf t meta */
+  uint32_t compact;
+  uint32_t reserved;
+} cdb_dev_output;
+
+/* Allocates device columns for `rows` rows of a family (8 u64 columns) in *r. */
+cdb_status cdb_dev_rows_alloc(cdb_ctx* ctx, cdb_dev_rows* r, uint64_t rows, int ncols);
+void cdb_dev_rows_release(cdb_ctx* ctx, cdb_dev_rows* r);
+/* Runs the merge pipeline on the context's stream (or `stream` if non-NULL, a hipStream_t).
+ * out->*.n receive the output row counts. Synchronises before returning. */
+cdb_status cdb_merge_device(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts,
+                            cdb_dev_output* out, cdb_merge_stats* stats, void* stream);
+
+/* ------------------------------------------------------------------ synthetic inputs
+ * Seeded generator of replica states. Writes snapshot bytes
+ * (for the decode path and the oracle) or device rows (for HBM-resident benches). */
+typedef struct cdb_gen_config {
+  uint64_t seed;
+  uint64_t universe;      /* number of distinct keys */
+  uint32_t n_replicas;    /* R */
+  uint32_t key_permille;  /* probability (x1000) that a replica holds a key */
+  uint32_t mix_bytes, mix_counter, mix_set, mix_dict; /* type mix weights */
+  uint32_t conflict_ppm;  /* cross-replica type-conflict probability (x1e6) */
+  uint32_t tie_permille;  /* probability (x1000) that a time is forced to tie */
+  uint32_t max_nodes;     /* counter nodes per key: 1..max_nodes */
+  uint32_t mean_members;  /* set/dict members per key (uniform 0..2*mean) */
+  uint32_t member_universe; /* members drawn from this many per key */
+  uint32_t del_permille;  /* probability (x1000) that a member tag is a del */
+  uint32_t side_permille; /* probability (x1000) of an expires / deletes entry per key */
+  uint32_t value_min, value_max; /* Bytes value length range */
+  uint32_t shard, n_shards;      /* generate only keys with owner(kh) == shard (multi-GPU) */
+  uint32_t replica_lo, replica_hi; /* generate replicas [lo, hi) */
+} cdb_gen_config;
+void cdb_gen_default(cdb_gen_config* cfg);
+/* Snapshot bytes of replica r (writer layout). *out released with cdb_free. */
+cdb_status cdb_gen_snapshot(const cdb_gen_config* cfg, uint32_t replica, uint8_t** out, size_t* len);
+/* Device rows for replicas [replica_lo, replica_hi) generated directly in HBM. */
+cdb_status cdb_gen_device(cdb_ctx* ctx, const cdb_gen_config* cfg, cdb_dev_input* in);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CDB_MERGE_H */

@@ -153,7 +153,7 @@ struct Reader {
       case 2: { const uint8_t* q = bytes(3); if (!q) return false;
                 *out = ((int64_t)(f & 0x3F) << 24) | ((int64_t)q[0] << 16) | ((int64_t)q[1] << 8) | q[2]; return true; }
       default: { const uint8_t* q = bytes(8); if (!q) return false; uint64_t v = 0;
-                 for (int i = 0; i < 8; ++i) v = (v << 8) | q[i]; *out = (int64_t)v; return true; }
+                 for (int i = 0; i < 8; ++i) { v = (v << 8) | q[i]; } *out = (int64_t)v; return true; }
     }
   }
   bool len(size_t* out) {
@@ -443,7 +443,7 @@ void cdbo_free(void* p) { std::free(p); }
 
 // CPU baseline: decodes (untimed), then times ONLY the sequential fold into a fresh DB
 // (the reference's merge loop minus its per-entry DEBUG formatting), best of `reps`.
-// Returns the best fold time in ns; *entries = Data entries folded per run.
+// Returns the best fold time in ns; *entries = entries (Data/Expires/Deletes) folded per run.
 int64_t cdbo_time_fold(const uint8_t* const* bufs, const size_t* lens, int n, int reps,
                        uint64_t* entries) {
   int64_t best = -1;
@@ -453,7 +453,7 @@ int64_t cdbo_time_fold(const uint8_t* const* bufs, const size_t* lens, int n, in
     uint64_t cnt = 0;
     for (int i = 0; i < n; ++i) {
       if (decode(bufs[i], lens[i], 0, &snaps[i], &eo) != OK) return -1;
-      for (const auto& e : snaps[i]) cnt += e.kind == Entry::DATA;
+      cnt += snaps[i].size();  // Data + Expires + Deletes entries
     }
     *entries = cnt;
     DB db;

@@ -1,0 +1,183 @@
+"""GPU parity: the HIP merge engine (through the C-ABI) vs the oracle, on the same snapshot
+bytes. Bit-exact canonical dumps are required (integer/ordering work, no tolerance)."""
+import pytest
+
+import cdb_oracle
+import constdb_amd as cdb
+import constdb_oracle as o
+from snapgen import gen_replicas
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def db():
+    from constdb_amd import build
+    build.build()
+    return cdb.DB(cdb.Context(0))
+
+
+def _oracle(snaps, gc=None, members=False):
+    flags = 0
+    if gc is not None:
+        flags |= cdb_oracle.FLAG_GC | (cdb_oracle.FLAG_GC_MEMBERS if members else 0)
+    rc, dump, st = cdb_oracle.fold(snaps, flags=flags, gc_watermark=gc or 0)
+    assert rc == 0
+    return dump, st
+
+
+def _check(db, snaps, gc=None, members=False):
+    want, ost = _oracle(snaps, gc, members)
+    m = db.merge_snapshots(snaps, gc_watermark=gc, gc_members=members)
+    got = m.canonical_dump()
+    if got != want:
+        gl, wl = got.decode().splitlines(), want.decode().splitlines()
+        for i, (a, b) in enumerate(zip(gl, wl)):
+            if a != b:
+                raise AssertionError(f"first diff at line {i}:\n gpu   : {a}\n oracle: {b}\n"
+                                     f"(gpu {len(gl)} lines, oracle {len(wl)} lines)")
+        raise AssertionError(f"length differs: gpu {len(gl)} lines, oracle {len(wl)} lines")
+    assert m.stats.type_conflicts == ost.type_conflicts
+    assert m.stats.dict_merges == ost.dict_merges
+    return m
+
+
+# ------------------------------------------------------------------ KATs through the GPU
+def _snap(objs=None, deletes=None, expires=None):
+    d = o.DB()
+    d.data.update(objs or {})
+    d.deletes.update(deletes or {})
+    d.expires.update(expires or {})
+    return o.dump_all(d, o.NodeHeader())
+
+
+def _counter(nodes, ct=1):
+    c = o.Counter()
+    c.data.update(nodes)
+    c.cal_sum()
+    return o.Object(ct, 0, 0, o.OBJECT_ENC_COUNTER, c)
+
+
+def _set(adds, dels=None):
+    s = o.Set()
+    for m, t in adds.items():
+        s.set(m, None, t)
+    for m, t in (dels or {}).items():
+        s.rem(m, t)
+    return o.Object(1, 0, 0, o.OBJECT_ENC_SET, s)
+
+
+def test_kat_bytes_ties_and_maxima(db):
+    _check(db, [_snap({b"k": o.Object(10, 3, 1, o.OBJECT_ENC_BYTES, b"A")}),
+                _snap({b"k": o.Object(10, 9, 0, o.OBJECT_ENC_BYTES, b"B")}),
+                _snap({b"k": o.Object(9, 50, 70, o.OBJECT_ENC_BYTES, b"C")})])
+
+
+def test_kat_counter_order_dependence(db):
+    for order in ([(5, 10), (7, 11), (6, 12)], [(5, 10), (6, 12), (7, 11)]):
+        _check(db, [_snap({b"c": _counter({1: vt})}) for vt in order])
+
+
+def test_kat_counter_unmerged_keeps_load_total(db):
+    _check(db, [_snap({b"c": _counter({1: (5, 10), 2: (6, 1)})})])
+
+
+def test_kat_type_conflict(db):
+    m = _check(db, [_snap({b"k": _counter({1: (1, 1)})}),
+                    _snap({b"k": o.Object(99, 0, 0, o.OBJECT_ENC_BYTES, b"X")}),
+                    _snap({b"k": _counter({1: (4, 2)})})])
+    assert m.stats.type_conflicts == 1
+
+
+def test_kat_set_ties_and_remote_dels(db):
+    _check(db, [_snap({b"s": _set({b"a": 5, b"b": 7}, {b"d": 10})}),
+                _snap({b"s": _set({b"d": 10, b"e": 1}, {b"a": 9})}),
+                _snap({b"s": _set({b"b": 6})})])
+
+
+def test_kat_side_maps_and_gc(db):
+    snaps = [_snap(deletes={b"a": 5, b"b": 50, b"c": 6}, expires={b"x": 9}),
+             _snap(deletes={b"a": 20}, expires={b"x": 3})]
+    _check(db, snaps)
+    for wm in (0, 5, 6, 20, 49, 50, 1000):
+        _check(db, snaps, gc=wm)
+
+
+def test_strict_dict_panic(db):
+    d1, d2 = o.Dict(), o.Dict()
+    d1.set(b"f", b"x", 5)
+    d2.set(b"f", b"z", 6)
+    snaps = [_snap({b"h": o.Object(1, 0, 0, o.OBJECT_ENC_DICT, d1)}),
+             _snap({b"h": o.Object(1, 0, 0, o.OBJECT_ENC_DICT, d2)})]
+    _check(db, snaps)
+    with pytest.raises(cdb.DictMergeUnimplemented):
+        db.merge_snapshots(snaps, strict_dict_panic=True)
+
+
+def test_empty_inputs(db):
+    _check(db, [_snap()])
+    _check(db, [_snap(), _snap()])
+    assert db.merge_snapshots([]).canonical_dump() == b""
+
+
+# ------------------------------------------------------------------ randomized parity
+@pytest.mark.parametrize("seed", range(60))
+def test_random_small(db, seed):
+    snaps = gen_replicas(seed, n_replicas=1 + seed % 6, n_keys=30 + seed, big_times=seed % 3 == 0,
+                         p_conflict=0.1, p_side=0.2)
+    _check(db, snaps)
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_random_gc(db, seed):
+    snaps = gen_replicas(500 + seed, n_replicas=3, p_side=0.5)
+    _check(db, snaps, gc=seed % 9, members=bool(seed % 2))
+
+
+def test_many_replicas(db):
+    _check(db, gen_replicas(77, n_replicas=63, n_keys=50, p_key=0.3))
+
+
+@pytest.mark.parametrize("universe,replicas,seed", [(2000, 2, 1), (20000, 4, 2), (60000, 8, 3)])
+def test_generator_medium(db, universe, replicas, seed):
+    """C1/C2-shaped inputs (generator), thousands of buckets, two partition levels."""
+    cfg = cdb.gen_config(seed=seed, universe=universe, n_replicas=replicas, replica_hi=replicas)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(replicas)]
+    _check(db, snaps)
+
+
+def test_generator_set_heavy_gc(db):
+    """C3-shaped: set/dict heavy with tombstones, GC at the median time."""
+    cfg = cdb.gen_config(seed=3, universe=5000, n_replicas=4, replica_hi=4, mix_bytes=0, mix_counter=0,
+                         mix_set=50, mix_dict=50, mean_members=12, member_universe=40, del_permille=400,
+                         side_permille=300)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(4)]
+    wm = (1700000000000 + (1 << 19)) << 22
+    _check(db, snaps)
+    _check(db, snaps, gc=wm, members=True)
+
+
+def test_hot_bucket_path(db):
+    """A key whose members exceed the LDS capacity goes through the global-scratch path."""
+    big1, big2 = o.Set(), o.Set()
+    for j in range(3000):
+        big1.set(b"m%d" % j, None, j % 17)
+        if j % 3 == 0:
+            big2.set(b"m%d" % j, None, j % 13)
+        if j % 7 == 0:
+            big2.rem(b"x%d" % j, 5)
+    c1, c2 = o.Counter(), o.Counter()
+    for n in range(1500):
+        c1.data[n] = (n, n % 5)
+        c2.data[n] = (n * 2, n % 4)
+    objs1 = {b"big": o.Object(1, 0, 0, o.OBJECT_ENC_SET, big1), b"cnt": o.Object(1, 0, 0, o.OBJECT_ENC_COUNTER, c1)}
+    objs2 = {b"big": o.Object(2, 0, 0, o.OBJECT_ENC_SET, big2), b"cnt": o.Object(2, 0, 0, o.OBJECT_ENC_COUNTER, c2)}
+    m = _check(db, [_snap(objs1), _snap(objs2)])
+    assert m.stats.hot_buckets >= 1
+
+
+def test_deterministic(db):
+    snaps = gen_replicas(9, n_replicas=4)
+    a = db.merge_snapshots(snaps).canonical_dump()
+    b = db.merge_snapshots(snaps).canonical_dump()
+    assert a == b
