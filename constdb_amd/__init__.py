@@ -94,7 +94,7 @@ class BatchInfo(ctypes.Structure):
 
 
 class MergeOpts(ctypes.Structure):
-    _fields_ = [("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("gc_watermark", ctypes.c_uint64)]
+    _fields_ = [("flags", ctypes.c_uint32), ("force_tier", ctypes.c_uint32), ("gc_watermark", ctypes.c_uint64)]
 
 
 class MergeStats(ctypes.Structure):
@@ -316,11 +316,13 @@ class DB:
         self.ctx = ctx or Context(device)
 
     def merge_batches(self, batches: Sequence[Batch], strict_dict_panic: bool = False,
-                      gc_watermark: Optional[int] = None, gc_members: bool = False) -> Merged:
+                      gc_watermark: Optional[int] = None, gc_members: bool = False,
+                      force_tier: int = 0) -> Merged:
         n = len(batches)
         arr = (ctypes.c_void_p * max(n, 1))(*[b.handle for b in batches])
         opts = MergeOpts()
         opts.flags = (MERGE_STRICT_DICT_PANIC if strict_dict_panic else 0)
+        opts.force_tier = force_tier
         if gc_watermark is not None:
             opts.flags |= MERGE_GC_DELETES | (MERGE_GC_MEMBERS if gc_members else 0)
             opts.gc_watermark = gc_watermark

@@ -50,6 +50,7 @@ struct BucketArgs {
   uint64_t* mo[kMemberCols];
   uint32_t *kout, *nout, *mout;
   uint32_t flags;
+  uint32_t force_tier;
   uint64_t gc_wm;
   const uint64_t* last_bad;   // (pos,src)+1 of the newest garbage entry with t > wm; 0 = none
   unsigned long long* stats;
@@ -445,18 +446,11 @@ struct LdsPool {
   uint32_t misc[32];
 };
 
-__global__ void __launch_bounds__(kBktThreads) bucket_kernel(BucketArgs A, uint32_t nbuckets) {
+// Mid tier: buckets too large for one wave (bucket_wave.hip.h) but within the LDS pool.
+// Persistent over the device-side list written by the wave kernel (no host round trip).
+__global__ void __launch_bounds__(kBktThreads) bucket_mid_kernel(BucketArgs A, const uint32_t* __restrict__ list,
+                                                                 const uint32_t* __restrict__ count) {
   __shared__ LdsPool L;
-  const uint32_t b = blockIdx.x;
-  if (b >= nbuckets) return;
-  if (A.kcnt[b] > kCapK || A.ncnt[b] > kCapC || A.mcnt[b] > kCapC) {
-    if (threadIdx.x == 0) {
-      const uint32_t s = atomicAdd(A.hot_count, 1u);
-      A.hot_list[s] = b;
-      A.kout[b] = A.nout[b] = A.mout[b] = 0;
-    }
-    return;
-  }
   Scratch S;
   S.kh = L.kh; S.kf = L.kf; S.meta = L.meta;
   S.idx = L.idx; S.rk = L.rk; S.flag = L.flag; S.rank = L.rank; S.cnt = L.cnt;
@@ -465,8 +459,21 @@ __global__ void __launch_bounds__(kBktThreads) bucket_kernel(BucketArgs A, uint3
   S.c1 = L.c1; S.c2 = L.c2; S.cm = L.cm; S.rt = L.rt; S.rm = L.rm;
   S.ck = L.ck; S.cidx = L.cidx; S.crk = L.crk; S.cflag = L.cflag; S.crank = L.crank;
   S.st = L.st; S.misc = L.misc;
-  __syncthreads();
-  process_bucket(A, b, S);
+  const uint32_t total = *count;
+  for (uint32_t i = blockIdx.x; i < total; i += gridDim.x) {
+    const uint32_t b = list[i];
+    if (A.kcnt[b] > kCapK || A.ncnt[b] > kCapC || A.mcnt[b] > kCapC || A.force_tier >= 2) {
+      if (threadIdx.x == 0) {
+        const uint32_t s = atomicAdd(A.hot_count, 1u);
+        A.hot_list[s] = b;
+        A.kout[b] = A.nout[b] = A.mout[b] = 0;
+      }
+      continue;
+    }
+    __syncthreads();
+    process_bucket(A, b, S);
+    __syncthreads();
+  }
 }
 
 // Over-capacity buckets: the same algorithm with scratch in a global slab. Slab layout per

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "bucket.hip.h"
+#include "bucket_wave.hip.h"
 #include "engine.h"
 #include "partition.hip.h"
 
@@ -79,28 +80,36 @@ struct CompactArgs {
 };
 
 // Sparse-by-bucket outputs -> dense arrays; child ranges become absolute row indices.
+// One wave per bucket (buckets are wave-sized), grid-stride over buckets.
 __global__ void __launch_bounds__(256) compact_kernel(CompactArgs A, uint32_t nbuckets) {
-  const uint32_t b = blockIdx.x;
-  if (b >= nbuckets) return;
-  const uint32_t kn = A.kout[b], ks = A.kbase[b], kd = A.kdoff[b];
-  for (int c = 0; c < kKeyOutCols; ++c) {
-    for (uint32_t i = threadIdx.x; i < kn; i += blockDim.x) {
-      uint64_t v = A.ks[c][ks + i];
-      if (c == O_CREF) {
-        const uint64_t cnt = v & 0xFFFFFF;
-        const uint32_t T = meta_tag(A.ks[O_META][ks + i]);
-        const uint64_t begin = cnt ? (v >> 24) + (T == TAG_COUNTER ? A.ndoff[b] : A.mdoff[b]) : 0;
-        v = cref_pack(begin, cnt);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < nbuckets; b += nwaves) {
+    const uint32_t kn = A.kout[b], ks = A.kbase[b], kd = A.kdoff[b];
+    const uint32_t nn = A.nout[b], ns = A.nbase[b], ndo = A.ndoff[b];
+    const uint32_t mn = A.mout[b], ms = A.mbase[b], mdo = A.mdoff[b];
+    for (uint32_t i = lane; i < kn; i += 64) {
+#pragma unroll
+      for (int c = 0; c < kKeyOutCols; ++c) {
+        uint64_t v = A.ks[c][ks + i];
+        if (c == O_CREF) {
+          const uint64_t cnt = v & 0xFFFFFF;
+          const uint32_t T = meta_tag(A.ks[O_META][ks + i]);
+          const uint64_t begin = cnt ? (v >> 24) + (T == TAG_COUNTER ? ndo : mdo) : 0;
+          v = cref_pack(begin, cnt);
+        }
+        A.kd[c][kd + i] = v;
       }
-      A.kd[c][kd + i] = v;
+    }
+    for (uint32_t i = lane; i < nn; i += 64) {
+#pragma unroll
+      for (int c = 0; c < kNodeCols; ++c) A.nd[c][ndo + i] = A.ns[c][ns + i];
+    }
+    for (uint32_t i = lane; i < mn; i += 64) {
+#pragma unroll
+      for (int c = 0; c < kMemberCols; ++c) A.md[c][mdo + i] = A.ms[c][ms + i];
     }
   }
-  const uint32_t nn = A.nout[b], ns = A.nbase[b], ndo = A.ndoff[b];
-  for (int c = 0; c < kNodeCols; ++c)
-    for (uint32_t i = threadIdx.x; i < nn; i += blockDim.x) A.nd[c][ndo + i] = A.ns[c][ns + i];
-  const uint32_t mn = A.mout[b], ms = A.mbase[b], mdo = A.mdoff[b];
-  for (int c = 0; c < kMemberCols; ++c)
-    for (uint32_t i = threadIdx.x; i < mn; i += blockDim.x) A.md[c][mdo + i] = A.ms[c][ms + i];
 }
 
 template <typename T, typename OutT>
@@ -169,11 +178,12 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, int B
 }
 
 int choose_bucket_bits(uint64_t K, uint64_t N, uint64_t M) {
-  // ~384 rows of each family per bucket on average: the LDS path holds 1024.
-  const uint64_t need = std::max<uint64_t>({(K + 383) / 384, (N + 383) / 384, (M + 383) / 384, 1});
+  // Wave-sized buckets: ~32 key rows and ~20 rows of each child family on average, so
+  // nearly every bucket fits one wave (<= 64 per family); the rest take the LDS tier.
+  const uint64_t need = std::max<uint64_t>({(K + 31) / 32, (N + 19) / 20, (M + 19) / 20, 1});
   int B = 0;
   while ((1ull << B) < need) ++B;
-  return std::min(B, 24);
+  return std::min(B, 26);
 }
 
 }  // namespace
@@ -211,14 +221,17 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   Dir dk{dir, dir + dn, dir + 2 * dn, dir + 3 * dn, dir + 4 * dn};
   Dir dnd{dir + 5 * dn, dir + 6 * dn, dir + 7 * dn, dir + 8 * dn, dir + 9 * dn};
   Dir dm{dir + 10 * dn, dir + 11 * dn, dir + 12 * dn, dir + 13 * dn, dir + 14 * dn};
-  // misc: stats[8] u64 | last_bad u64 | totals[3] u64 | hot_count u32 (+pad) | hot_list[nb] u32
-  uint8_t* misc = (uint8_t*)ws_get(ctx, WS_MISC, 128 + nb * sizeof(uint32_t), &st);
+  // misc: stats[8] u64 | last_bad u64 | totals[3] u64 | hot_count u32 | big_count u32 |
+  //       hot_list[nb] u32 | big_list[nb] u32
+  uint8_t* misc = (uint8_t*)ws_get(ctx, WS_MISC, 128 + 2 * nb * sizeof(uint32_t), &st);
   if (!misc) return st;
   unsigned long long* d_stats = (unsigned long long*)misc;
   unsigned long long* d_last_bad = (unsigned long long*)(misc + 64);
   uint64_t* d_totals = (uint64_t*)(misc + 72);
   uint32_t* d_hot_count = (uint32_t*)(misc + 96);
+  uint32_t* d_big_count = (uint32_t*)(misc + 100);
   uint32_t* d_hot_list = (uint32_t*)(misc + 128);
+  uint32_t* d_big_list = d_hot_list + nb;
   CDB_HIP(hipMemsetAsync(misc, 0, 128, s), "memset misc");
 
   CDB_HIP(hipEventRecord(ctx->ev0, s), "event");
@@ -267,12 +280,20 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   A.flags = (flags & CDB_MERGE_STRICT_DICT_PANIC ? F_DICT_STRICT : 0) |
             (flags & CDB_MERGE_GC_DELETES ? F_GC_DELETES : 0) | (flags & CDB_MERGE_GC_MEMBERS ? F_GC_MEMBERS : 0);
   A.gc_wm = wm;
+  A.force_tier = opts ? opts->force_tier : 0;
   A.last_bad = (const uint64_t*)d_last_bad;
   A.stats = d_stats;
   A.hot_list = d_hot_list;
   A.hot_count = d_hot_count;
-  bucket_kernel<<<nb, kBktThreads, 0, s>>>(A, (uint32_t)nb);
-  CDB_HIP(hipGetLastError(), "bucket_kernel");
+  WaveArgs WA;
+  WA.A = A;
+  WA.nbuckets = (uint32_t)nb;
+  WA.big_list = d_big_list;
+  WA.big_count = d_big_count;
+  bucket_wave_kernel<<<(nb + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, 0, s>>>(WA);
+  CDB_HIP(hipGetLastError(), "bucket_wave_kernel");
+  bucket_mid_kernel<<<std::min<uint64_t>(nb, 2048), kBktThreads, 0, s>>>(A, d_big_list, d_big_count);
+  CDB_HIP(hipGetLastError(), "bucket_mid_kernel");
   CDB_HIP(hipEventRecord(ctx->ev_bucket, s), "event");
 
   // ---- 4. over-capacity buckets (same algorithm, global scratch)
@@ -324,7 +345,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   C.kbase = dk.base; C.nbase = dnd.base; C.mbase = dm.base;
   C.kout = dk.out; C.nout = dnd.out; C.mout = dm.out;
   C.kdoff = dk.doff; C.ndoff = dnd.doff; C.mdoff = dm.doff;
-  compact_kernel<<<nb, 256, 0, s>>>(C, (uint32_t)nb);
+  compact_kernel<<<(uint32_t)std::min<uint64_t>((nb + 3) / 4, 65536), 256, 0, s>>>(C, (uint32_t)nb);
   CDB_HIP(hipGetLastError(), "compact_kernel");
   CDB_HIP(hipEventRecord(ctx->ev1, s), "event");
 

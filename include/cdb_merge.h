@@ -108,7 +108,8 @@ enum {
 };
 typedef struct cdb_merge_opts {
   uint32_t flags;
-  uint32_t reserved;
+  uint32_t force_tier;   /* testing only: 0 = automatic; 1 = every bucket through the LDS
+                            workgroup tier; 2 = every bucket through the global-scratch tier */
   uint64_t gc_watermark; /* ReplicaManager::min_uuid (replica/replica.rs:87-89) */
 } cdb_merge_opts;
 

@@ -26,9 +26,9 @@ def _oracle(snaps, gc=None, members=False):
     return dump, st
 
 
-def _check(db, snaps, gc=None, members=False):
+def _check(db, snaps, gc=None, members=False, tier=0):
     want, ost = _oracle(snaps, gc, members)
-    m = db.merge_snapshots(snaps, gc_watermark=gc, gc_members=members)
+    m = db.merge_snapshots(snaps, gc_watermark=gc, gc_members=members, force_tier=tier)
     got = m.canonical_dump()
     if got != want:
         gl, wl = got.decode().splitlines(), want.decode().splitlines()
@@ -126,6 +126,28 @@ def test_random_small(db, seed):
     snaps = gen_replicas(seed, n_replicas=1 + seed % 6, n_keys=30 + seed, big_times=seed % 3 == 0,
                          p_conflict=0.1, p_side=0.2)
     _check(db, snaps)
+
+
+@pytest.mark.parametrize("tier", [1, 2])
+@pytest.mark.parametrize("seed", range(12))
+def test_random_forced_tier(db, seed, tier):
+    """The LDS workgroup tier and the global-scratch tier on every bucket."""
+    snaps = gen_replicas(900 + seed, n_replicas=1 + seed % 5, n_keys=40, p_conflict=0.1, p_side=0.3)
+    _check(db, snaps, gc=(seed % 7) if seed % 2 else None, members=bool(seed % 4 == 1), tier=tier)
+
+
+def test_mid_tier_natural(db):
+    """Buckets of a few hundred rows (above one wave, within the LDS pool)."""
+    objs1, objs2 = {}, {}
+    for k in range(6):
+        s1, s2 = o.Set(), o.Set()
+        for j in range(90):
+            s1.set(b"m%d" % j, None, (j * 7 + k) % 23)
+            if j % 2:
+                s2.set(b"m%d" % j, None, (j * 5 + k) % 19)
+        objs1[b"s%d" % k] = o.Object(1, 0, 0, o.OBJECT_ENC_SET, s1)
+        objs2[b"s%d" % k] = o.Object(2, 0, 0, o.OBJECT_ENC_SET, s2)
+    _check(db, [_snap(objs1), _snap(objs2)])
 
 
 @pytest.mark.parametrize("seed", range(20))
