@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--cpu-universe", type=int, default=1_000_000,
                     help="key universe of the bounded CPU-baseline sample (same generator config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="use the multi-GPU (RCCL all-to-all) path even when WORLD_SIZE == 1")
     return ap.parse_args()
 
 
@@ -84,7 +86,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if world > 1:
+    if world > 1 or args.force_dist:
         from constdb_amd import dist
         res = dist.run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes)
     else:

@@ -94,7 +94,8 @@ class BatchInfo(ctypes.Structure):
 
 
 class MergeOpts(ctypes.Structure):
-    _fields_ = [("flags", ctypes.c_uint32), ("force_tier", ctypes.c_uint32), ("gc_watermark", ctypes.c_uint64)]
+    _fields_ = [("flags", ctypes.c_uint32), ("force_tier", ctypes.c_uint32), ("gc_watermark", ctypes.c_uint64),
+                ("key_shift", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 class MergeStats(ctypes.Structure):
@@ -132,8 +133,8 @@ class GenConfig(ctypes.Structure):
 ABI_FUNCTIONS = (
     "cdb_ctx_create", "cdb_ctx_destroy", "cdb_last_error", "cdb_decode_snapshot", "cdb_batch_info_get",
     "cdb_batch_column", "cdb_batch_free", "cdb_merge", "cdb_merged_canonical_dump", "cdb_merged_free", "cdb_free",
-    "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_gen_default", "cdb_gen_snapshot",
-    "cdb_gen_device")
+    "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_partition_owner", "cdb_gen_default",
+    "cdb_gen_snapshot", "cdb_gen_device")
 
 _lib = None
 
@@ -168,6 +169,7 @@ def lib():
         "cdb_dev_rows_alloc": (c_st, [vp, P(DevRows), ctypes.c_uint64, ctypes.c_int]),
         "cdb_dev_rows_release": (None, [vp, P(DevRows)]),
         "cdb_merge_device": (c_st, [vp, P(DevInput), P(MergeOpts), P(DevOutput), P(MergeStats), vp]),
+        "cdb_partition_owner": (c_st, [vp, P(DevRows), ctypes.c_int, ctypes.c_int, P(DevRows), P(ctypes.c_uint64), vp]),
         "cdb_gen_default": (None, [P(GenConfig)]),
         "cdb_gen_snapshot": (c_st, [P(GenConfig), ctypes.c_uint32, P(vp), P(ctypes.c_size_t)]),
         "cdb_gen_device": (c_st, [vp, P(GenConfig), P(DevInput)]),

@@ -51,6 +51,7 @@ struct BucketArgs {
   uint32_t *kout, *nout, *mout;
   uint32_t flags;
   uint32_t force_tier;
+  int key_shift;
   uint64_t gc_wm;
   const uint64_t* last_bad;   // (pos,src)+1 of the newest garbage entry with t > wm; 0 = none
   unsigned long long* stats;
@@ -205,7 +206,8 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
   }
   __syncthreads();
   const int bb = A.bbits;
-  auto kdig = [&](uint32_t i) { return sub_digit(S.kh[i], bb, kDigBits); };
+  const int ks = A.key_shift;
+  auto kdig = [&](uint32_t i) { return sub_digit(S.kh[i] << ks, bb, kDigBits); };
   wg_sort(S.idx, S.rk, S.cnt, K, kDig, kdig, KeyLess{S}, S.misc, tmp);
 
   // segment starts (flag) and emit decisions (rank, scanned below)

@@ -25,6 +25,7 @@ enum WsSlot {
   WS_MISC,                                              // stats, last_bad, hot list
   WS_HOT,                                               // hot-bucket scratch slab
   WS_SCAN,                                              // scan partials
+  WS_OWNER,                                             // owner-partition directory
   WS_COUNT
 };
 

@@ -132,7 +132,7 @@ struct Dir {  // per-family bucket directory
 // Splits `n` rows of an NC-column family into 2^B buckets by the top bits of column 0.
 // Returns in `res` the columns holding the bucketed rows (one of in / A / B).
 template <int NC>
-cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, int B, uint64_t* const* A,
+cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, int B, int shift, uint64_t* const* A,
                             uint64_t* const* Bf, const Dir& d, uint64_t** res, uint64_t** spare,
                             hipStream_t s) {
   if (B == 0 || n == 0) {
@@ -158,14 +158,14 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, int B
     uint64_t* const* dst = (l % 2 == 0) ? A : Bf;
     const uint64_t nb = 1ull << btot;
     CDB_HIP(hipMemsetAsync(d.hist, 0, nb * sizeof(uint32_t), s), "memset hist");
-    part_hist_kernel<<<tiles, kPartThreads, 0, s>>>(cur[0], n, btot, bits[l], d.hist);
+    part_hist_kernel<<<tiles, kPartThreads, 0, s>>>(cur[0], n, btot, bits[l], shift, d.hist);
     CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, d.hist, nb, d.base, d.cursor, nullptr, s));
     ColSet<NC> ci, co;
     for (int c = 0; c < NC; ++c) {
       ci.c[c] = cur[c];
       co.c[c] = dst[c];
     }
-    part_scatter_kernel<NC><<<tiles, kPartThreads, 0, s>>>(ci, co, n, btot, bits[l], d.cursor);
+    part_scatter_kernel<NC><<<tiles, kPartThreads, 0, s>>>(ci, co, n, btot, bits[l], shift, d.cursor);
     CDB_HIP(hipGetLastError(), "partition");
     cur = dst;
   }
@@ -197,6 +197,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   const uint32_t flags = opts ? opts->flags : 0;
   const uint64_t wm = opts ? opts->gc_watermark : 0;
   const int B = choose_bucket_bits(K, N, M);
+  const int shift = opts ? (int)opts->key_shift : 0;
+  if (shift < 0 || shift > 16) return fail(ctx, CDB_BAD_ARGUMENT, "key_shift");
   const uint64_t nb = 1ull << B;
   cdb_status st = CDB_OK;
 
@@ -245,10 +247,10 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     nin[c] = in->nodes.col[c];
     min_[c] = in->members.col[c];
   }
-  CDB_TRY(partition_family<kKeyCols>(ctx, kin, K, B, KA, KB, dk, kb, ksp, s));
+  CDB_TRY(partition_family<kKeyCols>(ctx, kin, K, B, shift, KA, KB, dk, kb, ksp, s));
   // keys need 8 output columns: the spare buffer always has 8
-  CDB_TRY(partition_family<kNodeCols>(ctx, nin, N, B, NA, NB, dnd, ndb, nsp, s));
-  CDB_TRY(partition_family<kMemberCols>(ctx, min_, M, B, MA, MBf, dm, mbb, msp, s));
+  CDB_TRY(partition_family<kNodeCols>(ctx, nin, N, B, shift, NA, NB, dnd, ndb, nsp, s));
+  CDB_TRY(partition_family<kMemberCols>(ctx, min_, M, B, shift, MA, MBf, dm, mbb, msp, s));
   {  // sparse key outputs (8 columns) go to whichever ping-pong buffer is free
     uint64_t* const* free_k = (kb[0] == KA[0]) ? KB : KA;
     for (int c = 0; c < 8; ++c) ksp[c] = free_k[c];
@@ -281,6 +283,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
             (flags & CDB_MERGE_GC_DELETES ? F_GC_DELETES : 0) | (flags & CDB_MERGE_GC_MEMBERS ? F_GC_MEMBERS : 0);
   A.gc_wm = wm;
   A.force_tier = opts ? opts->force_tier : 0;
+  A.key_shift = shift;
   A.last_bad = (const uint64_t*)d_last_bad;
   A.stats = d_stats;
   A.hot_list = d_hot_list;
@@ -445,6 +448,46 @@ void cdb_dev_rows_release(cdb_ctx* ctx, cdb_dev_rows* r) {
   if (ctx) hipSetDevice(ctx->device);
   if (r && r->col[0]) hipFree(r->col[0]);
   if (r) std::memset(r, 0, sizeof *r);
+}
+
+cdb_status cdb_partition_owner(cdb_ctx* ctx, const cdb_dev_rows* in, int ncols, int owner_bits, cdb_dev_rows* out,
+                               uint64_t* counts, void* stream) {
+  if (!ctx || !in || !out || !counts || owner_bits < 0 || owner_bits > 9 || (ncols != 6 && ncols != 7 && ncols != 8))
+    return CDB_BAD_ARGUMENT;
+  if (in->n >= (1ull << 32)) return fail(ctx, CDB_BAD_ARGUMENT, "row count must be < 2^32");
+  hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  const uint64_t n = in->n, nb = 1ull << owner_bits;
+  cdb_status st = CDB_OK;
+  uint32_t* dir = (uint32_t*)ws_get(ctx, WS_OWNER, 3 * (nb + 1) * sizeof(uint32_t) + 64, &st);
+  if (!dir) return st;
+  uint32_t *hist = dir, *base = dir + nb + 1, *cursor = dir + 2 * (nb + 1);
+  CDB_HIP(hipMemsetAsync(hist, 0, nb * sizeof(uint32_t), s), "memset");
+  const uint64_t tiles = std::max<uint64_t>(1, (n + kPartTile - 1) / kPartTile);
+  if (n) {
+    part_hist_kernel<<<tiles, kPartThreads, 0, s>>>(in->col[0], n, owner_bits, owner_bits, 0, hist);
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, hist, nb, base, cursor, nullptr, s));
+    if (ncols == 6) {
+      ColSet<6> ci, co;
+      for (int c = 0; c < 6; ++c) { ci.c[c] = in->col[c]; co.c[c] = out->col[c]; }
+      part_scatter_kernel<6><<<tiles, kPartThreads, 0, s>>>(ci, co, n, owner_bits, owner_bits, 0, cursor);
+    } else if (ncols == 7) {
+      ColSet<7> ci, co;
+      for (int c = 0; c < 7; ++c) { ci.c[c] = in->col[c]; co.c[c] = out->col[c]; }
+      part_scatter_kernel<7><<<tiles, kPartThreads, 0, s>>>(ci, co, n, owner_bits, owner_bits, 0, cursor);
+    } else {
+      ColSet<8> ci, co;
+      for (int c = 0; c < 8; ++c) { ci.c[c] = in->col[c]; co.c[c] = out->col[c]; }
+      part_scatter_kernel<8><<<tiles, kPartThreads, 0, s>>>(ci, co, n, owner_bits, owner_bits, 0, cursor);
+    }
+    CDB_HIP(hipGetLastError(), "partition_owner");
+  }
+  std::vector<uint32_t> h(nb, 0);
+  CDB_HIP(hipMemcpyAsync(h.data(), hist, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");
+  CDB_HIP(hipStreamSynchronize(s), "sync");
+  for (uint64_t i = 0; i < nb; ++i) counts[i] = n ? h[i] : 0;
+  out->n = n;
+  return CDB_OK;
 }
 
 cdb_status cdb_merge_device(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts, cdb_dev_output* out,

@@ -34,21 +34,22 @@ __device__ __forceinline__ uint64_t bucket_bits_of(uint64_t h, int bits) {
 // hist[gb] += number of rows whose top `btot` bits of col0 are gb. Rows arrive grouped by
 // their top `btot - db` bits (the previous level's output), so a tile spans few prefixes.
 __global__ void __launch_bounds__(kPartThreads) part_hist_kernel(const uint64_t* __restrict__ col0, uint64_t n,
-                                                                 int btot, int db, uint32_t* __restrict__ hist) {
+                                                                 int btot, int db, int shift,
+                                                                 uint32_t* __restrict__ hist) {
   __shared__ uint32_t cnt[kPartLocalMax];
   const uint64_t tile0 = (uint64_t)blockIdx.x * kPartTile;
   if (tile0 >= n) return;
   const uint64_t tile1 = min(n, tile0 + kPartTile);
   const int pbits = btot - db;
-  const uint64_t plo = bucket_bits_of(col0[tile0], pbits);
-  const uint64_t phi = bucket_bits_of(col0[tile1 - 1], pbits);
+  const uint64_t plo = bucket_bits_of(col0[tile0] << shift, pbits);
+  const uint64_t phi = bucket_bits_of(col0[tile1 - 1] << shift, pbits);
   const uint64_t glo = plo << db;
   const uint64_t span = (phi - plo + 1) << db;
   const bool local = span <= (uint64_t)kPartLocalMax;
   for (int i = threadIdx.x; i < kPartLocalMax; i += kPartThreads) cnt[i] = 0;
   __syncthreads();
   for (uint64_t r = tile0 + threadIdx.x; r < tile1; r += kPartThreads) {
-    const uint64_t gb = bucket_bits_of(col0[r], btot);
+    const uint64_t gb = bucket_bits_of(col0[r] << shift, btot);
     if (local) atomicAdd(&cnt[gb - glo], 1u);
     else atomicAdd(&hist[gb], 1u);
   }
@@ -64,7 +65,7 @@ __global__ void __launch_bounds__(kPartThreads) part_hist_kernel(const uint64_t*
 // that each wave's stores are contiguous runs.
 template <int NC>
 __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> in, ColSet<NC> out, uint64_t n,
-                                                                    int btot, int db,
+                                                                    int btot, int db, int shift,
                                                                     uint32_t* __restrict__ cursor) {
   __shared__ uint32_t cnt[kPartLocalMax];   // per local bucket: count, then scan
   __shared__ uint32_t gbase[kPartLocalMax]; // reserved global start per local bucket
@@ -75,14 +76,14 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
   const uint64_t tile1 = min(n, tile0 + kPartTile);
   const int rows = (int)(tile1 - tile0);
   const int pbits = btot - db;
-  const uint64_t plo = bucket_bits_of(in.c[0][tile0], pbits);
-  const uint64_t phi = bucket_bits_of(in.c[0][tile1 - 1], pbits);
+  const uint64_t plo = bucket_bits_of(in.c[0][tile0] << shift, pbits);
+  const uint64_t phi = bucket_bits_of(in.c[0][tile1 - 1] << shift, pbits);
   const uint64_t glo = plo << db;
   const uint64_t span = (phi - plo + 1) << db;
 
   if (span > (uint64_t)kPartLocalMax) {  // wide tile: per-row global reservation
     for (int r = threadIdx.x; r < rows; r += kPartThreads) {
-      const uint64_t gb = bucket_bits_of(in.c[0][tile0 + r], btot);
+      const uint64_t gb = bucket_bits_of(in.c[0][tile0 + r] << shift, btot);
       const uint32_t d = atomicAdd(&cursor[gb], 1u);
 #pragma unroll
       for (int c = 0; c < NC; ++c) out.c[c][d] = in.c[c][tile0 + r];
@@ -97,7 +98,7 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
   for (int k = 0; k < kPartRowsPerThread; ++k) {
     const int r = threadIdx.x + k * kPartThreads;
     if (r < rows) {
-      lb[k] = (uint16_t)(bucket_bits_of(in.c[0][tile0 + r], btot) - glo);
+      lb[k] = (uint16_t)(bucket_bits_of(in.c[0][tile0 + r] << shift, btot) - glo);
       rk[k] = atomicAdd(&cnt[lb[k]], 1u);
     }
   }

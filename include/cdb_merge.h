@@ -111,6 +111,9 @@ typedef struct cdb_merge_opts {
   uint32_t force_tier;   /* testing only: 0 = automatic; 1 = every bucket through the LDS
                             workgroup tier; 2 = every bucket through the global-scratch tier */
   uint64_t gc_watermark; /* ReplicaManager::min_uuid (replica/replica.rs:87-89) */
+  uint32_t key_shift;    /* multi-GPU: the top `key_shift` bits of every key hash are the owner
+                            rank (all equal on one device), so local buckets use the bits below */
+  uint32_t reserved;
 } cdb_merge_opts;
 
 typedef struct cdb_merge_stats {
@@ -163,6 +166,14 @@ typedef struct cdb_dev_output {
   uint32_t compact;
   uint32_t reserved;
 } cdb_dev_output;
+
+/* Multi-GPU pack step: groups the rows of one family by owner rank = the
+ * top `owner_bits` bits of column 0 (key hash, or parent key hash for children, so a key and
+ * its children go to the same rank) into `out` (caller-allocated, >= in->n rows, same
+ * columns), and writes the 2^owner_bits per-owner row counts to the host array `counts`.
+ * The caller then exchanges the rows with an RCCL all-to-all (constdb_amd/dist.py). */
+cdb_status cdb_partition_owner(cdb_ctx* ctx, const cdb_dev_rows* in, int ncols, int owner_bits,
+                               cdb_dev_rows* out, uint64_t* counts, void* stream);
 
 /* Allocates device columns for `rows` rows of a family (8 u64 columns) in *r. */
 cdb_status cdb_dev_rows_alloc(cdb_ctx* ctx, cdb_dev_rows* r, uint64_t rows, int ncols);

@@ -203,3 +203,47 @@ def test_deterministic(db):
     a = db.merge_snapshots(snaps).canonical_dump()
     b = db.merge_snapshots(snaps).canonical_dump()
     assert a == b
+
+
+@pytest.mark.parametrize("shift", [1, 3])
+def test_key_shift_parity(db, shift):
+    """Multi-GPU ranks bucket on the hash bits below the owner bits; any shift is exact."""
+    cfg = cdb.gen_config(seed=5, universe=20000, n_replicas=4, replica_hi=4)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(4)]
+    want, _ = _oracle(snaps)
+    batches = [cdb.decode_snapshot(s) for s in snaps]
+    import ctypes
+    n = len(batches)
+    arr = (ctypes.c_void_p * n)(*[b.handle for b in batches])
+    opts = cdb.MergeOpts()
+    opts.key_shift = shift
+    st = cdb.MergeStats()
+    h = ctypes.c_void_p()
+    db.ctx.check(cdb.lib().cdb_merge(db.ctx.handle, arr, n, ctypes.byref(opts), ctypes.byref(h), ctypes.byref(st)))
+    assert cdb.Merged(db.ctx, h, st, batches).canonical_dump() == want
+
+
+@pytest.mark.parametrize("ncols,bits", [(7, 1), (6, 3), (8, 0)])
+def test_partition_owner(db, ncols, bits):
+    import ctypes
+    import torch
+    n = 50_000 + bits
+    g = torch.Generator().manual_seed(ncols * 10 + bits)
+    src = torch.randint(-2**62, 2**62, (ncols, n), dtype=torch.int64, generator=g).cuda()
+    dst = torch.empty_like(src)
+    rin, rout = cdb.DevRows(), cdb.DevRows()
+    for c in range(ncols):
+        rin.col[c] = src[c].data_ptr()
+        rout.col[c] = dst[c].data_ptr()
+    rin.n = n
+    counts = (ctypes.c_uint64 * (1 << bits))()
+    db.ctx.check(cdb.lib().cdb_partition_owner(db.ctx.handle, ctypes.byref(rin), ncols, bits, ctypes.byref(rout),
+                                               counts, None))
+    torch.cuda.synchronize()
+    s, d = src.cpu(), dst.cpu()
+    own = (s[0].view(torch.int64) >> (64 - bits)) & ((1 << bits) - 1) if bits else torch.zeros(n, dtype=torch.int64)
+    assert [counts[i] for i in range(1 << bits)] == torch.bincount(own, minlength=1 << bits).tolist()
+    downer = (d[0] >> (64 - bits)) & ((1 << bits) - 1) if bits else torch.zeros(n, dtype=torch.int64)
+    assert bool((downer[1:] >= downer[:-1]).all())              # grouped by owner
+    key = lambda t: sorted(map(tuple, t.T.tolist()))             # same multiset of rows
+    assert key(s) == key(d)
