@@ -44,7 +44,7 @@ struct BucketArgs {
   const uint64_t* nd[kNodeCols];
   const uint64_t* mb[kMemberCols];
   const uint32_t *kbase, *kcnt, *nbase, *ncnt, *mbase, *mcnt;
-  int bbits;
+  uint64_t nbuckets;          // bucket(h) = floor((h << key_shift) * nbuckets / 2^64)
   uint64_t* ko[kKeyOutCols];
   uint64_t* no[kNodeCols];
   uint64_t* mo[kMemberCols];
@@ -117,9 +117,12 @@ __device__ uint32_t wg_scan(uint32_t* a, uint32_t L, uint32_t* tmp /* >= 16 */) 
 
 struct KeyLess {
   const Scratch& S;
+  int shift;  // order by (kh << shift, kh, ...): monotone with the counting-sort digit
   __device__ bool operator()(uint32_t a, uint32_t b) const {
     if (a == kNone) return false;
     if (b == kNone) return true;
+    const uint64_t sa = S.kh[a] << shift, sb = S.kh[b] << shift;
+    if (sa != sb) return sa < sb;
     if (S.kh[a] != S.kh[b]) return S.kh[a] < S.kh[b];
     if (S.kf[a] != S.kf[b]) return S.kf[a] < S.kf[b];
     const uint32_t fa = tag_family(meta_tag(S.meta[a])), fb = tag_family(meta_tag(S.meta[b]));
@@ -205,10 +208,11 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
     S.meta[i] = A.k[K_META][kb + i];
   }
   __syncthreads();
-  const int bb = A.bbits;
   const int ks = A.key_shift;
-  auto kdig = [&](uint32_t i) { return sub_digit(S.kh[i] << ks, bb, kDigBits); };
-  wg_sort(S.idx, S.rk, S.cnt, K, kDig, kdig, KeyLess{S}, S.misc, tmp);
+  const uint64_t nbk = A.nbuckets;
+  // position inside the bucket: the fractional part of (h << shift) * nb / 2^64
+  auto kdig = [&](uint32_t i) { return (uint32_t)(((S.kh[i] << ks) * nbk) >> (64 - kDigBits)); };
+  wg_sort(S.idx, S.rk, S.cnt, K, kDig, kdig, KeyLess{S, ks}, S.misc, tmp);
 
   // segment starts (flag) and emit decisions (rank, scanned below)
   const uint64_t last_bad = (A.flags & F_GC_DELETES) ? *A.last_bad : 0;
@@ -317,9 +321,12 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
       const uint64_t m = C[C_META][base + i];
       // lower_bound over the sorted output keys on (kh, kf); the data row sorts first
       uint32_t lo = 0, hi = kout;
-      while (lo < hi) {
+      const uint64_t spkh = pkh << ks;
+      while (lo < hi) {  // output keys are in (kh << shift, kh, kf) order
         const uint32_t mid = (lo + hi) >> 1;
-        if (S.okh[mid] < pkh || (S.okh[mid] == pkh && S.okf[mid] < pkf)) lo = mid + 1;
+        const uint64_t sm = S.okh[mid] << ks;
+        const bool less = sm < spkh || (sm == spkh && (S.okh[mid] < pkh || (S.okh[mid] == pkh && S.okf[mid] < pkf)));
+        if (less) lo = mid + 1;
         else hi = mid;
       }
       uint32_t key = kNone;

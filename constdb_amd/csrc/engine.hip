@@ -129,17 +129,53 @@ struct Dir {  // per-family bucket directory
   uint32_t *hist, *base, *cursor, *out, *doff;
 };
 
-// Splits `n` rows of an NC-column family into 2^B buckets by the top bits of column 0.
+// Bucket plan: NB = d[0] * ... * d[levels-1] buckets, bucket(h) = floor((h << shift) * NB / 2^64).
+struct Plan {
+  int levels = 0;
+  uint32_t d[4] = {1, 1, 1, 1};
+  uint64_t nb = 1;
+};
+
+Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
+  // Wave-sized buckets: ~40 key rows and ~24 child rows (nodes + members) on average, so
+  // nearly every bucket fits one wave (64 lanes per family); the rest take the LDS tier.
+  const uint64_t want = std::max<uint64_t>({(K + 39) / 40, (N + M + 23) / 24, 1});
+  Plan p;
+  if (want <= 1) return p;
+  if (want <= 512) {
+    p.levels = 1;
+    p.d[0] = (uint32_t)want;
+  } else if (want <= 512ull * 512) {
+    p.levels = 2;
+    uint32_t a = 1;
+    while ((uint64_t)a * a < want) ++a;
+    p.d[0] = std::min<uint32_t>(a, 512);
+    p.d[1] = (uint32_t)((want + p.d[0] - 1) / p.d[0]);
+  } else {
+    p.levels = 3;
+    p.d[0] = 512;
+    const uint64_t rest = (want + 511) / 512;
+    uint32_t a = 1;
+    while ((uint64_t)a * a < rest) ++a;
+    p.d[1] = std::min<uint32_t>(a, 512);
+    p.d[2] = (uint32_t)std::min<uint64_t>((rest + p.d[1] - 1) / p.d[1], 512);
+  }
+  p.nb = 1;
+  for (int l = 0; l < p.levels; ++l) p.nb *= p.d[l];
+  return p;
+}
+
+// Splits `n` rows of an NC-column family into plan.nb buckets (key-hash order).
 // Returns in `res` the columns holding the bucketed rows (one of in / A / B).
 template <int NC>
-cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, int B, int shift, uint64_t* const* A,
-                            uint64_t* const* Bf, const Dir& d, uint64_t** res, uint64_t** spare,
-                            hipStream_t s) {
-  if (B == 0 || n == 0) {
+cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const Plan& plan, int shift,
+                            uint64_t* const* A, uint64_t* const* Bf, const Dir& d, uint64_t** res,
+                            uint64_t** spare, hipStream_t s) {
+  if (plan.levels == 0 || n == 0) {
     set_dir_kernel<<<1, 1, 0, s>>>(d.base, d.hist, (uint32_t)n);
-    if (B > 0) {  // n == 0 with buckets: every bucket empty
-      CDB_HIP(hipMemsetAsync(d.base, 0, sizeof(uint32_t) << B, s), "memset");
-      CDB_HIP(hipMemsetAsync(d.hist, 0, sizeof(uint32_t) << B, s), "memset");
+    if (plan.nb > 1) {  // n == 0 with buckets: every bucket empty
+      CDB_HIP(hipMemsetAsync(d.base, 0, sizeof(uint32_t) * plan.nb, s), "memset");
+      CDB_HIP(hipMemsetAsync(d.hist, 0, sizeof(uint32_t) * plan.nb, s), "memset");
     }
     for (int c = 0; c < NC; ++c) {
       res[c] = in[c];
@@ -147,27 +183,24 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, int B
     }
     return hip_check(ctx, hipGetLastError(), "set_dir");
   }
-  const int levels = (B + 8) / 9;
-  int bits[8];
-  for (int l = 0; l < levels; ++l) bits[l] = B / levels + (l < B % levels ? 1 : 0);
   const uint64_t tiles = (n + kPartTile - 1) / kPartTile;
   uint64_t* const* cur = in;
-  int btot = 0;
-  for (int l = 0; l < levels; ++l) {
-    btot += bits[l];
+  uint64_t nprev = 1;
+  for (int l = 0; l < plan.levels; ++l) {
     uint64_t* const* dst = (l % 2 == 0) ? A : Bf;
-    const uint64_t nb = 1ull << btot;
-    CDB_HIP(hipMemsetAsync(d.hist, 0, nb * sizeof(uint32_t), s), "memset hist");
-    part_hist_kernel<<<tiles, kPartThreads, 0, s>>>(cur[0], n, btot, bits[l], shift, d.hist);
-    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, d.hist, nb, d.base, d.cursor, nullptr, s));
+    const uint64_t ncur = nprev * plan.d[l];
+    CDB_HIP(hipMemsetAsync(d.hist, 0, ncur * sizeof(uint32_t), s), "memset hist");
+    part_hist_kernel<<<tiles, kPartThreads, 0, s>>>(cur[0], n, nprev, plan.d[l], shift, d.hist);
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, d.hist, ncur, d.base, d.cursor, nullptr, s));
     ColSet<NC> ci, co;
     for (int c = 0; c < NC; ++c) {
       ci.c[c] = cur[c];
       co.c[c] = dst[c];
     }
-    part_scatter_kernel<NC><<<tiles, kPartThreads, 0, s>>>(ci, co, n, btot, bits[l], shift, d.cursor);
+    part_scatter_kernel<NC><<<tiles, kPartThreads, 0, s>>>(ci, co, n, nprev, plan.d[l], shift, d.cursor);
     CDB_HIP(hipGetLastError(), "partition");
     cur = dst;
+    nprev = ncur;
   }
   uint64_t* const* other = (cur == A) ? Bf : A;
   for (int c = 0; c < NC; ++c) {
@@ -175,15 +208,6 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, int B
     spare[c] = other[c];
   }
   return CDB_OK;
-}
-
-int choose_bucket_bits(uint64_t K, uint64_t N, uint64_t M) {
-  // Wave-sized buckets: ~32 key rows and ~20 rows of each child family on average, so
-  // nearly every bucket fits one wave (<= 64 per family); the rest take the LDS tier.
-  const uint64_t need = std::max<uint64_t>({(K + 31) / 32, (N + 19) / 20, (M + 19) / 20, 1});
-  int B = 0;
-  while ((1ull << B) < need) ++B;
-  return std::min(B, 26);
 }
 
 }  // namespace
@@ -196,10 +220,10 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     return fail(ctx, CDB_BAD_ARGUMENT, "row counts must be < 2^32 per family per device");
   const uint32_t flags = opts ? opts->flags : 0;
   const uint64_t wm = opts ? opts->gc_watermark : 0;
-  const int B = choose_bucket_bits(K, N, M);
+  const Plan plan = make_plan(K, N, M);
   const int shift = opts ? (int)opts->key_shift : 0;
   if (shift < 0 || shift > 16) return fail(ctx, CDB_BAD_ARGUMENT, "key_shift");
-  const uint64_t nb = 1ull << B;
+  const uint64_t nb = plan.nb;
   cdb_status st = CDB_OK;
 
   // ---- workspace
@@ -247,10 +271,10 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     nin[c] = in->nodes.col[c];
     min_[c] = in->members.col[c];
   }
-  CDB_TRY(partition_family<kKeyCols>(ctx, kin, K, B, shift, KA, KB, dk, kb, ksp, s));
+  CDB_TRY(partition_family<kKeyCols>(ctx, kin, K, plan, shift, KA, KB, dk, kb, ksp, s));
   // keys need 8 output columns: the spare buffer always has 8
-  CDB_TRY(partition_family<kNodeCols>(ctx, nin, N, B, shift, NA, NB, dnd, ndb, nsp, s));
-  CDB_TRY(partition_family<kMemberCols>(ctx, min_, M, B, shift, MA, MBf, dm, mbb, msp, s));
+  CDB_TRY(partition_family<kNodeCols>(ctx, nin, N, plan, shift, NA, NB, dnd, ndb, nsp, s));
+  CDB_TRY(partition_family<kMemberCols>(ctx, min_, M, plan, shift, MA, MBf, dm, mbb, msp, s));
   {  // sparse key outputs (8 columns) go to whichever ping-pong buffer is free
     uint64_t* const* free_k = (kb[0] == KA[0]) ? KB : KA;
     for (int c = 0; c < 8; ++c) ksp[c] = free_k[c];
@@ -277,7 +301,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   A.kbase = dk.base; A.kcnt = dk.hist;
   A.nbase = dnd.base; A.ncnt = dnd.hist;
   A.mbase = dm.base; A.mcnt = dm.hist;
-  A.bbits = B;
+  A.nbuckets = nb;
   A.kout = dk.out; A.nout = dnd.out; A.mout = dm.out;
   A.flags = (flags & CDB_MERGE_STRICT_DICT_PANIC ? F_DICT_STRICT : 0) |
             (flags & CDB_MERGE_GC_DELETES ? F_GC_DELETES : 0) | (flags & CDB_MERGE_GC_MEMBERS ? F_GC_MEMBERS : 0);
@@ -465,20 +489,20 @@ cdb_status cdb_partition_owner(cdb_ctx* ctx, const cdb_dev_rows* in, int ncols, 
   CDB_HIP(hipMemsetAsync(hist, 0, nb * sizeof(uint32_t), s), "memset");
   const uint64_t tiles = std::max<uint64_t>(1, (n + kPartTile - 1) / kPartTile);
   if (n) {
-    part_hist_kernel<<<tiles, kPartThreads, 0, s>>>(in->col[0], n, owner_bits, owner_bits, 0, hist);
+    part_hist_kernel<<<tiles, kPartThreads, 0, s>>>(in->col[0], n, 1, (uint32_t)nb, 0, hist);
     CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, hist, nb, base, cursor, nullptr, s));
     if (ncols == 6) {
       ColSet<6> ci, co;
       for (int c = 0; c < 6; ++c) { ci.c[c] = in->col[c]; co.c[c] = out->col[c]; }
-      part_scatter_kernel<6><<<tiles, kPartThreads, 0, s>>>(ci, co, n, owner_bits, owner_bits, 0, cursor);
+      part_scatter_kernel<6><<<tiles, kPartThreads, 0, s>>>(ci, co, n, 1, (uint32_t)nb, 0, cursor);
     } else if (ncols == 7) {
       ColSet<7> ci, co;
       for (int c = 0; c < 7; ++c) { ci.c[c] = in->col[c]; co.c[c] = out->col[c]; }
-      part_scatter_kernel<7><<<tiles, kPartThreads, 0, s>>>(ci, co, n, owner_bits, owner_bits, 0, cursor);
+      part_scatter_kernel<7><<<tiles, kPartThreads, 0, s>>>(ci, co, n, 1, (uint32_t)nb, 0, cursor);
     } else {
       ColSet<8> ci, co;
       for (int c = 0; c < 8; ++c) { ci.c[c] = in->col[c]; co.c[c] = out->col[c]; }
-      part_scatter_kernel<8><<<tiles, kPartThreads, 0, s>>>(ci, co, n, owner_bits, owner_bits, 0, cursor);
+      part_scatter_kernel<8><<<tiles, kPartThreads, 0, s>>>(ci, co, n, 1, (uint32_t)nb, 0, cursor);
     }
     CDB_HIP(hipGetLastError(), "partition_owner");
   }

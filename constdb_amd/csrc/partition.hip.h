@@ -1,9 +1,9 @@
 // Bucket partition (MSD multisplit) and device-wide scans for gfx950.
 //
 // A row family (key rows, node rows, member rows — each a set of u64 SoA columns) is
-// split into 2^B buckets by the top B bits of column 0 (the key hash kh, or the parent
-// key hash pkh for children), so a key and all its children share a bucket. B is split
-// into levels of <= 9 bits: each level is one streaming pass (histogram pass over col 0,
+// split into NB buckets by floor(h * NB / 2^64) of column 0 (the key hash kh, or the parent
+// key hash pkh for children), so a key and all its children share a bucket. NB is a
+// product of per-level digit counts <= 512: each level is one streaming pass (histogram pass over col 0,
 // then a scatter pass that stages every column through LDS so that writes leave the CU
 // as contiguous per-digit runs). Rows inside a bucket end up in arbitrary order; the
 // bucket kernel sorts them by full identity, so results stay deterministic.
@@ -26,30 +26,31 @@ struct ColSet {
   uint64_t* c[NC];
 };
 
-__device__ __forceinline__ uint64_t bucket_bits_of(uint64_t h, int bits) {
-  return bits ? (h >> (64 - bits)) : 0;
-}
+// Bucket index of hash h among `nb` buckets: floor(h * nb / 2^64). Monotone in h, so for
+// N_{l+1} = N_l * d the level-(l+1) buckets refine the level-l ones (MSD partition with
+// bucket counts that need not be powers of two).
+__device__ __forceinline__ uint64_t bucket_of_n(uint64_t h, uint64_t nb) { return __umul64hi(h, nb); }
 
 // ---------------------------------------------------------------- histogram
 // hist[gb] += number of rows whose top `btot` bits of col0 are gb. Rows arrive grouped by
 // their top `btot - db` bits (the previous level's output), so a tile spans few prefixes.
 __global__ void __launch_bounds__(kPartThreads) part_hist_kernel(const uint64_t* __restrict__ col0, uint64_t n,
-                                                                 int btot, int db, int shift,
+                                                                 uint64_t nprev, uint32_t d, int shift,
                                                                  uint32_t* __restrict__ hist) {
   __shared__ uint32_t cnt[kPartLocalMax];
   const uint64_t tile0 = (uint64_t)blockIdx.x * kPartTile;
   if (tile0 >= n) return;
   const uint64_t tile1 = min(n, tile0 + kPartTile);
-  const int pbits = btot - db;
-  const uint64_t plo = bucket_bits_of(col0[tile0] << shift, pbits);
-  const uint64_t phi = bucket_bits_of(col0[tile1 - 1] << shift, pbits);
-  const uint64_t glo = plo << db;
-  const uint64_t span = (phi - plo + 1) << db;
+  const uint64_t ncur = nprev * d;
+  const uint64_t plo = bucket_of_n(col0[tile0] << shift, nprev);
+  const uint64_t phi = bucket_of_n(col0[tile1 - 1] << shift, nprev);
+  const uint64_t glo = plo * d;
+  const uint64_t span = (phi - plo + 1) * d;
   const bool local = span <= (uint64_t)kPartLocalMax;
   for (int i = threadIdx.x; i < kPartLocalMax; i += kPartThreads) cnt[i] = 0;
   __syncthreads();
   for (uint64_t r = tile0 + threadIdx.x; r < tile1; r += kPartThreads) {
-    const uint64_t gb = bucket_bits_of(col0[r] << shift, btot);
+    const uint64_t gb = bucket_of_n(col0[r] << shift, ncur);
     if (local) atomicAdd(&cnt[gb - glo], 1u);
     else atomicAdd(&hist[gb], 1u);
   }
@@ -65,7 +66,7 @@ __global__ void __launch_bounds__(kPartThreads) part_hist_kernel(const uint64_t*
 // that each wave's stores are contiguous runs.
 template <int NC>
 __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> in, ColSet<NC> out, uint64_t n,
-                                                                    int btot, int db, int shift,
+                                                                    uint64_t nprev, uint32_t d, int shift,
                                                                     uint32_t* __restrict__ cursor) {
   __shared__ uint32_t cnt[kPartLocalMax];   // per local bucket: count, then scan
   __shared__ uint32_t gbase[kPartLocalMax]; // reserved global start per local bucket
@@ -75,15 +76,15 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
   if (tile0 >= n) return;
   const uint64_t tile1 = min(n, tile0 + kPartTile);
   const int rows = (int)(tile1 - tile0);
-  const int pbits = btot - db;
-  const uint64_t plo = bucket_bits_of(in.c[0][tile0] << shift, pbits);
-  const uint64_t phi = bucket_bits_of(in.c[0][tile1 - 1] << shift, pbits);
-  const uint64_t glo = plo << db;
-  const uint64_t span = (phi - plo + 1) << db;
+  const uint64_t ncur = nprev * d;
+  const uint64_t plo = bucket_of_n(in.c[0][tile0] << shift, nprev);
+  const uint64_t phi = bucket_of_n(in.c[0][tile1 - 1] << shift, nprev);
+  const uint64_t glo = plo * d;
+  const uint64_t span = (phi - plo + 1) * d;
 
   if (span > (uint64_t)kPartLocalMax) {  // wide tile: per-row global reservation
     for (int r = threadIdx.x; r < rows; r += kPartThreads) {
-      const uint64_t gb = bucket_bits_of(in.c[0][tile0 + r] << shift, btot);
+      const uint64_t gb = bucket_of_n(in.c[0][tile0 + r] << shift, ncur);
       const uint32_t d = atomicAdd(&cursor[gb], 1u);
 #pragma unroll
       for (int c = 0; c < NC; ++c) out.c[c][d] = in.c[c][tile0 + r];
@@ -98,7 +99,7 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
   for (int k = 0; k < kPartRowsPerThread; ++k) {
     const int r = threadIdx.x + k * kPartThreads;
     if (r < rows) {
-      lb[k] = (uint16_t)(bucket_bits_of(in.c[0][tile0 + r] << shift, btot) - glo);
+      lb[k] = (uint16_t)(bucket_of_n(in.c[0][tile0 + r] << shift, ncur) - glo);
       rk[k] = atomicAdd(&cnt[lb[k]], 1u);
     }
   }
