@@ -78,6 +78,11 @@ def cpu_baseline(cdb, args):
 
 def main():
     args = parse()
+    # RCCL and the HIP runtime may print banners on the C-level stdout: keep fd 1 for the
+    # single JSON line and send everything else to stderr.
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+    sys.stdout = os.fdopen(os.dup(2), "w")
     import constdb_amd as cdb
     from constdb_amd import build as b
     b.build()
@@ -92,10 +97,12 @@ def main():
     else:
         res = run_single(cdb, args)
     if rank != 0:
+        os.close(json_fd)
         return
     if not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(cdb, args)
-    print(json.dumps(res), flush=True)
+    with os.fdopen(json_fd, "w") as out:
+        out.write(json.dumps(res) + "\n")
 
 
 def run_single(cdb, args):

@@ -150,6 +150,10 @@ def lib():
         return _lib
     if not os.path.exists(_LIB_PATH):
         raise OSError(f"{_LIB_PATH} missing: build it with `python constdb_amd/build.py`")
+    # NOTE: torch bundles its own libamdhip64.so.7 / libhsa-runtime64.so.1. A process that
+    # uses torch's GPU runtime AND this library must import torch first, so that our
+    # DT_NEEDED (soname libamdhip64.so.7) binds to the runtime torch already mapped; two
+    # HSA runtimes in one process do not share the GPU (see constdb_amd/dist.py, tests).
     L = ctypes.CDLL(_LIB_PATH)
     vp, c_st = ctypes.c_void_p, ctypes.c_int
     P = ctypes.POINTER

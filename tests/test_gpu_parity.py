@@ -1,6 +1,7 @@
 """GPU parity: the HIP merge engine (through the C-ABI) vs the oracle, on the same snapshot
 bytes. Bit-exact canonical dumps are required (integer/ordering work, no tolerance)."""
 import pytest
+import torch  # noqa: F401  -- before libcdbmerge loads: one HIP runtime per process (constdb_amd.lib)
 
 import cdb_oracle
 import constdb_amd as cdb
