@@ -163,7 +163,8 @@ def run_single(cdb, args):
                      "achieved": B / (bk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": B / (bk * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None},
         "stats": {"type_conflicts": st.type_conflicts, "dict_merges": st.dict_merges,
-                  "hot_buckets": st.hot_buckets, "orphans": st.orphan_children},
+                  "hot_buckets": st.hot_buckets, "wide_buckets": st.wide_buckets,
+                  "mid_buckets": st.mid_buckets, "orphans": st.orphan_children},
     }
     for fam in (dout.keys, dout.nodes, dout.members, din.keys, din.nodes, din.members):
         L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))

@@ -26,6 +26,7 @@ enum WsSlot {
   WS_HOT,                                               // hot-bucket scratch slab
   WS_SCAN,                                              // scan partials
   WS_OWNER,                                             // owner-partition directory
+  WS_PERM,                                              // final-level row permutations (u32)
   WS_COUNT
 };
 

@@ -58,6 +58,11 @@ __global__ void set_dir_kernel(uint32_t* base, uint32_t* cnt, uint32_t n) {
   cnt[0] = n;
 }
 
+__global__ void iota_kernel(uint32_t* p, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    p[i] = (uint32_t)i;
+}
+
 __global__ void gc_lastbad_kernel(const uint64_t* __restrict__ ct, const uint64_t* __restrict__ meta, uint64_t n,
                                   uint64_t wm, unsigned long long* out) {
   uint64_t best = 0;
@@ -80,34 +85,75 @@ struct CompactArgs {
 };
 
 // Sparse-by-bucket outputs -> dense arrays; child ranges become absolute row indices.
-// One wave per bucket (buckets are wave-sized), grid-stride over buckets.
-__global__ void __launch_bounds__(256) compact_kernel(CompactArgs A, uint32_t nbuckets) {
+// One wave per group of 64 consecutive buckets: the group's dense output rows are one
+// contiguous range (doff is an exclusive scan), so lane t of a pass copies dense row
+// doff[b0] + t from its bucket's sparse slot — coalesced stores, nearly coalesced loads.
+// The source bucket of a dense row is a 6-step binary search over the group's offsets.
+constexpr int kCompactWaves = 4;
+
+struct CompactLds {
+  uint32_t doff[64], sbase[64], ndoff[64], mdoff[64];
+};
+
+__device__ __forceinline__ int group_bucket(const uint32_t* rel, uint32_t t) {  // last j: rel[j] <= t
+  int j = 0;
+#pragma unroll
+  for (int step = 32; step > 0; step >>= 1) j = (rel[j + step] <= t) ? j + step : j;
+  return j;
+}
+
+__global__ void __launch_bounds__(kCompactWaves * 64) compact_kernel(CompactArgs A, uint32_t nbuckets) {
+  __shared__ CompactLds lds_all[kCompactWaves];
+  CompactLds& L = lds_all[threadIdx.x >> 6];
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
-  for (uint32_t b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < nbuckets; b += nwaves) {
-    const uint32_t kn = A.kout[b], ks = A.kbase[b], kd = A.kdoff[b];
-    const uint32_t nn = A.nout[b], ns = A.nbase[b], ndo = A.ndoff[b];
-    const uint32_t mn = A.mout[b], ms = A.mbase[b], mdo = A.mdoff[b];
-    for (uint32_t i = lane; i < kn; i += 64) {
-#pragma unroll
-      for (int c = 0; c < kKeyOutCols; ++c) {
-        uint64_t v = A.ks[c][ks + i];
-        if (c == O_CREF) {
-          const uint64_t cnt = v & 0xFFFFFF;
-          const uint32_t T = meta_tag(A.ks[O_META][ks + i]);
-          const uint64_t begin = cnt ? (v >> 24) + (T == TAG_COUNTER ? ndo : mdo) : 0;
-          v = cref_pack(begin, cnt);
-        }
-        A.kd[c][kd + i] = v;
+  const uint32_t ngroups = (nbuckets + 63) / 64;
+  const uint32_t nwaves = gridDim.x * kCompactWaves;
+  for (uint32_t g = blockIdx.x * kCompactWaves + (threadIdx.x >> 6); g < ngroups; g += nwaves) {
+    const uint32_t b0 = g * 64, nb = min(64u, nbuckets - b0);
+    const uint32_t b = b0 + min(lane, nb - 1);
+    const bool in = lane < nb;
+#pragma unroll 1
+    for (int fam = 0; fam < 3; ++fam) {
+      const uint32_t* out = fam == 0 ? A.kout : fam == 1 ? A.nout : A.mout;
+      const uint32_t* base = fam == 0 ? A.kbase : fam == 1 ? A.nbase : A.mbase;
+      const uint32_t* doff = fam == 0 ? A.kdoff : fam == 1 ? A.ndoff : A.mdoff;
+      const uint32_t d0 = doff[b0];
+      const uint32_t dl = doff[b0 + nb - 1] + out[b0 + nb - 1];
+      // padding lanes repeat the group end so the search never selects them
+      L.doff[lane] = in ? doff[b] - d0 : dl - d0;
+      L.sbase[lane] = base[b];
+      if (fam == 0) {
+        L.ndoff[lane] = A.ndoff[b];
+        L.mdoff[lane] = A.mdoff[b];
       }
-    }
-    for (uint32_t i = lane; i < nn; i += 64) {
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const uint32_t total = dl - d0;
+      for (uint32_t t = lane; t < total; t += 64) {
+        const int j = group_bucket(L.doff, t);
+        const uint32_t src = L.sbase[j] + (t - L.doff[j]), dst = d0 + t;
+        if (fam == 0) {
 #pragma unroll
-      for (int c = 0; c < kNodeCols; ++c) A.nd[c][ndo + i] = A.ns[c][ns + i];
-    }
-    for (uint32_t i = lane; i < mn; i += 64) {
+          for (int c = 0; c < kKeyOutCols; ++c) {
+            uint64_t v = A.ks[c][src];
+            if (c == O_CREF) {
+              const uint64_t cnt = v & 0xFFFFFF;
+              const uint32_t T = meta_tag(A.ks[O_META][src]);
+              const uint64_t begin = cnt ? (v >> 24) + (T == TAG_COUNTER ? L.ndoff[j] : L.mdoff[j]) : 0;
+              v = cref_pack(begin, cnt);
+            }
+            A.kd[c][dst] = v;
+          }
+        } else if (fam == 1) {
 #pragma unroll
-      for (int c = 0; c < kMemberCols; ++c) A.md[c][mdo + i] = A.ms[c][ms + i];
+          for (int c = 0; c < kNodeCols; ++c) A.nd[c][dst] = A.ns[c][src];
+        } else {
+#pragma unroll
+          for (int c = 0; c < kMemberCols; ++c) A.md[c][dst] = A.ms[c][src];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
   }
 }
@@ -137,9 +183,10 @@ struct Plan {
 };
 
 Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
-  // Wave-sized buckets: ~40 key rows and ~24 child rows (nodes + members) on average, so
-  // nearly every bucket fits one wave (64 lanes per family); the rest take the LDS tier.
-  const uint64_t want = std::max<uint64_t>({(K + 39) / 40, (N + M + 23) / 24, 1});
+  // Wave-sized buckets: ~40 key rows and ~40 child rows (nodes + members) on average.
+  // A wave holds 64 key rows (128 in the wide kernel) and 128 child rows, so only the
+  // far tail of the bucket-size distribution reaches the workgroup tier.
+  const uint64_t want = std::max<uint64_t>({(K + 39) / 40, (N + M + 39) / 40, 1});
   Plan p;
   if (want <= 1) return p;
   if (want <= 512) {
@@ -165,13 +212,16 @@ Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
   return p;
 }
 
-// Splits `n` rows of an NC-column family into plan.nb buckets (key-hash order).
-// Returns in `res` the columns holding the bucketed rows (one of in / A / B).
+// Splits `n` rows of an NC-column family into plan.nb buckets (key-hash order). Levels
+// 1..L-1 move the columns; the last level writes only `perm`, so bucket b's rows are
+// res[*][perm[base[b] .. base[b] + hist[b])]. Returns in `res` the columns holding the
+// rows (one of in / A / B) and in `spare` a free buffer of the same shape.
 template <int NC>
 cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const Plan& plan, int shift,
                             uint64_t* const* A, uint64_t* const* Bf, const Dir& d, uint64_t** res,
-                            uint64_t** spare, hipStream_t s) {
+                            uint64_t** spare, uint32_t* perm, hipStream_t s) {
   if (plan.levels == 0 || n == 0) {
+    if (n) iota_kernel<<<(uint32_t)std::min<uint64_t>((n + 255) / 256, 4096), 256, 0, s>>>(perm, n);
     set_dir_kernel<<<1, 1, 0, s>>>(d.base, d.hist, (uint32_t)n);
     if (plan.nb > 1) {  // n == 0 with buckets: every bucket empty
       CDB_HIP(hipMemsetAsync(d.base, 0, sizeof(uint32_t) * plan.nb, s), "memset");
@@ -187,6 +237,7 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const
   uint64_t* const* cur = in;
   uint64_t nprev = 1;
   for (int l = 0; l < plan.levels; ++l) {
+    const bool last = l + 1 == plan.levels;
     uint64_t* const* dst = (l % 2 == 0) ? A : Bf;
     const uint64_t ncur = nprev * plan.d[l];
     CDB_HIP(hipMemsetAsync(d.hist, 0, ncur * sizeof(uint32_t), s), "memset hist");
@@ -197,9 +248,15 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const
       ci.c[c] = cur[c];
       co.c[c] = dst[c];
     }
-    part_scatter_kernel<NC><<<tiles, kPartThreads, 0, s>>>(ci, co, n, nprev, plan.d[l], shift, d.cursor);
-    CDB_HIP(hipGetLastError(), "partition");
-    cur = dst;
+    if (last) {
+      part_scatter_kernel<1, true><<<tiles, kPartThreads, 0, s>>>(ColSet<1>{{ci.c[0]}}, ColSet<1>{{nullptr}}, n,
+                                                                  nprev, plan.d[l], shift, d.cursor, perm);
+      CDB_HIP(hipGetLastError(), "partition (index level)");
+    } else {
+      part_scatter_kernel<NC><<<tiles, kPartThreads, 0, s>>>(ci, co, n, nprev, plan.d[l], shift, d.cursor);
+      CDB_HIP(hipGetLastError(), "partition");
+      cur = dst;
+    }
     nprev = ncur;
   }
   uint64_t* const* other = (cur == A) ? Bf : A;
@@ -248,8 +305,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   Dir dnd{dir + 5 * dn, dir + 6 * dn, dir + 7 * dn, dir + 8 * dn, dir + 9 * dn};
   Dir dm{dir + 10 * dn, dir + 11 * dn, dir + 12 * dn, dir + 13 * dn, dir + 14 * dn};
   // misc: stats[8] u64 | last_bad u64 | totals[3] u64 | hot_count u32 | big_count u32 |
-  //       hot_list[nb] u32 | big_list[nb] u32
-  uint8_t* misc = (uint8_t*)ws_get(ctx, WS_MISC, 128 + 2 * nb * sizeof(uint32_t), &st);
+  //       wide_count u32 | hot_list[nb] u32 | big_list[nb] u32 | wide_list[nb] u32
+  uint8_t* misc = (uint8_t*)ws_get(ctx, WS_MISC, 128 + 3 * nb * sizeof(uint32_t), &st);
   if (!misc) return st;
   unsigned long long* d_stats = (unsigned long long*)misc;
   unsigned long long* d_last_bad = (unsigned long long*)(misc + 64);
@@ -258,6 +315,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   uint32_t* d_big_count = (uint32_t*)(misc + 100);
   uint32_t* d_hot_list = (uint32_t*)(misc + 128);
   uint32_t* d_big_list = d_hot_list + nb;
+  uint32_t* d_wide_count = (uint32_t*)(misc + 104);
+  uint32_t* d_wide_list = d_big_list + nb;
   CDB_HIP(hipMemsetAsync(misc, 0, 128, s), "memset misc");
 
   CDB_HIP(hipEventRecord(ctx->ev0, s), "event");
@@ -271,10 +330,13 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     nin[c] = in->nodes.col[c];
     min_[c] = in->members.col[c];
   }
-  CDB_TRY(partition_family<kKeyCols>(ctx, kin, K, plan, shift, KA, KB, dk, kb, ksp, s));
+  uint32_t* perm = (uint32_t*)ws_get(ctx, WS_PERM, (K + N + M + 3) * sizeof(uint32_t), &st);
+  if (!perm) return st;
+  uint32_t *kperm = perm, *nperm = perm + K, *mperm = perm + K + N;
+  CDB_TRY(partition_family<kKeyCols>(ctx, kin, K, plan, shift, KA, KB, dk, kb, ksp, kperm, s));
   // keys need 8 output columns: the spare buffer always has 8
-  CDB_TRY(partition_family<kNodeCols>(ctx, nin, N, plan, shift, NA, NB, dnd, ndb, nsp, s));
-  CDB_TRY(partition_family<kMemberCols>(ctx, min_, M, plan, shift, MA, MBf, dm, mbb, msp, s));
+  CDB_TRY(partition_family<kNodeCols>(ctx, nin, N, plan, shift, NA, NB, dnd, ndb, nsp, nperm, s));
+  CDB_TRY(partition_family<kMemberCols>(ctx, min_, M, plan, shift, MA, MBf, dm, mbb, msp, mperm, s));
   {  // sparse key outputs (8 columns) go to whichever ping-pong buffer is free
     uint64_t* const* free_k = (kb[0] == KA[0]) ? KB : KA;
     for (int c = 0; c < 8; ++c) ksp[c] = free_k[c];
@@ -298,6 +360,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     A.mo[c] = msp[c];
   }
   for (int c = 0; c < kKeyOutCols; ++c) A.ko[c] = ksp[c];
+  A.kp = kperm; A.np = nperm; A.mp = mperm;
   A.kbase = dk.base; A.kcnt = dk.hist;
   A.nbase = dnd.base; A.ncnt = dnd.hist;
   A.mbase = dm.base; A.mcnt = dm.hist;
@@ -317,16 +380,21 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   WA.nbuckets = (uint32_t)nb;
   WA.big_list = d_big_list;
   WA.big_count = d_big_count;
+  WA.wide_list = d_wide_list;
+  WA.wide_count = d_wide_count;
   bucket_wave_kernel<<<(nb + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, 0, s>>>(WA);
   CDB_HIP(hipGetLastError(), "bucket_wave_kernel");
+  bucket_wide_kernel<<<std::min<uint64_t>((nb + kWavesPerWG - 1) / kWavesPerWG, 1024), kWavesPerWG * 64, 0, s>>>(WA);
+  CDB_HIP(hipGetLastError(), "bucket_wide_kernel");
   bucket_mid_kernel<<<std::min<uint64_t>(nb, 2048), kBktThreads, 0, s>>>(A, d_big_list, d_big_count);
   CDB_HIP(hipGetLastError(), "bucket_mid_kernel");
   CDB_HIP(hipEventRecord(ctx->ev_bucket, s), "event");
 
   // ---- 4. over-capacity buckets (same algorithm, global scratch)
-  uint32_t hot = 0;
-  CDB_HIP(hipMemcpyAsync(&hot, d_hot_count, sizeof hot, hipMemcpyDeviceToHost, s), "d2h");
+  uint32_t counts[3] = {0, 0, 0};  // hot, big (mid tier), wide
+  CDB_HIP(hipMemcpyAsync(counts, d_hot_count, sizeof counts, hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipStreamSynchronize(s), "sync");
+  const uint32_t hot = counts[0];
   if (hot) {
     std::vector<uint32_t> ids(hot), kc(hot), nc(hot), mc(hot);
     CDB_HIP(hipMemcpy(ids.data(), d_hot_list, hot * sizeof(uint32_t), hipMemcpyDeviceToHost), "d2h");
@@ -372,7 +440,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   C.kbase = dk.base; C.nbase = dnd.base; C.mbase = dm.base;
   C.kout = dk.out; C.nout = dnd.out; C.mout = dm.out;
   C.kdoff = dk.doff; C.ndoff = dnd.doff; C.mdoff = dm.doff;
-  compact_kernel<<<(uint32_t)std::min<uint64_t>((nb + 3) / 4, 65536), 256, 0, s>>>(C, (uint32_t)nb);
+  compact_kernel<<<(uint32_t)std::min<uint64_t>((nb + 64 * kCompactWaves - 1) / (64 * kCompactWaves), 16384),
+                   64 * kCompactWaves, 0, s>>>(C, (uint32_t)nb);
   CDB_HIP(hipGetLastError(), "compact_kernel");
   CDB_HIP(hipEventRecord(ctx->ev1, s), "event");
 
@@ -399,6 +468,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     stats->duplicate_rows = hs[ST_DUP_ROWS];
     stats->orphan_children = hs[ST_ORPHANS];
     stats->hot_buckets = hot;
+    stats->wide_buckets = counts[2];
+    stats->mid_buckets = counts[1];
     float ms = 0;
     hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
     stats->device_ms = ms;

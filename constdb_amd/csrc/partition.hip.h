@@ -5,7 +5,9 @@
 // key hash pkh for children), so a key and all its children share a bucket. NB is a
 // product of per-level digit counts <= 512: each level is one streaming pass (histogram pass over col 0,
 // then a scatter pass that stages every column through LDS so that writes leave the CU
-// as contiguous per-digit runs). Rows inside a bucket end up in arbitrary order; the
+// as contiguous per-digit runs). The last level moves only a u32 row index (a
+// permutation): its segments are ~1000 rows, so the bucket kernels' gathers through the
+// permutation hit rows that are L2/MALL resident instead of re-streaming every column. Rows inside a bucket end up in arbitrary order; the
 // bucket kernel sorts them by full identity, so results stay deterministic.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -63,11 +65,13 @@ __global__ void __launch_bounds__(kPartThreads) part_hist_kernel(const uint64_t*
 // ---------------------------------------------------------------- scatter
 // Moves every column of every row to out[cursor[gb]++] (per-tile ranges reserved with one
 // global atomic per touched bucket). Columns are staged through LDS in bucket order so
-// that each wave's stores are contiguous runs.
-template <int NC>
+// that each wave's stores are contiguous runs. IDX: index-only final level — writes the
+// u32 row index (to perm) instead of moving the NC columns.
+template <int NC, bool IDX = false>
 __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> in, ColSet<NC> out, uint64_t n,
                                                                     uint64_t nprev, uint32_t d, int shift,
-                                                                    uint32_t* __restrict__ cursor) {
+                                                                    uint32_t* __restrict__ cursor,
+                                                                    uint32_t* __restrict__ perm = nullptr) {
   __shared__ uint32_t cnt[kPartLocalMax];   // per local bucket: count, then scan
   __shared__ uint32_t gbase[kPartLocalMax]; // reserved global start per local bucket
   __shared__ uint16_t slot_lb[kPartTile];   // local bucket of each staged slot
@@ -86,8 +90,12 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
     for (int r = threadIdx.x; r < rows; r += kPartThreads) {
       const uint64_t gb = bucket_of_n(in.c[0][tile0 + r] << shift, ncur);
       const uint32_t d = atomicAdd(&cursor[gb], 1u);
+      if (IDX) {
+        perm[d] = (uint32_t)(tile0 + r);
+      } else {
 #pragma unroll
-      for (int c = 0; c < NC; ++c) out.c[c][d] = in.c[c][tile0 + r];
+        for (int c = 0; c < NC; ++c) out.c[c][d] = in.c[c][tile0 + r];
+      }
     }
     return;
   }
@@ -142,6 +150,20 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
     }
   }
   __syncthreads();
+  if (IDX) {
+    uint32_t* st32 = reinterpret_cast<uint32_t*>(stage);
+#pragma unroll
+    for (int k = 0; k < kPartRowsPerThread; ++k) {
+      const int r = threadIdx.x + k * kPartThreads;
+      if (r < rows) st32[slot[k]] = (uint32_t)(tile0 + r);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < rows; j += kPartThreads) {
+      const int b = slot_lb[j];
+      perm[gbase[b] + (j - cnt[b])] = st32[j];
+    }
+    return;
+  }
 #pragma unroll 1
   for (int c = 0; c < NC; ++c) {
 #pragma unroll

@@ -109,7 +109,8 @@ enum {
 typedef struct cdb_merge_opts {
   uint32_t flags;
   uint32_t force_tier;   /* testing only: 0 = automatic; 1 = every bucket through the LDS
-                            workgroup tier; 2 = every bucket through the global-scratch tier */
+                            workgroup tier; 2 = every bucket through the global-scratch tier;
+                            3 = every bucket through the wide (128-key-row) wave kernel */
   uint64_t gc_watermark; /* ReplicaManager::min_uuid (replica/replica.rs:87-89) */
   uint32_t key_shift;    /* multi-GPU: the top `key_shift` bits of every key hash are the owner
                             rank (all equal on one device), so local buckets use the bits below */
@@ -126,6 +127,8 @@ typedef struct cdb_merge_stats {
   uint64_t duplicate_rows;   /* same key twice in one snapshot (never written by db.rs:122-136) */
   uint64_t orphan_children;  /* child rows whose key row is missing (malformed input) */
   uint64_t hot_buckets;      /* buckets handled by the over-capacity path */
+  uint64_t wide_buckets;     /* buckets handled by the wide wave kernel (65..128 key rows) */
+  uint64_t mid_buckets;      /* buckets handled by the LDS workgroup tier */
   double   device_ms;        /* device time of the whole merge pipeline (HIP events) */
   double   partition_ms;     /* bucket partition of the three row families */
   double   bucket_ms;        /* fused bucket-merge kernel (the dominant kernel) */

@@ -129,10 +129,11 @@ def test_random_small(db, seed):
     _check(db, snaps)
 
 
-@pytest.mark.parametrize("tier", [1, 2])
+@pytest.mark.parametrize("tier", [1, 2, 3])
 @pytest.mark.parametrize("seed", range(12))
 def test_random_forced_tier(db, seed, tier):
-    """The LDS workgroup tier and the global-scratch tier on every bucket."""
+    """The LDS workgroup tier, the global-scratch tier and the wide wave kernel on every
+    bucket."""
     snaps = gen_replicas(900 + seed, n_replicas=1 + seed % 5, n_keys=40, p_conflict=0.1, p_side=0.3)
     _check(db, snaps, gc=(seed % 7) if seed % 2 else None, members=bool(seed % 4 == 1), tier=tier)
 
@@ -167,6 +168,18 @@ def test_generator_medium(db, universe, replicas, seed):
     cfg = cdb.gen_config(seed=seed, universe=universe, n_replicas=replicas, replica_hi=replicas)
     snaps = [cdb.gen_snapshot(cfg, r) for r in range(replicas)]
     _check(db, snaps)
+
+
+def test_wave_tiers_natural(db):
+    """Bucket sizes vary: some buckets exceed 64 key rows (wide wave kernel) or 64 child rows
+    (two child rows per lane); all stay exact."""
+    cfg = cdb.gen_config(seed=21, universe=120000, n_replicas=8, replica_hi=8, mean_members=6)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(8)]
+    m = _check(db, snaps)
+    assert m.stats.wide_buckets > 0
+    assert m.stats.mid_buckets + m.stats.hot_buckets < m.stats.wide_buckets
+    m3 = _check(db, snaps, tier=3)
+    assert m3.stats.wide_buckets > m.stats.wide_buckets
 
 
 def test_generator_set_heavy_gc(db):
