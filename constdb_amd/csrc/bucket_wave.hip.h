@@ -1,8 +1,7 @@
 // Wave-per-bucket merge kernels (gfx950, wave64) — the hot path of the merge.
 //
 // One 64-lane wave owns one bucket and never synchronises with another wave. Rows sit in
-// registers, E per lane (row i = lane + 64 e), so a bucket holds up to 64*KE key rows and
-// 128 child rows:
+// registers, E per lane (row i = lane + 64 e):
 //   1. keys: each lane loads its rows (coalesced); a register bitonic network over
 //      __shfl_xor sorts (kh, family|pos|src|idx); equal kh with different kf (a 64-bit
 //      collision) hands the bucket to the exact-comparator workgroup tier before anything
@@ -20,9 +19,10 @@
 //      LWWHash::set's later-wins-ties rule (lwwhash.rs:87-107);
 //   4. counter sums (cal_sum, type_counter.rs:89-91) and child ranges; outputs are
 //      written by the tail slots (ballot + mbcnt ranks).
-// bucket_wave_kernel (KE = 1) runs every bucket; one with more than 64 key rows goes to
-// bucket_wide_kernel (KE = 2, 128 key rows, fewer waves per CU for its larger LDS), and
-// anything beyond that, collisions and forced tiers go to the workgroup tier (bucket.hip.h).
+// bucket_wave_kernel (KE = 1: 64 key rows, 128 child rows) runs every bucket; one over that
+// goes to bucket_wide_kernel (KE = 2: 128 key rows, 256 child rows; fewer waves per CU for
+// its larger LDS), and anything beyond that, collisions and forced tiers go to the
+// workgroup tier (bucket.hip.h).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -33,17 +33,18 @@
 namespace cdb {
 
 constexpr int kWavesPerWG = 4;
-constexpr int kChildCap = 128;  // children: up to two rows per lane
 
+// Per-wave LDS. KE = key rows per lane (1 or 2); child rows per lane: 2 (KE = 1) or 4.
 template <int KE>
 struct WaveLds {
-  static constexpr int KC = 64 * KE;
+  static constexpr int KC = 64 * KE;                // key-row capacity
+  static constexpr int CC = KE == 1 ? 128 : 256;    // child-row capacity
   uint64_t okh[KC], okf[KC], ovm[KC], osum[KC];
   uint32_t otp[KC], ocnt[KC], ocb[KC];
-  uint32_t sidx[KC > kChildCap ? KC : kChildCap];
+  uint32_t sidx[KC > CC ? KC : CC];
   union {  // per-row staging, gathered through sidx after each sort
-    uint64_t col[5][KC];          // key rows (KC_*)
-    uint64_t ccol[4][kChildCap];  // child rows (CC_*)
+    uint64_t col[5][KC];   // key rows (KC_*)
+    uint64_t ccol[4][CC];  // child rows (CC_*)
   };
 };
 
@@ -68,8 +69,9 @@ __device__ __forceinline__ bool lt2(uint64_t a0, uint64_t a1, uint64_t b0, uint6
 }
 
 // Ascending bitonic sort of 64*E two-word elements, element i = (lane, e), i = lane + 64 e.
-// Rows carry their staging index in the low bits of w1, so a compare-exchange moves two
-// words. Sentinels are all-ones.
+// Stages with j >= 64 compare two elements of the same lane (no data movement); the rest
+// exchange over __shfl_xor. Rows carry their staging index in the low bits of w1, so a
+// compare-exchange moves two words. Sentinels are all-ones.
 template <int E>
 __device__ __forceinline__ void wave_bitonic(uint64_t (&w0)[E], uint64_t (&w1)[E]) {
   const int lane = threadIdx.x & 63;
@@ -77,13 +79,20 @@ __device__ __forceinline__ void wave_bitonic(uint64_t (&w0)[E], uint64_t (&w1)[E
   for (int kk = 2; kk <= 64 * E; kk <<= 1) {
 #pragma unroll
     for (int j = kk >> 1; j > 0; j >>= 1) {
-      if (j == 64) {  // partner is the lane's other element; kk == 128 sorts ascending
-        const bool sw = lt2(w0[E - 1], w1[E - 1], w0[0], w1[0]);
-        const uint64_t a0 = w0[0], a1 = w1[0];
-        w0[0] = sw ? w0[E - 1] : w0[0];
-        w1[0] = sw ? w1[E - 1] : w1[0];
-        w0[E - 1] = sw ? a0 : w0[E - 1];
-        w1[E - 1] = sw ? a1 : w1[E - 1];
+      if (j >= 64) {
+        const int je = j / 64;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          if (e & je) continue;
+          const int f = e | je;
+          const bool up = ((64 * e) & kk) == 0;  // lower element keeps the min when ascending
+          const bool sw = up ? lt2(w0[f], w1[f], w0[e], w1[e]) : lt2(w0[e], w1[e], w0[f], w1[f]);
+          const uint64_t a0 = w0[e], a1 = w1[e];
+          w0[e] = sw ? w0[f] : w0[e];
+          w1[e] = sw ? w1[f] : w1[e];
+          w0[f] = sw ? a0 : w0[f];
+          w1[f] = sw ? a1 : w1[f];
+        }
       } else {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
@@ -103,12 +112,16 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {  // set bits of m
 }
 __device__ __forceinline__ uint64_t upto(int lane) { return lane == 63 ? ~0ull : ((2ull << lane) - 1); }
 
-// Position of the segment head for slot (lane, e): the highest head bit at or below it.
+// Position of the segment head for slot (lane, e): the highest head bit at or below it
+// (the slot itself is live, so position 0 is a head and the search always succeeds).
 template <int E>
 __device__ __forceinline__ int seg_head(const uint64_t (&H)[E], int e, int lane) {
   const uint64_t m = H[e] & upto(lane);
-  if (E == 1 || m) return 64 * e + 63 - __clzll(m);
-  return 64 * (e - 1) + 63 - __clzll(H[e > 0 ? e - 1 : 0]);  // E == 2: head in the first half
+  if (m) return 64 * e + 63 - __clzll(m);
+#pragma unroll
+  for (int f = E - 1; f >= 0; --f)
+    if (f < e && H[f]) return 64 * f + 63 - __clzll(H[f]);
+  return 0;
 }
 
 __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x) {
@@ -120,7 +133,7 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x)
 struct WaveArgs {
   BucketArgs A;
   uint32_t nbuckets;
-  uint32_t* wide_list;  // buckets with 64 < K <= 128 (bucket_wide_kernel)
+  uint32_t* wide_list;  // buckets over the main kernel's capacity (bucket_wide_kernel)
   uint32_t* wide_count;
   uint32_t* big_list;   // buckets for the workgroup tier
   uint32_t* big_count;
@@ -134,7 +147,7 @@ struct ChildOut {
   unsigned long long orph, gcm;  // per-lane counts
 };
 
-// Stages 3-4 for up to 64*E child rows (nodes in [0, N), members in [N, N+M)). Returns
+// Stages 3-4 for up to 64*E child rows (nodes in [0, N), members in [N, N+M)); E <= CC/64. Returns
 // false on a 64-bit id-hash collision (the bucket then goes to the exact tier; nothing has
 // been written).
 template <int E, int KE>
@@ -305,11 +318,12 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   auto push = [&](uint32_t* list, uint32_t* count) {
     if (lane == 0) list[atomicAdd(count, 1u)] = b;
   };
-  if (A.force_tier == 1 || A.force_tier == 2 || N + M > kChildCap || K > 128) {
+  constexpr uint32_t KC = WaveLds<KE>::KC, CC = WaveLds<KE>::CC;
+  if (A.force_tier == 1 || A.force_tier == 2 || N + M > WaveLds<2>::CC || K > WaveLds<2>::KC) {
     push(W.big_list, W.big_count);
     return;
   }
-  if (K > 64 * KE || (KE == 1 && A.force_tier == 3)) {
+  if (K > KC || N + M > CC || (KE == 1 && A.force_tier == 3)) {
     push(spill_list, spill_count);
     return;
   }
@@ -472,8 +486,13 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
 
   // ------------------------------------------------------------ 3-4. children
   ChildOut co;
-  const bool ok = (N + M <= 64) ? children_stage<1, KE>(A, L, lane, N, M, nb0, mb0, kout, co)
-                                : children_stage<2, KE>(A, L, lane, N, M, nb0, mb0, kout, co);
+  bool ok;
+  if (N + M <= 64)
+    ok = children_stage<1, KE>(A, L, lane, N, M, nb0, mb0, kout, co);
+  else if (KE == 1 || N + M <= 128)
+    ok = children_stage<2, KE>(A, L, lane, N, M, nb0, mb0, kout, co);
+  else
+    ok = children_stage<(KE == 1 ? 2 : 4), KE>(A, L, lane, N, M, nb0, mb0, kout, co);
   if (!ok) {  // id-hash collision: exact tier
     push(W.big_list, W.big_count);
     return;
@@ -529,7 +548,7 @@ __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_kernel(WaveArgs 
   wave_bucket<1>(W, lds_all[wv], b, lane, W.wide_list, W.wide_count);
 }
 
-// Buckets of 65..128 key rows (listed by bucket_wave_kernel), persistent over the list.
+// Buckets over bucket_wave_kernel's capacity (listed by it), persistent over the list.
 __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_kernel(WaveArgs W) {
   __shared__ WaveLds<2> lds_all[kWavesPerWG];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;

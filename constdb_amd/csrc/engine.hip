@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -189,23 +190,28 @@ Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
   const uint64_t want = std::max<uint64_t>({(K + 39) / 40, (N + M + 39) / 40, 1});
   Plan p;
   if (want <= 1) return p;
+  // The last level moves only a row index, so it takes a large fan-out (segments of
+  // ~d_last buckets, a few hundred KB, stay cache-resident for the bucket kernels' gathers)
+  // and the column-moving levels get small fan-outs (long contiguous write runs).
+  uint32_t dlast = 256;
+  if (const char* e = std::getenv("CDB_PLAN_DLAST")) dlast = (uint32_t)std::max(2, std::min(512, std::atoi(e)));
   if (want <= 512) {
     p.levels = 1;
     p.d[0] = (uint32_t)want;
-  } else if (want <= 512ull * 512) {
-    p.levels = 2;
-    uint32_t a = 1;
-    while ((uint64_t)a * a < want) ++a;
-    p.d[0] = std::min<uint32_t>(a, 512);
-    p.d[1] = (uint32_t)((want + p.d[0] - 1) / p.d[0]);
   } else {
-    p.levels = 3;
-    p.d[0] = 512;
-    const uint64_t rest = (want + 511) / 512;
-    uint32_t a = 1;
-    while ((uint64_t)a * a < rest) ++a;
-    p.d[1] = std::min<uint32_t>(a, 512);
-    p.d[2] = (uint32_t)std::min<uint64_t>((rest + p.d[1] - 1) / p.d[1], 512);
+    const uint64_t rest = (want + dlast - 1) / dlast;
+    if (rest <= 512) {
+      p.levels = 2;
+      p.d[0] = (uint32_t)rest;
+      p.d[1] = dlast;
+    } else {
+      p.levels = 3;
+      uint32_t a = 1;
+      while ((uint64_t)a * a < rest) ++a;
+      p.d[0] = std::min<uint32_t>(a, 512);
+      p.d[1] = (uint32_t)std::min<uint64_t>((rest + p.d[0] - 1) / p.d[0], 512);
+      p.d[2] = (uint32_t)std::min<uint64_t>((want + (uint64_t)p.d[0] * p.d[1] - 1) / ((uint64_t)p.d[0] * p.d[1]), 512);
+    }
   }
   p.nb = 1;
   for (int l = 0; l < p.levels; ++l) p.nb *= p.d[l];

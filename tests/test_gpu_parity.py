@@ -182,6 +182,17 @@ def test_wave_tiers_natural(db):
     assert m3.stats.wide_buckets > m.stats.wide_buckets
 
 
+@pytest.mark.parametrize("tier", [0, 3])
+def test_wide_children(db, tier):
+    """Set/dict keys with up to 8 x 24 member rows: buckets of 129..256 child rows take the
+    wide kernel's four-rows-per-lane path."""
+    cfg = cdb.gen_config(seed=33, universe=30000, n_replicas=8, replica_hi=8, mix_bytes=10, mix_counter=10,
+                         mix_set=40, mix_dict=40, mean_members=12, member_universe=24, del_permille=300)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(8)]
+    m = _check(db, snaps, tier=tier)
+    assert m.stats.wide_buckets > 0
+
+
 def test_generator_set_heavy_gc(db):
     """C3-shaped: set/dict heavy with tombstones, GC at the median time."""
     cfg = cdb.gen_config(seed=3, universe=5000, n_replicas=4, replica_hi=4, mix_bytes=0, mix_counter=0,
