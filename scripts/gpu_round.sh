@@ -1,8 +1,18 @@
+#!/bin/bash
+# One GPU verification round: parity tests, full bench (with CPU baseline), kernel-trace
+# stats of the same bench command, FETCH/WRITE PMC passes for the HBM traffic figure.
+# Usage (from gpurun): TAG=r1e bash scripts/gpu_round.sh
 set -o pipefail
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_${TAG:-r1d}.log 2>&1 && \
-timeout -k 10 300 python bench.py --universe-per-gpu 4000000 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_small_${TAG:-r1d}.json 2> gpurun_out/bench_small_${TAG:-r1d}.err && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG:-r1d} -o run -- python bench.py --universe-per-gpu 4000000 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_${TAG:-r1d}.log 2>&1 && \
-timeout -k 10 400 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_full_${TAG:-r1d}.json 2> gpurun_out/bench_full_${TAG:-r1d}.err
-echo EXIT $?
+T=${TAG:-r1e}
+O=gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_$T.log 2>&1 || { echo "pytest failed"; exit 1; }
+timeout -k 10 400 python bench.py --steps 5 --warmup 2 > $O/bench_full_$T.json 2> $O/bench_full_$T.err || { echo "bench failed"; exit 2; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$T -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_$T.log 2>&1 || { echo "prof failed"; exit 3; }
+if [ -z "$NO_PMC" ]; then
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 200 rocprofv3 --pmc $c --kernel-include-regex "${KREGEX:-bucket_wave|part_scatter|compact}" --output-format csv -d $O/pmc_${T}_$c -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_${T}_$c.log 2>&1 || { echo "pmc $c failed"; exit 4; }
+  done
+fi
+echo "round ok"
