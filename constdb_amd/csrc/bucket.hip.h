@@ -35,8 +35,14 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 enum Stat {
   ST_TYPE_CONFLICTS = 0, ST_DICT_MERGES, ST_DELETES_GCED, ST_MEMBERS_GCED, ST_DUP_ROWS,
-  ST_ORPHANS, ST_HOT, ST_COUNT
+  ST_ORPHANS, ST_HOT, ST_WIDE, ST_COUNT
 };
+// Statistics are counted into kStatShards shards of kStatStride u64 (one 128-B line each):
+// millions of waves adding to ONE word serialise at its memory-side atomic unit.
+constexpr int kStatShards = 512, kStatStride = 16;
+__device__ __forceinline__ unsigned long long* stat_shard(unsigned long long* stats) {
+  return stats + (size_t)(blockIdx.x & (kStatShards - 1)) * kStatStride;
+}
 enum : uint32_t { F_DICT_STRICT = 1, F_GC_DELETES = 2, F_GC_MEMBERS = 4 };
 
 struct BucketArgs {
@@ -443,7 +449,7 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
   }
   __syncthreads();
   for (int i = threadIdx.x; i < ST_COUNT; i += blockDim.x)
-    if (S.st[i]) atomicAdd(&A.stats[i], S.st[i]);
+    if (S.st[i]) atomicAdd(&stat_shard(A.stats)[i], S.st[i]);
 }
 
 // LDS carve for the fast path.

@@ -1,28 +1,32 @@
 // Wave-per-bucket merge kernels (gfx950, wave64) — the hot path of the merge.
 //
-// One 64-lane wave owns one bucket and never synchronises with another wave. Rows sit in
-// registers, E per lane (row i = lane + 64 e):
-//   1. keys: each lane loads its rows (coalesced); a register bitonic network over
-//      __shfl_xor sorts (kh, family|pos|src|idx); equal kh with different kf (a 64-bit
-//      collision) hands the bucket to the exact-comparator workgroup tier before anything
-//      is written;
+// One 64-lane wave owns one bucket and never synchronises with another wave.
+//   0. every global load of the bucket is issued up front: the row indices (the final
+//      partition level is index-only), then all key columns and all child columns, so a
+//      bucket costs one dependent pair of round trips instead of one pair per family;
+//   1. keys: each row gets ONE 64-bit sort word (kh low 44 bits | family | pos | slot); a
+//      lane's rank is the number of smaller words (a K-step loop over LDS broadcasts — for
+//      ~40 rows cheaper than a bitonic network and proportional to the bucket, not to 64),
+//      and rows are scattered to their rank. Words equal in the kh part but different in
+//      (kh, kf) (a 2^-44 event per pair) and two rows of one (key, family, pos) (duplicate
+//      keys in one snapshot) hand the bucket to the exact-comparator workgroup tier before
+//      anything is written, so the order (kh, family, pos, src) is exact here;
 //   2. key folds: the tail slot of each (key, family) segment replays the reference's
-//      sequential fold over its segment (<= R rows, read from LDS in sorted order):
+//      sequential fold over its segment (<= R rows, already in sorted order in LDS):
 //        data     DB::merge_entry / Object::merge   (db.rs:31-43, object.rs:63-83)
 //        expires / deletes: last (pos, src) wins   (db.rs:68-76), DB::gc (db.rs:82-95);
 //   3. children: counter nodes and set/dict members share the slots (a key has one type);
 //      each finds its key by binary search over the wave's sorted output keys (LDS), is
 //      kept if its element has the key's head type (object.rs:80) and, for members of a
 //      non-head position, only if it is an add (SetIter/DictIter, lwwhash.rs:319-323);
-//      sorted by (key rank, id hash, pos|src), folded per (key, node) with
-//      Counter::merge's head-t rule (type_counter.rs:59-87) or per (key, member) with
-//      LWWHash::set's later-wins-ties rule (lwwhash.rs:87-107);
+//      ranked by one word (key rank | id hash low 42 bits | pos | slot), folded per
+//      (key, node) with Counter::merge's head-t rule (type_counter.rs:59-87) or per
+//      (key, member) with LWWHash::set's later-wins-ties rule (lwwhash.rs:87-107);
 //   4. counter sums (cal_sum, type_counter.rs:89-91) and child ranges; outputs are
 //      written by the tail slots (ballot + mbcnt ranks).
 // bucket_wave_kernel (KE = 1: 64 key rows, 128 child rows) runs every bucket; one over that
-// goes to bucket_wide_kernel (KE = 2: 128 key rows, 256 child rows; fewer waves per CU for
-// its larger LDS), and anything beyond that, collisions and forced tiers go to the
-// workgroup tier (bucket.hip.h).
+// goes to bucket_wide_kernel (KE = 2: 128 key rows, 256 child rows), and anything beyond
+// that, collisions, duplicates and forced tiers go to the workgroup tier (bucket.hip.h).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -33,78 +37,27 @@
 namespace cdb {
 
 constexpr int kWavesPerWG = 4;
+constexpr uint64_t kM44 = (1ull << 44) - 1, kM42 = (1ull << 42) - 1;
 
-// Per-wave LDS. KE = key rows per lane (1 or 2); child rows per lane: 2 (KE = 1) or 4.
+// Per-wave LDS. KE = key rows per lane (1 or 2); child rows per lane CE = 2 KE.
 template <int KE>
 struct WaveLds {
-  static constexpr int KC = 64 * KE;                // key-row capacity
-  static constexpr int CC = KE == 1 ? 128 : 256;    // child-row capacity
-  uint64_t okh[KC], okf[KC], ovm[KC], osum[KC];
+  static constexpr int KC = 64 * KE;       // key-row capacity
+  static constexpr int CC = 128 * KE;      // child-row capacity
+  uint64_t okh[KC], okf[KC], ovm[KC], osum[KC];  // output keys, sorted
   uint32_t otp[KC], ocnt[KC], ocb[KC];
-  uint32_t sidx[KC > CC ? KC : CC];
-  union {  // per-row staging, gathered through sidx after each sort
-    uint64_t col[5][KC];   // key rows (KC_*)
-    uint64_t ccol[4][CC];  // child rows (CC_*)
+  uint64_t sw[CC + 2];                     // sort words (keys, then children), sorted in place
+  union {                                  // rows in sorted order
+    uint64_t col[7][KC];                   // key rows: KS_*
+    uint64_t ccol[4][CC];                  // child rows: CS_*
   };
 };
+enum { KS_KH = 0, KS_KF, KS_CT, KS_UT, KS_DT, KS_AUX, KS_META };
+enum { CS_ID1 = 0, CS_C2, CS_T, CS_META };  // C2 = node value | member id2
 
 __device__ __forceinline__ void wave_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_wave_barrier();
-}
-
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
-  return (uint64_t)__shfl_xor((unsigned long long)v, m, 64);
-}
-__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
-  return (uint64_t)__shfl_up((unsigned long long)v, d, 64);
-}
-__device__ __forceinline__ uint64_t bcast63(uint64_t v) {
-  return (uint64_t)__shfl((unsigned long long)v, 63, 64);
-}
-
-// Branch-free lexicographic (a0, a1) < (b0, b1).
-__device__ __forceinline__ bool lt2(uint64_t a0, uint64_t a1, uint64_t b0, uint64_t b1) {
-  return (a0 < b0) | ((a0 == b0) & (a1 < b1));
-}
-
-// Ascending bitonic sort of 64*E two-word elements, element i = (lane, e), i = lane + 64 e.
-// Stages with j >= 64 compare two elements of the same lane (no data movement); the rest
-// exchange over __shfl_xor. Rows carry their staging index in the low bits of w1, so a
-// compare-exchange moves two words. Sentinels are all-ones.
-template <int E>
-__device__ __forceinline__ void wave_bitonic(uint64_t (&w0)[E], uint64_t (&w1)[E]) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int kk = 2; kk <= 64 * E; kk <<= 1) {
-#pragma unroll
-    for (int j = kk >> 1; j > 0; j >>= 1) {
-      if (j >= 64) {
-        const int je = j / 64;
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          if (e & je) continue;
-          const int f = e | je;
-          const bool up = ((64 * e) & kk) == 0;  // lower element keeps the min when ascending
-          const bool sw = up ? lt2(w0[f], w1[f], w0[e], w1[e]) : lt2(w0[e], w1[e], w0[f], w1[f]);
-          const uint64_t a0 = w0[e], a1 = w1[e];
-          w0[e] = sw ? w0[f] : w0[e];
-          w1[e] = sw ? w1[f] : w1[e];
-          w0[f] = sw ? a0 : w0[f];
-          w1[f] = sw ? a1 : w1[f];
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const uint64_t o0 = shfl_xor64(w0[e], j), o1 = shfl_xor64(w1[e], j);
-          const bool keep_min = ((lane & j) == 0) == (((lane + 64 * e) & kk) == 0);
-          const bool take = keep_min ? lt2(o0, o1, w0[e], w1[e]) : lt2(w0[e], w1[e], o0, o1);
-          w0[e] = take ? o0 : w0[e];
-          w1[e] = take ? o1 : w1[e];
-        }
-      }
-    }
-  }
 }
 
 __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {  // set bits of mask below my lane
@@ -130,255 +83,139 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x)
   return x;
 }
 
+// rk[e] = #{j < n : sw[j] < w[e]} for the first EA of my words; sw[n] must be ~0 when n is
+// odd (the loop reads pairs). Words are distinct, so ranks are a permutation of [0, n).
+template <int EA, int E>
+__device__ __forceinline__ void rank_count(const uint64_t* sw, uint32_t n, const uint64_t (&w)[E],
+                                           uint32_t (&rk)[E]) {
+#pragma unroll
+  for (int e = 0; e < EA; ++e) rk[e] = 0;
+  const uint32_t n2 = (n + 1) & ~1u;
+#pragma unroll 4
+  for (uint32_t j = 0; j < n2; j += 2) {
+    const uint64_t a = sw[j], b = sw[j + 1];  // same address in every lane: LDS broadcast
+#pragma unroll
+    for (int e = 0; e < EA; ++e) rk[e] += (uint32_t)(a < w[e]) + (uint32_t)(b < w[e]);
+  }
+}
+
 struct WaveArgs {
   BucketArgs A;
   uint32_t nbuckets;
-  uint32_t* wide_list;  // buckets over the main kernel's capacity (bucket_wide_kernel)
-  uint32_t* wide_count;
   uint32_t* big_list;   // buckets for the workgroup tier
   uint32_t* big_count;
 };
 
-enum { KC_CT = 0, KC_UT, KC_DT, KC_META, KC_KF };  // key staging columns
-enum { CC_ID1 = 0, CC_C2, CC_T, CC_META };        // child staging: C2 = node value | member id2
-
-struct ChildOut {
-  uint32_t nout, mout;
-  unsigned long long orph, gcm;  // per-lane counts
-};
-
-// Stages 3-4 for up to 64*E child rows (nodes in [0, N), members in [N, N+M)); E <= CC/64. Returns
-// false on a 64-bit id-hash collision (the bucket then goes to the exact tier; nothing has
-// been written).
-template <int E, int KE>
-__device__ __forceinline__ bool children_stage(const BucketArgs& A, WaveLds<KE>& L, int lane, uint32_t N,
-                                               uint32_t M, uint32_t nb0, uint32_t mb0, uint32_t kout,
-                                               ChildOut& co) {
-  uint64_t w0[E], w1[E];
-  unsigned long long orph = 0, gcm = 0;
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const uint32_t c = lane + 64 * e;
-    w0[e] = ~0ull;
-    w1[e] = ~0ull;
-    if (c < N + M) {
-      const bool isn = c < N;
-      const uint64_t* const* C = isn ? A.nd : A.mb;
-      const uint32_t row = isn ? A.np[nb0 + c] : A.mp[mb0 + (c - N)];
-      const uint64_t cpkh = C[C_PKH][row], cpkf = C[C_PKF][row];
-      const uint64_t id1 = C[C_ID1][row], m = C[C_META][row];
-      L.ccol[CC_ID1][c] = id1;
-      L.ccol[CC_C2][c] = C[C_ID2][row];
-      L.ccol[CC_T][c] = C[C_T][row];
-      L.ccol[CC_META][c] = m;
-      uint32_t lo = 0, hi = kout;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        const bool less = lt2(L.okh[mid], L.okf[mid], cpkh, cpkf);
-        lo = less ? mid + 1 : lo;
-        hi = less ? hi : mid;
-      }
-      uint32_t key = 255;
-      if (lo < kout && L.okh[lo] == cpkh && L.okf[lo] == cpkf && (L.otp[lo] & 0xFF) <= TAG_SET) {
-        const uint32_t KT = L.otp[lo] & 0xFF, khp = L.otp[lo] >> 8, p = meta_pos(m);
-        const bool type_ok = isn ? KT == TAG_COUNTER : (KT == TAG_SET || KT == TAG_DICT);
-        const bool elem_ok = (L.ovm[lo] >> p) & 1;
-        const bool cand = isn || meta_tag(m) == KIND_ADD || p == khp;  // remote dels ignored
-        if (type_ok && elem_ok && cand) key = lo;
-      } else {
-        ++orph;
-      }
-      if (key != 255) {
-        const uint64_t ih = isn ? mix64(id1) : id1;
-        w0[e] = ((uint64_t)key << 56) | (ih >> 8);
-        w1[e] = (meta_order(m) << 8) | c;
-      }
-    }
-  }
-  wave_bitonic<E>(w0, w1);
-  bool live[E], knode[E];
-  uint32_t idx[E], ckey[E];
-  uint64_t cid1[E], cid2[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    live[e] = (w0[e] >> 56) < 255u;  // valid rows sort before invalid and empty slots
-    idx[e] = (uint32_t)(w1[e] & 0xFF);
-    L.sidx[lane + 64 * e] = idx[e];
-  }
-  wave_sync();
-  bool coll = false;
-  uint64_t H[E], Lv[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    ckey[e] = (uint32_t)(w0[e] >> 56) & (WaveLds<KE>::KC - 1);
-    knode[e] = live[e] && (L.otp[ckey[e]] & 0xFF) == TAG_COUNTER;
-    cid1[e] = live[e] ? L.ccol[CC_ID1][idx[e]] : 0;
-    cid2[e] = (live[e] && !knode[e]) ? L.ccol[CC_C2][idx[e]] : 0;
-    uint64_t p0 = shfl_up64(w0[e], 1), pid1 = shfl_up64(cid1[e], 1), pid2 = shfl_up64(cid2[e], 1);
-    if (e > 0) {  // position 64e - 1 is lane 63's previous element
-      const int ep = e > 0 ? e - 1 : 0;
-      const uint64_t x0 = bcast63(w0[ep]), x1 = bcast63(cid1[ep]), x2 = bcast63(cid2[ep]);
-      p0 = lane == 0 ? x0 : p0;
-      pid1 = lane == 0 ? x1 : pid1;
-      pid2 = lane == 0 ? x2 : pid2;
-    }
-    const bool first = lane == 0 && e == 0;
-    coll |= live[e] && !first && p0 == w0[e] && (pid1 != cid1[e] || pid2 != cid2[e]);
-    H[e] = __ballot(live[e] && (first || p0 != w0[e]));
-    Lv[e] = __ballot(live[e]);
-  }
-  if (__ballot(coll)) return false;
-
-  uint64_t En[E], Em[E], c_v[E], c_t[E], c_m[E];
-  bool cemit[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int en = e + 1 < E ? e + 1 : e;
-    const bool nxt_head = lane < 63 ? ((H[e] >> (lane + 1)) & 1) : (e + 1 < E && (H[en] & 1));
-    const bool nxt_live = lane < 63 ? ((Lv[e] >> (lane + 1)) & 1) : (e + 1 < E && (Lv[en] & 1));
-    const bool ctail = live[e] && (nxt_head || !nxt_live);
-    const int pos = lane + 64 * e;
-    c_v[e] = c_t[e] = c_m[e] = 0;
-    cemit[e] = false;
-    if (ctail) {
-      const int hl = seg_head<E>(H, e, lane);
-      const uint32_t r0 = L.sidx[hl];
-      if (knode[e]) {  // Counter::merge per node (type_counter.rs:60-84): the head's t is kept
-        const uint64_t t0 = L.ccol[CC_T][r0];
-        uint64_t v = L.ccol[CC_C2][r0];
-        for (int q = hl + 1; q <= pos; ++q) {
-          const uint32_t r = L.sidx[q];
-          const uint64_t tt = L.ccol[CC_T][r], vv = L.ccol[CC_C2][r];
-          v = tt > t0 ? vv : (tt == t0 ? imax64(v, vv) : v);
-        }
-        c_v[e] = v;
-        c_t[e] = t0;
-        const uint64_t mh = L.ccol[CC_META][r0];
-        c_m[e] = meta_pack(0, meta_pos(mh), meta_src(mh));
-        cemit[e] = true;
-      } else {  // LWWHash::set chain (lwwhash.rs:87-107): the later candidate wins ties
-        uint32_t w = r0;
-        uint64_t tw = L.ccol[CC_T][r0];
-        for (int q = hl + 1; q <= pos; ++q) {
-          const uint32_t r = L.sidx[q];
-          const uint64_t tr = L.ccol[CC_T][r];
-          const bool later = !(tw > tr);
-          w = later ? r : w;
-          tw = later ? tr : tw;
-        }
-        c_t[e] = tw;
-        c_m[e] = L.ccol[CC_META][w];
-        cemit[e] = true;
-        if ((A.flags & F_GC_MEMBERS) && meta_tag(c_m[e]) == KIND_DEL && tw < A.gc_wm) {
-          cemit[e] = false;
-          ++gcm;
-        }
-      }
-    }
-    En[e] = __ballot(cemit[e] && knode[e]);
-    Em[e] = __ballot(cemit[e] && !knode[e]);
-  }
-  uint32_t nbase = 0, mbase = 0;
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    if (cemit[e]) {
-      const uint32_t crank = (knode[e] ? nbase : mbase) + lane_rank(knode[e] ? En[e] : Em[e]);
-      const uint32_t o = (knode[e] ? nb0 : mb0) + crank;
-      uint64_t* const* O = knode[e] ? A.no : A.mo;
-      const uint32_t k = ckey[e];
-      O[C_PKH][o] = L.okh[k];
-      O[C_PKF][o] = L.okf[k];
-      O[C_ID1][o] = cid1[e];
-      O[C_ID2][o] = knode[e] ? c_v[e] : cid2[e];
-      O[C_T][o] = c_t[e];
-      O[C_META][o] = c_m[e];
-      if (knode[e] && (L.ovm[k] & kVmaskMerged))
-        atomicAdd((unsigned long long*)&L.osum[k], (unsigned long long)c_v[e]);
-      atomicMin(&L.ocb[k], crank);
-      atomicAdd(&L.ocnt[k], 1u);
-    }
-    nbase += __popcll(En[e]);
-    mbase += __popcll(Em[e]);
-  }
-  wave_sync();
-  co.nout = nbase;
-  co.mout = mbase;
-  co.orph = orph;
-  co.gcm = gcm;
-  return true;
-}
-
-// One bucket on one wave, up to 64*KE key rows. `spill` receives buckets over the key
-// capacity (KE = 1: the wide kernel; KE = 2: the workgroup tier).
+// One bucket on one wave, up to 64*KE key rows and 128*KE child rows. KE = 1 leaves buckets
+// over that capacity to bucket_wide_kernel and lists those over ITS capacity (and forced
+// tiers) for the workgroup tier.
 template <int KE>
-__device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, uint32_t b, int lane,
-                                            uint32_t* spill_list, uint32_t* spill_count) {
+__device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, uint32_t b, int lane) {
+  constexpr int CE = 2 * KE;
+  constexpr uint32_t KC = WaveLds<KE>::KC, CC = WaveLds<KE>::CC;
   const BucketArgs& A = W.A;
   const uint32_t K = A.kcnt[b], N = A.ncnt[b], M = A.mcnt[b];
   auto push = [&](uint32_t* list, uint32_t* count) {
     if (lane == 0) list[atomicAdd(count, 1u)] = b;
   };
-  constexpr uint32_t KC = WaveLds<KE>::KC, CC = WaveLds<KE>::CC;
-  if (A.force_tier == 1 || A.force_tier == 2 || N + M > WaveLds<2>::CC || K > WaveLds<2>::KC) {
-    push(W.big_list, W.big_count);
-    return;
-  }
-  if (K > KC || N + M > CC || (KE == 1 && A.force_tier == 3)) {
-    push(spill_list, spill_count);
-    return;
+  if (KE == 1) {  // the wide kernel finds its buckets itself (wide_bucket_candidate)
+    if (A.force_tier == 1 || A.force_tier == 2 || N + M > WaveLds<2>::CC || K > WaveLds<2>::KC) {
+      push(W.big_list, W.big_count);
+      return;
+    }
+    if (K > KC || N + M > CC || A.force_tier == 3) return;
   }
   const uint32_t kb = A.kbase[b], nb0 = A.nbase[b], mb0 = A.mbase[b];
+  const uint32_t C = N + M;
 
-  // ------------------------------------------------------------ 1. keys: load + sort
-  // w1 = family:2 | pos:6 | src:48 | idx:7 (pos < 64, kMaxPos)
-  uint64_t w0[KE], w1[KE];
+  // ------------------------------------------------------------ 0. all loads up front
+  uint32_t krow[KE], crow[CE];
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
     const uint32_t c = lane + 64 * e;
-    w0[e] = ~0ull;
-    w1[e] = ~0ull;
-    if (c < K) {
-      const uint32_t row = A.kp[kb + c];
-      const uint64_t meta = A.k[K_META][row];
-      w0[e] = A.k[K_KH][row];
-      w1[e] = ((uint64_t)tag_family(meta_tag(meta)) << 61) | (meta_order(meta) << 7) | c;
-      L.col[KC_CT][c] = A.k[K_CT][row];
-      L.col[KC_UT][c] = A.k[K_UT][row];
-      L.col[KC_DT][c] = A.k[K_DT][row];
-      L.col[KC_META][c] = meta;
-      L.col[KC_KF][c] = A.k[K_KF][row];
-    }
+    krow[e] = c < K ? A.kp[kb + c] : 0;
   }
-  wave_bitonic<KE>(w0, w1);
-  uint32_t idx[KE], fam[KE];
-  uint64_t kh[KE], kf[KE], Hk[KE];
-  bool kin[KE];
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    const uint32_t c = lane + 64 * e;
+    crow[e] = c < N ? A.np[nb0 + c] : (c < C ? A.mp[mb0 + (c - N)] : 0);
+  }
+  uint64_t kh[KE], kf[KE], kct[KE], kut[KE], kdt[KE], kaux[KE], kmeta[KE];
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
-    idx[e] = (uint32_t)(w1[e] & 127);
-    L.sidx[lane + 64 * e] = idx[e];
+    const uint32_t c = lane + 64 * e, r = krow[e];
+    const bool in = c < K;
+    kh[e] = in ? A.k[K_KH][r] : 0;
+    kf[e] = in ? A.k[K_KF][r] : 0;
+    kct[e] = in ? A.k[K_CT][r] : 0;
+    kut[e] = in ? A.k[K_UT][r] : 0;
+    kdt[e] = in ? A.k[K_DT][r] : 0;
+    kaux[e] = in ? A.k[K_AUX][r] : 0;
+    kmeta[e] = in ? A.k[K_META][r] : 0;
+  }
+  uint64_t cpkh[CE], cpkf[CE], cid1[CE], cid2[CE], ct_[CE], cm[CE];
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    const uint32_t c = lane + 64 * e, r = crow[e];
+    const bool in = c < C;
+    const uint64_t* const* S = c < N ? A.nd : A.mb;
+    cpkh[e] = in ? S[C_PKH][r] : 0;
+    cpkf[e] = in ? S[C_PKF][r] : 0;
+    cid1[e] = in ? S[C_ID1][r] : 0;
+    cid2[e] = in ? S[C_ID2][r] : 0;
+    ct_[e] = in ? S[C_T][r] : 0;
+    cm[e] = in ? S[C_META][r] : 0;
+  }
+
+  // ------------------------------------------------------------ 1. keys: rank + scatter
+  // word = kh[43:0] << 20 | family << 18 | pos << 12 | slot   (pos < 64, slot < 4096)
+  uint64_t w[KE];
+  uint32_t rk[KE];
+#pragma unroll
+  for (int e = 0; e < KE; ++e) {
+    const uint32_t c = lane + 64 * e;
+    w[e] = ((kh[e] & kM44) << 20) | ((uint64_t)tag_family(meta_tag(kmeta[e])) << 18) |
+           ((uint64_t)meta_pos(kmeta[e]) << 12) | c;
+    if (c < K) L.sw[c] = w[e];
+  }
+  if (lane == 0) L.sw[K] = ~0ull;
+  wave_sync();
+  rank_count<KE>(L.sw, K, w, rk);
+  wave_sync();
+#pragma unroll
+  for (int e = 0; e < KE; ++e) {
+    if (lane + 64 * e < K) {
+      const uint32_t s = rk[e];
+      L.sw[s] = w[e];
+      L.col[KS_KH][s] = kh[e];
+      L.col[KS_KF][s] = kf[e];
+      L.col[KS_CT][s] = kct[e];
+      L.col[KS_UT][s] = kut[e];
+      L.col[KS_DT][s] = kdt[e];
+      L.col[KS_AUX][s] = kaux[e];
+      L.col[KS_META][s] = kmeta[e];
+    }
   }
   wave_sync();
-  bool coll = false;
+  // sorted slot s = lane + 64 e from here on
+  uint32_t fam[KE];
+  uint64_t Hk[KE];
+  bool kin[KE], coll = false;
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
-    const uint32_t pos = lane + 64 * e;
-    kin[e] = pos < K;
-    kh[e] = w0[e];
-    fam[e] = (uint32_t)(w1[e] >> 61) & 3;
-    kf[e] = kin[e] ? L.col[KC_KF][idx[e]] : 0;
-    uint64_t pkh = shfl_up64(kh[e], 1), pkf = shfl_up64(kf[e], 1);
-    uint32_t pfam = __shfl_up(fam[e], 1, 64);
-    if (e > 0) {
-      const int ep = e > 0 ? e - 1 : 0;
-      const uint64_t x0 = bcast63(kh[ep]), x1 = bcast63(kf[ep]);
-      const uint32_t x2 = __shfl(fam[ep], 63, 64);
-      pkh = lane == 0 ? x0 : pkh;
-      pkf = lane == 0 ? x1 : pkf;
-      pfam = lane == 0 ? x2 : pfam;
-    }
-    coll |= kin[e] && pos > 0 && pkh == kh[e] && pkf != kf[e];  // 64-bit kh collision
-    Hk[e] = __ballot(kin[e] && (pos == 0 || pkh != kh[e] || pfam != fam[e]));
+    const uint32_t s = lane + 64 * e;
+    kin[e] = s < K;
+    const uint32_t sp = s > 0 ? s - 1 : 0;
+    w[e] = kin[e] ? L.sw[s] : ~0ull;
+    kh[e] = L.col[KS_KH][s];
+    kf[e] = L.col[KS_KF][s];
+    const uint64_t pw = L.sw[sp], pkh = L.col[KS_KH][sp], pkf = L.col[KS_KF][sp];
+    fam[e] = (uint32_t)(w[e] >> 18) & 3;
+    const bool same_key = kin[e] && s > 0 && (pw >> 20) == (w[e] >> 20);
+    // equal kh bits but another identity: a 2^-44 event (or a real 64-bit kh collision);
+    // equal (key, family, pos): duplicate keys in one snapshot, folded in src order there
+    coll |= same_key && (pkh != kh[e] || pkf != kf[e] || (pw >> 12) == (w[e] >> 12));
+    Hk[e] = __ballot(kin[e] && (s == 0 || (pw >> 18) != (w[e] >> 18)));
   }
   if (__ballot(coll)) {
     push(W.big_list, W.big_count);
@@ -390,7 +227,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   uint64_t o_ct[KE], o_ut[KE], o_dt[KE], o_meta[KE], o_win[KE];
   uint32_t o_T[KE], orank[KE];
   bool emit[KE];
-  unsigned long long st_conf = 0, st_dict = 0, st_dup = 0, st_gcd = 0;
+  unsigned long long st_conf = 0, st_dict = 0, st_gcd = 0;
   uint32_t kout = 0;
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
@@ -406,26 +243,21 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     emit[e] = false;
     if (ktail) {
       const int hl = seg_head<KE>(Hk, e, lane);
-      const uint32_t r0 = L.sidx[hl];
-      const uint64_t m0 = L.col[KC_META][r0];
+      const uint64_t m0 = L.col[KS_META][hl];
       const uint32_t T = meta_tag(m0);
       hp = meta_pos(m0);
-      const uint64_t ct0 = L.col[KC_CT][r0], ut0 = L.col[KC_UT][r0], dt0 = L.col[KC_DT][r0];
+      const uint64_t ct0 = L.col[KS_CT][hl], ut0 = L.col[KS_UT][hl], dt0 = L.col[KS_DT][hl];
       uint64_t ct = ct0, ut = ut0, dt = dt0;
       uint64_t win = meta_order(m0), lastm = m0;
-      uint32_t nvalid = 1, conflicts = 0, dups = 0, prevpos = hp;
+      uint32_t nvalid = 1, conflicts = 0;
       vm = 1ull << hp;
-      const uint64_t tl_ct = L.col[KC_CT][idx[e]];  // the segment's last row (side maps)
+      const uint64_t tl_ct = L.col[KS_CT][pos];  // the segment's last row (side maps)
       bool gc_hit = fm == 2 && meta_order(m0) + 1 > last_bad && ct0 == tl_ct;
       for (int q = hl + 1; q <= pos; ++q) {
-        const uint32_t r = L.sidx[q];
-        const uint64_t m = L.col[KC_META][r];
-        const uint32_t p = meta_pos(m);
-        dups += p == prevpos;
-        prevpos = p;
+        const uint64_t m = L.col[KS_META][q];
         lastm = m;
         if (fm != 0) {
-          gc_hit |= fm == 2 && meta_order(m) + 1 > last_bad && L.col[KC_CT][r] == tl_ct;
+          gc_hit |= fm == 2 && meta_order(m) + 1 > last_bad && L.col[KS_CT][q] == tl_ct;
           continue;
         }
         if (meta_tag(m) != T) {  // object.rs:80: type conflict, local kept
@@ -433,16 +265,15 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
           continue;
         }
         ++nvalid;
-        vm |= 1ull << p;
+        vm |= 1ull << meta_pos(m);
         if (T == TAG_BYTES) {  // object.rs:69-77
-          const uint64_t c2 = L.col[KC_CT][r];
+          const uint64_t c2 = L.col[KS_CT][q];
           if (ct < c2) win = meta_order(m);
           ct = max(ct, c2);
-          dt = max(dt, L.col[KC_DT][r]);
-          ut = max(ut, L.col[KC_UT][r]);
+          dt = max(dt, L.col[KS_DT][q]);
+          ut = max(ut, L.col[KS_UT][q]);
         }
       }
-      st_dup += dups;
       if (fm == 0) {
         st_conf += conflicts;
         if (T == TAG_DICT) st_dict += nvalid - 1;
@@ -455,7 +286,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
         o_win[e] = T == TAG_BYTES ? win : 0;
         vm |= (T == TAG_COUNTER && nvalid >= 2) ? kVmaskMerged : 0;
         // a counter that was never merged keeps its load-time total (aux, head row)
-        sum = (T == TAG_COUNTER && nvalid < 2) ? A.k[K_AUX][A.kp[kb + r0]] : 0;
+        sum = (T == TAG_COUNTER && nvalid < 2) ? L.col[KS_AUX][hl] : 0;
         emit[e] = true;
       } else {  // expires / deletes: plain overwrite, the last (pos, src) wins
         const bool removed = fm == 2 && (A.flags & F_GC_DELETES) && gc_hit;
@@ -484,19 +315,171 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   }
   wave_sync();
 
-  // ------------------------------------------------------------ 3-4. children
-  ChildOut co;
-  bool ok;
-  if (N + M <= 64)
-    ok = children_stage<1, KE>(A, L, lane, N, M, nb0, mb0, kout, co);
-  else if (KE == 1 || N + M <= 128)
-    ok = children_stage<2, KE>(A, L, lane, N, M, nb0, mb0, kout, co);
+  // ------------------------------------------------------------ 3. children: key lookup
+  // word = key rank << 56 | id hash[41:0] << 14 | pos << 8 | slot   (rank < 128, slot < 256)
+  unsigned long long orph = 0, gcm = 0;
+  uint32_t ckey[CE];
+  bool clive[CE];
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    const uint32_t c = lane + 64 * e;
+    clive[e] = false;
+    ckey[e] = 0;
+    if (c < C) {
+      const bool isn = c < N;
+      uint32_t lo = 0, hi = kout;  // lower bound on kh[43:0] (output keys are in word order)
+      const uint64_t t44 = cpkh[e] & kM44;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const bool less = (L.okh[mid] & kM44) < t44;
+        lo = less ? mid + 1 : lo;
+        hi = less ? hi : mid;
+      }
+      if (lo < kout && L.okh[lo] == cpkh[e] && L.okf[lo] == cpkf[e] && (L.otp[lo] & 0xFF) <= TAG_SET) {
+        const uint32_t KT = L.otp[lo] & 0xFF, khp = L.otp[lo] >> 8, p = meta_pos(cm[e]);
+        const bool type_ok = isn ? KT == TAG_COUNTER : (KT == TAG_SET || KT == TAG_DICT);
+        const bool elem_ok = (L.ovm[lo] >> p) & 1;
+        const bool cand = isn || meta_tag(cm[e]) == KIND_ADD || p == khp;  // remote dels ignored
+        clive[e] = type_ok && elem_ok && cand;
+        ckey[e] = lo;
+      } else {
+        ++orph;
+      }
+    }
+  }
+  // live children -> compact list of words, then rank
+  uint64_t cw[CE];
+  uint32_t crk[CE];
+  uint32_t nlive = 0;
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    const uint32_t c = lane + 64 * e;
+    const bool isn = c < N;
+    const uint64_t ih = isn ? mix64(cid1[e]) : cid1[e];
+    cw[e] = clive[e] ? (((uint64_t)ckey[e] << 56) | ((ih & kM42) << 14) | ((uint64_t)meta_pos(cm[e]) << 8) | c)
+                     : ~0ull;
+    const uint64_t Lm = __ballot(clive[e]);
+    if (clive[e]) L.sw[nlive + lane_rank(Lm)] = cw[e];
+    nlive += __popcll(Lm);
+  }
+  if (lane == 0) L.sw[nlive] = ~0ull;
+  wave_sync();
+  // a lane's live words sit at its input slots lane + 64 e, so rank the first ceil(C / 64)
+  if (CE >= 4 && C > 192)
+    rank_count<(CE >= 4 ? 4 : CE)>(L.sw, nlive, cw, crk);
+  else if (CE >= 3 && C > 128)
+    rank_count<(CE >= 3 ? 3 : CE)>(L.sw, nlive, cw, crk);
+  else if (C > 64)
+    rank_count<2>(L.sw, nlive, cw, crk);
   else
-    ok = children_stage<(KE == 1 ? 2 : 4), KE>(A, L, lane, N, M, nb0, mb0, kout, co);
-  if (!ok) {  // id-hash collision: exact tier
+    rank_count<1>(L.sw, nlive, cw, crk);
+  wave_sync();
+  // node rows keep id2 = value; for the identity check a node compares only its id
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    if (clive[e]) {
+      const uint32_t s = crk[e];
+      L.sw[s] = cw[e];
+      L.ccol[CS_ID1][s] = cid1[e];
+      L.ccol[CS_C2][s] = cid2[e];
+      L.ccol[CS_T][s] = ct_[e];
+      L.ccol[CS_META][s] = cm[e];
+    }
+  }
+  wave_sync();
+
+  // ------------------------------------------------------------ 4. child folds + outputs
+  bool live[CE], knode[CE], coll2 = false;
+  uint64_t H[CE], Lv[CE], sw_[CE], sid1[CE], sid2[CE];
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    const uint32_t s = lane + 64 * e;
+    live[e] = s < nlive;
+    const uint32_t sp = s > 0 ? s - 1 : 0;
+    sw_[e] = live[e] ? L.sw[s] : ~0ull;
+    const uint32_t k = (uint32_t)(sw_[e] >> 56) & (KC - 1);
+    knode[e] = live[e] && (L.otp[k] & 0xFF) == TAG_COUNTER;
+    sid1[e] = L.ccol[CS_ID1][s];
+    sid2[e] = knode[e] ? 0 : L.ccol[CS_C2][s];
+    const uint64_t pw = L.sw[sp], p1 = L.ccol[CS_ID1][sp], p2 = knode[e] ? 0 : L.ccol[CS_C2][sp];
+    const bool same = live[e] && s > 0 && (pw >> 14) == (sw_[e] >> 14);
+    coll2 |= same && (p1 != sid1[e] || p2 != sid2[e] || (pw >> 8) == (sw_[e] >> 8));
+    H[e] = __ballot(live[e] && (s == 0 || !same));
+    Lv[e] = __ballot(live[e]);
+  }
+  if (__ballot(coll2)) {  // id-hash collision or duplicate: exact tier (nothing written yet)
     push(W.big_list, W.big_count);
     return;
   }
+  uint64_t En[CE], Em[CE], c_v[CE], c_t[CE], c_m[CE];
+  bool cemit[CE];
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    const int en = e + 1 < CE ? e + 1 : e;
+    const bool nxt_head = lane < 63 ? ((H[e] >> (lane + 1)) & 1) : (e + 1 < CE && (H[en] & 1));
+    const bool nxt_live = lane < 63 ? ((Lv[e] >> (lane + 1)) & 1) : (e + 1 < CE && (Lv[en] & 1));
+    const bool ctail = live[e] && (nxt_head || !nxt_live);
+    const int pos = lane + 64 * e;
+    c_v[e] = c_t[e] = c_m[e] = 0;
+    cemit[e] = false;
+    if (ctail) {
+      const int hl = seg_head<CE>(H, e, lane);
+      if (knode[e]) {  // Counter::merge per node (type_counter.rs:60-84): the head's t is kept
+        const uint64_t t0 = L.ccol[CS_T][hl];
+        uint64_t v = L.ccol[CS_C2][hl];
+        for (int q = hl + 1; q <= pos; ++q) {
+          const uint64_t tt = L.ccol[CS_T][q], vv = L.ccol[CS_C2][q];
+          v = tt > t0 ? vv : (tt == t0 ? imax64(v, vv) : v);
+        }
+        c_v[e] = v;
+        c_t[e] = t0;
+        const uint64_t mh = L.ccol[CS_META][hl];
+        c_m[e] = meta_pack(0, meta_pos(mh), meta_src(mh));
+        cemit[e] = true;
+      } else {  // LWWHash::set chain (lwwhash.rs:87-107): the later candidate wins ties
+        int wq = hl;
+        uint64_t tw = L.ccol[CS_T][hl];
+        for (int q = hl + 1; q <= pos; ++q) {
+          const uint64_t tr = L.ccol[CS_T][q];
+          const bool later = !(tw > tr);
+          wq = later ? q : wq;
+          tw = later ? tr : tw;
+        }
+        c_t[e] = tw;
+        c_m[e] = L.ccol[CS_META][wq];
+        cemit[e] = true;
+        if ((A.flags & F_GC_MEMBERS) && meta_tag(c_m[e]) == KIND_DEL && tw < A.gc_wm) {
+          cemit[e] = false;
+          ++gcm;
+        }
+      }
+    }
+    En[e] = __ballot(cemit[e] && knode[e]);
+    Em[e] = __ballot(cemit[e] && !knode[e]);
+  }
+  uint32_t nbase = 0, mbase = 0;
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    if (cemit[e]) {
+      const uint32_t crank = (knode[e] ? nbase : mbase) + lane_rank(knode[e] ? En[e] : Em[e]);
+      const uint32_t o = (knode[e] ? nb0 : mb0) + crank;
+      uint64_t* const* O = knode[e] ? A.no : A.mo;
+      const uint32_t k = (uint32_t)(sw_[e] >> 56) & (KC - 1);
+      O[C_PKH][o] = L.okh[k];
+      O[C_PKF][o] = L.okf[k];
+      O[C_ID1][o] = sid1[e];
+      O[C_ID2][o] = knode[e] ? c_v[e] : sid2[e];
+      O[C_T][o] = c_t[e];
+      O[C_META][o] = c_m[e];
+      if (knode[e] && (L.ovm[k] & kVmaskMerged))
+        atomicAdd((unsigned long long*)&L.osum[k], (unsigned long long)c_v[e]);
+      atomicMin(&L.ocb[k], crank);
+      atomicAdd(&L.ocnt[k], 1u);
+    }
+    nbase += __popcll(En[e]);
+    mbase += __popcll(Em[e]);
+  }
+  wave_sync();
 
   // ------------------------------------------------------------ 5. key outputs
 #pragma unroll
@@ -515,18 +498,29 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   }
   if (lane == 0) {
     A.kout[b] = kout;
-    A.nout[b] = co.nout;
-    A.mout[b] = co.mout;
+    A.nout[b] = nbase;
+    A.mout[b] = mbase;
   }
-  const unsigned long long s0 = wave_sum_u64(st_conf), s1 = wave_sum_u64(st_dict), s2 = wave_sum_u64(st_dup),
-                           s3 = wave_sum_u64(co.orph), s4 = wave_sum_u64(st_gcd), s5 = wave_sum_u64(co.gcm);
-  if (lane == 0) {
-    if (s0) atomicAdd(&A.stats[ST_TYPE_CONFLICTS], s0);
-    if (s1) atomicAdd(&A.stats[ST_DICT_MERGES], s1);
-    if (s2) atomicAdd(&A.stats[ST_DUP_ROWS], s2);
-    if (s3) atomicAdd(&A.stats[ST_ORPHANS], s3);
-    if (s4) atomicAdd(&A.stats[ST_DELETES_GCED], s4);
-    if (s5) atomicAdd(&A.stats[ST_MEMBERS_GCED], s5);
+  unsigned long long* st = stat_shard(A.stats);
+  if (__ballot(st_conf)) {
+    const unsigned long long v = wave_sum_u64(st_conf);
+    if (lane == 0) atomicAdd(&st[ST_TYPE_CONFLICTS], v);
+  }
+  if (__ballot(st_dict)) {
+    const unsigned long long v = wave_sum_u64(st_dict);
+    if (lane == 0) atomicAdd(&st[ST_DICT_MERGES], v);
+  }
+  if (__ballot(orph)) {
+    const unsigned long long v = wave_sum_u64(orph);
+    if (lane == 0) atomicAdd(&st[ST_ORPHANS], v);
+  }
+  if (__ballot(st_gcd)) {
+    const unsigned long long v = wave_sum_u64(st_gcd);
+    if (lane == 0) atomicAdd(&st[ST_DELETES_GCED], v);
+  }
+  if (__ballot(gcm)) {
+    const unsigned long long v = wave_sum_u64(gcm);
+    if (lane == 0) atomicAdd(&st[ST_MEMBERS_GCED], v);
   }
 }
 
@@ -539,22 +533,49 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t i, uint32_t G) {
   return x * q + min(x, r) + j;
 }
 
-// Every bucket, one wave each (<= 64 key rows per wave).
+// Every bucket, one wave each (<= 64 key rows, <= 128 child rows per wave).
 __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_kernel(WaveArgs W) {
   __shared__ WaveLds<1> lds_all[kWavesPerWG];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t b = xcd_block(blockIdx.x, gridDim.x) * kWavesPerWG + wv;
   if (b >= W.nbuckets) return;
-  wave_bucket<1>(W, lds_all[wv], b, lane, W.wide_list, W.wide_count);
+  wave_bucket<1>(W, lds_all[wv], b, lane);
 }
 
-// Buckets over bucket_wave_kernel's capacity (listed by it), persistent over the list.
+// Buckets over bucket_wave_kernel's capacity but within this kernel's.
+__device__ __forceinline__ bool wide_bucket_candidate(const BucketArgs& A, uint32_t b) {
+  const uint32_t K = A.kcnt[b], C = A.ncnt[b] + A.mcnt[b];
+  if (A.force_tier == 1 || A.force_tier == 2 || C > WaveLds<2>::CC || K > WaveLds<2>::KC) return false;
+  return K > WaveLds<1>::KC || C > WaveLds<1>::CC || A.force_tier == 3;
+}
+
+// Persistent: each wave scans the bucket directory 64 buckets at a time (no global list,
+// so no single-word atomic shared by every wave) and merges the candidates one by one.
 __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_kernel(WaveArgs W) {
   __shared__ WaveLds<2> lds_all[kWavesPerWG];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t total = *W.wide_count;
-  for (uint32_t i = blockIdx.x * kWavesPerWG + wv; i < total; i += gridDim.x * kWavesPerWG)
-    wave_bucket<2>(W, lds_all[wv], W.wide_list[i], lane, W.big_list, W.big_count);
+  const uint32_t groups = (W.nbuckets + 63) / 64;
+  unsigned long long found = 0;
+  for (uint32_t g = blockIdx.x * kWavesPerWG + wv; g < groups; g += gridDim.x * kWavesPerWG) {
+    const uint32_t b = g * 64 + lane;
+    uint64_t m = __ballot(b < W.nbuckets && wide_bucket_candidate(W.A, b));
+    found += __popcll(m);
+    while (m) {
+      const int i = __builtin_ctzll(m);
+      m &= m - 1;
+      wave_bucket<2>(W, lds_all[wv], g * 64 + i, lane);
+    }
+  }
+  if (lane == 0 && found) atomicAdd(&stat_shard(W.A.stats)[ST_WIDE], found);
+}
+
+// Sums the statistic shards into out[0 .. ST_COUNT).
+__global__ void stats_reduce_kernel(const unsigned long long* __restrict__ shards, unsigned long long* out) {
+  for (int i = threadIdx.x; i < ST_COUNT; i += blockDim.x) {
+    unsigned long long s = 0;
+    for (int k = 0; k < kStatShards; ++k) s += shards[(size_t)k * kStatStride + i];
+    out[i] = s;
+  }
 }
 
 }  // namespace cdb

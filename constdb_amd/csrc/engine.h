@@ -27,6 +27,7 @@ enum WsSlot {
   WS_SCAN,                                              // scan partials
   WS_OWNER,                                             // owner-partition directory
   WS_PERM,                                              // final-level row permutations (u32)
+  WS_STATS,                                             // statistic shards
   WS_COUNT
 };
 

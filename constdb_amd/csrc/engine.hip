@@ -311,8 +311,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   Dir dnd{dir + 5 * dn, dir + 6 * dn, dir + 7 * dn, dir + 8 * dn, dir + 9 * dn};
   Dir dm{dir + 10 * dn, dir + 11 * dn, dir + 12 * dn, dir + 13 * dn, dir + 14 * dn};
   // misc: stats[8] u64 | last_bad u64 | totals[3] u64 | hot_count u32 | big_count u32 |
-  //       wide_count u32 | hot_list[nb] u32 | big_list[nb] u32 | wide_list[nb] u32
-  uint8_t* misc = (uint8_t*)ws_get(ctx, WS_MISC, 128 + 3 * nb * sizeof(uint32_t), &st);
+  //       hot_list[nb] u32 | big_list[nb] u32
+  uint8_t* misc = (uint8_t*)ws_get(ctx, WS_MISC, 128 + 2 * nb * sizeof(uint32_t), &st);
   if (!misc) return st;
   unsigned long long* d_stats = (unsigned long long*)misc;
   unsigned long long* d_last_bad = (unsigned long long*)(misc + 64);
@@ -321,9 +321,11 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   uint32_t* d_big_count = (uint32_t*)(misc + 100);
   uint32_t* d_hot_list = (uint32_t*)(misc + 128);
   uint32_t* d_big_list = d_hot_list + nb;
-  uint32_t* d_wide_count = (uint32_t*)(misc + 104);
-  uint32_t* d_wide_list = d_big_list + nb;
   CDB_HIP(hipMemsetAsync(misc, 0, 128, s), "memset misc");
+  unsigned long long* d_shards =
+      (unsigned long long*)ws_get(ctx, WS_STATS, kStatShards * kStatStride * sizeof(unsigned long long), &st);
+  if (!d_shards) return st;
+  CDB_HIP(hipMemsetAsync(d_shards, 0, kStatShards * kStatStride * sizeof(unsigned long long), s), "memset stats");
 
   CDB_HIP(hipEventRecord(ctx->ev0, s), "event");
   // ---- 1. bucket partition of each family by (parent) key hash
@@ -378,7 +380,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   A.force_tier = opts ? opts->force_tier : 0;
   A.key_shift = shift;
   A.last_bad = (const uint64_t*)d_last_bad;
-  A.stats = d_stats;
+  A.stats = d_shards;
   A.hot_list = d_hot_list;
   A.hot_count = d_hot_count;
   WaveArgs WA;
@@ -386,18 +388,17 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   WA.nbuckets = (uint32_t)nb;
   WA.big_list = d_big_list;
   WA.big_count = d_big_count;
-  WA.wide_list = d_wide_list;
-  WA.wide_count = d_wide_count;
   bucket_wave_kernel<<<(nb + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, 0, s>>>(WA);
   CDB_HIP(hipGetLastError(), "bucket_wave_kernel");
-  bucket_wide_kernel<<<std::min<uint64_t>((nb + kWavesPerWG - 1) / kWavesPerWG, 1024), kWavesPerWG * 64, 0, s>>>(WA);
+  bucket_wide_kernel<<<(uint32_t)std::min<uint64_t>((nb + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024),
+                       kWavesPerWG * 64, 0, s>>>(WA);
   CDB_HIP(hipGetLastError(), "bucket_wide_kernel");
   bucket_mid_kernel<<<std::min<uint64_t>(nb, 2048), kBktThreads, 0, s>>>(A, d_big_list, d_big_count);
   CDB_HIP(hipGetLastError(), "bucket_mid_kernel");
   CDB_HIP(hipEventRecord(ctx->ev_bucket, s), "event");
 
   // ---- 4. over-capacity buckets (same algorithm, global scratch)
-  uint32_t counts[3] = {0, 0, 0};  // hot, big (mid tier), wide
+  uint32_t counts[2] = {0, 0};  // hot, big (mid tier)
   CDB_HIP(hipMemcpyAsync(counts, d_hot_count, sizeof counts, hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipStreamSynchronize(s), "sync");
   const uint32_t hot = counts[0];
@@ -449,6 +450,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   compact_kernel<<<(uint32_t)std::min<uint64_t>((nb + 64 * kCompactWaves - 1) / (64 * kCompactWaves), 16384),
                    64 * kCompactWaves, 0, s>>>(C, (uint32_t)nb);
   CDB_HIP(hipGetLastError(), "compact_kernel");
+  stats_reduce_kernel<<<1, 64, 0, s>>>(d_shards, d_stats);
+  CDB_HIP(hipGetLastError(), "stats_reduce_kernel");
   CDB_HIP(hipEventRecord(ctx->ev1, s), "event");
 
   uint64_t totals[3];
@@ -474,7 +477,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     stats->duplicate_rows = hs[ST_DUP_ROWS];
     stats->orphan_children = hs[ST_ORPHANS];
     stats->hot_buckets = hot;
-    stats->wide_buckets = counts[2];
+    stats->wide_buckets = hs[ST_WIDE];
     stats->mid_buckets = counts[1];
     float ms = 0;
     hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1);
