@@ -106,65 +106,129 @@ struct WaveArgs {
   uint32_t* big_count;
 };
 
-// One bucket on one wave, up to 64*KE key rows and 128*KE child rows. KE = 1 leaves buckets
-// over that capacity to bucket_wide_kernel and lists those over ITS capacity (and forced
-// tiers) for the workgroup tier.
+// A bucket's directory entry (row counts and first row of each family).
+struct WaveDir {
+  uint32_t K = 0, N = 0, M = 0, kb = 0, nb0 = 0, mb0 = 0;
+};
+__device__ __forceinline__ WaveDir load_dir(const BucketArgs& A, uint32_t b) {
+  WaveDir d;
+  d.K = A.kcnt[b];
+  d.N = A.ncnt[b];
+  d.M = A.mcnt[b];
+  d.kb = A.kbase[b];
+  d.nb0 = A.nbase[b];
+  d.mb0 = A.mbase[b];
+  return d;
+}
+
+// Row indices of a bucket's rows (the last partition level is index-only).
 template <int KE>
-__device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, uint32_t b, int lane) {
+struct WavePerm {
+  uint32_t krow[KE], crow[2 * KE];
+};
+template <int KE>
+__device__ __forceinline__ void load_perm(const BucketArgs& A, const WaveDir& d, int lane, WavePerm<KE>& p) {
+  const uint32_t C = d.N + d.M;
+#pragma unroll
+  for (int e = 0; e < KE; ++e) {
+    const uint32_t c = lane + 64 * e;
+    p.krow[e] = c < d.K ? A.kp[d.kb + c] : 0;
+  }
+#pragma unroll
+  for (int e = 0; e < 2 * KE; ++e) {
+    const uint32_t c = lane + 64 * e;
+    p.crow[e] = c < d.N ? A.np[d.nb0 + c] : (c < C ? A.mp[d.mb0 + (c - d.N)] : 0);
+  }
+}
+
+// Every input column of a bucket, one key row and two child rows per lane and KE.
+template <int KE>
+struct WaveIn {
+  WaveDir d;
+  uint64_t kh[KE], kf[KE], kct[KE], kut[KE], kdt[KE], kaux[KE], kmeta[KE];
+  uint64_t cpkh[2 * KE], cpkf[2 * KE], cid1[2 * KE], cid2[2 * KE], ct[2 * KE], cm[2 * KE];
+};
+template <int KE>
+__device__ __forceinline__ void load_cols(const BucketArgs& A, const WaveDir& d, const WavePerm<KE>& p, int lane,
+                                          WaveIn<KE>& in) {
+  in.d = d;
+  const uint32_t C = d.N + d.M;
+#pragma unroll
+  for (int e = 0; e < KE; ++e) {
+    const uint32_t c = lane + 64 * e, r = p.krow[e];
+    const bool ok = c < d.K;
+    in.kh[e] = ok ? A.k[K_KH][r] : 0;
+    in.kf[e] = ok ? A.k[K_KF][r] : 0;
+    in.kct[e] = ok ? A.k[K_CT][r] : 0;
+    in.kut[e] = ok ? A.k[K_UT][r] : 0;
+    in.kdt[e] = ok ? A.k[K_DT][r] : 0;
+    in.kaux[e] = ok ? A.k[K_AUX][r] : 0;
+    in.kmeta[e] = ok ? A.k[K_META][r] : 0;
+  }
+#pragma unroll
+  for (int e = 0; e < 2 * KE; ++e) {
+    const uint32_t c = lane + 64 * e, r = p.crow[e];
+    const bool ok = c < C;
+    const uint64_t* const* S = c < d.N ? A.nd : A.mb;
+    in.cpkh[e] = ok ? S[C_PKH][r] : 0;
+    in.cpkf[e] = ok ? S[C_PKF][r] : 0;
+    in.cid1[e] = ok ? S[C_ID1][r] : 0;
+    in.cid2[e] = ok ? S[C_ID2][r] : 0;
+    in.ct[e] = ok ? S[C_T][r] : 0;
+    in.cm[e] = ok ? S[C_META][r] : 0;
+  }
+}
+
+// One bucket on one wave, up to 64*KE key rows and 128*KE child rows, from the columns in
+// `in`. KE = 1 leaves buckets over that capacity to bucket_wide_kernel and lists those over
+// ITS capacity (and forced tiers) for the workgroup tier. `next()` runs exactly once, as
+// soon as `in` is dead (after the children are staged in LDS): the streaming kernel issues
+// the next bucket's loads there, so they are in flight while this bucket's children fold.
+template <int KE, typename Next>
+__device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, uint32_t b, int lane,
+                                            const WaveIn<KE>& in, Next&& next) {
   constexpr int CE = 2 * KE;
   constexpr uint32_t KC = WaveLds<KE>::KC, CC = WaveLds<KE>::CC;
   const BucketArgs& A = W.A;
-  const uint32_t K = A.kcnt[b], N = A.ncnt[b], M = A.mcnt[b];
+  const uint32_t K = in.d.K, N = in.d.N, M = in.d.M;
   auto push = [&](uint32_t* list, uint32_t* count) {
     if (lane == 0) list[atomicAdd(count, 1u)] = b;
   };
   if (KE == 1) {  // the wide kernel finds its buckets itself (wide_bucket_candidate)
     if (A.force_tier == 1 || A.force_tier == 2 || N + M > WaveLds<2>::CC || K > WaveLds<2>::KC) {
+      next();
       push(W.big_list, W.big_count);
       return;
     }
-    if (K > KC || N + M > CC || A.force_tier == 3) return;
+    if (K > KC || N + M > CC || A.force_tier == 3) {
+      next();
+      return;
+    }
   }
-  const uint32_t kb = A.kbase[b], nb0 = A.nbase[b], mb0 = A.mbase[b];
+  const uint32_t kb = in.d.kb, nb0 = in.d.nb0, mb0 = in.d.mb0;
   const uint32_t C = N + M;
 
-  // ------------------------------------------------------------ 0. all loads up front
-  uint32_t krow[KE], crow[CE];
-#pragma unroll
-  for (int e = 0; e < KE; ++e) {
-    const uint32_t c = lane + 64 * e;
-    krow[e] = c < K ? A.kp[kb + c] : 0;
-  }
-#pragma unroll
-  for (int e = 0; e < CE; ++e) {
-    const uint32_t c = lane + 64 * e;
-    crow[e] = c < N ? A.np[nb0 + c] : (c < C ? A.mp[mb0 + (c - N)] : 0);
-  }
+  // ------------------------------------------------------------ 0. the bucket's columns
   uint64_t kh[KE], kf[KE], kct[KE], kut[KE], kdt[KE], kaux[KE], kmeta[KE];
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
-    const uint32_t c = lane + 64 * e, r = krow[e];
-    const bool in = c < K;
-    kh[e] = in ? A.k[K_KH][r] : 0;
-    kf[e] = in ? A.k[K_KF][r] : 0;
-    kct[e] = in ? A.k[K_CT][r] : 0;
-    kut[e] = in ? A.k[K_UT][r] : 0;
-    kdt[e] = in ? A.k[K_DT][r] : 0;
-    kaux[e] = in ? A.k[K_AUX][r] : 0;
-    kmeta[e] = in ? A.k[K_META][r] : 0;
+    kh[e] = in.kh[e];
+    kf[e] = in.kf[e];
+    kct[e] = in.kct[e];
+    kut[e] = in.kut[e];
+    kdt[e] = in.kdt[e];
+    kaux[e] = in.kaux[e];
+    kmeta[e] = in.kmeta[e];
   }
   uint64_t cpkh[CE], cpkf[CE], cid1[CE], cid2[CE], ct_[CE], cm[CE];
 #pragma unroll
   for (int e = 0; e < CE; ++e) {
-    const uint32_t c = lane + 64 * e, r = crow[e];
-    const bool in = c < C;
-    const uint64_t* const* S = c < N ? A.nd : A.mb;
-    cpkh[e] = in ? S[C_PKH][r] : 0;
-    cpkf[e] = in ? S[C_PKF][r] : 0;
-    cid1[e] = in ? S[C_ID1][r] : 0;
-    cid2[e] = in ? S[C_ID2][r] : 0;
-    ct_[e] = in ? S[C_T][r] : 0;
-    cm[e] = in ? S[C_META][r] : 0;
+    cpkh[e] = in.cpkh[e];
+    cpkf[e] = in.cpkf[e];
+    cid1[e] = in.cid1[e];
+    cid2[e] = in.cid2[e];
+    ct_[e] = in.ct[e];
+    cm[e] = in.cm[e];
   }
 
   // ------------------------------------------------------------ 1. keys: rank + scatter
@@ -218,6 +282,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     Hk[e] = __ballot(kin[e] && (s == 0 || (pw >> 18) != (w[e] >> 18)));
   }
   if (__ballot(coll)) {
+    next();
     push(W.big_list, W.big_count);
     return;
   }
@@ -387,6 +452,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     }
   }
   wave_sync();
+  next();  // this bucket's input registers are dead from here on
 
   // ------------------------------------------------------------ 4. child folds + outputs
   bool live[CE], knode[CE], coll2 = false;
@@ -524,22 +590,116 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   }
 }
 
+constexpr uint32_t kXcds = 8;
+
+// Every bucket, one wave each (<= 64 key rows, <= 128 child rows per wave). Persistent and
+// software-pipelined (the launch is a multiple of 8 workgroups that fills the chip once):
+//   * workgroups are dispatched round-robin over the 8 XCDs (each with its own L2), so
+//     blockIdx % 8 is the XCD; XCD x owns the contiguous bucket range [x nb/8, (x+1) nb/8),
+//     whose buckets share final partition segments that then stay in that XCD's L2, and its
+//     waves take the range's buckets round-robin (the XCD's waves sweep it together);
+//   * a bucket costs three dependent memory round trips (directory -> row indices ->
+//     columns). While a wave folds bucket i's children, the loads of bucket i+1 are already
+//     in flight: PF = 2 issues its column gathers there (and bucket i+2's row indices), PF = 1
+//     only its row indices (fewer live registers, more resident waves: the gathers are then
+//     issued at the top of the iteration). The directory entries are fetched a bucket ahead.
+template <int PF>
+__device__ __forceinline__ void wave_stream(const WaveArgs& W, WaveLds<1>* lds_all, uint32_t b, uint32_t hi,
+                                            uint32_t stride) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const BucketArgs& A = W.A;
+  if (b >= hi) return;
+  // A directory entry is one vector load: lane f < 6 reads field f, then readlane.
+  const uint32_t* dir_f = lane == 0 ? A.kcnt : lane == 1 ? A.ncnt : lane == 2 ? A.mcnt
+                        : lane == 3 ? A.kbase : lane == 4 ? A.nbase : A.mbase;
+  auto dir_issue = [&](uint32_t bb) -> uint32_t { return (lane < 6 && bb < hi) ? dir_f[bb] : 0u; };
+  auto dir_take = [&](uint32_t v) {
+    WaveDir d;
+    d.K = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+    d.N = (uint32_t)__builtin_amdgcn_readlane((int)v, 1);
+    d.M = (uint32_t)__builtin_amdgcn_readlane((int)v, 2);
+    d.kb = (uint32_t)__builtin_amdgcn_readlane((int)v, 3);
+    d.nb0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 4);
+    d.mb0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 5);
+    return d;
+  };
+  WaveIn<1> cur;
+  WavePerm<1> p;
+  if (PF == 2) {
+    WaveDir dn;  // directory of the next bucket (its row indices are in p)
+    {
+      const WaveDir d0 = dir_take(dir_issue(b));
+      load_perm<1>(A, d0, lane, p);
+      load_cols<1>(A, d0, p, lane, cur);
+      dn = dir_take(dir_issue(b + stride));
+      load_perm<1>(A, dn, lane, p);
+    }
+    uint32_t dv = dir_issue(b + 2 * stride);
+    for (;;) {
+      const uint32_t bn = b + stride;
+      wave_bucket<1>(W, lds_all[wv], b, lane, cur, [&]() {
+        // dv is the oldest load in flight: take it before issuing the column gathers, so
+        // that waiting for it never waits for them
+        const WaveDir dnn = dir_take(dv);
+        load_cols<1>(A, dn, p, lane, cur);  // bucket bn (no loads past the range: empty dir)
+        load_perm<1>(A, dnn, lane, p);      // bucket bn + stride
+        dn = dnn;
+        dv = dir_issue(bn + 2 * stride);
+      });
+      if (bn >= hi) break;
+      b = bn;
+    }
+  } else {
+    WaveDir dc = dir_take(dir_issue(b));  // this bucket (its row indices are in p)
+    load_perm<1>(A, dc, lane, p);
+    uint32_t dv = dir_issue(b + stride);
+    for (;;) {
+      const uint32_t bn = b + stride;
+      load_cols<1>(A, dc, p, lane, cur);
+      wave_bucket<1>(W, lds_all[wv], b, lane, cur, [&]() {
+        dc = dir_take(dv);             // bucket bn
+        load_perm<1>(A, dc, lane, p);
+        dv = dir_issue(bn + stride);
+      });
+      if (bn >= hi) break;
+      b = bn;
+    }
+  }
+}
+
 // Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2). Remap so
 // that XCD x runs one contiguous range of blocks: neighbouring buckets share a final
 // partition segment, whose rows then stay in one L2.
 __device__ __forceinline__ uint32_t xcd_block(uint32_t i, uint32_t G) {
-  constexpr uint32_t kXcd = 8;
-  const uint32_t q = G / kXcd, r = G % kXcd, x = i % kXcd, j = i / kXcd;
+  const uint32_t q = G / kXcds, r = G % kXcds, x = i % kXcds, j = i / kXcds;
   return x * q + min(x, r) + j;
 }
 
-// Every bucket, one wave each (<= 64 key rows, <= 128 child rows per wave).
-__global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_kernel(WaveArgs W) {
+// G > 0: each wave runs G consecutive buckets (the grid covers every bucket once, in
+// dispatch order, so the chip's active buckets stay a narrow window of the bucket range);
+// G == 0: persistent grid, XCD x sweeps [x nb/8, (x+1) nb/8) with its waves round-robin.
+template <int PF>
+__device__ __forceinline__ void wave_dispatch(const WaveArgs& W, WaveLds<1>* lds_all, uint32_t G) {
+  const int wv = threadIdx.x >> 6;
+  if (G) {
+    const uint32_t b0 = (xcd_block(blockIdx.x, gridDim.x) * kWavesPerWG + wv) * G;
+    wave_stream<PF>(W, lds_all, b0, min(W.nbuckets, b0 + G), 1);
+  } else {
+    const uint32_t x = blockIdx.x % kXcds;
+    const uint32_t lo = (uint32_t)((uint64_t)W.nbuckets * x / kXcds);
+    const uint32_t hi = (uint32_t)((uint64_t)W.nbuckets * (x + 1) / kXcds);
+    wave_stream<PF>(W, lds_all, lo + (blockIdx.x / kXcds) * kWavesPerWG + wv, hi,
+                    (gridDim.x / kXcds) * kWavesPerWG);
+  }
+}
+
+__global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_kernel(WaveArgs W, uint32_t G) {
   __shared__ WaveLds<1> lds_all[kWavesPerWG];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t b = xcd_block(blockIdx.x, gridDim.x) * kWavesPerWG + wv;
-  if (b >= W.nbuckets) return;
-  wave_bucket<1>(W, lds_all[wv], b, lane);
+  wave_dispatch<2>(W, lds_all, G);
+}
+__global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_pf1_kernel(WaveArgs W, uint32_t G) {
+  __shared__ WaveLds<1> lds_all[kWavesPerWG];
+  wave_dispatch<1>(W, lds_all, G);
 }
 
 // Buckets over bucket_wave_kernel's capacity but within this kernel's.
@@ -563,7 +723,13 @@ __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_kernel(WaveArgs 
     while (m) {
       const int i = __builtin_ctzll(m);
       m &= m - 1;
-      wave_bucket<2>(W, lds_all[wv], g * 64 + i, lane);
+      const uint32_t bb = g * 64 + i;
+      const WaveDir d = load_dir(W.A, bb);
+      WavePerm<2> p;
+      WaveIn<2> in;
+      load_perm<2>(W.A, d, lane, p);
+      load_cols<2>(W.A, d, p, lane, in);
+      wave_bucket<2>(W, lds_all[wv], bb, lane, in, []() {});
     }
   }
   if (lane == 0 && found) atomicAdd(&stat_shard(W.A.stats)[ST_WIDE], found);

@@ -15,6 +15,7 @@ struct cdb_ctx {
   std::string last_error;
   struct Buf { void* p = nullptr; size_t bytes = 0; };
   Buf ws[32];  // named workspace slots, grown on demand, reused across calls
+  uint32_t wave_slots[2] = {0, 0};  // resident streaming-wave-kernel workgroups per variant (0 = not queried)
 };
 
 namespace cdb {
@@ -33,6 +34,7 @@ enum WsSlot {
 
 cdb_status fail(cdb_ctx* ctx, cdb_status st, const std::string& msg);
 cdb_status hip_check(cdb_ctx* ctx, hipError_t e, const char* what);
+cdb_status launch_check(cdb_ctx* ctx, hipStream_t s, const char* what);
 void* ws_get(cdb_ctx* ctx, int slot, size_t bytes, cdb_status* st);
 
 }  // namespace cdb

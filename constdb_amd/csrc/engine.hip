@@ -25,6 +25,15 @@ cdb_status hip_check(cdb_ctx* ctx, hipError_t e, const char* what) {
               std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Launch check. With CDB_SYNC_CHECK set, also synchronises so that a device fault is
+// reported at the kernel that caused it (debugging aid; off in normal runs).
+cdb_status launch_check(cdb_ctx* ctx, hipStream_t s, const char* what) {
+  static const bool sync = std::getenv("CDB_SYNC_CHECK") != nullptr;
+  cdb_status st = hip_check(ctx, hipGetLastError(), what);
+  if (st == CDB_OK && sync) st = hip_check(ctx, hipStreamSynchronize(s), what);
+  return st;
+}
+
 void* ws_get(cdb_ctx* ctx, int slot, size_t bytes, cdb_status* st) {
   cdb_ctx::Buf& b = ctx->ws[slot];
   if (b.bytes >= bytes && b.p) return b.p;
@@ -169,7 +178,7 @@ cdb_status exclusive_scan(cdb_ctx* ctx, const T* in, uint64_t n, OutT* out, OutT
   scan_reduce_kernel<T><<<tiles, kScanThreads, 0, s>>>(in, n, sums);
   scan_sums_kernel<<<1, kScanThreads, 0, s>>>(sums, tiles, d_total);
   scan_apply_kernel<T, OutT><<<tiles, kScanThreads, 0, s>>>(in, n, sums, out, out2);
-  return hip_check(ctx, hipGetLastError(), "scan");
+  return launch_check(ctx, s, "scan");
 }
 
 struct Dir {  // per-family bucket directory
@@ -187,7 +196,9 @@ Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
   // Wave-sized buckets: ~40 key rows and ~40 child rows (nodes + members) on average.
   // A wave holds 64 key rows (128 in the wide kernel) and 128 child rows, so only the
   // far tail of the bucket-size distribution reaches the workgroup tier.
-  const uint64_t want = std::max<uint64_t>({(K + 39) / 40, (N + M + 39) / 40, 1});
+  uint64_t target = 40;
+  if (const char* e = std::getenv("CDB_PLAN_TARGET")) target = (uint64_t)std::max(8, std::min(60, std::atoi(e)));
+  const uint64_t want = std::max<uint64_t>({(K + target - 1) / target, (N + M + target - 1) / target, 1});
   Plan p;
   if (want <= 1) return p;
   // The last level moves only a row index, so it takes a large fan-out (segments of
@@ -248,6 +259,7 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const
     const uint64_t ncur = nprev * plan.d[l];
     CDB_HIP(hipMemsetAsync(d.hist, 0, ncur * sizeof(uint32_t), s), "memset hist");
     part_hist_kernel<<<tiles, kPartThreads, 0, s>>>(cur[0], n, nprev, plan.d[l], shift, d.hist);
+    CDB_TRY(launch_check(ctx, s, "part_hist"));
     CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, d.hist, ncur, d.base, d.cursor, nullptr, s));
     ColSet<NC> ci, co;
     for (int c = 0; c < NC; ++c) {
@@ -257,10 +269,10 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const
     if (last) {
       part_scatter_kernel<1, true><<<tiles, kPartThreads, 0, s>>>(ColSet<1>{{ci.c[0]}}, ColSet<1>{{nullptr}}, n,
                                                                   nprev, plan.d[l], shift, d.cursor, perm);
-      CDB_HIP(hipGetLastError(), "partition (index level)");
+      CDB_TRY(launch_check(ctx, s, "partition (index level)"));
     } else {
       part_scatter_kernel<NC><<<tiles, kPartThreads, 0, s>>>(ci, co, n, nprev, plan.d[l], shift, d.cursor);
-      CDB_HIP(hipGetLastError(), "partition");
+      CDB_TRY(launch_check(ctx, s, "partition"));
       cur = dst;
     }
     nprev = ncur;
@@ -271,6 +283,45 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const
     spare[c] = other[c];
   }
   return CDB_OK;
+}
+
+// Persistent launch of the streaming wave kernel: every resident workgroup slot of the chip
+// once, a multiple of the 8 XCDs, and no more workgroups than there are buckets to share out.
+// CDB_WAVE_PF=1 selects the variant that prefetches only row indices (see bucket_wave.hip.h).
+bool wave_pf1() {
+  static const bool pf1 = [] {
+    const char* e = std::getenv("CDB_WAVE_PF");
+    return e && std::atoi(e) == 1;
+  }();
+  return pf1;
+}
+
+// Buckets per wave of the wave kernel (CDB_WAVE_G; 0 = persistent grid).
+uint32_t wave_g() {
+  static const uint32_t g = [] {
+    const char* e = std::getenv("CDB_WAVE_G");
+    return e ? (uint32_t)std::max(0, std::min(64, std::atoi(e))) : 4u;
+  }();
+  return g;
+}
+
+uint32_t wave_grid(cdb_ctx* ctx, uint64_t nb) {
+  if (const uint32_t G = wave_g()) return (uint32_t)((nb + (uint64_t)G * kWavesPerWG - 1) / ((uint64_t)G * kWavesPerWG));
+  const int v = wave_pf1() ? 1 : 0;
+  if (!ctx->wave_slots[v]) {
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus < 1)
+      cus = 256;
+    const hipError_t e = v ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bucket_wave_pf1_kernel,
+                                                                         kWavesPerWG * 64, 0)
+                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bucket_wave_kernel,
+                                                                         kWavesPerWG * 64, 0);
+    if (e != hipSuccess || per_cu < 1) per_cu = 1;
+    ctx->wave_slots[v] = (uint32_t)(cus * per_cu);
+  }
+  const uint64_t want = (nb + kWavesPerWG - 1) / kWavesPerWG;
+  const uint64_t g = std::min<uint64_t>(ctx->wave_slots[v], want);
+  return (uint32_t)std::max<uint64_t>(kXcds, (g + kXcds - 1) / kXcds * kXcds);
 }
 
 }  // namespace
@@ -350,11 +401,36 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     for (int c = 0; c < 8; ++c) ksp[c] = free_k[c];
   }
 
+  if (std::getenv("CDB_VERIFY_PARTITION")) {  // debugging aid: perm must be a permutation
+    CDB_HIP(hipStreamSynchronize(s), "sync");
+    const uint64_t fam_n[3] = {K, N, M};
+    const uint32_t* fam_p[3] = {kperm, nperm, mperm};
+    const Dir* fam_d[3] = {&dk, &dnd, &dm};
+    for (int f = 0; f < 3; ++f) {
+      const uint64_t n = fam_n[f];
+      if (!n) continue;
+      std::vector<uint32_t> hp(n), hb(nb), hc(nb);
+      CDB_HIP(hipMemcpy(hp.data(), fam_p[f], n * 4, hipMemcpyDeviceToHost), "d2h");
+      CDB_HIP(hipMemcpy(hb.data(), fam_d[f]->base, nb * 4, hipMemcpyDeviceToHost), "d2h");
+      CDB_HIP(hipMemcpy(hc.data(), fam_d[f]->hist, nb * 4, hipMemcpyDeviceToHost), "d2h");
+      std::vector<uint8_t> seen(n, 0);
+      uint64_t bad = 0, tot = 0;
+      for (uint64_t i = 0; i < n; ++i) {
+        if (hp[i] >= n || seen[hp[i]]) ++bad;
+        else seen[hp[i]] = 1;
+      }
+      for (uint64_t b = 0; b < nb; ++b) tot += hc[b];
+      if (bad || tot != n)
+        return fail(ctx, CDB_DEVICE_ERROR, "partition verify: family " + std::to_string(f) + " n=" + std::to_string(n) +
+                                               " bad=" + std::to_string(bad) + " total=" + std::to_string(tot) +
+                                               " levels=" + std::to_string(plan.levels) + " nb=" + std::to_string(nb));
+    }
+  }
   CDB_HIP(hipEventRecord(ctx->ev_part, s), "event");
   // ---- 2. GC watermark scan (DB::gc's LIFO stop point)
   if ((flags & CDB_MERGE_GC_DELETES) && K) {
     gc_lastbad_kernel<<<1024, 256, 0, s>>>(in->keys.col[K_CT], in->keys.col[K_META], K, wm, d_last_bad);
-    CDB_HIP(hipGetLastError(), "gc_lastbad");
+    CDB_TRY(launch_check(ctx, s, "gc_lastbad"));
   }
 
   // ---- 3. fused bucket merge
@@ -388,13 +464,16 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   WA.nbuckets = (uint32_t)nb;
   WA.big_list = d_big_list;
   WA.big_count = d_big_count;
-  bucket_wave_kernel<<<(nb + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, 0, s>>>(WA);
-  CDB_HIP(hipGetLastError(), "bucket_wave_kernel");
+  if (wave_pf1())
+    bucket_wave_pf1_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
+  else
+    bucket_wave_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
+  CDB_TRY(launch_check(ctx, s, "bucket_wave_kernel"));
   bucket_wide_kernel<<<(uint32_t)std::min<uint64_t>((nb + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024),
                        kWavesPerWG * 64, 0, s>>>(WA);
-  CDB_HIP(hipGetLastError(), "bucket_wide_kernel");
+  CDB_TRY(launch_check(ctx, s, "bucket_wide_kernel"));
   bucket_mid_kernel<<<std::min<uint64_t>(nb, 2048), kBktThreads, 0, s>>>(A, d_big_list, d_big_count);
-  CDB_HIP(hipGetLastError(), "bucket_mid_kernel");
+  CDB_TRY(launch_check(ctx, s, "bucket_mid_kernel"));
   CDB_HIP(hipEventRecord(ctx->ev_bucket, s), "event");
 
   // ---- 4. over-capacity buckets (same algorithm, global scratch)
@@ -426,7 +505,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     A.hot_scratch = (uint64_t*)slab;
     A.hot_scratch_off = d_off;
     bucket_hot_kernel<<<hot, kBktThreads, 0, s>>>(A);
-    CDB_HIP(hipGetLastError(), "bucket_hot_kernel");
+    CDB_TRY(launch_check(ctx, s, "bucket_hot_kernel"));
   }
 
   // ---- 5. dense compaction into the caller's output columns
@@ -449,9 +528,9 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   C.kdoff = dk.doff; C.ndoff = dnd.doff; C.mdoff = dm.doff;
   compact_kernel<<<(uint32_t)std::min<uint64_t>((nb + 64 * kCompactWaves - 1) / (64 * kCompactWaves), 16384),
                    64 * kCompactWaves, 0, s>>>(C, (uint32_t)nb);
-  CDB_HIP(hipGetLastError(), "compact_kernel");
+  CDB_TRY(launch_check(ctx, s, "compact_kernel"));
   stats_reduce_kernel<<<1, 64, 0, s>>>(d_shards, d_stats);
-  CDB_HIP(hipGetLastError(), "stats_reduce_kernel");
+  CDB_TRY(launch_check(ctx, s, "stats_reduce_kernel"));
   CDB_HIP(hipEventRecord(ctx->ev1, s), "event");
 
   uint64_t totals[3];
@@ -584,7 +663,7 @@ cdb_status cdb_partition_owner(cdb_ctx* ctx, const cdb_dev_rows* in, int ncols, 
       for (int c = 0; c < 8; ++c) { ci.c[c] = in->col[c]; co.c[c] = out->col[c]; }
       part_scatter_kernel<8><<<tiles, kPartThreads, 0, s>>>(ci, co, n, 1, (uint32_t)nb, 0, cursor);
     }
-    CDB_HIP(hipGetLastError(), "partition_owner");
+    CDB_TRY(launch_check(ctx, s, "partition_owner"));
   }
   std::vector<uint32_t> h(nb, 0);
   CDB_HIP(hipMemcpyAsync(h.data(), hist, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");

@@ -18,10 +18,11 @@
 namespace cdb {
 namespace {  // internal linkage: included by several translation units
 
-constexpr int kPartThreads = 512;
-constexpr int kPartTile = 4096;       // rows per workgroup tile
+constexpr int kPartThreads = 1024;
+constexpr int kPartTile = 8192;       // rows staged through LDS at once (one sub-tile)
 constexpr int kPartRowsPerThread = kPartTile / kPartThreads;
 constexpr int kPartLocalMax = 2048;   // local (tile) bucket slots held in LDS
+constexpr int kPF = 2;                // partition scatter: columns prefetched ahead
 
 template <int NC>
 struct ColSet {
@@ -34,15 +35,16 @@ struct ColSet {
 __device__ __forceinline__ uint64_t bucket_of_n(uint64_t h, uint64_t nb) { return __umul64hi(h, nb); }
 
 // ---------------------------------------------------------------- histogram
-// hist[gb] += number of rows whose top `btot` bits of col0 are gb. Rows arrive grouped by
-// their top `btot - db` bits (the previous level's output), so a tile spans few prefixes.
+// hist[gb] += number of rows in bucket gb. Rows arrive grouped by their previous-level
+// bucket, so a workgroup's kPartTile rows span few parents and count in LDS; one global
+// atomic per (workgroup, touched bucket).
 __global__ void __launch_bounds__(kPartThreads) part_hist_kernel(const uint64_t* __restrict__ col0, uint64_t n,
                                                                  uint64_t nprev, uint32_t d, int shift,
                                                                  uint32_t* __restrict__ hist) {
   __shared__ uint32_t cnt[kPartLocalMax];
   const uint64_t tile0 = (uint64_t)blockIdx.x * kPartTile;
   if (tile0 >= n) return;
-  const uint64_t tile1 = min(n, tile0 + kPartTile);
+  const uint64_t tile1 = tile0 + kPartTile < n ? tile0 + kPartTile : n;
   const uint64_t ncur = nprev * d;
   const uint64_t plo = bucket_of_n(col0[tile0] << shift, nprev);
   const uint64_t phi = bucket_of_n(col0[tile1 - 1] << shift, nprev);
@@ -62,69 +64,17 @@ __global__ void __launch_bounds__(kPartThreads) part_hist_kernel(const uint64_t*
       if (cnt[i]) atomicAdd(&hist[glo + i], cnt[i]);
 }
 
-// ---------------------------------------------------------------- scatter
-// Moves every column of every row to out[cursor[gb]++] (per-tile ranges reserved with one
-// global atomic per touched bucket). Columns are staged through LDS in bucket order so
-// that each wave's stores are contiguous runs. IDX: index-only final level — writes the
-// u32 row index (to perm) instead of moving the NC columns.
-template <int NC, bool IDX = false>
-__global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> in, ColSet<NC> out, uint64_t n,
-                                                                    uint64_t nprev, uint32_t d, int shift,
-                                                                    uint32_t* __restrict__ cursor,
-                                                                    uint32_t* __restrict__ perm = nullptr) {
-  __shared__ uint32_t cnt[kPartLocalMax];   // per local bucket: count, then scan
-  __shared__ uint32_t gbase[kPartLocalMax]; // reserved global start per local bucket
-  __shared__ uint16_t slot_lb[kPartTile];   // local bucket of each staged slot
-  __shared__ uint64_t stage[kPartTile];
-  const uint64_t tile0 = (uint64_t)blockIdx.x * kPartTile;
-  if (tile0 >= n) return;
-  const uint64_t tile1 = min(n, tile0 + kPartTile);
-  const int rows = (int)(tile1 - tile0);
-  const uint64_t ncur = nprev * d;
-  const uint64_t plo = bucket_of_n(in.c[0][tile0] << shift, nprev);
-  const uint64_t phi = bucket_of_n(in.c[0][tile1 - 1] << shift, nprev);
-  const uint64_t glo = plo * d;
-  const uint64_t span = (phi - plo + 1) * d;
-
-  if (span > (uint64_t)kPartLocalMax) {  // wide tile: per-row global reservation
-    for (int r = threadIdx.x; r < rows; r += kPartThreads) {
-      const uint64_t gb = bucket_of_n(in.c[0][tile0 + r] << shift, ncur);
-      const uint32_t d = atomicAdd(&cursor[gb], 1u);
-      if (IDX) {
-        perm[d] = (uint32_t)(tile0 + r);
-      } else {
-#pragma unroll
-        for (int c = 0; c < NC; ++c) out.c[c][d] = in.c[c][tile0 + r];
-      }
-    }
-    return;
-  }
-  for (int i = threadIdx.x; i < kPartLocalMax; i += kPartThreads) cnt[i] = 0;
-  __syncthreads();
-  uint16_t lb[kPartRowsPerThread];
-  uint32_t rk[kPartRowsPerThread];
-#pragma unroll
-  for (int k = 0; k < kPartRowsPerThread; ++k) {
-    const int r = threadIdx.x + k * kPartThreads;
-    if (r < rows) {
-      lb[k] = (uint16_t)(bucket_of_n(in.c[0][tile0 + r] << shift, ncur) - glo);
-      rk[k] = atomicAdd(&cnt[lb[k]], 1u);
-    }
-  }
-  __syncthreads();
-  // reserve global ranges, then turn cnt into an exclusive scan (single wave scan)
-  for (int i = threadIdx.x; i < (int)span; i += kPartThreads)
-    if (cnt[i]) gbase[i] = atomicAdd(&cursor[glo + i], cnt[i]);
-  __syncthreads();
+// Exclusive scan of a[0..span) in place by the first wave; returns nothing (LDS result).
+__device__ __forceinline__ void wave0_exclusive_scan(uint32_t* a, int span) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    const int per = ((int)span + 63) / 64;
+    const int per = (span + 63) / 64;
     uint32_t s = 0;
     for (int j = 0; j < per; ++j) {
       const int i = lane * per + j;
-      if (i < (int)span) s += cnt[i];
+      if (i < span) s += a[i];
     }
-    uint32_t incl = s;  // wave-wide inclusive scan of per-lane sums
+    uint32_t incl = s;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t v = __shfl_up(incl, o, 64);
       if (lane >= o) incl += v;
@@ -132,14 +82,84 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
     uint32_t run = incl - s;
     for (int j = 0; j < per; ++j) {
       const int i = lane * per + j;
-      if (i < (int)span) {
-        const uint32_t c = cnt[i];
-        cnt[i] = run;
+      if (i < span) {
+        const uint32_t c = a[i];
+        a[i] = run;
         run += c;
       }
     }
   }
+}
+
+// ---------------------------------------------------------------- scatter
+// Moves every column of every row of a kPartTile tile to its bucket's range (one global
+// atomic per (tile, touched bucket) reserves it). Columns are staged through LDS in bucket
+// order so that each wave's stores are contiguous runs; column c + kPF is requested before
+// column c is staged. IDX: index-only final level — writes the u32 row index (to perm)
+// instead of moving the NC columns.
+template <int NC, bool IDX = false>
+__global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> in, ColSet<NC> out, uint64_t n,
+                                                                    uint64_t nprev, uint32_t d, int shift,
+                                                                    uint32_t* __restrict__ cursor,
+                                                                    uint32_t* __restrict__ perm = nullptr) {
+  __shared__ uint32_t cnt[kPartLocalMax];   // per local bucket: count, then its exclusive scan
+  __shared__ uint32_t delta[kPartLocalMax]; // global row of staged slot j = delta[bucket] + j
+  __shared__ uint16_t slot_lb[kPartTile];   // local bucket of each staged slot
+  __shared__ uint64_t stage[kPartTile];
+  const uint64_t tile0 = (uint64_t)blockIdx.x * kPartTile;
+  if (tile0 >= n) return;
+  const uint64_t tile1 = tile0 + kPartTile < n ? tile0 + kPartTile : n;
+  const int rows = (int)(tile1 - tile0);
+  const uint64_t ncur = nprev * d;
+  const uint64_t plo = bucket_of_n(in.c[0][tile0] << shift, nprev);
+  const uint64_t phi = bucket_of_n(in.c[0][tile1 - 1] << shift, nprev);
+  const uint64_t glo = plo * d;
+  const uint64_t span64 = (phi - plo + 1) * d;
+
+  if (span64 > (uint64_t)kPartLocalMax) {  // wide tile: per-row global reservation
+    for (int r = threadIdx.x; r < rows; r += kPartThreads) {
+      const uint64_t gb = bucket_of_n(in.c[0][tile0 + r] << shift, ncur);
+      const uint32_t p = atomicAdd(&cursor[gb], 1u);
+      if (IDX) {
+        perm[p] = (uint32_t)(tile0 + r);
+      } else {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) out.c[c][p] = in.c[c][tile0 + r];
+      }
+    }
+    return;
+  }
+  const int span = (int)span64;
+  for (int i = threadIdx.x; i < span; i += kPartThreads) cnt[i] = 0;
+  constexpr int NV = IDX ? 1 : NC;
+  uint64_t v[NV][kPartRowsPerThread];
+  auto load_col = [&](int c) {
+#pragma unroll
+    for (int k = 0; k < kPartRowsPerThread; ++k) {
+      const int r = threadIdx.x + k * kPartThreads;
+      v[c][k] = r < rows ? __builtin_nontemporal_load(&in.c[c][tile0 + r]) : 0;
+    }
+  };
+#pragma unroll
+  for (int c = 0; c < (NV < kPF ? NV : kPF); ++c) load_col(c);
   __syncthreads();
+  uint16_t lb[kPartRowsPerThread];
+  uint32_t rk[kPartRowsPerThread];
+#pragma unroll
+  for (int k = 0; k < kPartRowsPerThread; ++k) {
+    const int r = threadIdx.x + k * kPartThreads;
+    if (r < rows) {
+      lb[k] = (uint16_t)(bucket_of_n(v[0][k] << shift, ncur) - glo);
+      rk[k] = atomicAdd(&cnt[lb[k]], 1u);
+    }
+  }
+  __syncthreads();
+  // reserve each touched bucket's range, then scan the counts
+  for (int i = threadIdx.x; i < span; i += kPartThreads) delta[i] = cnt[i] ? atomicAdd(&cursor[glo + i], cnt[i]) : 0;
+  __syncthreads();
+  wave0_exclusive_scan(cnt, span);
+  __syncthreads();
+  for (int i = threadIdx.x; i < span; i += kPartThreads) delta[i] -= cnt[i];
   uint32_t slot[kPartRowsPerThread];
 #pragma unroll
   for (int k = 0; k < kPartRowsPerThread; ++k) {
@@ -158,24 +178,19 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
       if (r < rows) st32[slot[k]] = (uint32_t)(tile0 + r);
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < rows; j += kPartThreads) {
-      const int b = slot_lb[j];
-      perm[gbase[b] + (j - cnt[b])] = st32[j];
-    }
+    for (int j = threadIdx.x; j < rows; j += kPartThreads) perm[delta[slot_lb[j]] + j] = st32[j];
     return;
   }
-#pragma unroll 1
-  for (int c = 0; c < NC; ++c) {
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    if (c + kPF < NV) load_col(c + kPF < NV ? c + kPF : 0);
 #pragma unroll
     for (int k = 0; k < kPartRowsPerThread; ++k) {
       const int r = threadIdx.x + k * kPartThreads;
-      if (r < rows) stage[slot[k]] = in.c[c][tile0 + r];
+      if (r < rows) stage[slot[k]] = v[c][k];
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < rows; j += kPartThreads) {
-      const int b = slot_lb[j];
-      out.c[c][gbase[b] + (j - cnt[b])] = stage[j];
-    }
+    for (int j = threadIdx.x; j < rows; j += kPartThreads) out.c[c][delta[slot_lb[j]] + j] = stage[j];
     __syncthreads();
   }
 }
