@@ -693,7 +693,23 @@ __device__ __forceinline__ void wave_dispatch(const WaveArgs& W, WaveLds<1>* lds
   }
 }
 
-__global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_kernel(WaveArgs W, uint32_t G) {
+// One bucket per wave, no loop: the fewest live registers and so the most resident waves
+// (5 per SIMD), which is what hides the bucket's memory round trips best (measured: the
+// pipelined variants below lose more to their lower occupancy than they gain).
+__global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_kernel(WaveArgs W) {
+  __shared__ WaveLds<1> lds_all[kWavesPerWG];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t b = xcd_block(blockIdx.x, gridDim.x) * kWavesPerWG + wv;
+  if (b >= W.nbuckets) return;
+  const WaveDir d = load_dir(W.A, b);
+  WavePerm<1> p;
+  WaveIn<1> in;
+  load_perm<1>(W.A, d, lane, p);
+  load_cols<1>(W.A, d, p, lane, in);
+  wave_bucket<1>(W, lds_all[wv], b, lane, in, []() {});
+}
+
+__global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_pf2_kernel(WaveArgs W, uint32_t G) {
   __shared__ WaveLds<1> lds_all[kWavesPerWG];
   wave_dispatch<2>(W, lds_all, G);
 }

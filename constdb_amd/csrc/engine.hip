@@ -285,36 +285,37 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const
   return CDB_OK;
 }
 
-// Persistent launch of the streaming wave kernel: every resident workgroup slot of the chip
-// once, a multiple of the 8 XCDs, and no more workgroups than there are buckets to share out.
-// CDB_WAVE_PF=1 selects the variant that prefetches only row indices (see bucket_wave.hip.h).
-bool wave_pf1() {
-  static const bool pf1 = [] {
+// Wave-kernel variant (CDB_WAVE_PF, default 0): 0 = one bucket per wave (bucket_wave_kernel);
+// 1 / 2 = the software-pipelined kernels, which prefetch the next bucket's row indices (1)
+// or also its columns (2) and run CDB_WAVE_G buckets per wave (0 = a persistent grid).
+int wave_pf() {
+  static const int pf = [] {
     const char* e = std::getenv("CDB_WAVE_PF");
-    return e && std::atoi(e) == 1;
+    return e ? std::max(0, std::min(2, std::atoi(e))) : 0;
   }();
-  return pf1;
+  return pf;
 }
 
-// Buckets per wave of the wave kernel (CDB_WAVE_G; 0 = persistent grid).
 uint32_t wave_g() {
   static const uint32_t g = [] {
     const char* e = std::getenv("CDB_WAVE_G");
-    return e ? (uint32_t)std::max(0, std::min(64, std::atoi(e))) : 4u;
+    return e ? (uint32_t)std::max(0, std::min(64, std::atoi(e))) : 8u;
   }();
   return g;
 }
 
 uint32_t wave_grid(cdb_ctx* ctx, uint64_t nb) {
+  const int pf = wave_pf();
+  if (pf == 0) return (uint32_t)((nb + kWavesPerWG - 1) / kWavesPerWG);
   if (const uint32_t G = wave_g()) return (uint32_t)((nb + (uint64_t)G * kWavesPerWG - 1) / ((uint64_t)G * kWavesPerWG));
-  const int v = wave_pf1() ? 1 : 0;
-  if (!ctx->wave_slots[v]) {
+  const int v = pf - 1;
+  if (!ctx->wave_slots[v]) {  // persistent: every resident workgroup slot once, a multiple of 8
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus < 1)
       cus = 256;
-    const hipError_t e = v ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bucket_wave_pf1_kernel,
+    const hipError_t e = v ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bucket_wave_pf2_kernel,
                                                                          kWavesPerWG * 64, 0)
-                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bucket_wave_kernel,
+                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bucket_wave_pf1_kernel,
                                                                          kWavesPerWG * 64, 0);
     if (e != hipSuccess || per_cu < 1) per_cu = 1;
     ctx->wave_slots[v] = (uint32_t)(cus * per_cu);
@@ -464,10 +465,12 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   WA.nbuckets = (uint32_t)nb;
   WA.big_list = d_big_list;
   WA.big_count = d_big_count;
-  if (wave_pf1())
+  if (wave_pf() == 0)
+    bucket_wave_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA);
+  else if (wave_pf() == 1)
     bucket_wave_pf1_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
   else
-    bucket_wave_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
+    bucket_wave_pf2_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
   CDB_TRY(launch_check(ctx, s, "bucket_wave_kernel"));
   bucket_wide_kernel<<<(uint32_t)std::min<uint64_t>((nb + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024),
                        kWavesPerWG * 64, 0, s>>>(WA);

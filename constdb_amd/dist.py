@@ -50,19 +50,59 @@ def exchange_counts(send_counts: Sequence[Sequence[int]], device=None) -> List[L
     return [[r[s][f] for s in range(world)] for f in range(nf)]
 
 
-def exchange_columns(send_cols, send_counts: Sequence[int], recv_counts: Sequence[int], recv_cols=None):
+# Largest piece one (source, destination) pair moves in one collective: RCCL's point-to-point
+# transfers misbehave past 2^31 bytes (a 2.2 GB self-transfer never completed on MI355X), so
+# bigger pairs move in several rounds.
+MAX_PIECE_BYTES = 1 << 30
+
+
+def exchange_columns(send_cols, send_counts: Sequence[int], recv_counts: Sequence[int], recv_cols=None,
+                     max_piece_bytes: int = MAX_PIECE_BYTES):
     """All-to-all of one family's columns. send_cols: list of 1-D int64 tensors grouped by
     destination (rows for rank 0 first, ...). Returns the received columns (source-rank
-    order). Works with any torch.distributed backend (RCCL on GPUs, gloo in CPU tests)."""
+    order). Works with any torch.distributed backend (RCCL on GPUs, gloo in CPU tests).
+    Each column moves with dist.all_to_all over per-peer views (no staging copies), in as
+    many rounds as the largest (source, destination) piece needs."""
     import torch
     import torch.distributed as dist
+    world = len(send_counts)
     total = int(sum(recv_counts))
+    soff = [0] * (world + 1)
+    roff = [0] * (world + 1)
+    for d in range(world):
+        soff[d + 1] = soff[d] + int(send_counts[d])
+        roff[d + 1] = roff[d] + int(recv_counts[d])
     out = []
     for c, col in enumerate(send_cols):
         dst = recv_cols[c][:total] if recv_cols is not None else torch.empty(total, dtype=col.dtype,
                                                                              device=col.device)
-        dist.all_to_all_single(dst, col, output_split_sizes=list(map(int, recv_counts)),
-                               input_split_sizes=list(map(int, send_counts)))
+        piece = max(1, max_piece_bytes // col.element_size())
+        # every rank runs the same number of rounds: the largest pair anywhere decides
+        most = torch.tensor([max(max(send_counts), max(recv_counts))], dtype=torch.int64, device=col.device)
+        dist.all_reduce(most, op=dist.ReduceOp.MAX)
+        rounds = max(1, -(-int(most.item()) // piece))
+        if rounds == 1:
+            dist.all_to_all_single(dst, col[:soff[world]], output_split_sizes=[int(x) for x in recv_counts],
+                                   input_split_sizes=[int(x) for x in send_counts])
+            out.append(dst)
+            continue
+        lists = dist.get_backend() != "gloo"  # gloo has no list all_to_all: stage each round
+        for r in range(rounds):
+            a = r * piece
+            ins = [col[soff[d] + min(a, int(send_counts[d])): soff[d] + min(a + piece, int(send_counts[d]))]
+                   for d in range(world)]
+            outs = [dst[roff[s] + min(a, int(recv_counts[s])): roff[s] + min(a + piece, int(recv_counts[s]))]
+                    for s in range(world)]
+            if lists:
+                dist.all_to_all(outs, ins)
+            else:
+                got = torch.empty(sum(o.numel() for o in outs), dtype=col.dtype, device=col.device)
+                dist.all_to_all_single(got, torch.cat(ins), output_split_sizes=[o.numel() for o in outs],
+                                       input_split_sizes=[i.numel() for i in ins])
+                k = 0
+                for o in outs:
+                    o.copy_(got[k:k + o.numel()])
+                    k += o.numel()
         out.append(dst)
     return out
 
@@ -76,12 +116,18 @@ def _rows_from_tensor(cdb, t, n):
     return r
 
 
+def _log(rank, msg):
+    import sys
+    print(f"[rank {rank} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local_rank)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
+    _log(rank, "process group up")
     ob = owner_bits(world)
     L = cdb.lib()
     ctx = cdb.Context(local_rank)
@@ -91,6 +137,7 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
     cfg = c4_config(cdb, universe, R, args.seed, lo, hi)
     din = cdb.DevInput()
     ctx.check(L.cdb_gen_device(ctx.handle, ctypes.byref(cfg), ctypes.byref(din)))
+    _log(rank, f"generated {din.keys.n} key rows")
     fams_in = [din.keys, din.nodes, din.members]
     n_in = [f.n for f in fams_in]
     send = [torch.empty((FAMILY_COLS[f], max(n_in[f], 1)), dtype=torch.int64, device=dev) for f in range(3)]
@@ -99,16 +146,27 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
     st = cdb.MergeStats()
     counts = (ctypes.c_uint64 * world)()
     state = {}
+    # One explicit stream for the whole step: torch makes it wait for each RCCL collective, and
+    # the library's kernels run on it too (the legacy default stream's handle is 0, which the
+    # library would read as "use the context's own stream" -- unordered with the exchange).
+    cs = torch.cuda.Stream(device=dev)
 
     def step():
+        with torch.cuda.stream(cs):
+            _step()
+
+    def _step():
         stream = torch.cuda.current_stream().cuda_stream
+        assert stream, "the merge must run on the exchange's (non-default) stream"
         send_counts = []
         for f in range(3):
             out_rows = _rows_from_tensor(cdb, send[f], n_in[f])
             ctx.check(L.cdb_partition_owner(ctx.handle, ctypes.byref(fams_in[f]), FAMILY_COLS[f], ob,
                                             ctypes.byref(out_rows), counts, ctypes.c_void_p(stream)))
             send_counts.append([counts[d] for d in range(world)])
+        _log(rank, "packed") if not state.get("quiet") else None
         recv_counts = exchange_counts(send_counts, device=dev)
+        _log(rank, f"counts exchanged {recv_counts}") if not state.get("quiet") else None
         recv = []
         for f in range(3):
             total = sum(recv_counts[f])
@@ -120,6 +178,9 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
             cols = [send[f][c][:n_in[f]] for c in range(FAMILY_COLS[f])]
             exchange_columns(cols, send_counts[f], recv_counts[f], recv_cols=buf)
             recv.append((buf, total))
+        if not state.get("quiet"):  # first (warmup) step: locate a stall in the log
+            torch.cuda.current_stream().synchronize()
+            _log(rank, "rows exchanged")
         din2 = cdb.DevInput()
         din2.keys = _rows_from_tensor(cdb, recv[0][0], recv[0][1])
         din2.nodes = _rows_from_tensor(cdb, recv[1][0], recv[1][1])
@@ -140,9 +201,12 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
         dout.compact = 1
         ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(din2), ctypes.byref(opts), ctypes.byref(dout),
                                      ctypes.byref(st), ctypes.c_void_p(stream)))
+        _log(rank, "merged") if not state.get("quiet") else None
+        state["quiet"] = True
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
         step()
+        _log(rank, f"warmup step {i} done")
     bucket_ms = 0.0
     dist.barrier()
     torch.cuda.synchronize()

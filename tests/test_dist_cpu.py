@@ -31,7 +31,7 @@ def _owner(col0, world):
     return (col0.astype(np.uint64) >> np.uint64(64 - b)).astype(np.int64) if b else np.zeros_like(col0)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, piece=None):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -45,7 +45,8 @@ def _worker(rank, world, port, q):
         counts = np.bincount(own, minlength=world).tolist()
         recv_counts = cdist.exchange_counts([counts])
         cols = [torch.from_numpy(np.ascontiguousarray(packed[c])) for c in range(packed.shape[0])]
-        got = cdist.exchange_columns(cols, counts, recv_counts[0])
+        kw = {"max_piece_bytes": piece} if piece else {}
+        got = cdist.exchange_columns(cols, counts, recv_counts[0], **kw)
         got = np.vstack([g.numpy()[None, :] for g in got])
         want = np.hstack([r[:, _owner(r[0], world) == rank] for r in (_rows(s) for s in range(world))])
         ok = sorted(map(tuple, got.T.tolist())) == sorted(map(tuple, want.T.tolist()))
@@ -55,13 +56,15 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_exchange_gloo(world):
+@pytest.mark.parametrize("world,piece", [(2, None), (4, None), (2, 800), (4, 2000)])
+def test_exchange_gloo(world, piece):
+    """The column exchange; a small piece limit forces the multi-round path that keeps every
+    (source, destination) transfer under RCCL's 2^31-byte limit at full size."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, piece)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(world))
