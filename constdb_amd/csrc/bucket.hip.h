@@ -46,11 +46,11 @@ __device__ __forceinline__ unsigned long long* stat_shard(unsigned long long* st
 enum : uint32_t { F_DICT_STRICT = 1, F_GC_DELETES = 2, F_GC_MEMBERS = 4 };
 
 struct BucketArgs {
-  const uint64_t* k[kKeyCols];
-  const uint64_t* nd[kNodeCols];
-  const uint64_t* mb[kMemberCols];
+  // Partitioned rows, AoS: key row r is kr[r * kKeyStride + K_*], node / member row r is
+  // nr / mr[r * kChildStride + C_*].
+  const uint64_t *kr, *nr, *mr;
   // Row permutations: the final partition level is index-only, so bucket b's i-th key row
-  // is k[*][kp[kbase[b] + i]] (rows of one bucket lie in one small, cache-resident segment).
+  // is row kp[kbase[b] + i] (rows of one bucket lie in one small, cache-resident segment).
   const uint32_t *kp, *np, *mp;
   const uint32_t *kbase, *kcnt, *nbase, *ncnt, *mbase, *mcnt;
   uint64_t nbuckets;          // bucket(h) = floor((h << key_shift) * nbuckets / 2^64)
@@ -70,6 +70,13 @@ struct BucketArgs {
   uint64_t* hot_scratch;      // hot kernel: global scratch slab
   const uint64_t* hot_scratch_off;  // per hot bucket, u64 offset into the slab
 };
+
+__device__ __forceinline__ uint64_t kget(const BucketArgs& A, int c, uint32_t r) {
+  return A.kr[(uint64_t)r * kKeyStride + c];
+}
+__device__ __forceinline__ uint64_t cget(const uint64_t* C, int c, uint32_t r) {
+  return C[(uint64_t)r * kChildStride + c];
+}
 
 // Scratch: every array the bucket algorithm needs, wherever it lives.
 struct Scratch {
@@ -212,9 +219,9 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
 
   // ------------------------------------------------------------ key phase
   for (uint32_t i = threadIdx.x; i < K; i += blockDim.x) {
-    S.kh[i] = A.k[K_KH][A.kp[kb + i]];
-    S.kf[i] = A.k[K_KF][A.kp[kb + i]];
-    S.meta[i] = A.k[K_META][A.kp[kb + i]];
+    S.kh[i] = kget(A, K_KH, A.kp[kb + i]);
+    S.kf[i] = kget(A, K_KF, A.kp[kb + i]);
+    S.meta[i] = kget(A, K_META, A.kp[kb + i]);
   }
   __syncthreads();
   const int ks = A.key_shift;
@@ -241,10 +248,10 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
       while (e < K && S.kh[S.idx[e]] == S.kh[x] && S.kf[S.idx[e]] == S.kf[x] &&
              meta_tag(S.meta[S.idx[e]]) == TAG_DELETE)
         ++e;
-      const uint64_t tfin = A.k[K_CT][A.kp[kb + S.idx[e - 1]]];
+      const uint64_t tfin = kget(A, K_CT, A.kp[kb + S.idx[e - 1]]);
       for (uint32_t q = j; q < e; ++q) {  // DB::gc (db.rs:82-95)
         const uint32_t r = S.idx[q];
-        if (meta_order(S.meta[r]) + 1 > last_bad && A.k[K_CT][A.kp[kb + r]] == tfin) { emit = 0; break; }
+        if (meta_order(S.meta[r]) + 1 > last_bad && kget(A, K_CT, A.kp[kb + r]) == tfin) { emit = 0; break; }
       }
       if (!emit) atomicAdd(&S.st[ST_DELETES_GCED], 1ull);
     }
@@ -263,11 +270,11 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
     const uint32_t o = S.rank[j];
     const uint64_t hm = S.meta[h];
     const uint32_t T = meta_tag(hm), hp = meta_pos(hm);
-    uint64_t ct = A.k[K_CT][A.kp[kb + h]], ut = A.k[K_UT][A.kp[kb + h]], dt = A.k[K_DT][A.kp[kb + h]];
+    uint64_t ct = kget(A, K_CT, A.kp[kb + h]), ut = kget(A, K_UT, A.kp[kb + h]), dt = kget(A, K_DT, A.kp[kb + h]);
     uint64_t win = 0, vm = 1ull << hp, outmeta = hm, osum = 0;
     if (T == TAG_EXPIRE || T == TAG_DELETE) {  // plain overwrite: the last (pos, src) wins
       const uint32_t l = S.idx[e - 1];
-      ct = A.k[K_CT][A.kp[kb + l]];
+      ct = kget(A, K_CT, A.kp[kb + l]);
       outmeta = S.meta[l];
       win = meta_order(outmeta);
       ut = dt = 0;
@@ -281,11 +288,11 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
         ++nvalid;
         vm |= 1ull << meta_pos(m);
         if (T == TAG_BYTES) {  // object.rs:69-77
-          const uint64_t c2 = A.k[K_CT][A.kp[kb + r]];
+          const uint64_t c2 = kget(A, K_CT, A.kp[kb + r]);
           if (ct < c2) win = meta_order(m);
           ct = max(ct, c2);
-          dt = max(dt, A.k[K_DT][A.kp[kb + r]]);
-          ut = max(ut, A.k[K_UT][A.kp[kb + r]]);
+          dt = max(dt, kget(A, K_DT, A.kp[kb + r]));
+          ut = max(ut, kget(A, K_UT, A.kp[kb + r]));
         } else if (T == TAG_DICT) {
           ++dicts;
         }
@@ -294,7 +301,7 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
       if (dicts) atomicAdd(&S.st[ST_DICT_MERGES], (unsigned long long)dicts);
       if (T == TAG_COUNTER) {
         if (nvalid >= 2) vm |= kVmaskMerged;       // cal_sum after Counter::merge
-        else osum = A.k[K_AUX][A.kp[kb + h]];           // load-time total (type_counter.rs:114-124)
+        else osum = kget(A, K_AUX, A.kp[kb + h]);           // load-time total (type_counter.rs:114-124)
         win = 0;
       } else if (T != TAG_BYTES) {
         win = 0;
@@ -323,12 +330,12 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
   for (int fam = 0; fam < 2; ++fam) {
     const bool nodes = fam == 0;
     const uint32_t n = nodes ? N : M, base = nodes ? nb : mb;
-    const uint64_t* const* C = nodes ? A.nd : A.mb;
+    const uint64_t* C = nodes ? A.nr : A.mr;
     const uint32_t* P = nodes ? A.np : A.mp;  // bucket order -> row
     uint64_t* const* O = nodes ? A.no : A.mo;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-      const uint64_t pkh = C[C_PKH][P[base + i]], pkf = C[C_PKF][P[base + i]];
-      const uint64_t m = C[C_META][P[base + i]];
+      const uint64_t pkh = cget(C, C_PKH, P[base + i]), pkf = cget(C, C_PKF, P[base + i]);
+      const uint64_t m = cget(C, C_META, P[base + i]);
       // lower_bound over the sorted output keys on (kh, kf); the data row sorts first
       uint32_t lo = 0, hi = kout;
       const uint64_t spkh = pkh << ks;
@@ -350,8 +357,8 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
         atomicAdd(&S.st[ST_ORPHANS], 1ull);
       }
       S.ck[i] = key == kNone ? kout : key;  // invalid rows sort last (digit kout)
-      S.c1[i] = C[C_ID1][P[base + i]];
-      S.c2[i] = nodes ? 0 : C[C_ID2][P[base + i]];
+      S.c1[i] = cget(C, C_ID1, P[base + i]);
+      S.c2[i] = nodes ? 0 : cget(C, C_ID2, P[base + i]);
       S.cm[i] = m;
     }
     __syncthreads();
@@ -379,11 +386,11 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
           ++e;
         }
         if (nodes) {  // Counter::merge per node (type_counter.rs:60-84): t of the head kept
-          const uint64_t t0 = C[C_T][P[base + x]];
-          uint64_t v = C[C_ID2][P[base + x]];
+          const uint64_t t0 = cget(C, C_T, P[base + x]);
+          uint64_t v = cget(C, C_ID2, P[base + x]);
           for (uint32_t q = j + 1; q < e; ++q) {
             const uint32_t r = S.cidx[q];
-            const uint64_t tt = C[C_T][P[base + r]], vv = C[C_ID2][P[base + r]];
+            const uint64_t tt = cget(C, C_T, P[base + r]), vv = cget(C, C_ID2, P[base + r]);
             if (tt > t0) v = vv;
             else if (tt == t0) v = imax64(v, vv);
           }
@@ -392,10 +399,10 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
           emit = 1;
         } else {  // LWWHash::set chain (lwwhash.rs:87-107): ties go to the later candidate
           uint32_t w = x;
-          uint64_t tw = C[C_T][P[base + x]];
+          uint64_t tw = cget(C, C_T, P[base + x]);
           for (uint32_t q = j + 1; q < e; ++q) {
             const uint32_t r = S.cidx[q];
-            const uint64_t tr = C[C_T][P[base + r]];
+            const uint64_t tr = cget(C, C_T, P[base + r]);
             if (!(tw > tr)) { w = r; tw = tr; }
           }
           S.rt[j] = tw;
@@ -423,7 +430,7 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
       O[C_ID1][base + o] = S.c1[x];
       if (nodes) {
         O[C_ID2][base + o] = S.rt[j];
-        O[C_T][base + o] = C[C_T][P[base + x]];
+        O[C_T][base + o] = cget(C, C_T, P[base + x]);
         if (S.ovm[key] & kVmaskMerged) atomicAdd((unsigned long long*)&S.osum[key], (unsigned long long)S.rt[j]);
       } else {
         O[C_ID2][base + o] = S.c2[x];

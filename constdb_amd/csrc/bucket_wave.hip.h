@@ -151,31 +151,44 @@ struct WaveIn {
 template <int KE>
 __device__ __forceinline__ void load_cols(const BucketArgs& A, const WaveDir& d, const WavePerm<KE>& p, int lane,
                                           WaveIn<KE>& in) {
+  // A lane reads its own row: three 16-B pieces (+ one 8-B word for a key row's meta), all
+  // from the row's one (key) or two (child) cache lines.
   in.d = d;
   const uint32_t C = d.N + d.M;
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
-    const uint32_t c = lane + 64 * e, r = p.krow[e];
-    const bool ok = c < d.K;
-    in.kh[e] = ok ? A.k[K_KH][r] : 0;
-    in.kf[e] = ok ? A.k[K_KF][r] : 0;
-    in.kct[e] = ok ? A.k[K_CT][r] : 0;
-    in.kut[e] = ok ? A.k[K_UT][r] : 0;
-    in.kdt[e] = ok ? A.k[K_DT][r] : 0;
-    in.kaux[e] = ok ? A.k[K_AUX][r] : 0;
-    in.kmeta[e] = ok ? A.k[K_META][r] : 0;
+    const uint32_t c = lane + 64 * e;
+    in.kh[e] = in.kf[e] = in.kct[e] = in.kut[e] = in.kdt[e] = in.kaux[e] = in.kmeta[e] = 0;
+    if (c < d.K) {
+      const uint64_t* row = A.kr + (uint64_t)p.krow[e] * kKeyStride;
+      const ulonglong2 q0 = reinterpret_cast<const ulonglong2*>(row)[0];
+      const ulonglong2 q1 = reinterpret_cast<const ulonglong2*>(row)[1];
+      const ulonglong2 q2 = reinterpret_cast<const ulonglong2*>(row)[2];
+      in.kh[e] = q0.x;
+      in.kf[e] = q0.y;
+      in.kct[e] = q1.x;
+      in.kut[e] = q1.y;
+      in.kdt[e] = q2.x;
+      in.kaux[e] = q2.y;
+      in.kmeta[e] = row[K_META];
+    }
   }
 #pragma unroll
   for (int e = 0; e < 2 * KE; ++e) {
-    const uint32_t c = lane + 64 * e, r = p.crow[e];
-    const bool ok = c < C;
-    const uint64_t* const* S = c < d.N ? A.nd : A.mb;
-    in.cpkh[e] = ok ? S[C_PKH][r] : 0;
-    in.cpkf[e] = ok ? S[C_PKF][r] : 0;
-    in.cid1[e] = ok ? S[C_ID1][r] : 0;
-    in.cid2[e] = ok ? S[C_ID2][r] : 0;
-    in.ct[e] = ok ? S[C_T][r] : 0;
-    in.cm[e] = ok ? S[C_META][r] : 0;
+    const uint32_t c = lane + 64 * e;
+    in.cpkh[e] = in.cpkf[e] = in.cid1[e] = in.cid2[e] = in.ct[e] = in.cm[e] = 0;
+    if (c < C) {
+      const uint64_t* row = (c < d.N ? A.nr : A.mr) + (uint64_t)p.crow[e] * kChildStride;
+      const ulonglong2 q0 = reinterpret_cast<const ulonglong2*>(row)[0];
+      const ulonglong2 q1 = reinterpret_cast<const ulonglong2*>(row)[1];
+      const ulonglong2 q2 = reinterpret_cast<const ulonglong2*>(row)[2];
+      in.cpkh[e] = q0.x;
+      in.cpkf[e] = q0.y;
+      in.cid1[e] = q1.x;
+      in.cid2[e] = q1.y;
+      in.ct[e] = q2.x;
+      in.cm[e] = q2.y;
+    }
   }
 }
 

@@ -49,6 +49,9 @@ constexpr uint64_t kVmaskMerged = 1ull << 63;
 //   node out   : pkh pkf node v t meta             (meta: head (pos,src) of the segment)
 //   member out : pkh pkf mh mf t meta              (meta: kind | winner (pos,src))
 constexpr int kKeyCols = 7, kNodeCols = 6, kMemberCols = 6, kKeyOutCols = 8;
+// Partitioned rows as the bucket kernels read them (AoS records, columns in the order above):
+// a key row is 8 words (the 8th is padding: one aligned 64-B line), a child row 6 words.
+constexpr int kKeyStride = 8, kChildStride = 6;
 enum KeyCol { K_KH = 0, K_KF, K_CT, K_UT, K_DT, K_AUX, K_META };
 enum ChildCol { C_PKH = 0, C_PKF, C_ID1, C_ID2, C_T, C_META };  // node: ID2 = v
 enum KeyOutCol { O_KH = 0, O_KF, O_CT, O_UT, O_DT, O_META, O_WIN, O_CREF };

@@ -29,6 +29,7 @@ enum WsSlot {
   WS_OWNER,                                             // owner-partition directory
   WS_PERM,                                              // final-level row permutations (u32)
   WS_STATS,                                             // statistic shards
+  WS_KHCOL,                                             // key-hash column of the row level
   WS_COUNT
 };
 

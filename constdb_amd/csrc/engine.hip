@@ -190,6 +190,7 @@ struct Plan {
   int levels = 0;
   uint32_t d[4] = {1, 1, 1, 1};
   uint64_t nb = 1;
+  bool seg_final = false;  // the last level runs per row-level segment (part_final_kernel)
 };
 
 Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
@@ -200,15 +201,32 @@ Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
   if (const char* e = std::getenv("CDB_PLAN_TARGET")) target = (uint64_t)std::max(8, std::min(60, std::atoi(e)));
   const uint64_t want = std::max<uint64_t>({(K + target - 1) / target, (N + M + target - 1) / target, 1});
   Plan p;
-  if (want <= 1) return p;
   // The last level moves only a row index, so it takes a large fan-out (segments of
   // ~d_last buckets, a few hundred KB, stay cache-resident for the bucket kernels' gathers)
   // and the column-moving levels get small fan-outs (long contiguous write runs).
   uint32_t dlast = 256;
   if (const char* e = std::getenv("CDB_PLAN_DLAST")) dlast = (uint32_t)std::max(2, std::min(512, std::atoi(e)));
-  if (want <= 512) {
-    p.levels = 1;
-    p.d[0] = (uint32_t)want;
+  // Mode 2 (default): ONE moving level of fan-out d0 <= 2048 that writes rows, then the
+  // per-segment final level (fan-out d1 <= 8192). Segments are then ~13 MB (all families): the
+  // bucket kernels' row reads come from the Infinity Cache, one line per row, instead of
+  // needing a second full column-moving pass to make segments L2-sized (mode 1).
+  int mode = 2;
+  if (const char* e = std::getenv("CDB_PLAN_MODE")) mode = std::atoi(e);
+  uint64_t d0pref = 1024;  // measured: 1024 beats 2048 (longer write runs, same row reads)
+  if (const char* e = std::getenv("CDB_PLAN_D0")) d0pref = (uint64_t)std::max(64, std::min(2048, std::atoi(e)));
+  if (mode == 2 && want > 4096 && want <= (uint64_t)kPartLocalMax * kFinalMaxD) {
+    p.levels = 2;
+    p.seg_final = true;
+    const uint64_t d0min = (want + kFinalMaxD - 1) / kFinalMaxD;
+    p.d[0] = (uint32_t)std::min<uint64_t>(kPartLocalMax, std::max(d0min, std::min(d0pref, (want + 63) / 64)));
+    p.d[1] = (uint32_t)((want + p.d[0] - 1) / p.d[0]);
+    p.nb = (uint64_t)p.d[0] * p.d[1];
+    return p;
+  }
+  if (want <= 512) {  // one moving level that only turns the columns into rows
+    p.levels = 2;
+    p.d[0] = 1;
+    p.d[1] = (uint32_t)want;
   } else {
     const uint64_t rest = (want + dlast - 1) / dlast;
     if (rest <= 512) {
@@ -230,57 +248,67 @@ Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
 }
 
 // Splits `n` rows of an NC-column family into plan.nb buckets (key-hash order). Levels
-// 1..L-1 move the columns; the last level writes only `perm`, so bucket b's rows are
-// res[*][perm[base[b] .. base[b] + hist[b])]. Returns in `res` the columns holding the
-// rows (one of in / A / B) and in `spare` a free buffer of the same shape.
-template <int NC>
+// 0..L-3 move the columns (SoA ping-pong through A / B); level L-2 moves them into W-word
+// rows (AoS) in one of A / B, viewed as n x W words, and copies column 0 to `khcol`; the
+// last level writes only `perm`, so bucket b's rows are rows[perm[base[b] .. base[b] +
+// hist[b])]. Returns the row buffer in `rows` and the other ping-pong buffer in `spare`.
+template <int NC, int W>
 cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const Plan& plan, int shift,
-                            uint64_t* const* A, uint64_t* const* Bf, const Dir& d, uint64_t** res,
-                            uint64_t** spare, uint32_t* perm, hipStream_t s) {
-  if (plan.levels == 0 || n == 0) {
-    if (n) iota_kernel<<<(uint32_t)std::min<uint64_t>((n + 255) / 256, 4096), 256, 0, s>>>(perm, n);
-    set_dir_kernel<<<1, 1, 0, s>>>(d.base, d.hist, (uint32_t)n);
-    if (plan.nb > 1) {  // n == 0 with buckets: every bucket empty
-      CDB_HIP(hipMemsetAsync(d.base, 0, sizeof(uint32_t) * plan.nb, s), "memset");
-      CDB_HIP(hipMemsetAsync(d.hist, 0, sizeof(uint32_t) * plan.nb, s), "memset");
-    }
-    for (int c = 0; c < NC; ++c) {
-      res[c] = in[c];
-      spare[c] = A[c];
-    }
-    return hip_check(ctx, hipGetLastError(), "set_dir");
+                            uint64_t* const* A, uint64_t* const* Bf, const Dir& d, uint64_t** rows,
+                            uint64_t** spare, uint64_t* khcol, uint32_t* perm, hipStream_t s) {
+  if (n == 0) {
+    CDB_HIP(hipMemsetAsync(d.base, 0, sizeof(uint32_t) * plan.nb, s), "memset");
+    CDB_HIP(hipMemsetAsync(d.hist, 0, sizeof(uint32_t) * plan.nb, s), "memset");
+    *rows = A[0];
+    for (int c = 0; c < NC; ++c) spare[c] = Bf[c];
+    return CDB_OK;
   }
   const uint64_t tiles = (n + kPartTile - 1) / kPartTile;
   uint64_t* const* cur = in;
   uint64_t nprev = 1;
   for (int l = 0; l < plan.levels; ++l) {
-    const bool last = l + 1 == plan.levels;
+    const int kind = l + 1 == plan.levels ? 2 : (l + 2 == plan.levels ? 1 : 0);  // 0 SoA, 1 rows, 2 index
     uint64_t* const* dst = (l % 2 == 0) ? A : Bf;
     const uint64_t ncur = nprev * plan.d[l];
+    const uint64_t* col0 = kind == 2 ? khcol : cur[0];
+    if (kind == 2 && plan.seg_final) {
+      // the row level's directory (nprev segments) moves to out/doff, free until the merge;
+      // the final level writes the bucket directory over base/hist
+      CDB_HIP(hipMemcpyAsync(d.out, d.base, nprev * sizeof(uint32_t), hipMemcpyDeviceToDevice, s), "d2d");
+      CDB_HIP(hipMemcpyAsync(d.doff, d.hist, nprev * sizeof(uint32_t), hipMemcpyDeviceToDevice, s), "d2d");
+      part_final_kernel<<<(uint32_t)nprev, kFinalThreads, 0, s>>>(khcol, d.out, d.doff, nprev, plan.d[l], shift,
+                                                                  d.base, d.hist, perm);
+      CDB_TRY(launch_check(ctx, s, "partition (final level)"));
+      nprev = ncur;
+      continue;
+    }
     CDB_HIP(hipMemsetAsync(d.hist, 0, ncur * sizeof(uint32_t), s), "memset hist");
-    part_hist_kernel<<<tiles, kPartThreads, 0, s>>>(cur[0], n, nprev, plan.d[l], shift, d.hist);
+    part_hist_kernel<<<tiles, kPartThreads, 0, s>>>(col0, n, nprev, plan.d[l], shift, d.hist);
     CDB_TRY(launch_check(ctx, s, "part_hist"));
     CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, d.hist, ncur, d.base, d.cursor, nullptr, s));
-    ColSet<NC> ci, co;
-    for (int c = 0; c < NC; ++c) {
-      ci.c[c] = cur[c];
-      co.c[c] = dst[c];
-    }
-    if (last) {
-      part_scatter_kernel<1, true><<<tiles, kPartThreads, 0, s>>>(ColSet<1>{{ci.c[0]}}, ColSet<1>{{nullptr}}, n,
+    if (kind == 2) {
+      part_scatter_kernel<1, true><<<tiles, kPartThreads, 0, s>>>(ColSet<1>{{khcol}}, ColSet<1>{{nullptr}}, n,
                                                                   nprev, plan.d[l], shift, d.cursor, perm);
       CDB_TRY(launch_check(ctx, s, "partition (index level)"));
     } else {
-      part_scatter_kernel<NC><<<tiles, kPartThreads, 0, s>>>(ci, co, n, nprev, plan.d[l], shift, d.cursor);
-      CDB_TRY(launch_check(ctx, s, "partition"));
+      ColSet<NC> ci, co;
+      for (int c = 0; c < NC; ++c) {
+        ci.c[c] = cur[c];
+        co.c[c] = dst[c];
+      }
+      if (kind == 1) {
+        part_scatter_aos_kernel<NC, W><<<(n + kAosTile - 1) / kAosTile, kPartThreads, 0, s>>>(
+            ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor);
+        CDB_TRY(launch_check(ctx, s, "partition (row level)"));
+        *rows = dst[0];
+        for (int c = 0; c < NC; ++c) spare[c] = (dst == A ? Bf : A)[c];
+      } else {
+        part_scatter_kernel<NC><<<tiles, kPartThreads, 0, s>>>(ci, co, n, nprev, plan.d[l], shift, d.cursor);
+        CDB_TRY(launch_check(ctx, s, "partition"));
+      }
       cur = dst;
     }
     nprev = ncur;
-  }
-  uint64_t* const* other = (cur == A) ? Bf : A;
-  for (int c = 0; c < NC; ++c) {
-    res[c] = cur[c];
-    spare[c] = other[c];
   }
   return CDB_OK;
 }
@@ -381,7 +409,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
 
   CDB_HIP(hipEventRecord(ctx->ev0, s), "event");
   // ---- 1. bucket partition of each family by (parent) key hash
-  uint64_t *kb[8], *ksp[8], *ndb[6], *nsp[6], *mbb[6], *msp[6];
+  uint64_t *krows = nullptr, *nrows = nullptr, *mrows = nullptr;
+  uint64_t *ksp[8], *nsp[6], *msp[6];
   uint64_t* kin[8];
   uint64_t* nin[6];
   uint64_t* min_[6];
@@ -392,13 +421,16 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   }
   uint32_t* perm = (uint32_t*)ws_get(ctx, WS_PERM, (K + N + M + 3) * sizeof(uint32_t), &st);
   if (!perm) return st;
+  uint64_t* khcol = (uint64_t*)ws_get(ctx, WS_KHCOL, (K + N + M + 3) * sizeof(uint64_t), &st);
+  if (!khcol) return st;
   uint32_t *kperm = perm, *nperm = perm + K, *mperm = perm + K + N;
-  CDB_TRY(partition_family<kKeyCols>(ctx, kin, K, plan, shift, KA, KB, dk, kb, ksp, kperm, s));
-  // keys need 8 output columns: the spare buffer always has 8
-  CDB_TRY(partition_family<kNodeCols>(ctx, nin, N, plan, shift, NA, NB, dnd, ndb, nsp, nperm, s));
-  CDB_TRY(partition_family<kMemberCols>(ctx, min_, M, plan, shift, MA, MBf, dm, mbb, msp, mperm, s));
-  {  // sparse key outputs (8 columns) go to whichever ping-pong buffer is free
-    uint64_t* const* free_k = (kb[0] == KA[0]) ? KB : KA;
+  CDB_TRY(partition_family<kKeyCols, kKeyStride>(ctx, kin, K, plan, shift, KA, KB, dk, &krows, ksp, khcol, kperm, s));
+  CDB_TRY(partition_family<kNodeCols, kChildStride>(ctx, nin, N, plan, shift, NA, NB, dnd, &nrows, nsp, khcol + K,
+                                                    nperm, s));
+  CDB_TRY(partition_family<kMemberCols, kChildStride>(ctx, min_, M, plan, shift, MA, MBf, dm, &mrows, msp,
+                                                      khcol + K + N, mperm, s));
+  {  // sparse key outputs (8 columns) go to the ping-pong buffer that does not hold the rows
+    uint64_t* const* free_k = (krows == KA[0]) ? KB : KA;
     for (int c = 0; c < 8; ++c) ksp[c] = free_k[c];
   }
 
@@ -437,10 +469,10 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   // ---- 3. fused bucket merge
   BucketArgs A;
   std::memset(&A, 0, sizeof A);
-  for (int c = 0; c < kKeyCols; ++c) A.k[c] = kb[c];
+  A.kr = krows;
+  A.nr = nrows;
+  A.mr = mrows;
   for (int c = 0; c < kNodeCols; ++c) {
-    A.nd[c] = ndb[c];
-    A.mb[c] = mbb[c];
     A.no[c] = nsp[c];
     A.mo[c] = msp[c];
   }

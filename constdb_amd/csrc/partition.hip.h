@@ -195,6 +195,150 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
   }
 }
 
+// ---------------------------------------------------------------- scatter to rows (AoS)
+// The last column-moving level: the same multisplit, but each row leaves as one W-word record
+// (W = 8 for key rows, whose 8th word is zero padding: one aligned 64-B line per row; W = 6 for
+// child rows) and column 0 also goes to `khcol` for the index level. The bucket kernels then
+// fetch a row with 16-B loads from one or two lines instead of one gathered line per column.
+// Rows are staged whole through LDS (2048-row tiles) and leave as 16-B pieces, W/2 lanes per
+// row, so each store instruction writes whole rows of one digit run.
+constexpr int kAosTile = 2048;
+
+template <int NC, int W>
+__global__ void __launch_bounds__(kPartThreads) part_scatter_aos_kernel(ColSet<NC> in, uint64_t* __restrict__ aos,
+                                                                        uint64_t* __restrict__ khcol, uint64_t n,
+                                                                        uint64_t nprev, uint32_t d, int shift,
+                                                                        uint32_t* __restrict__ cursor) {
+  static_assert(W % 2 == 0 && W >= NC, "rows leave as 16-B pieces");
+  constexpr int RPT = kAosTile / kPartThreads;
+  __shared__ uint32_t cnt[kPartLocalMax];
+  __shared__ uint32_t delta[kPartLocalMax];
+  __shared__ uint16_t slot_lb[kAosTile];
+  __shared__ __attribute__((aligned(16))) uint64_t stage[kAosTile * W];
+  const uint64_t tile0 = (uint64_t)blockIdx.x * kAosTile;
+  if (tile0 >= n) return;
+  const uint64_t tile1 = tile0 + kAosTile < n ? tile0 + kAosTile : n;
+  const int rows = (int)(tile1 - tile0);
+  const uint64_t ncur = nprev * d;
+  const uint64_t plo = bucket_of_n(in.c[0][tile0] << shift, nprev);
+  const uint64_t phi = bucket_of_n(in.c[0][tile1 - 1] << shift, nprev);
+  const uint64_t glo = plo * d;
+  const uint64_t span64 = (phi - plo + 1) * d;
+
+  if (span64 > (uint64_t)kPartLocalMax) {  // wide tile: per-row global reservation
+    for (int r = threadIdx.x; r < rows; r += kPartThreads) {
+      const uint64_t h = in.c[0][tile0 + r];
+      const uint32_t p = atomicAdd(&cursor[bucket_of_n(h << shift, ncur)], 1u);
+#pragma unroll
+      for (int c = 0; c < W; ++c) aos[(uint64_t)p * W + c] = c < NC ? in.c[c < NC ? c : 0][tile0 + r] : 0;
+      khcol[p] = h;
+    }
+    return;
+  }
+  const int span = (int)span64;
+  for (int i = threadIdx.x; i < span; i += kPartThreads) cnt[i] = 0;
+  uint64_t v0[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int r = threadIdx.x + k * kPartThreads;
+    v0[k] = r < rows ? __builtin_nontemporal_load(&in.c[0][tile0 + r]) : 0;
+  }
+  __syncthreads();
+  uint16_t lb[RPT];
+  uint32_t rk[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int r = threadIdx.x + k * kPartThreads;
+    if (r < rows) {
+      lb[k] = (uint16_t)(bucket_of_n(v0[k] << shift, ncur) - glo);
+      rk[k] = atomicAdd(&cnt[lb[k]], 1u);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < span; i += kPartThreads) delta[i] = cnt[i] ? atomicAdd(&cursor[glo + i], cnt[i]) : 0;
+  __syncthreads();
+  wave0_exclusive_scan(cnt, span);
+  __syncthreads();
+  for (int i = threadIdx.x; i < span; i += kPartThreads) delta[i] -= cnt[i];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int r = threadIdx.x + k * kPartThreads;
+    if (r < rows) {
+      const uint32_t s = cnt[lb[k]] + rk[k];
+      slot_lb[s] = lb[k];
+      uint64_t* row = &stage[(uint32_t)s * W];
+      row[0] = v0[k];
+#pragma unroll
+      for (int c = 1; c < W; ++c) row[c] = c < NC ? __builtin_nontemporal_load(&in.c[c < NC ? c : 0][tile0 + r]) : 0;
+    }
+  }
+  __syncthreads();
+  constexpr int Q = W / 2;  // 16-B pieces per row
+  for (int i = threadIdx.x; i < rows * Q; i += kPartThreads) {
+    const int j = i / Q, q = i - j * Q;
+    const uint64_t dst = (uint64_t)(delta[slot_lb[j]] + (uint32_t)j) * W + 2 * q;
+    *reinterpret_cast<ulonglong2*>(&aos[dst]) = *reinterpret_cast<const ulonglong2*>(&stage[j * W + 2 * q]);
+  }
+  for (int j = threadIdx.x; j < rows; j += kPartThreads) khcol[delta[slot_lb[j]] + j] = stage[j * W];
+}
+
+// ---------------------------------------------------------------- final level, per segment
+// The last (index-only) level when it follows a row level of large fan-out: segment s (the
+// rows of row-level bucket s, contiguous in `khcol` order) is split into d1 buckets by ONE
+// workgroup: an LDS histogram of the segment, its scan (the bucket directory of the segment,
+// written straight to base_out / hist_out), and an LDS-cursor scatter of row indices into
+// perm. No global histogram pass, no device-wide scan, no global atomics; the segment's
+// key-hash column (~1 MB) is read twice, the second time from L2.
+constexpr int kFinalThreads = 1024;
+constexpr int kFinalMaxD = 8192;
+
+__global__ void __launch_bounds__(kFinalThreads) part_final_kernel(const uint64_t* __restrict__ khcol,
+                                                                   const uint32_t* __restrict__ sbase,
+                                                                   const uint32_t* __restrict__ scnt, uint64_t nseg,
+                                                                   uint32_t d1, int shift,
+                                                                   uint32_t* __restrict__ base_out,
+                                                                   uint32_t* __restrict__ hist_out,
+                                                                   uint32_t* __restrict__ perm) {
+  __shared__ uint32_t cnt[kFinalMaxD];
+  __shared__ uint32_t part[kFinalThreads / 64];
+  const uint32_t s = blockIdx.x;
+  const uint32_t b0 = sbase[s], n = scnt[s];
+  const uint64_t ntot = nseg * d1;
+  const uint64_t g0 = (uint64_t)s * d1;
+  for (uint32_t j = threadIdx.x; j < d1; j += kFinalThreads) cnt[j] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += kFinalThreads)
+    atomicAdd(&cnt[(uint32_t)(bucket_of_n(khcol[b0 + i] << shift, ntot) - g0)], 1u);
+  __syncthreads();
+  // exclusive scan of cnt[0 .. d1): thread t owns a run of `per` consecutive entries
+  const uint32_t per = (d1 + kFinalThreads - 1) / kFinalThreads;
+  const uint32_t j0 = threadIdx.x * per, j1 = min(d1, j0 + per);
+  uint32_t run = 0;
+  for (uint32_t j = j0; j < j1; ++j) run += cnt[j];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = run;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) part[w] = incl;
+  __syncthreads();
+  uint32_t off = incl - run;
+  for (int k = 0; k < w; ++k) off += part[k];
+  for (uint32_t j = j0; j < j1; ++j) {
+    const uint32_t c = cnt[j];
+    hist_out[g0 + j] = c;
+    base_out[g0 + j] = b0 + off;
+    cnt[j] = off;  // becomes the bucket's cursor
+    off += c;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += kFinalThreads) {
+    const uint32_t j = (uint32_t)(bucket_of_n(khcol[b0 + i] << shift, ntot) - g0);
+    perm[b0 + atomicAdd(&cnt[j], 1u)] = b0 + i;
+  }
+}
+
 // ---------------------------------------------------------------- scans
 constexpr int kScanThreads = 256;
 constexpr int kScanItems = 8;  // items per thread
