@@ -61,6 +61,18 @@ def alg_bytes(st, set_frac=0.5):
             + (st.member_rows_in + st.member_rows_out) * wm)
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the bucket phase, from the committed rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes of this same bench command (scripts/gpu_round.sh -> pmc_traffic.py);
+    None when no such measurement is committed."""
+    f = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    try:
+        with open(f) as fh:
+            return float(json.load(fh)["bucket_phase_bytes"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(cdb, args):
     """The oracle's single-thread C++ fold (kind "port": the Rust reference cannot be built
     here) on a bounded sample of the same generator config; decode is excluded."""
@@ -159,9 +171,11 @@ def run_single(cdb, args):
         "hbm_gbs_alg": B / (ms * 1e-3) / 1e9,
         "phases_ms": {"partition": part_ms / args.steps, "bucket_merge": bk, "finish": fin_ms / args.steps,
                       "device_total": dev_ms / args.steps},
-        "roofline": {"bound": "hbm", "kernel": "bucket_kernel",
+        "roofline": {"bound": "hbm",
+                     "kernel": "bucket phase = bucket_wave_kernel + bucket_wide_kernel + bucket_mid_kernel",
                      "achieved": B / (bk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": B / (bk * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None},
+                     "frac": B / (bk * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "alg_bytes": B, "traffic": pmc_traffic()},
         "stats": {"type_conflicts": st.type_conflicts, "dict_merges": st.dict_merges,
                   "hot_buckets": st.hot_buckets, "wide_buckets": st.wide_buckets,
                   "mid_buckets": st.mid_buckets, "orphans": st.orphan_children},

@@ -212,7 +212,7 @@ Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
   // needing a second full column-moving pass to make segments L2-sized (mode 1).
   int mode = 2;
   if (const char* e = std::getenv("CDB_PLAN_MODE")) mode = std::atoi(e);
-  uint64_t d0pref = 1024;  // measured: 1024 beats 2048 (longer write runs, same row reads)
+  uint64_t d0pref = 768;  // measured on the C4 shard: 768 < 1024 < 512 < 2048 ms/step
   if (const char* e = std::getenv("CDB_PLAN_D0")) d0pref = (uint64_t)std::max(64, std::min(2048, std::atoi(e)));
   if (mode == 2 && want > 4096 && want <= (uint64_t)kPartLocalMax * kFinalMaxD) {
     p.levels = 2;

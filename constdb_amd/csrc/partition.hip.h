@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_aos_kernel(ColSet<N
 // perm. No global histogram pass, no device-wide scan, no global atomics; the segment's
 // key-hash column (~1 MB) is read twice, the second time from L2.
 constexpr int kFinalThreads = 1024;
-constexpr int kFinalMaxD = 8192;
+constexpr int kFinalMaxD = 16384;
 
 __global__ void __launch_bounds__(kFinalThreads) part_final_kernel(const uint64_t* __restrict__ khcol,
                                                                    const uint32_t* __restrict__ sbase,
@@ -307,8 +307,20 @@ __global__ void __launch_bounds__(kFinalThreads) part_final_kernel(const uint64_
   const uint64_t g0 = (uint64_t)s * d1;
   for (uint32_t j = threadIdx.x; j < d1; j += kFinalThreads) cnt[j] = 0;
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n; i += kFinalThreads)
-    atomicAdd(&cnt[(uint32_t)(bucket_of_n(khcol[b0 + i] << shift, ntot) - g0)], 1u);
+  // 8 independent loads in flight per thread, then their LDS atomics
+  constexpr int U = 8;
+  for (uint32_t i0 = 0; i0 < n; i0 += U * kFinalThreads) {
+    uint64_t h[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * kFinalThreads + threadIdx.x;
+      h[u] = i < n ? khcol[b0 + i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + u * kFinalThreads + threadIdx.x < n)
+        atomicAdd(&cnt[(uint32_t)(bucket_of_n(h[u] << shift, ntot) - g0)], 1u);
+  }
   __syncthreads();
   // exclusive scan of cnt[0 .. d1): thread t owns a run of `per` consecutive entries
   const uint32_t per = (d1 + kFinalThreads - 1) / kFinalThreads;
@@ -333,9 +345,18 @@ __global__ void __launch_bounds__(kFinalThreads) part_final_kernel(const uint64_
     off += c;
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < n; i += kFinalThreads) {
-    const uint32_t j = (uint32_t)(bucket_of_n(khcol[b0 + i] << shift, ntot) - g0);
-    perm[b0 + atomicAdd(&cnt[j], 1u)] = b0 + i;
+  for (uint32_t i0 = 0; i0 < n; i0 += U * kFinalThreads) {
+    uint64_t h[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * kFinalThreads + threadIdx.x;
+      h[u] = i < n ? khcol[b0 + i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = i0 + u * kFinalThreads + threadIdx.x;
+      if (i < n) perm[b0 + atomicAdd(&cnt[(uint32_t)(bucket_of_n(h[u] << shift, ntot) - g0)], 1u)] = b0 + i;
+    }
   }
 }
 
