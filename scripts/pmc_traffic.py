@@ -15,7 +15,7 @@ def load(d, counter):
     for f in glob.glob(f"{d}/**/run_counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"].startswith(counter):
-                name = r["Kernel_Name"].split("(")[0].replace("cdb::", "").replace("(anonymous namespace)::", "")
+                name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("cdb::", "")
                 name = name.replace("void ", "")
                 per[name].append(float(r["Counter_Value"]) * 1024.0)
     return per
