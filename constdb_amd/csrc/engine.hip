@@ -193,6 +193,16 @@ struct Plan {
   bool seg_final = false;  // the last level runs per row-level segment (part_final_kernel)
 };
 
+// Tile of the row-level scatter (CDB_AOS_TILE = 1024 or 2048).
+int aos_tile() {
+  static const int t = [] {
+    const char* e = std::getenv("CDB_AOS_TILE");
+    const int v = e ? std::atoi(e) : 1024;
+    return v == 2048 || v == 512 ? v : 1024;
+  }();
+  return t;
+}
+
 Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
   // Wave-sized buckets: ~40 key rows and ~40 child rows (nodes + members) on average.
   // A wave holds 64 key rows (128 in the wide kernel) and 128 child rows, so only the
@@ -214,11 +224,12 @@ Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
   if (const char* e = std::getenv("CDB_PLAN_MODE")) mode = std::atoi(e);
   uint64_t d0pref = 768;  // measured on the C4 shard: 768 < 1024 < 512 < 2048 ms/step
   if (const char* e = std::getenv("CDB_PLAN_D0")) d0pref = (uint64_t)std::max(64, std::min(2048, std::atoi(e)));
-  if (mode == 2 && want > 4096 && want <= (uint64_t)kPartLocalMax * kFinalMaxD) {
+  const uint64_t dcap = aos_tile() == 2048 ? 2048 : 1024;  // local digit slots of the row-level kernel
+  if (mode == 2 && want > 4096 && want <= dcap * kFinalMaxD) {
     p.levels = 2;
     p.seg_final = true;
     const uint64_t d0min = (want + kFinalMaxD - 1) / kFinalMaxD;
-    p.d[0] = (uint32_t)std::min<uint64_t>(kPartLocalMax, std::max(d0min, std::min(d0pref, (want + 63) / 64)));
+    p.d[0] = (uint32_t)std::min<uint64_t>(dcap, std::max(d0min, std::min(d0pref, (want + 63) / 64)));
     p.d[1] = (uint32_t)((want + p.d[0] - 1) / p.d[0]);
     p.nb = (uint64_t)p.d[0] * p.d[1];
     return p;
@@ -297,8 +308,15 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const
         co.c[c] = dst[c];
       }
       if (kind == 1) {
-        part_scatter_aos_kernel<NC, W><<<(n + kAosTile - 1) / kAosTile, kPartThreads, 0, s>>>(
-            ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor);
+        if (aos_tile() == 2048)
+          part_scatter_aos_kernel<NC, W, 2048, 2048><<<(n + 2047) / 2048, kPartThreads, 0, s>>>(
+              ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor);
+        else if (aos_tile() == 512)
+          part_scatter_aos_kernel<NC, W, 512, 1024><<<(n + 511) / 512, kPartThreads, 0, s>>>(
+              ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor);
+        else
+          part_scatter_aos_kernel<NC, W, 1024, 1024><<<(n + 1023) / 1024, kPartThreads, 0, s>>>(
+              ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor);
         CDB_TRY(launch_check(ctx, s, "partition (row level)"));
         *rows = dst[0];
         for (int c = 0; c < NC; ++c) spare[c] = (dst == A ? Bf : A)[c];

@@ -202,17 +202,19 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
 // fetch a row with 16-B loads from one or two lines instead of one gathered line per column.
 // Rows are staged whole through LDS (2048-row tiles) and leave as 16-B pieces, W/2 lanes per
 // row, so each store instruction writes whole rows of one digit run.
-constexpr int kAosTile = 2048;
-
-template <int NC, int W>
+// TILE = 1024 (two workgroups per CU, so one's barriers and scan overlap the other's memory
+// traffic) or 2048 (one workgroup per CU, longer per-digit runs); LMAX = local digit slots.
+template <int NC, int W, int TILE = 1024, int LMAX = 1024>
 __global__ void __launch_bounds__(kPartThreads) part_scatter_aos_kernel(ColSet<NC> in, uint64_t* __restrict__ aos,
                                                                         uint64_t* __restrict__ khcol, uint64_t n,
                                                                         uint64_t nprev, uint32_t d, int shift,
                                                                         uint32_t* __restrict__ cursor) {
   static_assert(W % 2 == 0 && W >= NC, "rows leave as 16-B pieces");
-  constexpr int RPT = kAosTile / kPartThreads;
-  __shared__ uint32_t cnt[kPartLocalMax];
-  __shared__ uint32_t delta[kPartLocalMax];
+  constexpr int kAosTile = TILE;
+  constexpr int kLocal = LMAX;
+  constexpr int RPT = (kAosTile + kPartThreads - 1) / kPartThreads;
+  __shared__ uint32_t cnt[kLocal];
+  __shared__ uint32_t delta[kLocal];
   __shared__ uint16_t slot_lb[kAosTile];
   __shared__ __attribute__((aligned(16))) uint64_t stage[kAosTile * W];
   const uint64_t tile0 = (uint64_t)blockIdx.x * kAosTile;
@@ -225,7 +227,7 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_aos_kernel(ColSet<N
   const uint64_t glo = plo * d;
   const uint64_t span64 = (phi - plo + 1) * d;
 
-  if (span64 > (uint64_t)kPartLocalMax) {  // wide tile: per-row global reservation
+  if (span64 > (uint64_t)kLocal) {  // wide tile: per-row global reservation
     for (int r = threadIdx.x; r < rows; r += kPartThreads) {
       const uint64_t h = in.c[0][tile0 + r];
       const uint32_t p = atomicAdd(&cursor[bucket_of_n(h << shift, ncur)], 1u);
