@@ -112,60 +112,77 @@ __device__ __forceinline__ int group_bucket(const uint32_t* rel, uint32_t t) {  
   return j;
 }
 
+// One wave per (group of 64 buckets, family): three independent tasks per group, so more
+// waves are in flight; each lane copies two dense rows per pass (their loads overlap). The
+// family is a template parameter, so every column pointer is a kernel-argument register
+// (selecting pointers by a run-time family put the argument arrays in scratch).
+template <int FAM>
+__device__ __forceinline__ void compact_row(const CompactArgs& A, const CompactLds& L, uint32_t t, uint32_t d0) {
+  const int j = group_bucket(L.doff, t);
+  const uint32_t src = L.sbase[j] + (t - L.doff[j]), dst = d0 + t;
+  if constexpr (FAM == 0) {
+    uint64_t v[kKeyOutCols];
+#pragma unroll
+    for (int c = 0; c < kKeyOutCols; ++c) v[c] = A.ks[c][src];
+    const uint64_t cnt = v[O_CREF] & 0xFFFFFF;
+    const uint32_t T = meta_tag(v[O_META]);
+    const uint64_t begin = cnt ? (v[O_CREF] >> 24) + (T == TAG_COUNTER ? L.ndoff[j] : L.mdoff[j]) : 0;
+    v[O_CREF] = cref_pack(begin, cnt);
+#pragma unroll
+    for (int c = 0; c < kKeyOutCols; ++c) A.kd[c][dst] = v[c];
+  } else if constexpr (FAM == 1) {
+    uint64_t v[kNodeCols];
+#pragma unroll
+    for (int c = 0; c < kNodeCols; ++c) v[c] = A.ns[c][src];
+#pragma unroll
+    for (int c = 0; c < kNodeCols; ++c) A.nd[c][dst] = v[c];
+  } else {
+    uint64_t v[kMemberCols];
+#pragma unroll
+    for (int c = 0; c < kMemberCols; ++c) v[c] = A.ms[c][src];
+#pragma unroll
+    for (int c = 0; c < kMemberCols; ++c) A.md[c][dst] = v[c];
+  }
+}
+
+template <int FAM>
+__device__ __forceinline__ void compact_group(const CompactArgs& A, CompactLds& L, uint32_t g, uint32_t nbuckets) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t b0 = g * 64, nb = min(64u, nbuckets - b0);
+  const uint32_t b = b0 + min(lane, nb - 1);
+  const bool in = lane < nb;
+  const uint32_t* out = FAM == 0 ? A.kout : FAM == 1 ? A.nout : A.mout;
+  const uint32_t* base = FAM == 0 ? A.kbase : FAM == 1 ? A.nbase : A.mbase;
+  const uint32_t* doff = FAM == 0 ? A.kdoff : FAM == 1 ? A.ndoff : A.mdoff;
+  const uint32_t d0 = doff[b0];
+  const uint32_t dl = doff[b0 + nb - 1] + out[b0 + nb - 1];
+  // padding lanes repeat the group end so the search never selects them
+  L.doff[lane] = in ? doff[b] - d0 : dl - d0;
+  L.sbase[lane] = base[b];
+  if (FAM == 0) {
+    L.ndoff[lane] = A.ndoff[b];
+    L.mdoff[lane] = A.mdoff[b];
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const uint32_t total = dl - d0;
+  uint32_t t = lane;
+  for (; t + 64 < total; t += 128) {
+    compact_row<FAM>(A, L, t, d0);
+    compact_row<FAM>(A, L, t + 64, d0);
+  }
+  if (t < total) compact_row<FAM>(A, L, t, d0);
+}
+
 __global__ void __launch_bounds__(kCompactWaves * 64) compact_kernel(CompactArgs A, uint32_t nbuckets) {
   __shared__ CompactLds lds_all[kCompactWaves];
   CompactLds& L = lds_all[threadIdx.x >> 6];
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t ngroups = (nbuckets + 63) / 64;
-  const uint32_t nwaves = gridDim.x * kCompactWaves;
-  for (uint32_t g = blockIdx.x * kCompactWaves + (threadIdx.x >> 6); g < ngroups; g += nwaves) {
-    const uint32_t b0 = g * 64, nb = min(64u, nbuckets - b0);
-    const uint32_t b = b0 + min(lane, nb - 1);
-    const bool in = lane < nb;
-#pragma unroll 1
-    for (int fam = 0; fam < 3; ++fam) {
-      const uint32_t* out = fam == 0 ? A.kout : fam == 1 ? A.nout : A.mout;
-      const uint32_t* base = fam == 0 ? A.kbase : fam == 1 ? A.nbase : A.mbase;
-      const uint32_t* doff = fam == 0 ? A.kdoff : fam == 1 ? A.ndoff : A.mdoff;
-      const uint32_t d0 = doff[b0];
-      const uint32_t dl = doff[b0 + nb - 1] + out[b0 + nb - 1];
-      // padding lanes repeat the group end so the search never selects them
-      L.doff[lane] = in ? doff[b] - d0 : dl - d0;
-      L.sbase[lane] = base[b];
-      if (fam == 0) {
-        L.ndoff[lane] = A.ndoff[b];
-        L.mdoff[lane] = A.mdoff[b];
-      }
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const uint32_t total = dl - d0;
-      for (uint32_t t = lane; t < total; t += 64) {
-        const int j = group_bucket(L.doff, t);
-        const uint32_t src = L.sbase[j] + (t - L.doff[j]), dst = d0 + t;
-        if (fam == 0) {
-#pragma unroll
-          for (int c = 0; c < kKeyOutCols; ++c) {
-            uint64_t v = A.ks[c][src];
-            if (c == O_CREF) {
-              const uint64_t cnt = v & 0xFFFFFF;
-              const uint32_t T = meta_tag(A.ks[O_META][src]);
-              const uint64_t begin = cnt ? (v >> 24) + (T == TAG_COUNTER ? L.ndoff[j] : L.mdoff[j]) : 0;
-              v = cref_pack(begin, cnt);
-            }
-            A.kd[c][dst] = v;
-          }
-        } else if (fam == 1) {
-#pragma unroll
-          for (int c = 0; c < kNodeCols; ++c) A.nd[c][dst] = A.ns[c][src];
-        } else {
-#pragma unroll
-          for (int c = 0; c < kMemberCols; ++c) A.md[c][dst] = A.ms[c][src];
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-  }
+  const uint32_t task = blockIdx.x * kCompactWaves + (threadIdx.x >> 6);
+  const uint32_t g = task / 3, fam = task - g * 3;
+  if (g * 64 >= nbuckets) return;
+  if (fam == 0) compact_group<0>(A, L, g, nbuckets);
+  else if (fam == 1) compact_group<1>(A, L, g, nbuckets);
+  else compact_group<2>(A, L, g, nbuckets);
 }
 
 template <typename T, typename OutT>
@@ -579,8 +596,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   C.kbase = dk.base; C.nbase = dnd.base; C.mbase = dm.base;
   C.kout = dk.out; C.nout = dnd.out; C.mout = dm.out;
   C.kdoff = dk.doff; C.ndoff = dnd.doff; C.mdoff = dm.doff;
-  compact_kernel<<<(uint32_t)std::min<uint64_t>((nb + 64 * kCompactWaves - 1) / (64 * kCompactWaves), 16384),
-                   64 * kCompactWaves, 0, s>>>(C, (uint32_t)nb);
+  compact_kernel<<<(uint32_t)((3 * ((nb + 63) / 64) + kCompactWaves - 1) / kCompactWaves), 64 * kCompactWaves, 0,
+                   s>>>(C, (uint32_t)nb);
   CDB_TRY(launch_check(ctx, s, "compact_kernel"));
   stats_reduce_kernel<<<1, 64, 0, s>>>(d_shards, d_stats);
   CDB_TRY(launch_check(ctx, s, "stats_reduce_kernel"));
