@@ -272,3 +272,91 @@ def test_partition_owner(db, ncols, bits):
     assert bool((downer[1:] >= downer[:-1]).all())              # grouped by owner
     key = lambda t: sorted(map(tuple, t.T.tolist()))             # same multiset of rows
     assert key(s) == key(d)
+
+
+# ------------------------------------------------------------------ BASELINE-scale checks
+def _c4(universe, replicas=8, seed=4):
+    """bench.py's C4 generator config at a given key universe."""
+    return cdb.gen_config(seed=seed, universe=universe, n_replicas=replicas, key_permille=500, mix_bytes=60,
+                          mix_counter=30, mix_set=5, mix_dict=5, conflict_ppm=1000, tie_permille=20, max_nodes=8,
+                          mean_members=4, member_universe=16, del_permille=200, side_permille=20, value_min=8,
+                          value_max=32, replica_hi=replicas)
+
+
+@pytest.mark.parametrize("gc", [None, 1])
+def test_c4_shape_1m_keys_bit_exact(db, gc):
+    """C4's shape at a 1M-key universe x 8 replicas (~4.3M entries): the large-plan path (row
+    level + per-segment final level, ~100K buckets) against the C++ oracle, bit for bit."""
+    cfg = _c4(1_000_000)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(8)]
+    wm = None if gc is None else (1700000000000 + (1 << 18)) << 22
+    _check(db, snaps, gc=wm)
+
+
+def _dev_merge(ctx, din, torch):
+    """Merges device rows into torch-owned output columns; returns (outputs, stats)."""
+    L = cdb.lib()
+    dout = cdb.DevOutput()
+    outs = []
+    for fam, (rows, ncol) in enumerate(((din.keys, 8), (din.nodes, 6), (din.members, 6))):
+        t = torch.empty((ncol, max(rows.n, 1)), dtype=torch.int64, device="cuda")
+        r = cdb.DevRows()
+        for c in range(ncol):
+            r.col[c] = t[c].data_ptr()
+        r.n = 0
+        setattr(dout, ("keys", "nodes", "members")[fam], r)
+        outs.append(t)
+    dout.compact = 1
+    st = cdb.MergeStats()
+    import ctypes
+    ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(din), ctypes.byref(cdb.MergeOpts()), ctypes.byref(dout),
+                                 ctypes.byref(st), None))
+    torch.cuda.synchronize()
+    return [outs[0][:, :dout.keys.n], outs[1][:, :dout.nodes.n], outs[2][:, :dout.members.n]], st
+
+
+def test_full_c4_shard_invariants(db):
+    """bench.py's full workload (62.5M-key universe x 8 replicas, ~270M key rows, generated in
+    HBM): size-independent properties of the result, checked on the GPU with torch.
+      * determinism: a second merge of the same rows is bit-identical;
+      * every key's child range lies inside the child outputs, ranges tile them exactly, and
+        every child row names its key (pkh, pkf == kh, kf);
+      * a merged counter's `win` is the wrapping sum of its nodes' values (cal_sum).
+    The same generator at a 1M-key universe is checked bit-exact against the oracle above."""
+    import ctypes
+    ctx = db.ctx
+    L = cdb.lib()
+    din = cdb.DevInput()
+    ctx.check(L.cdb_gen_device(ctx.handle, ctypes.byref(_c4(62_500_000)), ctypes.byref(din)))
+    try:
+        (k, n, m), st = _dev_merge(ctx, din, torch)
+        assert st.key_rows_in > 250_000_000 and st.key_rows_out > 0
+        (k2, n2, m2), _ = _dev_merge(ctx, din, torch)
+        for a, b in ((k, k2), (n, n2), (m, m2)):
+            assert a.shape == b.shape and torch.equal(a, b)
+        del k2, n2, m2
+        cref = k[7]
+        cnt = cref & 0xFFFFFF
+        begin = cref >> 24
+        tag = (k[5] >> 56) & 0xFF
+        is_counter = tag == 0
+        is_lww = (tag == 4) | (tag == 5)
+        assert bool((cnt[~(is_counter | is_lww)] == 0).all())
+        owners = {}
+        for name, sel, child in (("nodes", is_counter, n), ("members", is_lww, m)):
+            idx = torch.nonzero(sel & (cnt > 0), as_tuple=True)[0]
+            c, b0 = cnt[idx], begin[idx]
+            assert int(c.sum()) == child.shape[1], name
+            order = torch.argsort(b0)
+            idx, b0, c = idx[order], b0[order], c[order]
+            assert int(b0[0]) == 0 and bool((b0[1:] == (b0 + c)[:-1]).all()), name  # ranges tile the rows
+            owner = torch.repeat_interleave(idx, c)          # child row -> its key row
+            assert bool((child[0] == k[0][owner]).all()) and bool((child[1] == k[1][owner]).all()), name
+            owners[name] = owner
+        # cal_sum (type_counter.rs:89-91): a counter's win is the wrapping sum of its nodes' v
+        # (the generator never repeats a node id inside one counter, so merged or not)
+        sums = torch.zeros(k.shape[1], dtype=torch.int64, device="cuda").index_add_(0, owners["nodes"], n[3])
+        assert bool((sums[is_counter] == k[6][is_counter]).all())
+    finally:
+        for fam in (din.keys, din.nodes, din.members):
+            L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
