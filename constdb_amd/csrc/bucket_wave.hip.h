@@ -192,6 +192,79 @@ __device__ __forceinline__ void load_cols(const BucketArgs& A, const WaveDir& d,
   }
 }
 
+// Decoupled look-back (single-pass prefix over buckets in dispatch order). Publishes bucket
+// b's output counts (flag A), walks back over its predecessors 64 at a time until every family
+// meets an inclusive prefix (flag P), then publishes its own inclusive prefixes. Returns the
+// exclusive prefixes. Buckets are dispatched in increasing order (one per wave, no XCD remap),
+// so the lowest unfinished bucket is always resident and never waits: the walk terminates.
+// A bounded spin turns a broken invariant into an error flag instead of a hang.
+constexpr unsigned long long kLbA = 1ull << 62, kLbP = 2ull << 62, kLbV = kLbA - 1;
+constexpr uint32_t kLbSpinLimit = 1u << 16;  // ~0.1 s of polling
+
+__device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long lb_load(unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void lookback(const BucketArgs& A, uint32_t b, int lane, uint32_t ak, uint32_t an,
+                                         uint32_t am, uint64_t& xk, uint64_t& xn, uint64_t& xm) {
+  if (lane == 0) {
+    lb_store(&A.lb_k[b], kLbA | ak);
+    lb_store(&A.lb_n[b], kLbA | an);
+    lb_store(&A.lb_m[b], kLbA | am);
+  }
+  uint64_t acc[3] = {0, 0, 0};
+  bool done[3] = {false, false, false};
+  unsigned long long* st[3] = {A.lb_k, A.lb_n, A.lb_m};
+  int64_t j = (int64_t)b - 1;
+  uint32_t spins = 0;
+  while (j >= 0 && !(done[0] && done[1] && done[2])) {
+    const int64_t q = j - lane;
+    unsigned long long v[3];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) v[f] = q >= 0 ? lb_load(&st[f][q]) : kLbP;  // before bucket 0: prefix 0
+    bool retry = false;
+    int first_p[3];
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      const uint64_t pm = __ballot((v[f] >> 62) == 2), xm_ = __ballot((v[f] >> 62) == 0);
+      first_p[f] = pm ? __builtin_ctzll(pm) : 64;
+      const uint64_t upto_p = first_p[f] >= 63 ? ~0ull : ((2ull << first_p[f]) - 1);
+      retry |= !done[f] && (xm_ & upto_p) != 0;
+    }
+    if (retry) {
+      if (++spins > kLbSpinLimit) {  // cannot happen with in-order dispatch; never hang
+        if (lane == 0) atomicOr(A.lb_err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      if (done[f]) continue;
+      acc[f] += wave_sum_u64(lane <= first_p[f] ? (v[f] & kLbV) : 0);
+      done[f] = first_p[f] < 64;
+    }
+    j -= 64;
+  }
+  xk = acc[0];
+  xn = acc[1];
+  xm = acc[2];
+  if (lane == 0) {
+    lb_store(&A.lb_k[b], kLbP | (xk + ak));
+    lb_store(&A.lb_n[b], kLbP | (xn + an));
+    lb_store(&A.lb_m[b], kLbP | (xm + am));
+    if (b + 1 == A.nbuckets) {
+      A.lb_tot[0] = xk + ak;
+      A.lb_tot[1] = xn + an;
+      A.lb_tot[2] = xm + am;
+    }
+  }
+}
+
 // One bucket on one wave, up to 64*KE key rows and 128*KE child rows, from the columns in
 // `in`. KE = 1 leaves buckets over that capacity to bucket_wide_kernel and lists those over
 // ITS capacity (and forced tiers) for the workgroup tier. `next()` runs exactly once, as
@@ -204,7 +277,17 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   constexpr uint32_t KC = WaveLds<KE>::KC, CC = WaveLds<KE>::CC;
   const BucketArgs& A = W.A;
   const uint32_t K = in.d.K, N = in.d.N, M = in.d.M;
+  // single-pass placement: every bucket of this kernel takes part in the look-back, those
+  // left to another tier with zero counts (their outputs are compacted after that tier)
+  const bool dense = KE == 1 && A.lb_k != nullptr;
+  auto pass_on = [&]() {
+    if (dense) {
+      uint64_t x0, x1, x2;
+      lookback(A, b, lane, 0, 0, 0, x0, x1, x2);
+    }
+  };
   auto push = [&](uint32_t* list, uint32_t* count) {
+    pass_on();
     if (lane == 0) list[atomicAdd(count, 1u)] = b;
   };
   if (KE == 1) {  // the wide kernel finds its buckets itself (wide_bucket_candidate)
@@ -215,6 +298,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     }
     if (K > KC || N + M > CC || A.force_tier == 3) {
       next();
+      pass_on();
       return;
     }
   }
@@ -536,13 +620,27 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     En[e] = __ballot(cemit[e] && knode[e]);
     Em[e] = __ballot(cemit[e] && !knode[e]);
   }
+  // output positions: the bucket's sparse slots (input offsets), or dense offsets from the
+  // look-back over every earlier bucket's output counts
+  uint64_t xk = kb, xn = nb0, xm = mb0;
+  if (dense) {
+    uint32_t an = 0, am = 0;
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      an += __popcll(En[e]);
+      am += __popcll(Em[e]);
+    }
+    lookback(A, b, lane, kout, an, am, xk, xn, xm);
+  }
+  uint64_t* const* NO = dense ? A.dno : A.no;
+  uint64_t* const* MO = dense ? A.dmo : A.mo;
   uint32_t nbase = 0, mbase = 0;
 #pragma unroll
   for (int e = 0; e < CE; ++e) {
     if (cemit[e]) {
       const uint32_t crank = (knode[e] ? nbase : mbase) + lane_rank(knode[e] ? En[e] : Em[e]);
-      const uint32_t o = (knode[e] ? nb0 : mb0) + crank;
-      uint64_t* const* O = knode[e] ? A.no : A.mo;
+      const uint64_t o = (knode[e] ? xn : xm) + crank;
+      uint64_t* const* O = knode[e] ? NO : MO;
       const uint32_t k = (uint32_t)(sw_[e] >> 56) & (KC - 1);
       O[C_PKH][o] = L.okh[k];
       O[C_PKF][o] = L.okf[k];
@@ -561,24 +659,28 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   wave_sync();
 
   // ------------------------------------------------------------ 5. key outputs
+  uint64_t* const* KO = dense ? A.dko : A.ko;
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
     if (emit[e]) {
-      const uint32_t r = orank[e], o = kb + r;
-      A.ko[O_KH][o] = kh[e];
-      A.ko[O_KF][o] = kf[e];
-      A.ko[O_CT][o] = o_ct[e];
-      A.ko[O_UT][o] = o_ut[e];
-      A.ko[O_DT][o] = o_dt[e];
-      A.ko[O_META][o] = o_meta[e];
-      A.ko[O_WIN][o] = (fam[e] == 0 && o_T[e] == TAG_COUNTER) ? L.osum[r] : o_win[e];
-      A.ko[O_CREF][o] = cref_pack(L.ocnt[r] ? L.ocb[r] : 0, L.ocnt[r]);
+      const uint32_t r = orank[e];
+      const uint64_t o = xk + r;
+      KO[O_KH][o] = kh[e];
+      KO[O_KF][o] = kf[e];
+      KO[O_CT][o] = o_ct[e];
+      KO[O_UT][o] = o_ut[e];
+      KO[O_DT][o] = o_dt[e];
+      KO[O_META][o] = o_meta[e];
+      KO[O_WIN][o] = (fam[e] == 0 && o_T[e] == TAG_COUNTER) ? L.osum[r] : o_win[e];
+      // child ranges: bucket-relative (compaction makes them absolute), or absolute already
+      const uint64_t cb = dense ? (o_T[e] == TAG_COUNTER ? xn : xm) : 0;
+      KO[O_CREF][o] = cref_pack(L.ocnt[r] ? cb + L.ocb[r] : 0, L.ocnt[r]);
     }
   }
-  if (lane == 0) {
-    A.kout[b] = kout;
-    A.nout[b] = nbase;
-    A.mout[b] = mbase;
+  if (lane == 0) {  // a dense bucket leaves nothing for compaction
+    A.kout[b] = dense ? 0 : kout;
+    A.nout[b] = dense ? 0 : nbase;
+    A.mout[b] = dense ? 0 : mbase;
   }
   unsigned long long* st = stat_shard(A.stats);
   if (__ballot(st_conf)) {
@@ -712,7 +814,9 @@ __device__ __forceinline__ void wave_dispatch(const WaveArgs& W, WaveLds<1>* lds
 __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_kernel(WaveArgs W) {
   __shared__ WaveLds<1> lds_all[kWavesPerWG];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t b = xcd_block(blockIdx.x, gridDim.x) * kWavesPerWG + wv;
+  // buckets in dispatch order (the look-back relies on it; an XCD remap measured no faster
+  // with whole-row reads)
+  const uint32_t b = blockIdx.x * kWavesPerWG + wv;
   if (b >= W.nbuckets) return;
   const WaveDir d = load_dir(W.A, b);
   WavePerm<1> p;

@@ -30,6 +30,7 @@ enum WsSlot {
   WS_PERM,                                              // final-level row permutations (u32)
   WS_STATS,                                             // statistic shards
   WS_KHCOL,                                             // key-hash column of the row level
+  WS_LOOKBACK,                                          // output look-back status words
   WS_COUNT
 };
 

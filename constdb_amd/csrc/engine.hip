@@ -92,6 +92,7 @@ struct CompactArgs {
   const uint64_t* ms[kMemberCols];
   uint64_t* md[kMemberCols];
   const uint32_t *kbase, *nbase, *mbase, *kout, *nout, *mout, *kdoff, *ndoff, *mdoff;
+  const unsigned long long* base_tot;  // dense rows already placed by the wave tier, per family
 };
 
 // Sparse-by-bucket outputs -> dense arrays; child ranges become absolute row indices.
@@ -119,14 +120,16 @@ __device__ __forceinline__ int group_bucket(const uint32_t* rel, uint32_t t) {  
 template <int FAM>
 __device__ __forceinline__ void compact_row(const CompactArgs& A, const CompactLds& L, uint32_t t, uint32_t d0) {
   const int j = group_bucket(L.doff, t);
-  const uint32_t src = L.sbase[j] + (t - L.doff[j]), dst = d0 + t;
+  const uint32_t src = L.sbase[j] + (t - L.doff[j]);
+  const uint64_t dst = A.base_tot[FAM] + d0 + t;
   if constexpr (FAM == 0) {
     uint64_t v[kKeyOutCols];
 #pragma unroll
     for (int c = 0; c < kKeyOutCols; ++c) v[c] = A.ks[c][src];
     const uint64_t cnt = v[O_CREF] & 0xFFFFFF;
     const uint32_t T = meta_tag(v[O_META]);
-    const uint64_t begin = cnt ? (v[O_CREF] >> 24) + (T == TAG_COUNTER ? L.ndoff[j] : L.mdoff[j]) : 0;
+    const uint64_t begin =
+        cnt ? (v[O_CREF] >> 24) + (T == TAG_COUNTER ? A.base_tot[1] + L.ndoff[j] : A.base_tot[2] + L.mdoff[j]) : 0;
     v[O_CREF] = cref_pack(begin, cnt);
 #pragma unroll
     for (int c = 0; c < kKeyOutCols; ++c) A.kd[c][dst] = v[c];
@@ -527,6 +530,32 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   A.stats = d_shards;
   A.hot_list = d_hot_list;
   A.hot_count = d_hot_count;
+  // look-back status words (3 x nb) | wave-tier totals (3) | error flag. Off by default
+  // (CDB_LOOKBACK=1 turns it on): it removes the compaction of the wave tier's rows (finish
+  // 6.6 -> 0.8 ms on the C4 shard) but a bucket's counts are known only at its very end, so
+  // waves queue behind their slowest predecessor and the bucket phase goes 19 -> 48 ms.
+  static const bool lookback_on = [] {
+    const char* e = std::getenv("CDB_LOOKBACK");
+    return e && std::atoi(e) == 1;
+  }();
+  const bool dense = lookback_on && wave_pf() == 0;
+  unsigned long long* lbw =
+      (unsigned long long*)ws_get(ctx, WS_LOOKBACK, (3 * nb + 4) * sizeof(unsigned long long) + 64, &st);
+  if (!lbw) return st;
+  unsigned long long* d_lb_tot = lbw + 3 * nb;  // zero unless the wave tier places rows
+  CDB_HIP(hipMemsetAsync(lbw, 0, (3 * nb + 4) * sizeof(unsigned long long), s), "memset lookback");
+  if (dense) {
+    A.lb_k = lbw;
+    A.lb_n = lbw + nb;
+    A.lb_m = lbw + 2 * nb;
+    A.lb_tot = d_lb_tot;
+    A.lb_err = (uint32_t*)(d_lb_tot + 3);
+    for (int c = 0; c < kKeyOutCols; ++c) A.dko[c] = out->keys.col[c];
+    for (int c = 0; c < kNodeCols; ++c) {
+      A.dno[c] = out->nodes.col[c];
+      A.dmo[c] = out->members.col[c];
+    }
+  }
   WaveArgs WA;
   WA.A = A;
   WA.nbuckets = (uint32_t)nb;
@@ -596,6 +625,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   C.kbase = dk.base; C.nbase = dnd.base; C.mbase = dm.base;
   C.kout = dk.out; C.nout = dnd.out; C.mout = dm.out;
   C.kdoff = dk.doff; C.ndoff = dnd.doff; C.mdoff = dm.doff;
+  C.base_tot = d_lb_tot;
   compact_kernel<<<(uint32_t)((3 * ((nb + 63) / 64) + kCompactWaves - 1) / kCompactWaves), 64 * kCompactWaves, 0,
                    s>>>(C, (uint32_t)nb);
   CDB_TRY(launch_check(ctx, s, "compact_kernel"));
@@ -604,10 +634,14 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   CDB_HIP(hipEventRecord(ctx->ev1, s), "event");
 
   uint64_t totals[3];
-  unsigned long long hs[ST_COUNT];
+  unsigned long long hs[ST_COUNT], wave_tot[4];
   CDB_HIP(hipMemcpyAsync(totals, d_totals, sizeof totals, hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipMemcpyAsync(hs, d_stats, sizeof hs, hipMemcpyDeviceToHost, s), "d2h");
+  CDB_HIP(hipMemcpyAsync(wave_tot, d_lb_tot, sizeof wave_tot, hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipStreamSynchronize(s), "sync");
+  if ((uint32_t)wave_tot[3])
+    return fail(ctx, CDB_DEVICE_ERROR, "output look-back did not converge (bucket dispatch order violated)");
+  for (int f = 0; f < 3; ++f) totals[f] += wave_tot[f];
   out->keys.n = totals[0];
   out->nodes.n = totals[1];
   out->members.n = totals[2];
