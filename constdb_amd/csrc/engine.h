@@ -12,6 +12,8 @@ struct cdb_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_part = nullptr, ev_bucket = nullptr;
+  hipStream_t side = nullptr;                         // the wide tier runs beside the wave tier
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;    // (timing disabled)
   std::string last_error;
   struct Buf { void* p = nullptr; size_t bytes = 0; };
   Buf ws[32];  // named workspace slots, grown on demand, reused across calls

@@ -561,6 +561,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   WA.nbuckets = (uint32_t)nb;
   WA.big_list = d_big_list;
   WA.big_count = d_big_count;
+  CDB_HIP(hipEventRecord(ctx->ev_fork, s), "event");  // inputs of both bucket tiers are ready
   if (wave_pf() == 0)
     bucket_wave_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA);
   else if (wave_pf() == 1)
@@ -568,9 +569,19 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   else
     bucket_wave_pf2_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
   CDB_TRY(launch_check(ctx, s, "bucket_wave_kernel"));
-  bucket_wide_kernel<<<(uint32_t)std::min<uint64_t>((nb + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024),
-                       kWavesPerWG * 64, 0, s>>>(WA);
-  CDB_TRY(launch_check(ctx, s, "bucket_wide_kernel"));
+  {  // the wide tier's buckets are disjoint from the wave tier's: it runs on a side stream
+     // and fills the wave kernel's tail (CDB_WIDE_SERIAL=1 runs it after the wave kernel)
+    static const bool serial = std::getenv("CDB_WIDE_SERIAL") != nullptr;
+    hipStream_t ws = serial ? s : ctx->side;
+    const uint32_t g = (uint32_t)std::min<uint64_t>((nb + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024);
+    if (!serial) CDB_HIP(hipStreamWaitEvent(ws, ctx->ev_fork, 0), "wait");
+    bucket_wide_kernel<<<g, kWavesPerWG * 64, 0, ws>>>(WA);
+    CDB_TRY(launch_check(ctx, ws, "bucket_wide_kernel"));
+    if (!serial) {
+      CDB_HIP(hipEventRecord(ctx->ev_join, ws), "event");
+      CDB_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0), "wait");
+    }
+  }
   bucket_mid_kernel<<<std::min<uint64_t>(nb, 2048), kBktThreads, 0, s>>>(A, d_big_list, d_big_count);
   CDB_TRY(launch_check(ctx, s, "bucket_mid_kernel"));
   CDB_HIP(hipEventRecord(ctx->ev_bucket, s), "event");
@@ -691,6 +702,9 @@ cdb_status cdb_ctx_create(cdb_ctx** out, int device) {
   ctx->device = device;
   cdb_status st = hip_check(ctx, hipSetDevice(device), "hipSetDevice");
   if (st == CDB_OK) st = hip_check(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "stream");
+  if (st == CDB_OK) st = hip_check(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking), "stream");
+  if (st == CDB_OK) st = hip_check(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming), "event");
+  if (st == CDB_OK) st = hip_check(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming), "event");
   if (st == CDB_OK) st = hip_check(ctx, hipEventCreate(&ctx->ev0), "event");
   if (st == CDB_OK) st = hip_check(ctx, hipEventCreate(&ctx->ev1), "event");
   if (st == CDB_OK) st = hip_check(ctx, hipEventCreate(&ctx->ev_part), "event");
@@ -712,6 +726,9 @@ void cdb_ctx_destroy(cdb_ctx* ctx) {
   if (ctx->ev1) hipEventDestroy(ctx->ev1);
   if (ctx->ev_part) hipEventDestroy(ctx->ev_part);
   if (ctx->ev_bucket) hipEventDestroy(ctx->ev_bucket);
+  if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
+  if (ctx->ev_join) hipEventDestroy(ctx->ev_join);
+  if (ctx->side) hipStreamDestroy(ctx->side);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
 }
