@@ -108,6 +108,12 @@ class MergeStats(ctypes.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+class ReplicaEntry(ctypes.Structure):
+    _fields_ = [("addr", ctypes.c_char_p), ("alias", ctypes.c_char_p), ("node_id", ctypes.c_uint64),
+                ("uuid_he_sent", ctypes.c_uint64), ("add_time", ctypes.c_uint64), ("del_time", ctypes.c_uint64),
+                ("has_add", ctypes.c_uint32), ("has_del", ctypes.c_uint32)]
+
+
 class DevRows(ctypes.Structure):
     _fields_ = [("col", ctypes.c_void_p * 8), ("n", ctypes.c_uint64)]
 
@@ -132,7 +138,8 @@ class GenConfig(ctypes.Structure):
 # exported C-ABI function names (tests check the .so exports every one of them)
 ABI_FUNCTIONS = (
     "cdb_ctx_create", "cdb_ctx_destroy", "cdb_last_error", "cdb_decode_snapshot", "cdb_batch_info_get",
-    "cdb_batch_column", "cdb_batch_free", "cdb_merge", "cdb_merged_canonical_dump", "cdb_merged_free", "cdb_free",
+    "cdb_batch_column", "cdb_batch_free", "cdb_merge", "cdb_merged_canonical_dump", "cdb_merged_replicas",
+    "cdb_merged_free", "cdb_free",
     "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_partition_owner", "cdb_gen_default",
     "cdb_gen_snapshot", "cdb_gen_device")
 
@@ -168,6 +175,7 @@ def lib():
         "cdb_batch_free": (None, [vp]),
         "cdb_merge": (c_st, [vp, P(vp), ctypes.c_uint32, P(MergeOpts), P(vp), P(MergeStats)]),
         "cdb_merged_canonical_dump": (c_st, [vp, vp, P(vp), P(ctypes.c_size_t)]),
+        "cdb_merged_replicas": (c_st, [vp, P(P(ReplicaEntry)), P(ctypes.c_size_t)]),
         "cdb_merged_free": (None, [vp]),
         "cdb_free": (None, [vp]),
         "cdb_dev_rows_alloc": (c_st, [vp, P(DevRows), ctypes.c_uint64, ctypes.c_int]),
@@ -301,6 +309,24 @@ class Merged:
             return ctypes.string_at(out.value, n.value) if n.value else b""
         finally:
             lib().cdb_free(out)
+
+    def replicas(self):
+        """The merged replica table (cdb_merged_replicas, replica/pull.rs:131-156): one dict per
+        addr, sorted by addr, with the LWWHash add tag (node_id, alias, uuid_he_sent,
+        add_time) and/or del tag (del_time)."""
+        ptr = ctypes.POINTER(ReplicaEntry)()
+        n = ctypes.c_size_t()
+        self._ctx.check(lib().cdb_merged_replicas(self._h, ctypes.byref(ptr), ctypes.byref(n)))
+        out = []
+        for i in range(n.value):
+            e = ptr[i]
+            d = {"addr": e.addr.decode()}
+            if e.has_add:
+                d["add"] = (e.add_time, e.node_id, e.alias.decode(), e.uuid_he_sent)
+            if e.has_del:
+                d["del"] = e.del_time
+            out.append(d)
+        return out
 
     def __del__(self):
         try:

@@ -14,8 +14,8 @@ struct ByteRef {  // a byte range inside Batch::raw
   uint64_t off, len;
 };
 
-struct ReplicaAdd { uint64_t add_time, node_id; std::string alias, addr; uint64_t uuid; };
-struct ReplicaDel { std::string addr; uint64_t t; };
+struct ReplicaAdd { uint64_t add_time, node_id; std::string alias, addr; uint64_t uuid; uint32_t seq; };
+struct ReplicaDel { std::string addr; uint64_t t; uint32_t seq; };  // seq: order among the replica entries
 
 struct Batch {
   std::vector<uint8_t> raw;  // the snapshot bytes: arena for keys, values, members

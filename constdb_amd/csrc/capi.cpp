@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -25,6 +26,10 @@ struct cdb_batch {
 struct cdb_merged {
   std::vector<std::shared_ptr<cdb::Batch>> inputs;  // pos -> decoded batch (byte arenas)
   std::vector<uint64_t> k[cdb::kKeyOutCols], nd[cdb::kNodeCols], mb[cdb::kMemberCols];
+  // replica-metadata merge, computed on first request
+  bool replicas_done = false;
+  std::vector<std::string> rep_str;          // addr / alias storage (stable: reserved up front)
+  std::vector<cdb_replica_entry> replicas;
 };
 
 using namespace cdb;
@@ -293,6 +298,94 @@ cdb_status cdb_merged_canonical_dump(cdb_ctx* ctx, cdb_merged* m, char** out, si
   std::memcpy(*out, o.data(), o.size());
   (*out)[o.size()] = 0;
   *len = o.size();
+  return CDB_OK;
+}
+
+// Replica-metadata merge (replica/pull.rs:131-156): ReplicaManager::add_replica / remove_replica
+// over LWWHash<addr, ReplicaMeta> (replica/replica.rs:29-35, crdt/lwwhash.rs:87-128).
+cdb_status cdb_merged_replicas(cdb_merged* m, const cdb_replica_entry** out, size_t* n) {
+  if (!m || !out || !n) return CDB_BAD_ARGUMENT;
+  if (!m->replicas_done) {
+    struct Add { uint64_t t, id, uuid; std::string alias; };
+    std::map<std::string, Add> add;        // addr -> (add_time, meta)
+    std::map<std::string, uint64_t> del;   // addr -> del_time
+    auto set = [&](const std::string& k, const Add& v) {  // lwwhash.rs:87-107
+      auto d = del.find(k);
+      if (d != del.end() && d->second > v.t) return;
+      auto a = add.find(k);
+      if (a != add.end()) {
+        if (a->second.t > v.t) return;
+        a->second = v;
+      } else {
+        if (d != del.end()) del.erase(d);
+        add.emplace(k, v);
+      }
+    };
+    auto rem = [&](const std::string& k, uint64_t t) {  // lwwhash.rs:109-128
+      auto a = add.find(k);
+      if (a != add.end() && a->second.t > t) return;
+      auto d = del.find(k);
+      if (d != del.end()) {
+        if (d->second > t) return;
+        d->second = t;
+      } else {
+        del.emplace(k, t);
+        if (a != add.end()) add.erase(a);
+      }
+    };
+    const uint64_t myself = m->inputs.empty() ? 0 : m->inputs[0]->node_id;
+    for (size_t i = 0; i < m->inputs.size(); ++i) {
+      const Batch& b = *m->inputs[i];
+      if (i == 0) {  // the local ReplicaManager itself: its maps as dumped (replica.rs:100-119)
+        for (const ReplicaAdd& r : b.replica_add) add[r.addr] = Add{r.add_time, r.node_id, r.uuid, r.alias};
+        for (const ReplicaDel& r : b.replica_del) del[r.addr] = r.t;
+        continue;
+      }
+      size_t ia = 0, id = 0;  // the two lists merged back into stream order
+      while (ia < b.replica_add.size() || id < b.replica_del.size()) {
+        const bool take_add =
+            id == b.replica_del.size() || (ia < b.replica_add.size() && b.replica_add[ia].seq < b.replica_del[id].seq);
+        if (take_add) {
+          const ReplicaAdd& r = b.replica_add[ia++];
+          if (r.node_id != myself) set(r.addr, Add{r.add_time, r.node_id, r.uuid, r.alias});  // pull.rs:133-135
+        } else {
+          const ReplicaDel& r = b.replica_del[id++];
+          rem(r.addr, r.t);
+        }
+      }
+    }
+    std::map<std::string, cdb_replica_entry> all;
+    m->rep_str.reserve(2 * (add.size() + del.size()) + 1);
+    auto keep = [&](const std::string& x) {
+      m->rep_str.push_back(x);
+      return m->rep_str.back().c_str();
+    };
+    for (auto& kv : add) {
+      cdb_replica_entry e{};
+      e.addr = keep(kv.first);
+      e.alias = keep(kv.second.alias);
+      e.node_id = kv.second.id;
+      e.uuid_he_sent = kv.second.uuid;
+      e.add_time = kv.second.t;
+      e.has_add = 1;
+      all[kv.first] = e;
+    }
+    for (auto& kv : del) {
+      auto it = all.find(kv.first);
+      if (it == all.end()) {
+        cdb_replica_entry e{};
+        e.addr = keep(kv.first);
+        e.alias = keep("");
+        it = all.emplace(kv.first, e).first;
+      }
+      it->second.del_time = kv.second;
+      it->second.has_del = 1;
+    }
+    for (auto& kv : all) m->replicas.push_back(kv.second);
+    m->replicas_done = true;
+  }
+  *out = m->replicas.empty() ? nullptr : m->replicas.data();
+  *n = m->replicas.size();
   return CDB_OK;
 }
 

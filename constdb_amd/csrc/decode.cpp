@@ -332,10 +332,12 @@ struct Decoder {
         ReplicaAdd r;
         if (!c.u64(&r.add_time) || !c.u64(&r.node_id) || !str(&r.alias) || !str(&r.addr) || !c.u64(&r.uuid))
           return fail();
+        r.seq = (uint32_t)(b->replica_add.size() + b->replica_del.size());
         b->replica_add.push_back(std::move(r));
       } else if (flag == 4) {  // SNAPSHOT_FLAG_REPLICA_REM
         ReplicaDel r;
         if (!str(&r.addr) || !c.u64(&r.t)) return fail();
+        r.seq = (uint32_t)(b->replica_add.size() + b->replica_del.size());
         b->replica_del.push_back(std::move(r));
       } else if (flag == 5 || flag == 6 || flag == 7) {  // DATAS / EXPIRES / DELETES
         uint64_t cnt;

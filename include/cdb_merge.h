@@ -142,6 +142,25 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n,
  * by id, then expires and deletes (the text format of oracle/constdb_oracle.py's
  * canonical_dump). *out is released with cdb_free. */
 cdb_status cdb_merged_canonical_dump(cdb_ctx* ctx, cdb_merged* m, char** out, size_t* len);
+
+/* Replica-metadata merge: the ReplicaManager's LWWHash<addr, ReplicaMeta>
+ * (replica/replica.rs:16-35) after the same fold. Input 0 is the local node: its ReplicaAdd /
+ * ReplicaDel entries are installed verbatim (its own add and del maps). Every later input's
+ * entries are then applied in stream order. A ReplicaAdd goes through add_replica ->
+ * LWWHash::set (lwwhash.rs:87-107) unless it names input 0's node id (pull.rs:133-135); a
+ * ReplicaDel goes through remove_replica -> LWWHash::rem (lwwhash.rs:109-128). The result is
+ * sorted by addr; strings are NUL-terminated and live as long as the merged result. Host-side:
+ * a few entries per snapshot. */
+typedef struct cdb_replica_entry {
+  const char* addr;
+  const char* alias;      /* ReplicaMeta.he.alias of the add tag ("" without one) */
+  uint64_t node_id;       /* ReplicaMeta.he.id of the add tag */
+  uint64_t uuid_he_sent;  /* ReplicaMeta.uuid_he_sent of the add tag */
+  uint64_t add_time;      /* add tag time (has_add) */
+  uint64_t del_time;      /* del tag time (has_del) */
+  uint32_t has_add, has_del;
+} cdb_replica_entry;
+cdb_status cdb_merged_replicas(cdb_merged* m, const cdb_replica_entry** out, size_t* n);
 void cdb_merged_free(cdb_merged* m);
 void cdb_free(void* p);
 

@@ -680,6 +680,43 @@ def fold_snapshots(snapshots: List[bytes], dict_panic: bool = False,
     return db
 
 
+def fold_replicas(snapshots: List[bytes], checksum_mode: str = "writer") -> List[dict]:
+    """Replica-metadata merge (replica/pull.rs:131-156): ReplicaManager.replicas is an
+    LWWHash<addr, ReplicaMeta> (replica/replica.rs:16-35). Snapshot 0 is the local node: its
+    ReplicaAdd / ReplicaDel entries ARE its add / del maps (dump_snapshot, replica.rs:100-119).
+    Every later snapshot is applied in stream order: ReplicaAdd -> add_replica -> set
+    (skipped when it names the local node id, pull.rs:133-135), ReplicaDel -> remove_replica
+    -> rem. Returns one dict per addr, sorted by addr (the shape of Merged.replicas())."""
+    h = LWWHash()
+    myself = None
+    for i, snap in enumerate(snapshots):
+        for e in load_snapshot(snap, checksum_mode):
+            if e.kind == "Node" and i == 0:
+                myself = e.args[0]
+            elif e.kind == "ReplicaAdd":
+                add_time, nid, alias, addr, uuid = e.args
+                if i == 0:
+                    h.add[addr.encode()] = (add_time, (nid, alias, uuid))
+                elif nid != myself:
+                    h.set(addr.encode(), (nid, alias, uuid), add_time)
+            elif e.kind == "ReplicaDel":
+                addr, t = e.args
+                if i == 0:
+                    h.dele[addr.encode()] = t
+                else:
+                    h.rem(addr.encode(), t)
+    out = []
+    for k in sorted(set(h.add) | set(h.dele)):
+        d = {"addr": k.decode()}
+        if k in h.add:
+            t, (nid, alias, uuid) = h.add[k]
+            d["add"] = (t, nid, alias, uuid)
+        if k in h.dele:
+            d["del"] = h.dele[k]
+        out.append(d)
+    return out
+
+
 # --------------------------------------------------------------------------------------
 # Canonical dump (the parity contract, SURVEY §8a): keys sorted by bytes, members by
 # bytes, counter nodes by id. Text, one record per line; identical format in

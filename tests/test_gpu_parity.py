@@ -360,3 +360,22 @@ def test_full_c4_shard_invariants(db):
     finally:
         for fam in (din.keys, din.nodes, din.members):
             L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
+
+
+# ------------------------------------------------------------------ replica metadata (§8f.4)
+@pytest.mark.parametrize("seed", range(8))
+def test_replica_metadata_merge(db, seed):
+    """cdb_merged_replicas vs the oracle's fold_replicas on random replica tables with tied
+    times, self-references and add/del interleavings (replica/pull.rs:131-156)."""
+    import random
+    rng = random.Random(seed)
+    addrs = [f"10.0.0.{i}:9000" for i in range(6)]
+    hdrs = []
+    for r in range(1 + seed % 4):
+        adds = [(rng.randint(1, 8), rng.choice([1, 2, 3, 7]), f"n{rng.randint(0, 9)}", rng.choice(addrs),
+                 rng.randint(0, 1 << 40)) for _ in range(rng.randint(0, 6))]
+        dels = [(rng.choice(addrs), rng.randint(1, 8)) for _ in range(rng.randint(0, 4))]
+        hdrs.append(o.NodeHeader(node_id=1 + r, replicas_add=adds, replicas_del=dels))
+    snaps = [o.dump_all(o.DB(), h) for h in hdrs]
+    m = db.merge_snapshots(snaps)
+    assert m.replicas() == o.fold_replicas(snaps)

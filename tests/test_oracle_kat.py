@@ -293,3 +293,29 @@ def test_canonical_dump_is_sorted_and_stable():
     assert o.canonical_dump(db).decode().splitlines() == [
         "K 61 5 1 0 0", " D 71 3", " A 79 2", " A 7a 1",
         "K 62 3 1 0 0", " V 00", "X 65 5", "R 64 4"]
+
+
+# ---------------------------------------------------------------- replica metadata (§8f.4)
+def test_kat_replica_metadata_merge():
+    """ReplicaManager's LWWHash<addr, ReplicaMeta> through the fold (replica/pull.rs:131-156,
+    replica/replica.rs:29-35, crdt/lwwhash.rs:87-128); expected values derived by hand."""
+    import constdb_oracle as o
+    empty = o.DB()
+    local = o.NodeHeader(node_id=1, replicas_add=[(5, 2, "a", "A", 50), (7, 4, "c", "C", 70)],
+                         replicas_del=[("B", 9)])
+    r1 = o.NodeHeader(node_id=2, replicas_add=[
+        (4, 2, "a-old", "A", 40),       # add older than A's add tag (5): rejected
+        (10, 3, "b", "B", 100),         # newer than B's del tag (9): B comes back, del tag dropped
+        (99, 1, "me", "SELF", 1)],      # names the local node: skipped (pull.rs:133-135)
+        replicas_del=[("A", 5), ("C", 6)])  # A: tie with its add -> removed; C: older -> kept
+    r2 = o.NodeHeader(node_id=3, replicas_add=[(5, 2, "a2", "A", 55)])  # tie with A's del: re-added
+    snaps = [o.dump_all(empty, h) for h in (local, r1, r2)]
+    got = o.fold_replicas(snaps)
+    assert got == [
+        {"addr": "A", "add": (5, 2, "a2", 55)},
+        {"addr": "B", "add": (10, 3, "b", 100)},
+        {"addr": "C", "add": (7, 4, "c", 70)},
+    ]
+    # local maps are installed verbatim, both tags kept
+    both = o.NodeHeader(node_id=1, replicas_add=[(8, 5, "d", "D", 1)], replicas_del=[("D", 3)])
+    assert o.fold_replicas([o.dump_all(empty, both)]) == [{"addr": "D", "add": (8, 5, "d", 1), "del": 3}]
