@@ -307,8 +307,8 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const
       // the final level writes the bucket directory over base/hist
       CDB_HIP(hipMemcpyAsync(d.out, d.base, nprev * sizeof(uint32_t), hipMemcpyDeviceToDevice, s), "d2d");
       CDB_HIP(hipMemcpyAsync(d.doff, d.hist, nprev * sizeof(uint32_t), hipMemcpyDeviceToDevice, s), "d2d");
-      part_final_kernel<<<(uint32_t)nprev, kFinalThreads, 0, s>>>(khcol, d.out, d.doff, nprev, plan.d[l], shift,
-                                                                  d.base, d.hist, perm);
+      part_final_kernel<<<(uint32_t)nprev, kFinalThreads, 0, s>>>(reinterpret_cast<const uint16_t*>(khcol), d.out,
+                                                                  d.doff, nprev, plan.d[l], d.base, d.hist, perm);
       CDB_TRY(launch_check(ctx, s, "partition (final level)"));
       nprev = ncur;
       continue;
@@ -328,15 +328,18 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const
         co.c[c] = dst[c];
       }
       if (kind == 1) {
+        // before a per-segment final level, leave each row's u16 digit in place of the key hash
+        uint16_t* dig = plan.seg_final ? reinterpret_cast<uint16_t*>(khcol) : nullptr;
+        const uint32_t d1 = plan.seg_final ? plan.d[l + 1] : 0;
         if (aos_tile() == 2048)
           part_scatter_aos_kernel<NC, W, 2048, 2048><<<(n + 2047) / 2048, kPartThreads, 0, s>>>(
-              ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor);
+              ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor, dig, d1);
         else if (aos_tile() == 512)
           part_scatter_aos_kernel<NC, W, 512, 1024><<<(n + 511) / 512, kPartThreads, 0, s>>>(
-              ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor);
+              ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor, dig, d1);
         else
           part_scatter_aos_kernel<NC, W, 1024, 1024><<<(n + 1023) / 1024, kPartThreads, 0, s>>>(
-              ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor);
+              ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor, dig, d1);
         CDB_TRY(launch_check(ctx, s, "partition (row level)"));
         *rows = dst[0];
         for (int c = 0; c < NC; ++c) spare[c] = (dst == A ? Bf : A)[c];

@@ -208,7 +208,11 @@ template <int NC, int W, int TILE = 1024, int LMAX = 1024>
 __global__ void __launch_bounds__(kPartThreads) part_scatter_aos_kernel(ColSet<NC> in, uint64_t* __restrict__ aos,
                                                                         uint64_t* __restrict__ khcol, uint64_t n,
                                                                         uint64_t nprev, uint32_t d, int shift,
-                                                                        uint32_t* __restrict__ cursor) {
+                                                                        uint32_t* __restrict__ cursor,
+                                                                        uint16_t* __restrict__ dig = nullptr,
+                                                                        uint32_t d1 = 0) {
+  // dig != nullptr (a per-segment final level follows): instead of the key-hash column, each
+  // row's digit inside its segment, floor(h * ncur * d1 / 2^64) - segment * d1, as a u16.
   static_assert(W % 2 == 0 && W >= NC, "rows leave as 16-B pieces");
   constexpr int kAosTile = TILE;
   constexpr int kLocal = LMAX;
@@ -230,10 +234,12 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_aos_kernel(ColSet<N
   if (span64 > (uint64_t)kLocal) {  // wide tile: per-row global reservation
     for (int r = threadIdx.x; r < rows; r += kPartThreads) {
       const uint64_t h = in.c[0][tile0 + r];
-      const uint32_t p = atomicAdd(&cursor[bucket_of_n(h << shift, ncur)], 1u);
+      const uint64_t gb = bucket_of_n(h << shift, ncur);
+      const uint32_t p = atomicAdd(&cursor[gb], 1u);
 #pragma unroll
       for (int c = 0; c < W; ++c) aos[(uint64_t)p * W + c] = c < NC ? in.c[c < NC ? c : 0][tile0 + r] : 0;
-      khcol[p] = h;
+      if (dig) dig[p] = (uint16_t)(bucket_of_n(h << shift, ncur * d1) - gb * d1);
+      else khcol[p] = h;
     }
     return;
   }
@@ -281,7 +287,14 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_aos_kernel(ColSet<N
     const uint64_t dst = (uint64_t)(delta[slot_lb[j]] + (uint32_t)j) * W + 2 * q;
     *reinterpret_cast<ulonglong2*>(&aos[dst]) = *reinterpret_cast<const ulonglong2*>(&stage[j * W + 2 * q]);
   }
-  for (int j = threadIdx.x; j < rows; j += kPartThreads) khcol[delta[slot_lb[j]] + j] = stage[j * W];
+  if (dig) {
+    for (int j = threadIdx.x; j < rows; j += kPartThreads) {
+      const uint64_t gb = glo + slot_lb[j];
+      dig[delta[slot_lb[j]] + j] = (uint16_t)(bucket_of_n(stage[j * W] << shift, ncur * d1) - gb * d1);
+    }
+  } else {
+    for (int j = threadIdx.x; j < rows; j += kPartThreads) khcol[delta[slot_lb[j]] + j] = stage[j * W];
+  }
 }
 
 // ---------------------------------------------------------------- final level, per segment
@@ -289,15 +302,15 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_aos_kernel(ColSet<N
 // rows of row-level bucket s, contiguous in `khcol` order) is split into d1 buckets by ONE
 // workgroup: an LDS histogram of the segment, its scan (the bucket directory of the segment,
 // written straight to base_out / hist_out), and an LDS-cursor scatter of row indices into
-// perm. No global histogram pass, no device-wide scan, no global atomics; the segment's
-// key-hash column (~1 MB) is read twice, the second time from L2.
+// perm. No global histogram pass, no device-wide scan, no global atomics; the row level left
+// each row's digit as a u16, read twice (2 B per row each time).
 constexpr int kFinalThreads = 1024;
 constexpr int kFinalMaxD = 16384;
 
-__global__ void __launch_bounds__(kFinalThreads) part_final_kernel(const uint64_t* __restrict__ khcol,
+__global__ void __launch_bounds__(kFinalThreads) part_final_kernel(const uint16_t* __restrict__ dig,
                                                                    const uint32_t* __restrict__ sbase,
                                                                    const uint32_t* __restrict__ scnt, uint64_t nseg,
-                                                                   uint32_t d1, int shift,
+                                                                   uint32_t d1,
                                                                    uint32_t* __restrict__ base_out,
                                                                    uint32_t* __restrict__ hist_out,
                                                                    uint32_t* __restrict__ perm) {
@@ -305,23 +318,21 @@ __global__ void __launch_bounds__(kFinalThreads) part_final_kernel(const uint64_
   __shared__ uint32_t part[kFinalThreads / 64];
   const uint32_t s = blockIdx.x;
   const uint32_t b0 = sbase[s], n = scnt[s];
-  const uint64_t ntot = nseg * d1;
   const uint64_t g0 = (uint64_t)s * d1;
   for (uint32_t j = threadIdx.x; j < d1; j += kFinalThreads) cnt[j] = 0;
   __syncthreads();
   // 8 independent loads in flight per thread, then their LDS atomics
   constexpr int U = 8;
   for (uint32_t i0 = 0; i0 < n; i0 += U * kFinalThreads) {
-    uint64_t h[U];
+    uint32_t h[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + u * kFinalThreads + threadIdx.x;
-      h[u] = i < n ? khcol[b0 + i] : 0;
+      h[u] = i < n ? dig[b0 + i] : 0;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      if (i0 + u * kFinalThreads + threadIdx.x < n)
-        atomicAdd(&cnt[(uint32_t)(bucket_of_n(h[u] << shift, ntot) - g0)], 1u);
+      if (i0 + u * kFinalThreads + threadIdx.x < n) atomicAdd(&cnt[h[u]], 1u);
   }
   __syncthreads();
   // exclusive scan of cnt[0 .. d1): thread t owns a run of `per` consecutive entries
@@ -348,16 +359,16 @@ __global__ void __launch_bounds__(kFinalThreads) part_final_kernel(const uint64_
   }
   __syncthreads();
   for (uint32_t i0 = 0; i0 < n; i0 += U * kFinalThreads) {
-    uint64_t h[U];
+    uint32_t h[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + u * kFinalThreads + threadIdx.x;
-      h[u] = i < n ? khcol[b0 + i] : 0;
+      h[u] = i < n ? dig[b0 + i] : 0;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = i0 + u * kFinalThreads + threadIdx.x;
-      if (i < n) perm[b0 + atomicAdd(&cnt[(uint32_t)(bucket_of_n(h[u] << shift, ntot) - g0)], 1u)] = b0 + i;
+      if (i < n) perm[b0 + atomicAdd(&cnt[h[u]], 1u)] = b0 + i;
     }
   }
 }
