@@ -250,3 +250,57 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
         L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
     dist.destroy_process_group()
     return res
+
+
+def sharded_merge(cdb, ctx, din, n_pos: int, stream=None):
+    """One sharded merge step, outside the bench's timing harness: pack this rank's rows by
+    owner (cdb_partition_owner), exchange them (RCCL on GPU tensors; gloo through host copies),
+    merge the received shard with key_shift = log2(N). Returns ([keys, nodes, members] output
+    column tensors, MergeStats). Used by the multi-process tests; bench.py runs the same steps
+    with persistent buffers."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    ob = owner_bits(world)
+    L = cdb.lib()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    on_host = dist.get_backend() == "gloo"
+    fams = [din.keys, din.nodes, din.members]
+    counts = (ctypes.c_uint64 * world)()
+    send, send_counts = [], []
+    for f, fam in enumerate(fams):
+        t = torch.empty((FAMILY_COLS[f], max(fam.n, 1)), dtype=torch.int64, device=dev)
+        ctx.check(L.cdb_partition_owner(ctx.handle, ctypes.byref(fam), FAMILY_COLS[f], ob,
+                                        ctypes.byref(_rows_from_tensor(cdb, t, fam.n)), counts, stream))
+        send.append(t)
+        send_counts.append([counts[d] for d in range(world)])
+    recv_counts = exchange_counts(send_counts, device=None if on_host else dev)
+    recv = []
+    for f in range(3):
+        cols = [send[f][c][:fams[f].n] for c in range(FAMILY_COLS[f])]
+        if on_host:
+            cols = [c.cpu() for c in cols]
+        got = exchange_columns(cols, send_counts[f], recv_counts[f])
+        total = int(sum(recv_counts[f]))
+        buf = torch.empty((FAMILY_COLS[f], max(total, 1)), dtype=torch.int64, device=dev)
+        for c, g in enumerate(got):
+            buf[c][:total].copy_(g)
+        recv.append((buf, total))
+    torch.cuda.synchronize()
+    d2 = cdb.DevInput()
+    d2.keys, d2.nodes, d2.members = (_rows_from_tensor(cdb, b, n) for b, n in recv)
+    d2.n_pos = n_pos
+    dout = cdb.DevOutput()
+    outs = []
+    for f, (b, n) in enumerate(recv):
+        t = torch.empty((OUT_COLS[f], max(n, 1)), dtype=torch.int64, device=dev)
+        outs.append(t)
+    dout.keys, dout.nodes, dout.members = (_rows_from_tensor(cdb, t, 0) for t in outs)
+    dout.compact = 1
+    opts = cdb.MergeOpts()
+    opts.key_shift = ob
+    st = cdb.MergeStats()
+    ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(d2), ctypes.byref(opts), ctypes.byref(dout),
+                                 ctypes.byref(st), stream))
+    torch.cuda.synchronize()
+    return [outs[0][:, :dout.keys.n], outs[1][:, :dout.nodes.n], outs[2][:, :dout.members.n]], st

@@ -230,10 +230,11 @@ def test_deterministic(db):
     assert a == b
 
 
-@pytest.mark.parametrize("shift", [1, 3])
-def test_key_shift_parity(db, shift):
-    """Multi-GPU ranks bucket on the hash bits below the owner bits; any shift is exact."""
-    cfg = cdb.gen_config(seed=5, universe=20000, n_replicas=4, replica_hi=4)
+@pytest.mark.parametrize("shift,universe", [(1, 20000), (3, 20000), (3, 300000)])
+def test_key_shift_parity(db, shift, universe):
+    """Multi-GPU ranks bucket on the hash bits below the owner bits; any shift is exact (the
+    300K-key case takes the row-level + per-segment plan)."""
+    cfg = cdb.gen_config(seed=5, universe=universe, n_replicas=4, replica_hi=4)
     snaps = [cdb.gen_snapshot(cfg, r) for r in range(4)]
     want, _ = _oracle(snaps)
     batches = [cdb.decode_snapshot(s) for s in snaps]
