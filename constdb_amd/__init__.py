@@ -137,7 +137,8 @@ class GenConfig(ctypes.Structure):
 
 # exported C-ABI function names (tests check the .so exports every one of them)
 ABI_FUNCTIONS = (
-    "cdb_ctx_create", "cdb_ctx_destroy", "cdb_last_error", "cdb_decode_snapshot", "cdb_batch_info_get",
+    "cdb_ctx_create", "cdb_ctx_destroy", "cdb_last_error", "cdb_decode_snapshot", "cdb_decode_snapshot_gpu",
+    "cdb_batch_info_get",
     "cdb_batch_column", "cdb_batch_free", "cdb_merge", "cdb_merged_canonical_dump", "cdb_merged_replicas",
     "cdb_merged_free", "cdb_free",
     "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_partition_owner", "cdb_gen_default",
@@ -170,6 +171,8 @@ def lib():
         "cdb_last_error": (ctypes.c_char_p, [vp]),
         "cdb_decode_snapshot": (c_st, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, P(vp),
                                        P(ctypes.c_size_t)]),
+        "cdb_decode_snapshot_gpu": (c_st, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, P(vp),
+                                           P(ctypes.c_size_t), P(ctypes.c_double), P(ctypes.c_double)]),
         "cdb_batch_info_get": (c_st, [vp, P(BatchInfo)]),
         "cdb_batch_column": (c_st, [vp, ctypes.c_int, ctypes.c_int, P(P(ctypes.c_uint64)), P(ctypes.c_uint64)]),
         "cdb_batch_free": (None, [vp]),
@@ -287,6 +290,27 @@ def decode_snapshot(data: bytes, reference_checksum: bool = False, allow_bad_che
         if h:
             lib().cdb_batch_free(h)
         _raise(st, offset=off.value)
+    return Batch(h)
+
+
+def decode_snapshot_gpu(ctx: "Context", data: bytes, reference_checksum: bool = False,
+                        allow_bad_checksum: bool = False, timing: Optional[dict] = None) -> Batch:
+    """decode_snapshot with the per-entry work on the GPU (cdb_decode_snapshot_gpu, SURVEY
+    §8f.1): same batch, same errors. `timing` (a dict) receives index_ms / device_ms."""
+    h = ctypes.c_void_p()
+    off = ctypes.c_size_t()
+    ims, dms = ctypes.c_double(), ctypes.c_double()
+    flags = DECODE_REFERENCE_CHECKSUM if reference_checksum else 0
+    st = lib().cdb_decode_snapshot_gpu(ctx.handle, bytes(data), len(data), flags, ctypes.byref(h), ctypes.byref(off),
+                                       ctypes.byref(ims), ctypes.byref(dms))
+    if timing is not None:
+        timing.update(index_ms=ims.value, device_ms=dms.value)
+    if st == INVALID_SNAPSHOT_CHECKSUM and allow_bad_checksum and h:
+        return Batch(h, checksum_ok=False)
+    if st != OK:
+        if h:
+            lib().cdb_batch_free(h)
+        _raise(st, ctx.last_error(), offset=off.value)
     return Batch(h)
 
 

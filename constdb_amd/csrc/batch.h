@@ -48,4 +48,20 @@ struct Batch {
 // Decoder (decode.cpp). Returns a cdb_status value.
 int decode_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off);
 
+// GPU decode (decode_gpu.hip): the host validates the stream and indexes its entries (same
+// errors and offsets as decode_snapshot; header, replica entries and checksum decoded as
+// usual, no key rows), then kernels parse every entry.
+struct EntryIndex {
+  std::vector<uint64_t> offset;    // byte offset of the entry (its key's length varint)
+  std::vector<uint8_t> kind;       // 0 DATAS, 1 EXPIRES, 2 DELETES (stream order)
+  std::vector<uint64_t> children;  // raw child count: counter nodes or set/dict tags
+};
+int index_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, EntryIndex* idx, size_t* err_off);
+struct DecodeTiming {
+  double index_ms = 0;   // host pass
+  double device_ms = 0;  // uploads, both kernels, downloads (HIP events)
+};
+bool decode_entry_children(const Batch& b, uint64_t off, uint64_t kh, uint64_t kf, Batch* side, uint64_t* total);
+
+
 }  // namespace cdb

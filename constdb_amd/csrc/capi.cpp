@@ -89,6 +89,22 @@ cdb_status cdb_decode_snapshot(cdb_ctx* ctx, const uint8_t* buf, size_t len, uin
   return (cdb_status)rc;
 }
 
+cdb_status cdb_decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags, cdb_batch** out,
+                                   size_t* err_offset, double* index_ms, double* device_ms) {
+  if (!out || (!buf && len)) return CDB_BAD_ARGUMENT;
+  *out = nullptr;
+  if (!ctx) return CDB_NO_DEVICE;
+  auto b = std::make_shared<Batch>();
+  size_t eo = 0;
+  DecodeTiming tm;
+  const int rc = decode_snapshot_gpu(ctx, buf, len, flags, b.get(), &eo, &tm);
+  if (err_offset) *err_offset = eo;
+  if (index_ms) *index_ms = tm.index_ms;
+  if (device_ms) *device_ms = tm.device_ms;
+  if (rc == CDB_OK || rc == CDB_INVALID_SNAPSHOT_CHECKSUM) *out = new cdb_batch{b};
+  return (cdb_status)rc;
+}
+
 cdb_status cdb_batch_info_get(const cdb_batch* cb, cdb_batch_info* info) {
   if (!cb || !info) return CDB_BAD_ARGUMENT;
   const Batch& b = *cb->b;

@@ -137,6 +137,7 @@ struct Decoder {
   Cursor c;
   Batch* b;
   const uint8_t* base;
+  EntryIndex* idx = nullptr;  // index mode (GPU decode): validate and record, no rows
 
   bool str(std::string* s) {
     ByteRef r;
@@ -154,6 +155,15 @@ struct Decoder {
   bool counter(uint64_t kh, uint64_t kf, uint64_t* total) {
     uint64_t cnt;
     if (!c.length(&cnt)) return false;
+    if (idx) {  // index mode: skip the triples, the GPU parses them
+      for (uint64_t i = 0; i < cnt; ++i) {
+        uint64_t x;
+        int64_t v;
+        if (!c.u64(&x) || !c.integer(&v) || !c.u64(&x)) return false;
+      }
+      idx->children.back() = cnt;
+      return true;
+    }
     struct N { uint64_t node, v, t; };
     std::vector<N> ns;
     ns.reserve(cnt < (1u << 20) ? cnt : (1u << 20));
@@ -199,6 +209,17 @@ struct Decoder {
     std::vector<Op> ops;
     uint64_t na;
     if (!c.length(&na)) return false;
+    if (idx) {  // index mode: skip the tags, the GPU parses them
+      ByteRef r;
+      uint64_t t, nd;
+      for (uint64_t i = 0; i < na; ++i)
+        if (!c.span(&r) || !c.u64(&t) || (is_dict && !c.span(&r))) return false;
+      if (!c.length(&nd)) return false;
+      for (uint64_t i = 0; i < nd; ++i)
+        if (!c.span(&r) || !c.u64(&t)) return false;
+      idx->children.back() = na + nd;
+      return true;
+    }
     ops.reserve(na);
     for (uint64_t i = 0; i < na; ++i) {
       Op o;
@@ -261,13 +282,18 @@ struct Decoder {
   }
 
   bool data_entry() {  // read_entry (snapshot.rs:280-287) + Object::load_snapshot
+    if (idx) {
+      idx->offset.push_back(c.off);
+      idx->kind.push_back(0);
+      idx->children.push_back(0);
+    }
     ByteRef k;
     if (!c.span(&k)) return false;
     uint64_t ct, ut, dt;
     if (!c.u64(&ct) || !c.u64(&ut) || !c.u64(&dt)) return false;
     uint8_t tag;
     if (!c.u8(&tag)) return false;
-    const Hash128 h = hash_bytes(base + k.off, k.len, kDomainKey);
+    const Hash128 h = idx ? Hash128{0, 0} : hash_bytes(base + k.off, k.len, kDomainKey);
     uint64_t aux = 0;
     ByteRef v{0, 0};
     switch (tag) {
@@ -285,7 +311,7 @@ struct Decoder {
         c.err = CDB_INVALID_TYPE;  // object.rs:121
         return false;
     }
-    push_key(h, ct, ut, dt, aux, tag, k, v);
+    if (!idx) push_key(h, ct, ut, dt, aux, tag, k, v);
     return true;
   }
 
@@ -304,9 +330,15 @@ struct Decoder {
   }
 
   bool side_entry(uint8_t tag) {  // read_key_int (snapshot.rs:289-295)
+    if (idx) {
+      idx->offset.push_back(c.off);
+      idx->kind.push_back(tag == TAG_EXPIRE ? 1 : 2);
+      idx->children.push_back(0);
+    }
     ByteRef k;
     uint64_t t;
     if (!c.span(&k) || !c.u64(&t)) return false;
+    if (idx) return true;
     const Hash128 h = hash_bytes(base + k.off, k.len, kDomainKey);
     push_key(h, t, 0, 0, 0, tag, k, ByteRef{0, 0});
     return true;
@@ -382,6 +414,29 @@ int decode_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, 
   Decoder d{Cursor{out->raw.data(), out->raw.size()}, out, out->raw.data()};
   *err_off = 0;
   return d.run(flags, err_off);
+}
+
+int index_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, EntryIndex* idx, size_t* err_off) {
+  out->raw.assign(buf, buf + len);
+  Decoder d{Cursor{out->raw.data(), out->raw.size()}, out, out->raw.data()};
+  d.idx = idx;
+  *err_off = 0;
+  return d.run(flags, err_off);
+}
+
+// The entries the GPU found too large for its per-entry dedup: decoded here, exactly as
+// decode_snapshot would, into `side` (rows in entry order, src fields relative to `side`).
+bool decode_entry_children(const Batch& b, uint64_t off, uint64_t kh, uint64_t kf, Batch* side, uint64_t* total) {
+  Decoder d{Cursor{b.raw.data(), b.raw.size()}, side, b.raw.data()};
+  d.c.off = off;
+  ByteRef k;
+  uint64_t ct, ut, dt;
+  uint8_t tag;
+  if (!d.c.span(&k) || !d.c.u64(&ct) || !d.c.u64(&ut) || !d.c.u64(&dt) || !d.c.u8(&tag)) return false;
+  *total = 0;
+  if (tag == TAG_COUNTER) return d.counter(kh, kf, total);
+  if (tag == TAG_SET || tag == TAG_DICT) return d.lwwhash(kh, kf, tag == TAG_DICT);
+  return true;
 }
 
 }  // namespace cdb

@@ -1,0 +1,477 @@
+// GPU snapshot decode: snapshot bytes -> the same columnar Batch as
+// decode.cpp, with the per-entry work on the GPU.
+//
+// The wire format (snapshot.rs:25-64,120-295) is a sequential varint stream: an entry's start
+// is known only after its predecessor is parsed. Two passes:
+//   1. host: index_snapshot() walks the stream once with the reference loader's checks (same
+//      status codes and offsets as decode_snapshot), decodes the header, replica entries and
+//      checksum, and records each entry's byte offset and raw child count. It hashes nothing
+//      and builds no rows;
+//   2. GPU, one thread per entry, over the bytes in HBM:
+//      count_kernel   parses the entry and counts the children the loader keeps after its
+//                     load-time dedup (type_counter.rs:111-126: the last of a repeated node id;
+//                     lwwhash.rs:207-226,341-358: set/rem replay per member);
+//      (scan of the counts: child row offsets)
+//      emit_kernel    parses it again and writes the key row (hash of the key bytes, times,
+//                     counter total, tag | src) and its kept child rows (member hashes).
+//   Entries whose children exceed the per-thread dedup limits (a key with thousands of
+//   members) are decoded on the host by decode.cpp's own functions into their reserved slots.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <vector>
+
+#include "batch.h"
+#include "engine.h"
+
+namespace cdb {
+namespace {
+
+constexpr uint32_t kHostTier = 0xFFFFFFFFu;
+constexpr uint32_t kNodeDedupMax = 64;    // nodes per counter deduplicated by one thread
+constexpr uint32_t kMemberDedupMax = 32;  // set/dict tags per object deduplicated by one thread
+constexpr int kDecThreads = 256;
+
+// read_integer (snapshot.rs:243-264): 2-bit size tag in the flag byte's top bits.
+__device__ __forceinline__ int64_t rd_int(const uint8_t* p, uint64_t& o) {
+  const uint32_t f = p[o++];
+  switch (f >> 6) {
+    case 0: return (int64_t)(f & 0x3F);
+    case 1: {
+      const int64_t v = ((int64_t)(f & 0x3F) << 8) | p[o];
+      o += 1;
+      return v;
+    }
+    case 2: {
+      const int64_t v = ((int64_t)(f & 0x3F) << 24) | ((int64_t)p[o] << 16) | ((int64_t)p[o + 1] << 8) | p[o + 2];
+      o += 3;
+      return v;
+    }
+    default: {
+      uint64_t v = 0;
+      for (int i = 0; i < 8; ++i) v = (v << 8) | p[o + i];
+      o += 8;
+      return (int64_t)v;
+    }
+  }
+}
+struct Span {
+  uint64_t off, len;
+};
+__device__ __forceinline__ Span rd_span(const uint8_t* p, uint64_t& o) {
+  Span s;
+  s.len = (uint64_t)rd_int(p, o);
+  s.off = o;
+  o += s.len;
+  return s;
+}
+
+struct DecArgs {
+  const uint8_t* raw;
+  const uint64_t* off;
+  const uint8_t* kind;
+  uint64_t n;
+  uint32_t *ncount, *mcount;        // count pass: kept children per entry (kHostTier: host decodes)
+  const uint64_t *noff, *moff;      // emit pass: first child row of each entry
+  uint64_t* k[7];                   // kh kf ct ut dt aux meta
+  uint64_t *kref_off, *kref_len, *vref_off, *vref_len;
+  uint64_t* nd[6];                  // pkh pkf node v t meta
+  uint64_t* mb[6];                  // pkh pkf mh mf t meta
+  uint64_t *mref_off, *mref_len, *mvref_off, *mvref_len;
+};
+
+struct Head {  // the part of a DATAS entry before the payload
+  Span key;
+  uint64_t ct, ut, dt;
+  uint32_t tag;
+};
+__device__ __forceinline__ Head rd_head(const uint8_t* p, uint64_t& o) {
+  Head h;
+  h.key = rd_span(p, o);
+  h.ct = (uint64_t)rd_int(p, o);
+  h.ut = (uint64_t)rd_int(p, o);
+  h.dt = (uint64_t)rd_int(p, o);
+  h.tag = p[o++];
+  return h;
+}
+
+
+// Keeps, per member, the op the loader's set/rem replay leaves holding the tag (lwwhash.rs:
+// 87-128 driven by load_snapshot): the first op, replaced by every later op whose time is
+// not older. `keep` bit j set = tag j is emitted.
+__device__ __forceinline__ uint32_t member_keep(const uint8_t* p, uint64_t o, bool dict, uint32_t na, uint32_t nd,
+                                                uint64_t* keep_lo /*bits 0..31*/) {
+  Hash128 h[kMemberDedupMax];
+  uint64_t t[kMemberDedupMax];
+  const uint32_t n = na + nd;
+  uint64_t q = o;
+  for (uint32_t j = 0; j < n; ++j) {
+    if (j == na) (void)rd_int(p, q);  // the dels' count
+    const Span m = rd_span(p, q);
+    t[j] = (uint64_t)rd_int(p, q);
+    if (dict && j < na) (void)rd_span(p, q);
+    h[j] = hash_bytes(p + m.off, m.len, kDomainMember);
+  }
+  uint64_t keep = 0;
+  uint32_t kept = 0;
+  for (uint32_t j = 0; j < n; ++j) {
+    int st = -1;
+    for (uint32_t i = 0; i < n; ++i) {
+      if (h[i].h != h[j].h || h[i].f != h[j].f) continue;
+      if (st >= 0 && t[st] > t[i]) continue;
+      st = (int)i;
+    }
+    if (st == (int)j) {
+      keep |= 1ull << j;
+      ++kept;
+    }
+  }
+  *keep_lo = keep;
+  return kept;
+}
+
+__global__ void __launch_bounds__(kDecThreads) count_kernel(DecArgs A) {
+  const uint64_t i = (uint64_t)blockIdx.x * kDecThreads + threadIdx.x;
+  if (i >= A.n) return;
+  uint32_t nc = 0, mc = 0;
+  if (A.kind[i] == 0) {
+    const uint8_t* p = A.raw;
+    uint64_t o = A.off[i];
+    const Head hd = rd_head(p, o);
+    if (hd.tag == TAG_COUNTER) {
+      const uint64_t cnt = (uint64_t)rd_int(p, o);
+      if (cnt > kNodeDedupMax) {
+        nc = kHostTier;
+      } else {
+        // node j is kept unless a later triple repeats its id (HashMap::insert keeps the last)
+        uint64_t q = o;
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const uint64_t id = (uint64_t)rd_int(p, q);
+          (void)rd_int(p, q);
+          (void)rd_int(p, q);
+          uint64_t r = q;
+          bool later = false;
+          for (uint32_t k = j + 1; k < cnt; ++k) {
+            later |= (uint64_t)rd_int(p, r) == id;
+            (void)rd_int(p, r);
+            (void)rd_int(p, r);
+          }
+          nc += later ? 0 : 1;
+        }
+      }
+    } else if (hd.tag == TAG_SET || hd.tag == TAG_DICT) {
+      const bool dict = hd.tag == TAG_DICT;
+      const uint32_t na = (uint32_t)rd_int(p, o);
+      uint64_t q = o;
+      for (uint32_t j = 0; j < na; ++j) {
+        (void)rd_span(p, q);
+        (void)rd_int(p, q);
+        if (dict) (void)rd_span(p, q);
+      }
+      const uint32_t nd = (uint32_t)rd_int(p, q);
+      if ((uint64_t)na + nd > kMemberDedupMax) {
+        mc = kHostTier;
+      } else {
+        uint64_t keep;
+        mc = member_keep(p, o, dict, na, nd, &keep);
+      }
+    }
+  }
+  A.ncount[i] = nc;
+  A.mcount[i] = mc;
+}
+
+__global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
+  const uint64_t i = (uint64_t)blockIdx.x * kDecThreads + threadIdx.x;
+  if (i >= A.n) return;
+  const uint8_t* p = A.raw;
+  uint64_t o = A.off[i];
+  if (A.kind[i] != 0) {  // EXPIRES / DELETES: key, t (read_key_int, snapshot.rs:289-295)
+    const Span key = rd_span(p, o);
+    const uint64_t t = (uint64_t)rd_int(p, o);
+    const Hash128 h = hash_bytes(p + key.off, key.len, kDomainKey);
+    A.k[0][i] = h.h;
+    A.k[1][i] = h.f;
+    A.k[2][i] = t;
+    A.k[3][i] = A.k[4][i] = A.k[5][i] = 0;
+    A.k[6][i] = meta_pack(A.kind[i] == 1 ? TAG_EXPIRE : TAG_DELETE, 0, i);
+    A.kref_off[i] = key.off;
+    A.kref_len[i] = key.len;
+    A.vref_off[i] = A.vref_len[i] = 0;
+    return;
+  }
+  const Head hd = rd_head(p, o);
+  const Hash128 h = hash_bytes(p + hd.key.off, hd.key.len, kDomainKey);
+  uint64_t aux = 0;
+  Span val{0, 0};
+  if (hd.tag == TAG_BYTES) {
+    val = rd_span(p, o);
+  } else if (hd.tag == TAG_COUNTER) {
+    const uint64_t cnt = (uint64_t)rd_int(p, o);
+    const bool host = A.ncount[i] == kHostTier;
+    uint64_t row = A.noff[i];
+    uint64_t q = o;
+    for (uint64_t j = 0; j < cnt; ++j) {
+      const uint64_t id = (uint64_t)rd_int(p, q);
+      const uint64_t v = (uint64_t)rd_int(p, q);
+      const uint64_t t = (uint64_t)rd_int(p, q);
+      aux += v;  // Counter::load_snapshot sums every value read (wrapping)
+      if (host) continue;
+      uint64_t r = q;
+      bool later = false;
+      for (uint64_t k = j + 1; k < cnt; ++k) {
+        later |= (uint64_t)rd_int(p, r) == id;
+        (void)rd_int(p, r);
+        (void)rd_int(p, r);
+      }
+      if (later) continue;
+      A.nd[0][row] = h.h;
+      A.nd[1][row] = h.f;
+      A.nd[2][row] = id;
+      A.nd[3][row] = v;
+      A.nd[4][row] = t;
+      A.nd[5][row] = meta_pack(0, 0, row);
+      ++row;
+    }
+  } else if ((hd.tag == TAG_SET || hd.tag == TAG_DICT) && A.mcount[i] != kHostTier) {
+    const bool dict = hd.tag == TAG_DICT;
+    const uint32_t na = (uint32_t)rd_int(p, o);
+    uint64_t q = o;
+    for (uint32_t j = 0; j < na; ++j) {
+      (void)rd_span(p, q);
+      (void)rd_int(p, q);
+      if (dict) (void)rd_span(p, q);
+    }
+    const uint32_t nd = (uint32_t)rd_int(p, q);
+    uint64_t keep;
+    member_keep(p, o, dict, na, nd, &keep);
+    uint64_t row = A.moff[i];
+    q = o;
+    for (uint32_t j = 0; j < na + nd; ++j) {
+      if (j == na) (void)rd_int(p, q);
+      const Span m = rd_span(p, q);
+      const uint64_t t = (uint64_t)rd_int(p, q);
+      Span v{0, 0};
+      if (dict && j < na) v = rd_span(p, q);
+      if (!((keep >> j) & 1)) continue;
+      const Hash128 mh = hash_bytes(p + m.off, m.len, kDomainMember);
+      A.mb[0][row] = h.h;
+      A.mb[1][row] = h.f;
+      A.mb[2][row] = mh.h;
+      A.mb[3][row] = mh.f;
+      A.mb[4][row] = t;
+      A.mb[5][row] = meta_pack(j < na ? KIND_ADD : KIND_DEL, 0, row);
+      A.mref_off[row] = m.off;
+      A.mref_len[row] = m.len;
+      A.mvref_off[row] = v.off;
+      A.mvref_len[row] = v.len;
+      ++row;
+    }
+  }
+  A.k[0][i] = h.h;
+  A.k[1][i] = h.f;
+  A.k[2][i] = hd.ct;
+  A.k[3][i] = hd.ut;
+  A.k[4][i] = hd.dt;
+  A.k[5][i] = aux;
+  A.k[6][i] = meta_pack(hd.tag, 0, i);
+  A.kref_off[i] = hd.key.off;
+  A.kref_len[i] = hd.key.len;
+  A.vref_off[i] = val.off;
+  A.vref_len[i] = val.len;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+struct EvPair {
+  hipEvent_t a = nullptr, b = nullptr;
+  EvPair() {
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+  }
+  ~EvPair() {
+    if (a) (void)hipEventDestroy(a);
+    if (b) (void)hipEventDestroy(b);
+  }
+};
+
+}  // namespace
+
+int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off,
+                        DecodeTiming* tm) {
+  EntryIndex idx;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = index_snapshot(buf, len, flags, out, &idx, err_off);
+  if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) return rc;
+  const uint64_t n = idx.offset.size();
+  if (n == 0) return rc;
+  hipSetDevice(ctx->device);
+  hipStream_t s = ctx->stream;
+  // one device block: raw | off | kind | counts | offsets | key cols | refs | node cols | member cols
+  std::vector<uint64_t> noff(n), moff(n);
+  std::vector<uint32_t> ncnt(n), mcnt(n);
+  DevBuf d_raw, d_meta;
+  if (hipMalloc(&d_raw.p, len + 16) != hipSuccess) return CDB_OUT_OF_MEMORY;
+  const size_t head = n * (8 + 1 + 4 + 4 + 8 + 8) + 64;
+  if (hipMalloc(&d_meta.p, head) != hipSuccess) return CDB_OUT_OF_MEMORY;
+  uint8_t* hm = (uint8_t*)d_meta.p;
+  uint64_t* d_off = (uint64_t*)hm;
+  uint64_t* d_noff = d_off + n;
+  uint64_t* d_moff = d_noff + n;
+  uint32_t* d_ncnt = (uint32_t*)(d_moff + n);
+  uint32_t* d_mcnt = d_ncnt + n;
+  uint8_t* d_kind = (uint8_t*)(d_mcnt + n);
+  EvPair ev;
+  hipEventRecord(ev.a, s);
+  hipMemcpyAsync(d_raw.p, out->raw.data(), len, hipMemcpyHostToDevice, s);
+  hipMemcpyAsync(d_off, idx.offset.data(), n * 8, hipMemcpyHostToDevice, s);
+  hipMemcpyAsync(d_kind, idx.kind.data(), n, hipMemcpyHostToDevice, s);
+  DecArgs A;
+  std::memset(&A, 0, sizeof A);
+  A.raw = (const uint8_t*)d_raw.p;
+  A.off = d_off;
+  A.kind = d_kind;
+  A.n = n;
+  A.ncount = d_ncnt;
+  A.mcount = d_mcnt;
+  const uint32_t grid = (uint32_t)((n + kDecThreads - 1) / kDecThreads);
+  count_kernel<<<grid, kDecThreads, 0, s>>>(A);
+  hipMemcpyAsync(ncnt.data(), d_ncnt, n * 4, hipMemcpyDeviceToHost, s);
+  hipMemcpyAsync(mcnt.data(), d_mcnt, n * 4, hipMemcpyDeviceToHost, s);
+  if (hipStreamSynchronize(s) != hipSuccess) return CDB_DEVICE_ERROR;
+  // entries past the per-thread dedup limits: decoded here, into slots reserved by the scan
+  struct HostEntry { uint64_t i; Batch rows; uint64_t total; };
+  std::vector<HostEntry> hosted;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (ncnt[i] != kHostTier && mcnt[i] != kHostTier) continue;
+    HostEntry he;
+    he.i = i;
+    uint64_t o = idx.offset[i];
+    // the key's hash, as decode.cpp computes it
+    const uint8_t* p = out->raw.data();
+    auto rint = [&](uint64_t& q) {
+      const uint32_t f = p[q++];
+      uint64_t v = f & 0x3F;
+      const int extra = (f >> 6) == 0 ? 0 : (f >> 6) == 1 ? 1 : (f >> 6) == 2 ? 3 : 8;
+      if (extra == 8) v = 0;
+      for (int k = 0; k < extra; ++k) v = (v << 8) | p[q++];
+      return v;
+    };
+    uint64_t q = o;
+    const uint64_t klen = rint(q);
+    const Hash128 h = hash_bytes(p + q, klen, kDomainKey);
+    if (!decode_entry_children(*out, o, h.h, h.f, &he.rows, &he.total)) return CDB_DEVICE_ERROR;
+    if (ncnt[i] == kHostTier) ncnt[i] = (uint32_t)he.rows.n_pkh.size();
+    if (mcnt[i] == kHostTier) mcnt[i] = (uint32_t)he.rows.m_pkh.size();
+    hosted.push_back(std::move(he));
+  }
+  uint64_t nn = 0, nm = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    noff[i] = nn;
+    moff[i] = nm;
+    nn += ncnt[i];
+    nm += mcnt[i];
+  }
+  // (the emit pass still sees the host tier's markers in the device copies of the counts)
+  DevBuf d_rows;
+  const size_t rows_words = n * 11 + nn * 6 + nm * 10 + 8;
+  if (hipMalloc(&d_rows.p, rows_words * 8) != hipSuccess) return CDB_OUT_OF_MEMORY;
+  uint64_t* w = (uint64_t*)d_rows.p;
+  for (int c = 0; c < 7; ++c, w += n) A.k[c] = w;
+  A.kref_off = w; w += n;
+  A.kref_len = w; w += n;
+  A.vref_off = w; w += n;
+  A.vref_len = w; w += n;
+  for (int c = 0; c < 6; ++c, w += nn) A.nd[c] = w;
+  for (int c = 0; c < 6; ++c, w += nm) A.mb[c] = w;
+  A.mref_off = w; w += nm;
+  A.mref_len = w; w += nm;
+  A.mvref_off = w; w += nm;
+  A.mvref_len = w; w += nm;
+  A.noff = d_noff;
+  A.moff = d_moff;
+  hipMemcpyAsync(d_noff, noff.data(), n * 8, hipMemcpyHostToDevice, s);
+  hipMemcpyAsync(d_moff, moff.data(), n * 8, hipMemcpyHostToDevice, s);
+  emit_kernel<<<grid, kDecThreads, 0, s>>>(A);
+  if (hipGetLastError() != hipSuccess) return CDB_DEVICE_ERROR;
+  // rows back into the host batch
+  Batch& b = *out;
+  std::vector<uint64_t>* kc[7] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
+  for (int c = 0; c < 7; ++c) {
+    kc[c]->resize(n);
+    hipMemcpyAsync(kc[c]->data(), A.k[c], n * 8, hipMemcpyDeviceToHost, s);
+  }
+  std::vector<uint64_t> ko(n), kl(n), vo(n), vl(n);
+  hipMemcpyAsync(ko.data(), A.kref_off, n * 8, hipMemcpyDeviceToHost, s);
+  hipMemcpyAsync(kl.data(), A.kref_len, n * 8, hipMemcpyDeviceToHost, s);
+  hipMemcpyAsync(vo.data(), A.vref_off, n * 8, hipMemcpyDeviceToHost, s);
+  hipMemcpyAsync(vl.data(), A.vref_len, n * 8, hipMemcpyDeviceToHost, s);
+  std::vector<uint64_t>* nc[6] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
+  std::vector<uint64_t>* mc[6] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
+  for (int c = 0; c < 6; ++c) {
+    nc[c]->resize(nn);
+    mc[c]->resize(nm);
+    if (nn) hipMemcpyAsync(nc[c]->data(), A.nd[c], nn * 8, hipMemcpyDeviceToHost, s);
+    if (nm) hipMemcpyAsync(mc[c]->data(), A.mb[c], nm * 8, hipMemcpyDeviceToHost, s);
+  }
+  std::vector<uint64_t> mo(nm), ml(nm), mvo(nm), mvl(nm);
+  if (nm) {
+    hipMemcpyAsync(mo.data(), A.mref_off, nm * 8, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(ml.data(), A.mref_len, nm * 8, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(mvo.data(), A.mvref_off, nm * 8, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(mvl.data(), A.mvref_len, nm * 8, hipMemcpyDeviceToHost, s);
+  }
+  hipEventRecord(ev.b, s);
+  if (hipStreamSynchronize(s) != hipSuccess) return CDB_DEVICE_ERROR;
+  if (tm) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, ev.a, ev.b);
+    tm->device_ms = ms;
+  }
+  b.key_ref.resize(n);
+  b.val_ref.resize(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    b.key_ref[i] = ByteRef{ko[i], kl[i]};
+    b.val_ref[i] = ByteRef{vo[i], vl[i]};
+  }
+  b.m_ref.resize(nm);
+  b.m_vref.resize(nm);
+  for (uint64_t i = 0; i < nm; ++i) {
+    b.m_ref[i] = ByteRef{mo[i], ml[i]};
+    b.m_vref[i] = ByteRef{mvo[i], mvl[i]};
+  }
+  // the host tier's children, src fields made absolute
+  for (const HostEntry& he : hosted) {
+    const Batch& r = he.rows;
+    for (size_t j = 0; j < r.n_pkh.size(); ++j) {
+      const uint64_t row = noff[he.i] + j;
+      b.n_pkh[row] = r.n_pkh[j];
+      b.n_pkf[row] = r.n_pkf[j];
+      b.n_node[row] = r.n_node[j];
+      b.n_v[row] = r.n_v[j];
+      b.n_t[row] = r.n_t[j];
+      b.n_meta[row] = meta_pack(0, 0, row);
+    }
+    for (size_t j = 0; j < r.m_pkh.size(); ++j) {
+      const uint64_t row = moff[he.i] + j;
+      b.m_pkh[row] = r.m_pkh[j];
+      b.m_pkf[row] = r.m_pkf[j];
+      b.m_h[row] = r.m_h[j];
+      b.m_f[row] = r.m_f[j];
+      b.m_t[row] = r.m_t[j];
+      b.m_meta[row] = meta_pack(meta_tag(r.m_meta[j]), 0, row);
+      b.m_ref[row] = r.m_ref[j];
+      b.m_vref[row] = r.m_vref[j];
+    }
+  }
+  return rc;
+}
+
+}  // namespace cdb

@@ -72,6 +72,16 @@ enum {
 cdb_status cdb_decode_snapshot(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags,
                                cdb_batch** out, size_t* err_offset);
 
+/* The same decode with the per-entry work on the GPU: a host pass validates
+ * the stream (identical status codes and offsets) and indexes its entries; HIP kernels parse
+ * every entry in parallel (varints, key and member hashes, the loader's load-time dedup) and
+ * emit the rows. The batch is identical to cdb_decode_snapshot's, field for field. Needs a
+ * device (CDB_NO_DEVICE otherwise). *index_ms / *device_ms (may be NULL) receive the host
+ * pass time and the device time (transfers included). */
+cdb_status cdb_decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags,
+                                   cdb_batch** out, size_t* err_offset, double* index_ms,
+                                   double* device_ms);
+
 typedef struct cdb_batch_info {
   uint64_t n_data;        /* SnapshotEntry::Data entries   (snapshot.rs:309) */
   uint64_t n_expires;     /* SnapshotEntry::Expires        (snapshot.rs:310) */
