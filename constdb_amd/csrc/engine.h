@@ -12,8 +12,10 @@ struct cdb_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_part = nullptr, ev_bucket = nullptr;
-  hipStream_t side = nullptr;                         // the wide tier runs beside the wave tier
+  hipStream_t side = nullptr;                         // the wide tier runs beside the wave tier;
+  hipStream_t side2 = nullptr;                        // node / member partitions beside the keys'
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;    // (timing disabled)
+  hipEvent_t ev_pfork = nullptr, ev_pn = nullptr, ev_pm = nullptr;
   std::string last_error;
   struct Buf { void* p = nullptr; size_t bytes = 0; };
   Buf ws[32];  // named workspace slots, grown on demand, reused across calls
@@ -27,7 +29,8 @@ enum WsSlot {
   WS_DIR,                                               // bucket directories + hist/cursor
   WS_MISC,                                              // stats, last_bad, hot list
   WS_HOT,                                               // hot-bucket scratch slab
-  WS_SCAN,                                              // scan partials
+  WS_SCAN,                                              // scan partials (keys, merge)
+  WS_SCAN2, WS_SCAN3,                                   // scan partials (nodes, members)
   WS_OWNER,                                             // owner-partition directory
   WS_PERM,                                              // final-level row permutations (u32)
   WS_STATS,                                             // statistic shards

@@ -190,10 +190,10 @@ __global__ void __launch_bounds__(kCompactWaves * 64) compact_kernel(CompactArgs
 
 template <typename T, typename OutT>
 cdb_status exclusive_scan(cdb_ctx* ctx, const T* in, uint64_t n, OutT* out, OutT* out2, uint64_t* d_total,
-                          hipStream_t s) {
+                          hipStream_t s, int slot = WS_SCAN) {
   const uint64_t tiles = std::max<uint64_t>(1, (n + kScanTile - 1) / kScanTile);
   cdb_status st = CDB_OK;
-  uint64_t* sums = (uint64_t*)ws_get(ctx, WS_SCAN, tiles * sizeof(uint64_t), &st);
+  uint64_t* sums = (uint64_t*)ws_get(ctx, slot, tiles * sizeof(uint64_t), &st);
   if (!sums) return st;
   scan_reduce_kernel<T><<<tiles, kScanThreads, 0, s>>>(in, n, sums);
   scan_sums_kernel<<<1, kScanThreads, 0, s>>>(sums, tiles, d_total);
@@ -286,7 +286,8 @@ Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
 template <int NC, int W>
 cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const Plan& plan, int shift,
                             uint64_t* const* A, uint64_t* const* Bf, const Dir& d, uint64_t** rows,
-                            uint64_t** spare, uint64_t* khcol, uint32_t* perm, hipStream_t s) {
+                            uint64_t** spare, uint64_t* khcol, uint32_t* perm, hipStream_t s,
+                            int scan_slot) {
   if (n == 0) {
     CDB_HIP(hipMemsetAsync(d.base, 0, sizeof(uint32_t) * plan.nb, s), "memset");
     CDB_HIP(hipMemsetAsync(d.hist, 0, sizeof(uint32_t) * plan.nb, s), "memset");
@@ -316,7 +317,7 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const
     CDB_HIP(hipMemsetAsync(d.hist, 0, ncur * sizeof(uint32_t), s), "memset hist");
     part_hist_kernel<<<tiles, kPartThreads, 0, s>>>(col0, n, nprev, plan.d[l], shift, d.hist);
     CDB_TRY(launch_check(ctx, s, "part_hist"));
-    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, d.hist, ncur, d.base, d.cursor, nullptr, s));
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, d.hist, ncur, d.base, d.cursor, nullptr, s, scan_slot));
     if (kind == 2) {
       part_scatter_kernel<1, true><<<tiles, kPartThreads, 0, s>>>(ColSet<1>{{khcol}}, ColSet<1>{{nullptr}}, n,
                                                                   nprev, plan.d[l], shift, d.cursor, perm);
@@ -465,11 +466,27 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   uint64_t* khcol = (uint64_t*)ws_get(ctx, WS_KHCOL, (K + N + M + 3) * sizeof(uint64_t), &st);
   if (!khcol) return st;
   uint32_t *kperm = perm, *nperm = perm + K, *mperm = perm + K + N;
-  CDB_TRY(partition_family<kKeyCols, kKeyStride>(ctx, kin, K, plan, shift, KA, KB, dk, &krows, ksp, khcol, kperm, s));
+  // the three families partition independently (own buffers, directories, scan scratch):
+  // nodes and members run on side streams beside the keys
+  static const bool part_serial = std::getenv("CDB_PART_SERIAL") != nullptr;
+  hipStream_t sn = part_serial ? s : ctx->side, sm = part_serial ? s : ctx->side2;
+  if (!part_serial) {
+    CDB_HIP(hipEventRecord(ctx->ev_pfork, s), "event");
+    CDB_HIP(hipStreamWaitEvent(sn, ctx->ev_pfork, 0), "wait");
+    CDB_HIP(hipStreamWaitEvent(sm, ctx->ev_pfork, 0), "wait");
+  }
+  CDB_TRY(partition_family<kKeyCols, kKeyStride>(ctx, kin, K, plan, shift, KA, KB, dk, &krows, ksp, khcol, kperm, s,
+                                                 WS_SCAN));
   CDB_TRY(partition_family<kNodeCols, kChildStride>(ctx, nin, N, plan, shift, NA, NB, dnd, &nrows, nsp, khcol + K,
-                                                    nperm, s));
+                                                    nperm, sn, WS_SCAN2));
   CDB_TRY(partition_family<kMemberCols, kChildStride>(ctx, min_, M, plan, shift, MA, MBf, dm, &mrows, msp,
-                                                      khcol + K + N, mperm, s));
+                                                      khcol + K + N, mperm, sm, WS_SCAN3));
+  if (!part_serial) {
+    CDB_HIP(hipEventRecord(ctx->ev_pn, sn), "event");
+    CDB_HIP(hipEventRecord(ctx->ev_pm, sm), "event");
+    CDB_HIP(hipStreamWaitEvent(s, ctx->ev_pn, 0), "wait");
+    CDB_HIP(hipStreamWaitEvent(s, ctx->ev_pm, 0), "wait");
+  }
   {  // sparse key outputs (8 columns) go to the ping-pong buffer that does not hold the rows
     uint64_t* const* free_k = (krows == KA[0]) ? KB : KA;
     for (int c = 0; c < 8; ++c) ksp[c] = free_k[c];
@@ -706,6 +723,9 @@ cdb_status cdb_ctx_create(cdb_ctx** out, int device) {
   cdb_status st = hip_check(ctx, hipSetDevice(device), "hipSetDevice");
   if (st == CDB_OK) st = hip_check(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "stream");
   if (st == CDB_OK) st = hip_check(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking), "stream");
+  if (st == CDB_OK) st = hip_check(ctx, hipStreamCreateWithFlags(&ctx->side2, hipStreamNonBlocking), "stream");
+  for (hipEvent_t* e : {&ctx->ev_pfork, &ctx->ev_pn, &ctx->ev_pm})
+    if (st == CDB_OK) st = hip_check(ctx, hipEventCreateWithFlags(e, hipEventDisableTiming), "event");
   if (st == CDB_OK) st = hip_check(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming), "event");
   if (st == CDB_OK) st = hip_check(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming), "event");
   if (st == CDB_OK) st = hip_check(ctx, hipEventCreate(&ctx->ev0), "event");
@@ -731,7 +751,10 @@ void cdb_ctx_destroy(cdb_ctx* ctx) {
   if (ctx->ev_bucket) hipEventDestroy(ctx->ev_bucket);
   if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) hipEventDestroy(ctx->ev_join);
+  for (hipEvent_t e : {ctx->ev_pfork, ctx->ev_pn, ctx->ev_pm})
+    if (e) hipEventDestroy(e);
   if (ctx->side) hipStreamDestroy(ctx->side);
+  if (ctx->side2) hipStreamDestroy(ctx->side2);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
 }
