@@ -30,6 +30,8 @@ BAD_ARGUMENT = 6
 DEVICE_ERROR = 7
 OUT_OF_MEMORY = 8
 NO_DEVICE = 9
+INVALID_REQUEST_MSG = 10
+NEED_MORE_MSG = 11
 
 DECODE_REFERENCE_CHECKSUM = 1
 MERGE_STRICT_DICT_PANIC = 1
@@ -65,6 +67,18 @@ class DictMergeUnimplemented(CstError):
     status = DICT_MERGE_UNIMPLEMENTED
 
 
+class InvalidRequestMsg(CstError):
+    status = INVALID_REQUEST_MSG
+
+    def __init__(self, offset: int):
+        super().__init__(f"malformed RESP message at offset {offset}")
+        self.offset = offset
+
+
+class NeedMoreMsg(CstError):
+    status = NEED_MORE_MSG
+
+
 class NoDevice(CstError):
     status = NO_DEVICE
 
@@ -75,12 +89,15 @@ class DeviceError(CstError):
 
 _ERRORS = {INVALID_SNAPSHOT_CHECKSUM: InvalidSnapshotChecksum, INVALID_TYPE: InvalidType,
            IO_ERROR: IoError, DICT_MERGE_UNIMPLEMENTED: DictMergeUnimplemented, NO_DEVICE: NoDevice,
-           DEVICE_ERROR: DeviceError, OUT_OF_MEMORY: DeviceError, BAD_ARGUMENT: ValueError}
+           DEVICE_ERROR: DeviceError, OUT_OF_MEMORY: DeviceError, BAD_ARGUMENT: ValueError,
+           NEED_MORE_MSG: NeedMoreMsg}
 
 
 def _raise(st: int, msg: str = "", offset: int = 0):
     if st == INVALID_SNAPSHOT:
         raise InvalidSnapshot(offset)
+    if st == INVALID_REQUEST_MSG:
+        raise InvalidRequestMsg(offset)
     cls = _ERRORS.get(st, CstError)
     raise cls(msg or f"cdb status {st}")
 
@@ -114,6 +131,24 @@ class ReplicaEntry(ctypes.Structure):
                 ("has_add", ctypes.c_uint32), ("has_del", ctypes.c_uint32)]
 
 
+class OpsInfo(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "n_messages", "n_ops", "n_node_args", "n_member_args", "applied", "duplicates", "lost", "unknown",
+        "unsupported", "cmd_errors", "replacks", "uuid_he_sent", "uuid_he_acked")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+class ApplyStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "ops_in", "node_args_in", "member_args_in", "key_rows_in", "key_rows_out", "node_rows_out",
+        "member_rows_out", "type_errors", "expired_on_query")] + [("device_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
 class DevRows(ctypes.Structure):
     _fields_ = [("col", ctypes.c_void_p * 8), ("n", ctypes.c_uint64)]
 
@@ -142,7 +177,7 @@ ABI_FUNCTIONS = (
     "cdb_batch_column", "cdb_batch_free", "cdb_merge", "cdb_merged_canonical_dump", "cdb_merged_replicas",
     "cdb_merged_free", "cdb_free",
     "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_partition_owner", "cdb_gen_default",
-    "cdb_gen_snapshot", "cdb_gen_device")
+    "cdb_gen_snapshot", "cdb_gen_device", "cdb_decode_ops", "cdb_ops_info_get", "cdb_ops_free", "cdb_apply_ops")
 
 _lib = None
 
@@ -188,6 +223,10 @@ def lib():
         "cdb_gen_default": (None, [P(GenConfig)]),
         "cdb_gen_snapshot": (c_st, [P(GenConfig), ctypes.c_uint32, P(vp), P(ctypes.c_size_t)]),
         "cdb_gen_device": (c_st, [vp, P(GenConfig), P(DevInput)]),
+        "cdb_decode_ops": (c_st, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, P(vp), P(ctypes.c_size_t)]),
+        "cdb_ops_info_get": (c_st, [vp, P(OpsInfo)]),
+        "cdb_ops_free": (None, [vp]),
+        "cdb_apply_ops": (c_st, [vp, vp, vp, P(vp), P(ApplyStats)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -314,6 +353,50 @@ def decode_snapshot_gpu(ctx: "Context", data: bytes, reference_checksum: bool = 
     return Batch(h)
 
 
+# ----------------------------------------------------------------- op stream
+class Ops:
+    """A decoded replicate stream (cdb_ops): op rows in stream order + the stream bytes."""
+
+    def __init__(self, handle, complete: bool = True, consumed: int = 0):
+        self._h = handle
+        self.complete = complete
+        self.consumed = consumed
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self) -> OpsInfo:
+        i = OpsInfo()
+        lib().cdb_ops_info_get(self._h, ctypes.byref(i))
+        return i
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().cdb_ops_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+def decode_ops(data: bytes, uuid_he_sent: int, allow_partial: bool = False) -> Ops:
+    """cdb_decode_ops (replica/pull.rs:184-235 up to the handlers): RESP framing, the uuid gate
+    and argument parsing. Raises InvalidRequestMsg(offset) on malformed RESP; a stream that ends
+    inside a message raises NeedMoreMsg unless allow_partial (then .complete is False and
+    .consumed the bytes used)."""
+    h = ctypes.c_void_p()
+    off = ctypes.c_size_t()
+    st = lib().cdb_decode_ops(None, bytes(data), len(data), uuid_he_sent, ctypes.byref(h), ctypes.byref(off))
+    if st == NEED_MORE_MSG and allow_partial and h:
+        return Ops(h, complete=False, consumed=off.value)
+    if st != OK:
+        if h:
+            lib().cdb_ops_free(h)
+        _raise(st, offset=off.value)
+    return Ops(h, consumed=len(data))
+
+
 # ----------------------------------------------------------------- merge
 class Merged:
     """A merge result (cdb_merged)."""
@@ -351,6 +434,16 @@ class Merged:
                 d["del"] = e.del_time
             out.append(d)
         return out
+
+    def apply_ops(self, ops: "Ops") -> "Merged":
+        """cdb_apply_ops: the op stream applied on the device on top of this result (SURVEY
+        §8f.2). Returns a new result; this one is unchanged."""
+        st = ApplyStats()
+        h = ctypes.c_void_p()
+        self._ctx.check(lib().cdb_apply_ops(self._ctx.handle, self._h, ops.handle, ctypes.byref(h), ctypes.byref(st)))
+        m = Merged(self._ctx, h, self.stats, self._inputs + [ops])
+        m.apply_stats = st
+        return m
 
     def __del__(self):
         try:

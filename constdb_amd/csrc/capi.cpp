@@ -13,6 +13,7 @@
 
 #include "batch.h"
 #include "engine.h"
+#include "ops.h"
 
 namespace cdb {
 cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts,
@@ -21,6 +22,11 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
 
 struct cdb_batch {
   std::shared_ptr<cdb::Batch> b;
+};
+
+struct cdb_ops {  // a decoded replicate stream (op rows + byte arena)
+  std::shared_ptr<cdb::Batch> b;
+  cdb_ops_info info;
 };
 
 struct cdb_merged {
@@ -402,6 +408,46 @@ cdb_status cdb_merged_replicas(cdb_merged* m, const cdb_replica_entry** out, siz
   }
   *out = m->replicas.empty() ? nullptr : m->replicas.data();
   *n = m->replicas.size();
+  return CDB_OK;
+}
+
+cdb_status cdb_decode_ops(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_he_sent, cdb_ops** out,
+                          size_t* err_offset) {
+  (void)ctx;
+  if (!out || (!buf && len)) return CDB_BAD_ARGUMENT;
+  *out = nullptr;
+  auto o = std::make_unique<cdb_ops>();
+  o->b = std::make_shared<Batch>();
+  size_t eo = 0;
+  const int rc = decode_ops(buf, len, uuid_he_sent, o->b.get(), &o->info, &eo);
+  if (err_offset) *err_offset = eo;
+  if (rc == CDB_OK || rc == CDB_NEED_MORE_MSG) *out = o.release();
+  return (cdb_status)rc;
+}
+
+cdb_status cdb_ops_info_get(const cdb_ops* ops, cdb_ops_info* info) {
+  if (!ops || !info) return CDB_BAD_ARGUMENT;
+  *info = ops->info;
+  return CDB_OK;
+}
+
+void cdb_ops_free(cdb_ops* ops) { delete ops; }
+
+cdb_status cdb_apply_ops(cdb_ctx* ctx, cdb_merged* state, const cdb_ops* ops, cdb_merged** out,
+                         cdb_apply_stats* stats) {
+  if (!ctx || !state || !ops || !out) return CDB_BAD_ARGUMENT;
+  *out = nullptr;
+  const uint32_t pos = (uint32_t)state->inputs.size();
+  if (pos >= 255) return fail(ctx, CDB_BAD_ARGUMENT, "at most 255 fold positions per result");
+  hipSetDevice(ctx->device);
+  auto m = std::make_unique<cdb_merged>();
+  m->inputs = state->inputs;
+  m->inputs.push_back(ops->b);
+  cdb_apply_stats local;
+  const cdb_status st = apply_ops_impl(ctx, state->k, state->nd, state->mb, *ops->b, pos, m->k, m->nd, m->mb,
+                                       stats ? stats : &local);
+  if (st != CDB_OK) return st;
+  *out = m.release();
   return CDB_OK;
 }
 

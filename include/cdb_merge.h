@@ -41,7 +41,9 @@ typedef enum cdb_status {
   CDB_BAD_ARGUMENT = 6,
   CDB_DEVICE_ERROR = 7,              /* a HIP call failed */
   CDB_OUT_OF_MEMORY = 8,
-  CDB_NO_DEVICE = 9                  /* no gfx950 device visible: the engine never falls back to the CPU */
+  CDB_NO_DEVICE = 9,                 /* no gfx950 device visible: the engine never falls back to the CPU */
+  CDB_INVALID_REQUEST_MSG = 10,      /* CstError::InvalidRequestMsg: malformed RESP  lib.rs:155, conn/buf_read.rs:114-200 */
+  CDB_NEED_MORE_MSG = 11             /* CstError::NeedMoreMsg: the stream ends inside a message  lib.rs:153 */
 } cdb_status;
 
 typedef struct cdb_ctx cdb_ctx;       /* device, streams, workspace */
@@ -173,6 +175,59 @@ typedef struct cdb_replica_entry {
 cdb_status cdb_merged_replicas(cdb_merged* m, const cdb_replica_entry** out, size_t* n);
 void cdb_merged_free(cdb_merged* m);
 void cdb_free(void* p);
+
+/* ------------------------------------------------------------------ op-stream apply
+ * Partial replication: after the snapshot, a replica receives `replicate` messages (RESP arrays
+ * `replicate <nodeid> <last_uuid> <uuid> <command> <args...>`, server.rs:290-314) and `replack`
+ * messages, and applies them one at a time (Puller::apply_his_replicates, replica/pull.rs:184-235).
+ *
+ * cdb_decode_ops replaces the per-message front half on the host: RESP framing
+ * (conn/buf_read.rs:114-210), the uuid gate against uuid_he_sent (pull.rs:199-209: a message
+ * whose last_uuid is behind is a duplicate and skipped; one that is ahead means lost commands
+ * and is dropped), the command lookup (cmd.rs:39-41) and each handler's argument parsing.
+ * It yields op rows in stream order. Replayed commands: set delbytes incr decr delcnt sadd srem
+ * delset hset hdel deldict. spop (random member on the replica, type_set.rs:82-111), del (never
+ * replicated) and the read/control commands are counted as `unsupported` and skipped; names not
+ * in the command table are `unknown` and skipped with the uuid advanced, like the reference.
+ * Returns CDB_INVALID_REQUEST_MSG (*err_offset = the message's offset) on malformed RESP, and
+ * CDB_NEED_MORE_MSG when the stream ends inside a message: then *out still holds every complete
+ * message before it and *err_offset = the bytes consumed.
+ *
+ * cdb_apply_ops replaces the handlers (cmd.rs:188-309, type_counter.rs:142-204,
+ * type_set.rs:13-134, type_hash.rs:11-119, DB::query db.rs:52-66) for the whole batch at once,
+ * on the device, on top of `state` (a merge result: the DB the snapshot sync produced, or an
+ * earlier apply). The result is a new merge result over the same inputs plus the op stream
+ * (its fold position = state's input count); `state` is left unchanged. */
+typedef struct cdb_ops cdb_ops;
+typedef struct cdb_ops_info {
+  uint64_t n_messages;     /* RESP messages decoded */
+  uint64_t n_ops;          /* op rows (commands that reach the DB) */
+  uint64_t n_node_args;    /* counter (node, delta) arguments: incr/decr (1), delcnt pairs */
+  uint64_t n_member_args;  /* set members / dict fields */
+  uint64_t applied;        /* replicate messages whose handler ran (pull.rs:218-222) */
+  uint64_t duplicates;     /* uuid_he_sent > last_uuid: skipped (pull.rs:205-206) */
+  uint64_t lost;           /* uuid_he_sent < last_uuid, or a malformed replicate: dropped (pull.rs:201-204) */
+  uint64_t unknown;        /* not in the command table (pull.rs:213-217) */
+  uint64_t unsupported;    /* in the table, not replayed (see above) */
+  uint64_t cmd_errors;     /* argument errors (WrongArity ...): logged by the reference, uuid advanced */
+  uint64_t replacks;
+  uint64_t uuid_he_sent;   /* after the stream */
+  uint64_t uuid_he_acked;
+} cdb_ops_info;
+cdb_status cdb_decode_ops(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_he_sent, cdb_ops** out,
+                          size_t* err_offset);
+cdb_status cdb_ops_info_get(const cdb_ops* ops, cdb_ops_info* info);
+void cdb_ops_free(cdb_ops* ops);
+
+typedef struct cdb_apply_stats {
+  uint64_t ops_in, node_args_in, member_args_in, key_rows_in;
+  uint64_t key_rows_out, node_rows_out, member_rows_out;
+  uint64_t type_errors;       /* CstError::InvalidType from a handler (as_mut_* on another type) */
+  uint64_t expired_on_query;  /* DB::query turned an expired key into a delete (db.rs:58-63) */
+  double device_ms;           /* device time of the apply pipeline (HIP events; transfers excluded) */
+} cdb_apply_stats;
+cdb_status cdb_apply_ops(cdb_ctx* ctx, cdb_merged* state, const cdb_ops* ops, cdb_merged** out,
+                         cdb_apply_stats* stats);
 
 /* ------------------------------------------------------------------ device level
  * The same merge over columnar rows already resident in HBM (what bench.py times, and
