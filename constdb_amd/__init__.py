@@ -177,7 +177,7 @@ ABI_FUNCTIONS = (
     "cdb_batch_column", "cdb_batch_free", "cdb_merge", "cdb_merged_canonical_dump", "cdb_merged_replicas",
     "cdb_merged_free", "cdb_free",
     "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_partition_owner", "cdb_gen_default",
-    "cdb_gen_snapshot", "cdb_gen_device", "cdb_decode_ops", "cdb_ops_info_get", "cdb_ops_free", "cdb_apply_ops")
+    "cdb_gen_snapshot", "cdb_gen_device", "cdb_decode_ops", "cdb_ops_info_get", "cdb_ops_free", "cdb_apply_ops", "cdb_gen_ops")
 
 _lib = None
 
@@ -226,6 +226,8 @@ def lib():
         "cdb_decode_ops": (c_st, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, P(vp), P(ctypes.c_size_t)]),
         "cdb_ops_info_get": (c_st, [vp, P(OpsInfo)]),
         "cdb_ops_free": (None, [vp]),
+        "cdb_gen_ops": (c_st, [P(GenConfig), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P(vp),
+                               P(ctypes.c_size_t)]),
         "cdb_apply_ops": (c_st, [vp, vp, vp, P(vp), P(ApplyStats)]),
     }
     for name, (res, args) in sig.items():
@@ -496,6 +498,19 @@ def gen_config(**overrides) -> GenConfig:
     for k, v in overrides.items():
         setattr(c, k, v)
     return c
+
+
+def gen_ops(cfg: GenConfig, n_ops: int, uuid_he_sent: int = 0, zipf_milli: int = 0) -> bytes:
+    """A seeded replicate stream over cfg's key universe (cdb_gen_ops)."""
+    out = ctypes.c_void_p()
+    n = ctypes.c_size_t()
+    st = lib().cdb_gen_ops(ctypes.byref(cfg), n_ops, uuid_he_sent, zipf_milli, ctypes.byref(out), ctypes.byref(n))
+    if st != OK:
+        _raise(st)
+    try:
+        return ctypes.string_at(out.value, n.value)
+    finally:
+        lib().cdb_free(out)
 
 
 def gen_snapshot(cfg: GenConfig, replica: int) -> bytes:

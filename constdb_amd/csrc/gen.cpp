@@ -2,6 +2,9 @@
 // format (server.rs:183-215, db.rs:122-136, object.rs:85-108, type_counter.rs:101-109,
 // crdt/lwwhash.rs:189-205/325-339; Bytes values length-prefixed as the loader expects,
 // object.rs:114-117).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -198,3 +201,103 @@ cdb_status cdb_gen_snapshot(const cdb_gen_config* cfg, uint32_t r, uint8_t** out
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- op streams
+namespace {
+struct RespWriter {  // WriteBuf::write_msg (conn/buf_write.rs:127-150)
+  std::vector<uint8_t> b;
+  void lit(const char* s) { b.insert(b.end(), s, s + std::strlen(s)); }
+  void num(int64_t v) {
+    char t[24];
+    const int n = std::snprintf(t, sizeof t, "%lld", (long long)v);
+    b.insert(b.end(), t, t + n);
+  }
+  void arr(int n) { lit("*"), num(n), lit("\r\n"); }
+  void integer(int64_t v) { lit(":"), num(v), lit("\r\n"); }
+  void bulk(const void* p, size_t n) {
+    lit("$"), num((int64_t)n), lit("\r\n");
+    const uint8_t* q = (const uint8_t*)p;
+    b.insert(b.end(), q, q + n);
+    lit("\r\n");
+  }
+  void bulk(const char* s) { bulk(s, std::strlen(s)); }
+};
+}  // namespace
+
+extern "C" cdb_status cdb_gen_ops(const cdb_gen_config* cfg, uint64_t n_ops, uint64_t uuid_he_sent,
+                                  uint32_t zipf_milli, uint8_t** out, size_t* len) {
+  if (!cfg || !out || !len) return CDB_BAD_ARGUMENT;
+  const GenModel g = model_of(*cfg);
+  RespWriter w;
+  w.b.reserve(n_ops * 48);
+  uint64_t last = uuid_he_sent;
+  const double s = zipf_milli / 1000.0;
+  uint8_t kb[24], mb[24];
+  const uint32_t mu = g.member_universe ? g.member_universe : 1;
+  for (uint64_t q = 0; q < n_ops; ++q) {
+    const uint64_t u0 = grnd(g, q, 0xFFFE, 1), u1 = grnd(g, q, 0xFFFE, 2), u2 = grnd(g, q, 0xFFFE, 3);
+    // key index: uniform, or a power-law skew (rank ~ x^(1/(1-s)) for x uniform in (0,1])
+    uint64_t i;
+    if (s <= 0) {
+      i = u0 % g.universe;
+    } else {
+      const double x = ((u0 >> 11) + 1) * (1.0 / 9007199254740992.0);
+      double r = std::pow(x, 1.0 / (1.0 - std::min(s, 0.99))) * (double)g.universe;
+      i = std::min<uint64_t>((uint64_t)r, g.universe - 1);
+      i = (i * 0x9E3779B97F4A7C15ull) % g.universe;  // hot keys spread over the key space
+    }
+    const Hash128 h = gen_key_hash(i);
+    if (!gen_in_shard(g, h.h)) continue;
+    const uint8_t tag = (u1 % 1000 < 2) ? gen_pick_type(g, u2) : gen_type(g, i, kAllReplicas);
+    // ~2^20 ms past the state's times, with 5 % of the ops older than the state
+    const uint64_t ms = (u1 >> 20) % 1000 < 50 ? kT0Ms + (u2 >> 24) % (1u << 20) : kT0Ms + (1u << 20) + q / 64;
+    const uint64_t uuid = (ms << 22) | (q & 0x3FFFFF);
+    const int kl = key_bytes(i, kb);
+    const uint32_t pick = (uint32_t)(u2 % 100);
+    const uint32_t nm = 1 + (uint32_t)((u2 >> 8) % 3);
+    const uint64_t node = 1 + (u0 >> 40) % (g.max_nodes ? g.max_nodes : 1);
+    const char* name;
+    int nargs = 1;  // key
+    if (tag == TAG_BYTES) {
+      name = pick < 95 ? "set" : "delbytes";
+      nargs += pick < 95;
+    } else if (tag == TAG_COUNTER) {
+      name = pick < 60 ? "incr" : pick < 97 ? "decr" : "delcnt";
+      if (pick >= 97) nargs += 2;
+    } else if (tag == TAG_SET) {
+      name = pick < 70 ? "sadd" : pick < 99 ? "srem" : "delset";
+      if (pick < 99) nargs += nm;
+    } else {
+      name = pick < 70 ? "hset" : pick < 99 ? "hdel" : "deldict";
+      if (pick < 99) nargs += pick < 70 ? 2 * nm : nm;
+    }
+    w.arr(5 + nargs);
+    w.bulk("replicate");
+    w.integer((int64_t)node);
+    w.integer((int64_t)last);
+    w.integer((int64_t)uuid);
+    w.bulk(name);
+    w.bulk(kb, kl);
+    last = uuid;
+    if (!std::strcmp(name, "set")) {
+      const uint32_t vl = g.value_min + (uint32_t)(u0 % (g.value_max >= g.value_min ? g.value_max - g.value_min + 1 : 1));
+      uint8_t v[64];
+      for (uint32_t b = 0; b < vl && b < 64; ++b) v[b] = (uint8_t)('a' + (grnd(g, q, 0xFFFE, 10 + b / 8) >> (8 * (b % 8))) % 26);
+      w.bulk(v, std::min<uint32_t>(vl, 64));
+    } else if (!std::strcmp(name, "delcnt")) {
+      w.integer((int64_t)node);
+      w.integer(-(int64_t)(u1 % 100));
+    } else if (nargs > 1) {
+      for (uint32_t j = 0; j < nm; ++j) {
+        const int ml = member_bytes((u0 >> 16) % mu + j, mb);
+        w.bulk(mb, ml);
+        if (!std::strcmp(name, "hset")) w.bulk("v", 1);
+      }
+    }
+  }
+  *out = (uint8_t*)std::malloc(std::max<size_t>(w.b.size(), 1));
+  if (!*out) return CDB_OUT_OF_MEMORY;
+  std::memcpy(*out, w.b.data(), w.b.size());
+  *len = w.b.size();
+  return CDB_OK;
+}

@@ -293,6 +293,13 @@ typedef struct cdb_gen_config {
 void cdb_gen_default(cdb_gen_config* cfg);
 /* Snapshot bytes of replica r (writer layout). *out released with cdb_free. */
 cdb_status cdb_gen_snapshot(const cdb_gen_config* cfg, uint32_t replica, uint8_t** out, size_t* len);
+/* A replicate stream of n_ops commands (the RESP messages server.rs:290-314 sends) over the
+ * same key universe: per key the generator's type (0.2 % other types: InvalidType), set/delbytes,
+ * incr/decr/delcnt, sadd/srem/delset, hset/hdel/deldict; uuids chained from uuid_he_sent, 5 %
+ * older than the snapshot times. Keys uniform (zipf_milli = 0) or power-law skewed (exponent
+ * zipf_milli/1000 < 1). *out released with cdb_free. */
+cdb_status cdb_gen_ops(const cdb_gen_config* cfg, uint64_t n_ops, uint64_t uuid_he_sent, uint32_t zipf_milli,
+                       uint8_t** out, size_t* len);
 /* Device rows for replicas [replica_lo, replica_hi) generated directly in HBM. */
 cdb_status cdb_gen_device(cdb_ctx* ctx, const cdb_gen_config* cfg, cdb_dev_input* in);
 

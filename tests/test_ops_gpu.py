@@ -99,3 +99,13 @@ def test_hot_key(db):
         sb.cmd(6 + i % 50, ["sadd", "srem", "delset"][i % 7 % 3], b"hot", b"m%d" % (i % 900))
     snap = o.dump_all(o.DB(), o.NodeHeader())
     _parity(db, [snap], sb.bytes())
+
+
+@pytest.mark.parametrize("zipf", [0, 900])
+def test_generated_stream_parity(db, zipf):
+    # the bench's generator (cdb_gen_ops) on a small universe, against the oracle
+    cfg = cdb.gen_config(seed=5 + zipf, universe=3000, n_replicas=2)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(2)]
+    stream = cdb.gen_ops(cfg, 20000, 0, zipf)
+    m2 = _parity(db, snaps, stream, 0)
+    assert m2.apply_stats.ops_in == 20000
