@@ -131,6 +131,20 @@ class ReplicaEntry(ctypes.Structure):
                 ("has_add", ctypes.c_uint32), ("has_del", ctypes.c_uint32)]
 
 
+class EncodeHeader(ctypes.Structure):
+    _fields_ = [("node_id", ctypes.c_uint64), ("alias", ctypes.c_char_p), ("alias_len", ctypes.c_size_t),
+                ("addr", ctypes.c_char_p), ("addr_len", ctypes.c_size_t), ("last_uuid", ctypes.c_uint64),
+                ("replicas", ctypes.POINTER(ReplicaEntry)), ("n_replicas", ctypes.c_size_t)]
+
+
+class EncodeStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("bytes", "data_entries", "expires", "deletes", "checksum")] + \
+               [(n, ctypes.c_double) for n in ("upload_ms", "device_ms", "crc_ms", "download_ms")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
 class OpsInfo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "n_messages", "n_ops", "n_node_args", "n_member_args", "applied", "duplicates", "lost", "unknown",
@@ -177,7 +191,8 @@ ABI_FUNCTIONS = (
     "cdb_batch_column", "cdb_batch_free", "cdb_merge", "cdb_merged_canonical_dump", "cdb_merged_replicas",
     "cdb_merged_free", "cdb_free",
     "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_partition_owner", "cdb_gen_default",
-    "cdb_gen_snapshot", "cdb_gen_device", "cdb_decode_ops", "cdb_ops_info_get", "cdb_ops_free", "cdb_apply_ops", "cdb_gen_ops")
+    "cdb_gen_snapshot", "cdb_gen_device", "cdb_decode_ops", "cdb_ops_info_get", "cdb_ops_free", "cdb_apply_ops", "cdb_gen_ops",
+    "cdb_encode_snapshot", "cdb_crc64_gpu")
 
 _lib = None
 
@@ -229,6 +244,8 @@ def lib():
         "cdb_gen_ops": (c_st, [P(GenConfig), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P(vp),
                                P(ctypes.c_size_t)]),
         "cdb_apply_ops": (c_st, [vp, vp, vp, P(vp), P(ApplyStats)]),
+        "cdb_encode_snapshot": (c_st, [vp, vp, P(EncodeHeader), P(vp), P(ctypes.c_size_t), P(EncodeStats)]),
+        "cdb_crc64_gpu": (c_st, [vp, ctypes.c_char_p, ctypes.c_size_t, P(ctypes.c_uint64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -236,6 +253,13 @@ def lib():
         f.argtypes = args
     _lib = L
     return L
+
+
+def crc64_gpu(ctx: "Context", data: bytes) -> int:
+    """CRC-64/Jones of `data` computed by the GPU checksum kernels (cdb_crc64_gpu)."""
+    c = ctypes.c_uint64()
+    ctx.check(lib().cdb_crc64_gpu(ctx.handle, data, len(data), ctypes.byref(c)))
+    return c.value
 
 
 # ----------------------------------------------------------------- context
@@ -436,6 +460,50 @@ class Merged:
                 d["del"] = e.del_time
             out.append(d)
         return out
+
+    def encode_snapshot(self, node_id: int = 1, alias: str = "n1", addr: str = "127.0.0.1:9001",
+                        last_uuid: int = 0, replicas="merged"):
+        """cdb_encode_snapshot: this result in the reference's snapshot wire format
+        (Server::dump_all, server.rs:183-215), laid out and checksummed on the GPU. `replicas`:
+        "merged" (this result's replica table, cdb_merged_replicas), None, or a list of dicts in
+        the shape replicas() returns. Returns (bytes, EncodeStats)."""
+        keep = []
+        if replicas == "merged":
+            ptr = ctypes.POINTER(ReplicaEntry)()
+            n = ctypes.c_size_t()
+            self._ctx.check(lib().cdb_merged_replicas(self._h, ctypes.byref(ptr), ctypes.byref(n)))
+            rep, nrep = ptr, n.value
+        elif not replicas:
+            rep, nrep = ctypes.POINTER(ReplicaEntry)(), 0
+        else:
+            arr = (ReplicaEntry * len(replicas))()
+            for i, d in enumerate(replicas):
+                e = arr[i]
+                a = d["addr"].encode()
+                keep.append(a)
+                e.addr = a
+                if "add" in d:
+                    t, nid, al, uuid = d["add"]
+                    al = al.encode()
+                    keep.append(al)
+                    e.has_add, e.add_time, e.node_id, e.alias, e.uuid_he_sent = 1, t, nid, al, uuid
+                else:
+                    e.alias = b""
+                if "del" in d:
+                    e.has_del, e.del_time = 1, d["del"]
+            rep, nrep = ctypes.cast(arr, ctypes.POINTER(ReplicaEntry)), len(replicas)
+            keep.append(arr)
+        a, ad = alias.encode(), addr.encode()
+        hdr = EncodeHeader(node_id, a, len(a), ad, len(ad), last_uuid, rep, nrep)
+        out = ctypes.c_void_p()
+        n = ctypes.c_size_t()
+        st = EncodeStats()
+        self._ctx.check(lib().cdb_encode_snapshot(self._ctx.handle, self._h, ctypes.byref(hdr), ctypes.byref(out),
+                                                  ctypes.byref(n), ctypes.byref(st)))
+        try:
+            return ctypes.string_at(out.value, n.value), st
+        finally:
+            lib().cdb_free(out)
 
     def apply_ops(self, ops: "Ops") -> "Merged":
         """cdb_apply_ops: the op stream applied on the device on top of this result (SURVEY

@@ -6,6 +6,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/cdb_merge.h"
 #include "common.h"
 
 namespace cdb {
@@ -65,3 +66,13 @@ bool decode_entry_children(const Batch& b, uint64_t off, uint64_t kh, uint64_t k
 
 
 }  // namespace cdb
+
+// A merge (or op-apply) result, host-resident; bytes resolve through inputs[pos].
+struct cdb_merged {
+  std::vector<std::shared_ptr<cdb::Batch>> inputs;  // pos -> decoded batch (byte arenas)
+  std::vector<uint64_t> k[cdb::kKeyOutCols], nd[cdb::kNodeCols], mb[cdb::kMemberCols];
+  // replica-metadata merge, computed on first request
+  bool replicas_done = false;
+  std::vector<std::string> rep_str;          // addr / alias storage (stable: reserved up front)
+  std::vector<cdb_replica_entry> replicas;
+};

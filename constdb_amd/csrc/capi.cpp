@@ -16,6 +16,9 @@
 #include "ops.h"
 
 namespace cdb {
+cdb_status encode_snapshot_impl(cdb_ctx* ctx, const cdb_merged& m, const cdb_encode_header& hdr, uint8_t** out,
+                                size_t* out_len, cdb_encode_stats* stats);
+cdb_status crc64_gpu_impl(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t* crc);
 cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts,
                              cdb_dev_output* out, cdb_merge_stats* stats, hipStream_t s);
 }
@@ -29,14 +32,6 @@ struct cdb_ops {  // a decoded replicate stream (op rows + byte arena)
   cdb_ops_info info;
 };
 
-struct cdb_merged {
-  std::vector<std::shared_ptr<cdb::Batch>> inputs;  // pos -> decoded batch (byte arenas)
-  std::vector<uint64_t> k[cdb::kKeyOutCols], nd[cdb::kNodeCols], mb[cdb::kMemberCols];
-  // replica-metadata merge, computed on first request
-  bool replicas_done = false;
-  std::vector<std::string> rep_str;          // addr / alias storage (stable: reserved up front)
-  std::vector<cdb_replica_entry> replicas;
-};
 
 using namespace cdb;
 
@@ -449,6 +444,23 @@ cdb_status cdb_apply_ops(cdb_ctx* ctx, cdb_merged* state, const cdb_ops* ops, cd
   if (st != CDB_OK) return st;
   *out = m.release();
   return CDB_OK;
+}
+
+cdb_status cdb_encode_snapshot(cdb_ctx* ctx, cdb_merged* m, const cdb_encode_header* hdr, uint8_t** out,
+                               size_t* len, cdb_encode_stats* stats) {
+  if (!ctx || !m || !hdr || !out || !len) return CDB_BAD_ARGUMENT;
+  if ((hdr->alias_len && !hdr->alias) || (hdr->addr_len && !hdr->addr) || (hdr->n_replicas && !hdr->replicas))
+    return CDB_BAD_ARGUMENT;
+  *out = nullptr;
+  *len = 0;
+  hipSetDevice(ctx->device);
+  return encode_snapshot_impl(ctx, *m, *hdr, out, len, stats);
+}
+
+cdb_status cdb_crc64_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t* crc) {
+  if (!ctx || !crc || (len && !buf)) return CDB_BAD_ARGUMENT;
+  hipSetDevice(ctx->device);
+  return crc64_gpu_impl(ctx, buf, len, crc);
 }
 
 void cdb_merged_free(cdb_merged* m) { delete m; }

@@ -173,6 +173,43 @@ typedef struct cdb_replica_entry {
   uint32_t has_add, has_del;
 } cdb_replica_entry;
 cdb_status cdb_merged_replicas(cdb_merged* m, const cdb_replica_entry** out, size_t* n);
+
+/* ------------------------------------------------------------------ snapshot encode
+ * Replaces Server::dump_all (src/server.rs:183-215) -> DB::dump (src/db.rs:122-136) ->
+ * SnapshotWriter::write_entry / Object::save_snapshot (src/snapshot.rs:25-64,
+ * src/object.rs:85-108, src/type_counter.rs:101-109, src/crdt/lwwhash.rs:189-205,325-339) ->
+ * ReplicaManager::dump_snapshot (src/replica/replica.rs:100-119), and the CRC-64/Jones of the
+ * whole stream (snapshot.rs:62-64, server.rs:205-207), for a merge result. The entries are
+ * sized, laid out by prefix scans and written by HIP kernels; the checksum is computed on the
+ * GPU (per-chunk CRC + GF(2) combination). Order: DATAS in the result's row order, then
+ * EXPIRES, then DELETES; within a Set/Dict the add map precedes the del map (the reference's
+ * HashMap order is unspecified, so any order is a valid dump). Bytes values carry their
+ * length (the loader's layout, object.rs:114-117). Replica entries are written
+ * as in dump_snapshot: every has_add entry as 0x03, then every has_del entry as 0x04, in array
+ * order (pass the cdb_merged_replicas result, or any other list). *out is released with
+ * cdb_free. */
+typedef struct cdb_encode_header {
+  uint64_t node_id;                   /* server.rs:193 */
+  const char* alias; size_t alias_len;
+  const char* addr; size_t addr_len;
+  uint64_t last_uuid;                 /* get_repl_last_uuid(), server.rs:198 */
+  const cdb_replica_entry* replicas; size_t n_replicas;
+} cdb_encode_header;
+typedef struct cdb_encode_stats {
+  uint64_t bytes;                     /* stream length incl. the 8 checksum bytes */
+  uint64_t data_entries, expires, deletes;
+  uint64_t checksum;                  /* CRC-64/Jones over bytes [0, len-8) */
+  double upload_ms;                   /* H2D of result rows, refs and byte arenas */
+  double device_ms;                   /* sizing scans + emit kernels + CRC (HIP events) */
+  double crc_ms;                      /* the CRC kernels alone */
+  double download_ms;                 /* D2H of the stream */
+} cdb_encode_stats;
+cdb_status cdb_encode_snapshot(cdb_ctx* ctx, cdb_merged* m, const cdb_encode_header* hdr, uint8_t** out,
+                               size_t* len, cdb_encode_stats* stats);
+/* CRC-64/Jones (reflected, init 0, no xorout; crc64 2.0.0 as used at snapshot.rs:3) of a
+ * host buffer, computed on the GPU with the same kernels. */
+cdb_status cdb_crc64_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t* crc);
+
 void cdb_merged_free(cdb_merged* m);
 void cdb_free(void* p);
 

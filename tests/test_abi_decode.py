@@ -21,10 +21,10 @@ def built():
 
 def test_header_symbols_exported():
     hdr = open(os.path.join(ROOT, "include", "cdb_merge.h")).read()
-    declared = set(re.findall(r"\b(cdb_[a-z_]+)\s*\(", hdr))
+    declared = set(re.findall(r"\b(cdb_[a-z0-9_]+)\s*\(", hdr))
     assert declared == set(cdb.ABI_FUNCTIONS)
     out = subprocess.check_output(["nm", "-D", "--defined-only", cdb.lib_path()]).decode()
-    exported = set(re.findall(r" T (cdb_[a-z_]+)$", out, re.M))
+    exported = set(re.findall(r" T (cdb_[a-z0-9_]+)$", out, re.M))
     assert declared <= exported, declared - exported
     L = cdb.lib()
     for name in declared:
