@@ -65,9 +65,6 @@ CDB_HD uint32_t vi_put(uint8_t* o, int64_t i) {
   for (int k = 0; k < 8; ++k) o[1 + k] = (uint8_t)((uint64_t)i >> (56 - 8 * k));
   return 9;
 }
-__device__ __forceinline__ void copy_bytes(uint8_t* o, const uint8_t* p, uint64_t n) {
-  for (uint64_t i = 0; i < n; ++i) o[i] = p[i];
-}
 
 // ------------------------------------------------------------------ CRC-64/Jones, reflected
 constexpr uint64_t kPolyR = 0x95AC9329AC4BC9B5ull;
@@ -322,27 +319,50 @@ __device__ __forceinline__ bool in_range(const EncIn& E, uint32_t parent, uint64
 struct MemV {
   uint64_t a, d, na;  // add-map bytes, del-map bytes, adds
 };
+// Child sizes, computed once: a member's (kl, k, t[, vl, v]) bytes with its kind in bit 63
+// (0 for rows outside every key's range), a node's (node, v, t) bytes. They are written into
+// the scans' own output arrays (pd, pn), which the scans then overwrite in place: the apply
+// kernel loads a tile's values before storing any of its prefixes.
+__global__ void member_size_kernel(EncIn E, const uint32_t* parent, uint64_t* msz) {
+  const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (j >= E.nm) return;
+  uint64_t cb, cc;
+  const uint32_t p = parent[j];
+  if (!in_range(E, p, j, &cb, &cc)) {
+    msz[j] = 0;
+    return;
+  }
+  const uint64_t mt = E.mmeta[j];
+  const uint8_t* q;
+  const ByteRef m = mem_span(E, mt, &q);
+  uint64_t sz = vi_len((int64_t)m.len) + m.len + vi_len((int64_t)E.mt[j]);  // (kl, k, t)
+  if (meta_tag(mt) == KIND_DEL) {
+    msz[j] = sz;
+    return;
+  }
+  if (meta_tag(E.kmeta[p - 1]) == TAG_DICT) {  // dict add: + (vl, v) (lwwhash.rs:194-195)
+    const ByteRef v = mval_span(E, mt, &q);
+    sz += vi_len((int64_t)v.len) + v.len;
+  }
+  msz[j] = (1ull << 63) | sz;
+}
+__global__ void node_size_kernel(EncIn E, const uint32_t* parent, uint64_t* nsz) {
+  const uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (j >= E.nn) return;
+  uint64_t cb, cc;
+  nsz[j] = in_range(E, parent[j], j, &cb, &cc)
+               ? vi_len((int64_t)E.nnode[j]) + vi_len((int64_t)E.nv[j]) + vi_len((int64_t)E.nt[j])
+               : 0;
+}
+
 struct MemberScan {
   using V = MemV;
-  EncIn E;
-  const uint32_t* parent;
-  uint64_t *pa, *pd, *pc;  // n + 1 entries
+  uint64_t *pa, *pd, *pc;  // n + 1 entries; pd holds the sizes on entry
   __device__ static V id() { return V{0, 0, 0}; }
   __device__ static V op(V x, V y) { return V{x.a + y.a, x.d + y.d, x.na + y.na}; }
   __device__ V load(uint64_t j) const {
-    uint64_t cb, cc;
-    const uint32_t p = parent[j];
-    if (!in_range(E, p, j, &cb, &cc)) return id();
-    const uint64_t mt = E.mmeta[j];
-    const uint8_t* q;
-    const ByteRef m = mem_span(E, mt, &q);
-    uint64_t sz = vi_len((int64_t)m.len) + m.len + vi_len((int64_t)E.mt[j]);  // (kl, k, t)
-    if (meta_tag(mt) == KIND_DEL) return V{0, sz, 0};
-    if (meta_tag(E.kmeta[p - 1]) == TAG_DICT) {  // dict add: + (vl, v) (lwwhash.rs:194-195)
-      const ByteRef v = mval_span(E, mt, &q);
-      sz += vi_len((int64_t)v.len) + v.len;
-    }
-    return V{sz, 0, 1};
+    const uint64_t z = pd[j], sz = z & ~(1ull << 63);
+    return z >> 63 ? V{sz, 0, 1} : V{0, sz, 0};
   }
   __device__ void store(uint64_t j, V ex, V) const {
     pa[j] = ex.a;
@@ -353,16 +373,10 @@ struct MemberScan {
 
 struct NodeScan {
   using V = uint64_t;
-  EncIn E;
-  const uint32_t* parent;
-  uint64_t* pn;  // n + 1 entries
+  uint64_t* pn;  // n + 1 entries; holds the sizes on entry
   __device__ static V id() { return 0; }
   __device__ static V op(V x, V y) { return x + y; }
-  __device__ V load(uint64_t j) const {
-    uint64_t cb, cc;
-    if (!in_range(E, parent[j], j, &cb, &cc)) return 0;
-    return vi_len((int64_t)E.nnode[j]) + vi_len((int64_t)E.nv[j]) + vi_len((int64_t)E.nt[j]);
-  }
+  __device__ V load(uint64_t j) const { return pn[j]; }
   __device__ void store(uint64_t j, V ex, V) const { pn[j] = ex; }
 };
 
@@ -412,10 +426,19 @@ struct KeyV {
   uint64_t b[3];  // bytes per section
   uint64_t c[3];  // entries per section
 };
+// per key row: fam << 62 | entry bytes (head + children), read by the key scan
+__global__ void key_size_kernel(EncIn E, const uint64_t* pn, const uint64_t* pa, const uint64_t* pd,
+                                const uint64_t* pc, uint64_t* ksz) {
+  const uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (r >= E.nk) return;
+  const KeyLayout L = key_layout(E, pn, pa, pd, pc, r);
+  ksz[r] = ((uint64_t)L.fam << 62) | L.total;
+}
+
 struct KeyScan {
   using V = KeyV;
-  EncIn E;
-  const uint64_t *pn, *pa, *pd, *pc;
+  const uint64_t* ksz;
+  uint64_t nk;
   uint64_t* koff;   // row offset inside its section
   KeyV* total;
   __device__ static V id() { return V{{0, 0, 0}, {0, 0, 0}}; }
@@ -423,14 +446,14 @@ struct KeyScan {
     return V{{x.b[0] + y.b[0], x.b[1] + y.b[1], x.b[2] + y.b[2]}, {x.c[0] + y.c[0], x.c[1] + y.c[1], x.c[2] + y.c[2]}};
   }
   __device__ V load(uint64_t r) const {
-    const KeyLayout L = key_layout(E, pn, pa, pd, pc, r);
+    const uint64_t z = ksz[r];
     V v = id();
-    v.b[L.fam] = L.total;
-    v.c[L.fam] = 1;
+    v.b[z >> 62] = z & ((1ull << 62) - 1);
+    v.c[z >> 62] = 1;
     return v;
   }
   __device__ void store(uint64_t r, V ex, V own) const {
-    if (r == E.nk) {
+    if (r == nk) {
       *total = ex;
       return;
     }
@@ -439,41 +462,106 @@ struct KeyScan {
   }
 };
 
-// 5. emit: key heads (and the count fields of their child maps)
-__global__ void emit_keys_kernel(EncIn E, const uint64_t* pn, const uint64_t* pa, const uint64_t* pd,
-                                 const uint64_t* pc, const uint64_t* koff, uint64_t base0, uint64_t base1,
-                                 uint64_t base2, uint8_t* out, uint64_t* childbase) {
-  const uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-  if (r >= E.nk) return;
-  const KeyLayout L = key_layout(E, pn, pa, pd, pc, r);
+// Byte copy from global memory with dword-aligned loads (keys and values are short and start
+// anywhere in the arena).
+__device__ __forceinline__ void copy_in(uint8_t* o, const uint8_t* p, uint64_t n) {
+  if (!n) return;
+  const uintptr_t a0 = (uintptr_t)p & ~(uintptr_t)3;
+  const uint32_t* w = (const uint32_t*)a0;
+  uint32_t sh = (uint32_t)((uintptr_t)p - a0);
+  uint32_t cur = *w;
+  for (uint64_t i = 0; i < n; ++i) {
+    o[i] = (uint8_t)(cur >> (8 * sh));
+    if (++sh == 4 && i + 1 < n) {
+      sh = 0;
+      cur = *++w;
+    }
+  }
+}
+
+// Writes a key row's head (everything but its children and a Set/Dict's del count).
+__device__ __forceinline__ void put_head(const EncIn& E, const KeyLayout& L, uint64_t r, uint8_t* o) {
   const uint64_t meta = E.kmeta[r];
   const uint32_t T = meta_tag(meta);
-  uint8_t* o = out + (L.fam == 0 ? base0 : L.fam == 1 ? base1 : base2) + koff[r];
   const uint8_t* q;
   const ByteRef k = key_span(E, meta, &q);
   o += vi_put(o, (int64_t)k.len);  // write_entry (snapshot.rs:48-52) / db.rs:127-134
-  copy_bytes(o, q, k.len);
+  copy_in(o, q, k.len);
   o += k.len;
   o += vi_put(o, (int64_t)E.kct[r]);
   if (L.fam) return;
   o += vi_put(o, (int64_t)E.kut[r]);  // object.rs:86-88
   o += vi_put(o, (int64_t)E.kdt[r]);
   *o++ = (uint8_t)T;
-  const uint64_t cc = E.kcref[r] & 0xFFFFFF;
   if (T == TAG_BYTES) {  // len, bytes (the loader's layout, object.rs:114-117)
     const ByteRef v = val_span(E, E.kwin[r], &q);
     o += vi_put(o, (int64_t)v.len);
-    copy_bytes(o, q, v.len);
-    return;
+    copy_in(o, q, v.len);
+  } else if (T == TAG_COUNTER) {
+    vi_put(o, (int64_t)(E.kcref[r] & 0xFFFFFF));  // type_counter.rs:102
+  } else {
+    vi_put(o, (int64_t)L.na);  // lwwhash.rs:190 / 326
   }
-  if (T == TAG_COUNTER) {
-    o += vi_put(o, (int64_t)cc);  // type_counter.rs:102
-    childbase[r] = (uint64_t)(o - out);
-    return;
+}
+
+// 5. emit: key heads. The entries of one workgroup's rows of one section are contiguous in the
+// stream, so they are assembled in LDS and written out with coalesced dword stores (spans
+// larger than the stage are written in place). A staged span also covers the rows' child
+// regions: those bytes are garbage here and are written by the node / member kernels, which
+// run after this one; the Set/Dict del counts inside them are written after the copies.
+constexpr uint32_t kStage = 32768;
+__global__ void __launch_bounds__(256) emit_keys_kernel(EncIn E, const uint64_t* pn, const uint64_t* pa,
+                                                        const uint64_t* pd, const uint64_t* pc, const uint64_t* koff,
+                                                        uint64_t base0, uint64_t base1, uint64_t base2, uint8_t* out,
+                                                        uint64_t* childbase) {
+  __shared__ uint8_t stage[kStage];
+  __shared__ unsigned long long s_lo[3], s_hi[3];
+  const uint32_t t = threadIdx.x;
+  const uint64_t r = blockIdx.x * (uint64_t)blockDim.x + t;
+  const bool valid = r < E.nk;
+  KeyLayout L{};
+  uint64_t o = 0;
+  if (t < 3) {
+    s_lo[t] = ~0ull;
+    s_hi[t] = 0;
   }
-  o += vi_put(o, (int64_t)L.na);  // lwwhash.rs:190 / 326
-  childbase[r] = (uint64_t)(o - out);
-  vi_put(o + L.add_bytes, (int64_t)L.nd);  // lwwhash.rs:198 / 331
+  __syncthreads();
+  if (valid) {
+    L = key_layout(E, pn, pa, pd, pc, r);
+    o = (L.fam == 0 ? base0 : L.fam == 1 ? base1 : base2) + koff[r];
+    atomicMin(&s_lo[L.fam], (unsigned long long)o);
+    atomicMax(&s_hi[L.fam], (unsigned long long)(o + L.total));
+  }
+  __syncthreads();
+  for (uint32_t f = 0; f < 3; ++f) {
+    const uint64_t lo = s_lo[f], hi = s_hi[f];
+    if (lo >= hi) continue;  // no rows of this section (uniform across the workgroup)
+    const bool staged = hi - lo <= kStage;
+    if (valid && L.fam == f) put_head(E, L, r, staged ? stage + (o - lo) : out + o);
+    __syncthreads();
+    if (staged) {
+      // head bytes up to a dword boundary, then dwords, then the tail
+      const uint64_t a = (lo + 3) & ~3ull, span = hi - lo;
+      const uint64_t lead = std::min<uint64_t>(a - lo, span);
+      if (t < lead) out[lo + t] = stage[t];
+      const uint64_t words = (span - lead) / 4;
+      for (uint64_t w = t; w < words; w += 256) {
+        const uint64_t b = lead + 4 * w;
+        const uint32_t v = (uint32_t)stage[b] | ((uint32_t)stage[b + 1] << 8) | ((uint32_t)stage[b + 2] << 16) |
+                           ((uint32_t)stage[b + 3] << 24);
+        *(uint32_t*)(out + a + 4 * w) = v;
+      }
+      const uint64_t done = lead + 4 * words;
+      if (t < span - done) out[lo + done + t] = stage[done + t];
+      __syncthreads();
+    }
+  }
+  if (!valid || L.fam) return;
+  const uint32_t T = meta_tag(E.kmeta[r]);
+  if (T == TAG_BYTES) return;
+  const uint64_t cb = o + L.head;  // where the children start
+  childbase[r] = cb;
+  if (T != TAG_COUNTER) vi_put(out + cb + L.add_bytes, (int64_t)L.nd);  // lwwhash.rs:198 / 331
 }
 
 __global__ void emit_nodes_kernel(EncIn E, const uint32_t* parent, const uint64_t* pn, const uint64_t* childbase,
@@ -509,13 +597,13 @@ __global__ void emit_members_kernel(EncIn E, const uint32_t* parent, const uint6
   const uint8_t* q;
   const ByteRef m = mem_span(E, mt, &q);
   o += vi_put(o, (int64_t)m.len);  // (kl, k, t[, vl, v]) lwwhash.rs:191-196 / 327-330
-  copy_bytes(o, q, m.len);
+  copy_in(o, q, m.len);
   o += m.len;
   o += vi_put(o, (int64_t)E.mt[j]);
   if (add && meta_tag(E.kmeta[p - 1]) == TAG_DICT) {
     const ByteRef v = mval_span(E, mt, &q);
     o += vi_put(o, (int64_t)v.len);
-    copy_bytes(o, q, v.len);
+    copy_in(o, q, v.len);
   }
 }
 
@@ -535,19 +623,13 @@ cdb_status h2d(cdb_ctx* ctx, void* dst, const void* src, size_t bytes, hipStream
 }
 
 template <class Tr>
-cdb_status run_scan(cdb_ctx* ctx, const Tr& tr, uint64_t n, hipStream_t s) {
+cdb_status run_scan(cdb_ctx* ctx, const Tr& tr, uint64_t n, void* scratch, hipStream_t s) {
   const uint64_t tiles = std::max<uint64_t>(1, (n + kSTile - 1) / kSTile);
-  DevMem sums;
-  cdb_status st = dalloc(ctx, sums, tiles * sizeof(typename Tr::V));
-  if (st != CDB_OK) return st;
-  auto* S = (typename Tr::V*)sums.p;
+  auto* S = (typename Tr::V*)scratch;
   tscan_reduce<Tr><<<tiles, kST, 0, s>>>(tr, n, S);
   tscan_sums<Tr><<<1, kST, 0, s>>>(tr, tiles, S, n);
   tscan_apply<Tr><<<tiles, kST, 0, s>>>(tr, n, S);
-  st = launch_check(ctx, s, "encode scan");
-  if (st != CDB_OK) return st;
-  // `sums` is freed when this returns: hipFree waits for the stream's work on it
-  return hip_check(ctx, hipStreamSynchronize(s), "encode scan sync");
+  return launch_check(ctx, s, "encode scan");
 }
 
 struct Varints {
@@ -647,7 +729,7 @@ cdb_status encode_snapshot_impl(cdb_ctx* ctx, const cdb_merged& m, const cdb_enc
   cdb_status st;
   if ((st = dalloc(ctx, dk, 6 * nk * 8)) != CDB_OK || (st = dalloc(ctx, dn, 3 * nn * 8)) != CDB_OK ||
       (st = dalloc(ctx, dm, 2 * nm * 8)) != CDB_OK || (st = dalloc(ctx, dpb, pb.size() * sizeof(PosBase))) != CDB_OK ||
-      (st = dalloc(ctx, dar, arena)) != CDB_OK || (st = dalloc(ctx, dkr, krow * sizeof(ByteRef))) != CDB_OK ||
+      (st = dalloc(ctx, dar, arena + 8)) != CDB_OK || (st = dalloc(ctx, dkr, krow * sizeof(ByteRef))) != CDB_OK ||
       (st = dalloc(ctx, dvr, krow * sizeof(ByteRef))) != CDB_OK ||
       (st = dalloc(ctx, dmr, mrow * sizeof(ByteRef))) != CDB_OK ||
       (st = dalloc(ctx, dmvr, mrow * sizeof(ByteRef))) != CDB_OK)
@@ -715,13 +797,22 @@ cdb_status encode_snapshot_impl(cdb_ctx* ctx, const cdb_merged& m, const cdb_enc
     return st;
   if (nk) mark_heads_kernel<<<(nk + 255) / 256, 256, 0, s>>>(E, nhead, mhead);
   if ((st = launch_check(ctx, s, "mark_heads")) != CDB_OK) return st;
-  if ((st = run_scan(ctx, ParentScan{nhead, nn}, nn, s)) != CDB_OK) return st;
-  if ((st = run_scan(ctx, ParentScan{mhead, nm}, nm, s)) != CDB_OK) return st;
+  DevMem dscr;  // scan tile sums, sized for the largest scan
+  const uint64_t max_rows = std::max(std::max(nk, nn), nm);
+  if ((st = dalloc(ctx, dscr, ((max_rows + kSTile - 1) / kSTile + 1) * sizeof(KeyV))) != CDB_OK) return st;
+  if ((st = run_scan(ctx, ParentScan{nhead, nn}, nn, dscr.p, s)) != CDB_OK) return st;
+  if ((st = run_scan(ctx, ParentScan{mhead, nm}, nm, dscr.p, s)) != CDB_OK) return st;
   uint64_t *pn = (uint64_t*)dpn.p, *pa = (uint64_t*)dpa.p, *pd = (uint64_t*)dpd.p, *pc = (uint64_t*)dpc.p;
-  if ((st = run_scan(ctx, NodeScan{E, nhead, pn}, nn, s)) != CDB_OK) return st;
-  if ((st = run_scan(ctx, MemberScan{E, mhead, pa, pd, pc}, nm, s)) != CDB_OK) return st;
+  if (nn) node_size_kernel<<<(nn + 255) / 256, 256, 0, s>>>(E, nhead, pn);
+  if (nm) member_size_kernel<<<(nm + 255) / 256, 256, 0, s>>>(E, mhead, pd);
+  if ((st = launch_check(ctx, s, "child sizes")) != CDB_OK) return st;
+  if ((st = run_scan(ctx, NodeScan{pn}, nn, dscr.p, s)) != CDB_OK) return st;
+  if ((st = run_scan(ctx, MemberScan{pa, pd, pc}, nm, dscr.p, s)) != CDB_OK) return st;
   uint64_t* koff = (uint64_t*)dko.p;
-  if ((st = run_scan(ctx, KeyScan{E, pn, pa, pd, pc, koff, (KeyV*)dtot.p}, nk, s)) != CDB_OK) return st;
+  uint64_t* ksz = (uint64_t*)dcb.p;  // the sizes live in the childbase buffer until the emit
+  if (nk) key_size_kernel<<<(nk + 255) / 256, 256, 0, s>>>(E, pn, pa, pd, pc, ksz);
+  if ((st = launch_check(ctx, s, "key_size")) != CDB_OK) return st;
+  if ((st = run_scan(ctx, KeyScan{ksz, nk, koff, (KeyV*)dtot.p}, nk, dscr.p, s)) != CDB_OK) return st;
   KeyV tot;
   if ((st = hip_check(ctx, hipMemcpyAsync(&tot, dtot.p, sizeof tot, hipMemcpyDeviceToHost, s), "d2h totals")) !=
           CDB_OK ||
