@@ -54,9 +54,10 @@ struct BucketArgs {
   const uint32_t *kp, *np, *mp;
   const uint32_t *kbase, *kcnt, *nbase, *ncnt, *mbase, *mcnt;
   uint64_t nbuckets;          // bucket(h) = floor((h << key_shift) * nbuckets / 2^64)
-  uint64_t* ko[kKeyOutCols];
-  uint64_t* no[kNodeCols];
-  uint64_t* mo[kMemberCols];
+  // Sparse-by-bucket outputs, AoS: key output row o is kos[o * kKeyOutCols + O_*] (one 64-B
+  // line), node / member output row o is nos / mos[o * kChildStride + C_*] (48 B). Whole rows
+  // are written and later read by the compaction with 16-B accesses.
+  uint64_t *kos, *nos, *mos;
   uint32_t *kout, *nout, *mout;
   uint32_t flags;
   uint32_t force_tier;
@@ -319,13 +320,13 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
       }
     }
     const uint64_t gkh = S.kh[h], gkf = S.kf[h];
-    A.ko[O_KH][kb + o] = gkh;
-    A.ko[O_KF][kb + o] = gkf;
-    A.ko[O_CT][kb + o] = ct;
-    A.ko[O_UT][kb + o] = ut;
-    A.ko[O_DT][kb + o] = dt;
-    A.ko[O_META][kb + o] = meta_pack(meta_tag(outmeta), meta_pos(outmeta), meta_src(outmeta));
-    A.ko[O_WIN][kb + o] = win;
+    A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_KH] = gkh;
+    A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_KF] = gkf;
+    A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_CT] = ct;
+    A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_UT] = ut;
+    A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_DT] = dt;
+    A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_META] = meta_pack(meta_tag(outmeta), meta_pos(outmeta), meta_src(outmeta));
+    A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_WIN] = win;
     S.okh[o] = gkh;
     S.okf[o] = gkf;
     S.ovm[o] = vm;
@@ -343,7 +344,7 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
     const uint32_t n = nodes ? N : M, base = nodes ? nb : mb;
     const uint64_t* C = nodes ? A.nr : A.mr;
     const uint32_t* P = nodes ? A.np : A.mp;  // bucket order -> row
-    uint64_t* const* O = nodes ? A.no : A.mo;
+    uint64_t* const O = nodes ? A.nos : A.mos;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
       const uint64_t pkh = cget(C, C_PKH, P[base + i]), pkf = cget(C, C_PKF, P[base + i]);
       const uint64_t m = cget(C, C_META, P[base + i]);
@@ -436,18 +437,18 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
       const bool emitted = (j + 1 < n ? S.crank[j + 1] : cout) != S.crank[j];
       if (!emitted) continue;
       const uint32_t x = S.cidx[j], o = S.crank[j], key = S.ck[x];
-      O[C_PKH][base + o] = S.okh[key];
-      O[C_PKF][base + o] = S.okf[key];
-      O[C_ID1][base + o] = S.c1[x];
+      O[(uint64_t)(base + o) * kChildStride + C_PKH] = S.okh[key];
+      O[(uint64_t)(base + o) * kChildStride + C_PKF] = S.okf[key];
+      O[(uint64_t)(base + o) * kChildStride + C_ID1] = S.c1[x];
       if (nodes) {
-        O[C_ID2][base + o] = S.rt[j];
-        O[C_T][base + o] = cget(C, C_T, P[base + x]);
+        O[(uint64_t)(base + o) * kChildStride + C_ID2] = S.rt[j];
+        O[(uint64_t)(base + o) * kChildStride + C_T] = cget(C, C_T, P[base + x]);
         if (S.ovm[key] & kVmaskMerged) atomicAdd((unsigned long long*)&S.osum[key], (unsigned long long)S.rt[j]);
       } else {
-        O[C_ID2][base + o] = S.c2[x];
-        O[C_T][base + o] = S.rt[j];
+        O[(uint64_t)(base + o) * kChildStride + C_ID2] = S.c2[x];
+        O[(uint64_t)(base + o) * kChildStride + C_T] = S.rt[j];
       }
-      O[C_META][base + o] = S.rm[j];
+      O[(uint64_t)(base + o) * kChildStride + C_META] = S.rm[j];
       atomicMin(&S.ocb[key], o);
       atomicAdd(&S.occ[key], 1u);
     }
@@ -457,8 +458,8 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
   // ------------------------------------------------------------ per-key finish
   for (uint32_t o = threadIdx.x; o < kout; o += blockDim.x) {
     const uint32_t T = S.otp[o] & 0xFF;
-    if (T == TAG_COUNTER) A.ko[O_WIN][kb + o] = S.osum[o];
-    A.ko[O_CREF][kb + o] = cref_pack(S.occ[o] ? S.ocb[o] : 0, S.occ[o]);
+    if (T == TAG_COUNTER) A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_WIN] = S.osum[o];
+    A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_CREF] = cref_pack(S.occ[o] ? S.ocb[o] : 0, S.occ[o]);
   }
   if (threadIdx.x == 0) {
     A.kout[b] = kout;

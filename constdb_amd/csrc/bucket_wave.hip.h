@@ -632,22 +632,28 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     }
     lookback(A, b, lane, kout, an, am, xk, xn, xm);
   }
-  uint64_t* const* NO = dense ? A.dno : A.no;
-  uint64_t* const* MO = dense ? A.dmo : A.mo;
   uint32_t nbase = 0, mbase = 0;
 #pragma unroll
   for (int e = 0; e < CE; ++e) {
     if (cemit[e]) {
       const uint32_t crank = (knode[e] ? nbase : mbase) + lane_rank(knode[e] ? En[e] : Em[e]);
       const uint64_t o = (knode[e] ? xn : xm) + crank;
-      uint64_t* const* O = knode[e] ? NO : MO;
       const uint32_t k = (uint32_t)(sw_[e] >> 56) & (KC - 1);
-      O[C_PKH][o] = L.okh[k];
-      O[C_PKF][o] = L.okf[k];
-      O[C_ID1][o] = sid1[e];
-      O[C_ID2][o] = knode[e] ? c_v[e] : sid2[e];
-      O[C_T][o] = c_t[e];
-      O[C_META][o] = c_m[e];
+      const uint64_t id2 = knode[e] ? c_v[e] : sid2[e];
+      if (dense) {
+        uint64_t* const* O = knode[e] ? A.dno : A.dmo;
+        O[C_PKH][o] = L.okh[k];
+        O[C_PKF][o] = L.okf[k];
+        O[C_ID1][o] = sid1[e];
+        O[C_ID2][o] = id2;
+        O[C_T][o] = c_t[e];
+        O[C_META][o] = c_m[e];
+      } else {  // one whole 48-B AoS row: three 16-B stores
+        ulonglong2* row = (ulonglong2*)((knode[e] ? A.nos : A.mos) + o * kChildStride);
+        row[0] = make_ulonglong2(L.okh[k], L.okf[k]);
+        row[1] = make_ulonglong2(sid1[e], id2);
+        row[2] = make_ulonglong2(c_t[e], c_m[e]);
+      }
       if (knode[e] && (L.ovm[k] & kVmaskMerged))
         atomicAdd((unsigned long long*)&L.osum[k], (unsigned long long)c_v[e]);
       atomicMin(&L.ocb[k], crank);
@@ -659,22 +665,31 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   wave_sync();
 
   // ------------------------------------------------------------ 5. key outputs
-  uint64_t* const* KO = dense ? A.dko : A.ko;
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
     if (emit[e]) {
       const uint32_t r = orank[e];
       const uint64_t o = xk + r;
-      KO[O_KH][o] = kh[e];
-      KO[O_KF][o] = kf[e];
-      KO[O_CT][o] = o_ct[e];
-      KO[O_UT][o] = o_ut[e];
-      KO[O_DT][o] = o_dt[e];
-      KO[O_META][o] = o_meta[e];
-      KO[O_WIN][o] = (fam[e] == 0 && o_T[e] == TAG_COUNTER) ? L.osum[r] : o_win[e];
+      const uint64_t win = (fam[e] == 0 && o_T[e] == TAG_COUNTER) ? L.osum[r] : o_win[e];
       // child ranges: bucket-relative (compaction makes them absolute), or absolute already
       const uint64_t cb = dense ? (o_T[e] == TAG_COUNTER ? xn : xm) : 0;
-      KO[O_CREF][o] = cref_pack(L.ocnt[r] ? cb + L.ocb[r] : 0, L.ocnt[r]);
+      const uint64_t cref = cref_pack(L.ocnt[r] ? cb + L.ocb[r] : 0, L.ocnt[r]);
+      if (dense) {
+        A.dko[O_KH][o] = kh[e];
+        A.dko[O_KF][o] = kf[e];
+        A.dko[O_CT][o] = o_ct[e];
+        A.dko[O_UT][o] = o_ut[e];
+        A.dko[O_DT][o] = o_dt[e];
+        A.dko[O_META][o] = o_meta[e];
+        A.dko[O_WIN][o] = win;
+        A.dko[O_CREF][o] = cref;
+      } else {  // one whole 64-B AoS row: four 16-B stores
+        ulonglong2* row = (ulonglong2*)(A.kos + o * kKeyOutCols);
+        row[0] = make_ulonglong2(kh[e], kf[e]);
+        row[1] = make_ulonglong2(o_ct[e], o_ut[e]);
+        row[2] = make_ulonglong2(o_dt[e], o_meta[e]);
+        row[3] = make_ulonglong2(win, cref);
+      }
     }
   }
   if (lane == 0) {  // a dense bucket leaves nothing for compaction

@@ -85,11 +85,9 @@ __global__ void gc_lastbad_kernel(const uint64_t* __restrict__ ct, const uint64_
 }
 
 struct CompactArgs {
-  const uint64_t* ks[kKeyOutCols];
+  const uint64_t *ks, *ns, *ms;  // sparse AoS outputs (BucketArgs::kos / nos / mos)
   uint64_t* kd[kKeyOutCols];
-  const uint64_t* ns[kNodeCols];
   uint64_t* nd[kNodeCols];
-  const uint64_t* ms[kMemberCols];
   uint64_t* md[kMemberCols];
   const uint32_t *kbase, *nbase, *mbase, *kout, *nout, *mout, *kdoff, *ndoff, *mdoff;
   const unsigned long long* base_tot;  // dense rows already placed by the wave tier, per family
@@ -124,8 +122,13 @@ __device__ __forceinline__ void compact_row(const CompactArgs& A, const CompactL
   const uint64_t dst = A.base_tot[FAM] + d0 + t;
   if constexpr (FAM == 0) {
     uint64_t v[kKeyOutCols];
+    const ulonglong2* row = (const ulonglong2*)(A.ks + (uint64_t)src * kKeyOutCols);
 #pragma unroll
-    for (int c = 0; c < kKeyOutCols; ++c) v[c] = A.ks[c][src];
+    for (int c = 0; c < kKeyOutCols / 2; ++c) {
+      const ulonglong2 q = row[c];
+      v[2 * c] = q.x;
+      v[2 * c + 1] = q.y;
+    }
     const uint64_t cnt = v[O_CREF] & 0xFFFFFF;
     const uint32_t T = meta_tag(v[O_META]);
     const uint64_t begin =
@@ -135,14 +138,24 @@ __device__ __forceinline__ void compact_row(const CompactArgs& A, const CompactL
     for (int c = 0; c < kKeyOutCols; ++c) A.kd[c][dst] = v[c];
   } else if constexpr (FAM == 1) {
     uint64_t v[kNodeCols];
+    const ulonglong2* row = (const ulonglong2*)(A.ns + (uint64_t)src * kChildStride);
 #pragma unroll
-    for (int c = 0; c < kNodeCols; ++c) v[c] = A.ns[c][src];
+    for (int c = 0; c < kNodeCols / 2; ++c) {
+      const ulonglong2 q = row[c];
+      v[2 * c] = q.x;
+      v[2 * c + 1] = q.y;
+    }
 #pragma unroll
     for (int c = 0; c < kNodeCols; ++c) A.nd[c][dst] = v[c];
   } else {
     uint64_t v[kMemberCols];
+    const ulonglong2* row = (const ulonglong2*)(A.ms + (uint64_t)src * kChildStride);
 #pragma unroll
-    for (int c = 0; c < kMemberCols; ++c) v[c] = A.ms[c][src];
+    for (int c = 0; c < kMemberCols / 2; ++c) {
+      const ulonglong2 q = row[c];
+      v[2 * c] = q.x;
+      v[2 * c + 1] = q.y;
+    }
 #pragma unroll
     for (int c = 0; c < kMemberCols; ++c) A.md[c][dst] = v[c];
   }
@@ -530,11 +543,11 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   A.kr = krows;
   A.nr = nrows;
   A.mr = mrows;
-  for (int c = 0; c < kNodeCols; ++c) {
-    A.no[c] = nsp[c];
-    A.mo[c] = msp[c];
-  }
-  for (int c = 0; c < kKeyOutCols; ++c) A.ko[c] = ksp[c];
+  // sparse outputs, AoS, in the ping-pong buffers that do not hold the rows (8 / 6 columns of
+  // K / N / M rows each: exactly K / N / M output rows)
+  A.kos = ksp[0];
+  A.nos = nsp[0];
+  A.mos = msp[0];
   A.kp = kperm; A.np = nperm; A.mp = mperm;
   A.kbase = dk.base; A.kcnt = dk.hist;
   A.nbase = dnd.base; A.ncnt = dnd.hist;
@@ -643,14 +656,12 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dnd.out, nb, dnd.doff, (uint32_t*)nullptr, d_totals + 1, s));
   CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dm.out, nb, dm.doff, (uint32_t*)nullptr, d_totals + 2, s));
   CompactArgs C;
-  for (int c = 0; c < kKeyOutCols; ++c) {
-    C.ks[c] = ksp[c];
-    C.kd[c] = out->keys.col[c];
-  }
+  C.ks = ksp[0];
+  C.ns = nsp[0];
+  C.ms = msp[0];
+  for (int c = 0; c < kKeyOutCols; ++c) C.kd[c] = out->keys.col[c];
   for (int c = 0; c < kNodeCols; ++c) {
-    C.ns[c] = nsp[c];
     C.nd[c] = out->nodes.col[c];
-    C.ms[c] = msp[c];
     C.md[c] = out->members.col[c];
   }
   C.kbase = dk.base; C.nbase = dnd.base; C.mbase = dm.base;
