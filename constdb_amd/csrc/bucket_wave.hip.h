@@ -37,6 +37,13 @@
 namespace cdb {
 
 constexpr int kWavesPerWG = 4;
+// Cooperative row loads (load_cols_coop) cut the vector-memory accesses per row 3-4x but were
+// measured slower on MI355X (wave kernel 16.2 -> 17.2 ms, wide 5.0 -> 8.8 ms on the C4 shard:
+// the LDS transpose and its syncs cost more than the saved accesses). Off by default.
+#ifndef CDB_COOP_LOADS
+#define CDB_COOP_LOADS 0
+#endif
+constexpr bool kCoopLoads = CDB_COOP_LOADS;
 constexpr uint64_t kM44 = (1ull << 44) - 1, kM42 = (1ull << 42) - 1;
 
 // Per-wave LDS. KE = key rows per lane (1 or 2); child rows per lane CE = 2 KE.
@@ -47,7 +54,7 @@ struct WaveLds {
   uint64_t okh[KC], okf[KC], ovm[KC], osum[KC];  // output keys, sorted
   uint32_t otp[KC], ocnt[KC], ocb[KC];
   uint64_t sw[CC + 2];                     // sort words (keys, then children), sorted in place
-  union {                                  // rows in sorted order
+  union __attribute__((aligned(16))) {     // rows in sorted order (and the load staging area)
     uint64_t col[7][KC];                   // key rows: KS_*
     uint64_t ccol[4][CC];                  // child rows: CS_*
   };
@@ -190,6 +197,83 @@ __device__ __forceinline__ void load_cols(const BucketArgs& A, const WaveDir& d,
       in.cm[e] = q2.y;
     }
   }
+}
+
+// One 64-row half of a bucket's child rows through the staging area (compile-time H: the
+// piece registers and the WaveIn slot are never indexed dynamically, which put them in scratch).
+template <int H, int KE>
+__device__ __forceinline__ void coop_child_half(ulonglong2* st, int lane, uint32_t C, WaveIn<KE>& in, ulonglong2 a0,
+                                                ulonglong2 a1, ulonglong2 a2) {
+  wave_sync();  // the previous reads of the staging area are done
+  st[lane] = a0;  // pieces x = 64 k + lane of this half
+  st[64 + lane] = a1;
+  st[128 + lane] = a2;
+  wave_sync();
+  const uint32_t c = 64 * H + lane;
+  const ulonglong2 q0 = st[lane * 3], q1 = st[lane * 3 + 1], q2 = st[lane * 3 + 2];
+  const bool v = c < C;
+  in.cpkh[H] = v ? q0.x : 0;
+  in.cpkf[H] = v ? q0.y : 0;
+  in.cid1[H] = v ? q1.x : 0;
+  in.cid2[H] = v ? q1.y : 0;
+  in.ct[H] = v ? q2.x : 0;
+  in.cm[H] = v ? q2.y : 0;
+}
+
+// The same columns, loaded cooperatively: a row's 16-B pieces are fetched by adjacent lanes
+// of ONE load instruction (4 lanes per 64-B key row, 3 per 48-B child row), so an instruction
+// touches 16 key rows (21 child rows) instead of 64 and the vector-memory path handles a
+// row's line once instead of once per piece (it was busy ~93 % of the kernel). Every global
+// load is issued up front; the pieces are then transposed through the wave's LDS row area
+// (L.col, free until the keys are scattered) into the lane-per-row registers of WaveIn.
+template <int KE>
+__device__ __forceinline__ void load_cols_coop(const BucketArgs& A, const WaveDir& d, const WavePerm<KE>& p, int lane,
+                                               WaveIn<KE>& in, WaveLds<KE>& L) {
+  static_assert(sizeof(L.ccol) >= 64 * KE * 64, "key rows are staged in the row area");
+  in.d = d;
+  const uint32_t C = d.N + d.M;
+  ulonglong2 kq[4 * KE], cq[6 * KE];
+#pragma unroll
+  for (int i = 0; i < 4 * KE; ++i) {  // key row r = 16 i + lane / 4, piece lane % 4
+    const uint32_t r = 16 * i + (lane >> 2);
+    const uint32_t ridx = (uint32_t)__shfl((int)p.krow[i >> 2], (int)(r & 63), 64);
+    // unconditional: slots past the bucket read row 0 (always allocated; one shared line) and
+    // are masked after the transpose (a select on the load became a scratch-backed flat load)
+    kq[i] = reinterpret_cast<const ulonglong2*>(A.kr + (uint64_t)ridx * kKeyStride)[lane & 3];
+  }
+#pragma unroll
+  for (int i = 0; i < 6 * KE; ++i) {  // child piece x = 64 i + lane: row x / 3 (of 64 h ..), piece x % 3
+    const int h = i / 3;                 // 64-row half: 3 instructions each
+    const uint32_t x = 64 * (i % 3) + lane, rl = x / 3, q = x - 3 * rl;
+    const uint32_t c = 64 * h + rl;
+    const uint32_t ridx = (uint32_t)__shfl((int)p.crow[h], (int)rl, 64);
+    const uint64_t* base = c < d.N ? A.nr : A.mr;
+    cq[i] = reinterpret_cast<const ulonglong2*>(base + (uint64_t)ridx * kChildStride)[q];
+  }
+  ulonglong2* st = reinterpret_cast<ulonglong2*>(&L.ccol[0][0]);
+#pragma unroll
+  for (int i = 0; i < 4 * KE; ++i) st[(16 * i + (lane >> 2)) * 4 + (lane & 3)] = kq[i];
+  wave_sync();
+#pragma unroll
+  for (int e = 0; e < KE; ++e) {
+    const uint32_t c = lane + 64 * e;
+    const ulonglong2 q0 = st[c * 4], q1 = st[c * 4 + 1], q2 = st[c * 4 + 2], q3 = st[c * 4 + 3];
+    const bool v = c < d.K;
+    in.kh[e] = v ? q0.x : 0;
+    in.kf[e] = v ? q0.y : 0;
+    in.kct[e] = v ? q1.x : 0;
+    in.kut[e] = v ? q1.y : 0;
+    in.kdt[e] = v ? q2.x : 0;
+    in.kaux[e] = v ? q2.y : 0;
+    in.kmeta[e] = v ? q3.x : 0;
+  }
+  coop_child_half<0>(st, lane, C, in, cq[0], cq[1], cq[2]);
+  coop_child_half<1>(st, lane, C, in, cq[3], cq[4], cq[5]);
+  if constexpr (KE == 2) {
+    coop_child_half<2>(st, lane, C, in, cq[6], cq[7], cq[8]);
+    coop_child_half<3>(st, lane, C, in, cq[9], cq[10], cq[11]);
+  }
+  wave_sync();  // the row area is the wave's again
 }
 
 // Decoupled look-back (single-pass prefix over buckets in dispatch order). Publishes bucket
@@ -837,7 +921,8 @@ __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_kernel(WaveArgs 
   WavePerm<1> p;
   WaveIn<1> in;
   load_perm<1>(W.A, d, lane, p);
-  load_cols<1>(W.A, d, p, lane, in);
+  if (kCoopLoads) load_cols_coop<1>(W.A, d, p, lane, in, lds_all[wv]);
+  else load_cols<1>(W.A, d, p, lane, in);
   wave_bucket<1>(W, lds_all[wv], b, lane, in, []() {});
 }
 
@@ -876,7 +961,8 @@ __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_kernel(WaveArgs 
       WavePerm<2> p;
       WaveIn<2> in;
       load_perm<2>(W.A, d, lane, p);
-      load_cols<2>(W.A, d, p, lane, in);
+      if (kCoopLoads) load_cols_coop<2>(W.A, d, p, lane, in, lds_all[wv]);
+      else load_cols<2>(W.A, d, p, lane, in);
       wave_bucket<2>(W, lds_all[wv], bb, lane, in, []() {});
     }
   }
