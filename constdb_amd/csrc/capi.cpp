@@ -3,6 +3,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -36,30 +37,6 @@ struct cdb_ops {  // a decoded replicate stream (op rows + byte arena)
 using namespace cdb;
 
 namespace {
-
-struct DevBlock {  // one allocation holding ncol columns of `rows` rows
-  uint64_t* p = nullptr;
-  ~DevBlock() {
-    if (p) hipFree(p);
-  }
-};
-
-cdb_status upload(cdb_ctx* ctx, DevBlock& blk, int ncol, uint64_t rows, const std::vector<const uint64_t*>& src_cols,
-                  cdb_dev_rows* r) {
-  const uint64_t n = std::max<uint64_t>(rows, 1);
-  cdb_status st = hip_check(ctx, hipMalloc(&blk.p, ncol * n * 8), "hipMalloc(input)");
-  if (st != CDB_OK) return st;
-  std::memset(r, 0, sizeof *r);
-  for (int c = 0; c < ncol; ++c) {
-    r->col[c] = blk.p + c * n;
-    if (rows && c < (int)src_cols.size() && src_cols[c]) {
-      st = hip_check(ctx, hipMemcpyAsync(r->col[c], src_cols[c], rows * 8, hipMemcpyHostToDevice, ctx->stream), "h2d");
-      if (st != CDB_OK) return st;
-    }
-  }
-  r->n = rows;
-  return CDB_OK;
-}
 
 std::string hex(const uint8_t* p, uint64_t n) {
   static const char* d = "0123456789abcdef";
@@ -147,70 +124,82 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, const c
   *out = nullptr;
   if (n > (uint32_t)kMaxPos) return fail(ctx, CDB_BAD_ARGUMENT, "at most 63 batches per merge");
   hipSetDevice(ctx->device);
-  // concatenate the batches in fold order, stamping pos = array index into meta
+  // batches are folded in array order: pos = array index, stamped into meta below
   uint64_t K = 0, N = 0, M = 0;
   for (uint32_t i = 0; i < n; ++i) {
     K += inputs[i]->b->n_keys();
     N += inputs[i]->b->n_nodes();
     M += inputs[i]->b->n_members();
   }
-  std::vector<uint64_t> hk[kKeyCols], hn[kNodeCols], hm[kMemberCols];
-  for (auto& v : hk) v.reserve(K);
-  for (auto& v : hn) v.reserve(N);
-  for (auto& v : hm) v.reserve(M);
-  auto restamp = [](uint64_t m, uint32_t pos) { return meta_pack(meta_tag(m), pos, meta_src(m)); };
-  for (uint32_t i = 0; i < n; ++i) {
-    const Batch& b = *inputs[i]->b;
-    hk[K_KH].insert(hk[K_KH].end(), b.kh.begin(), b.kh.end());
-    hk[K_KF].insert(hk[K_KF].end(), b.kf.begin(), b.kf.end());
-    hk[K_CT].insert(hk[K_CT].end(), b.ct.begin(), b.ct.end());
-    hk[K_UT].insert(hk[K_UT].end(), b.ut.begin(), b.ut.end());
-    hk[K_DT].insert(hk[K_DT].end(), b.dt.begin(), b.dt.end());
-    hk[K_AUX].insert(hk[K_AUX].end(), b.aux.begin(), b.aux.end());
-    for (uint64_t m : b.meta) hk[K_META].push_back(restamp(m, i));
-    hn[C_PKH].insert(hn[C_PKH].end(), b.n_pkh.begin(), b.n_pkh.end());
-    hn[C_PKF].insert(hn[C_PKF].end(), b.n_pkf.begin(), b.n_pkf.end());
-    hn[C_ID1].insert(hn[C_ID1].end(), b.n_node.begin(), b.n_node.end());
-    hn[C_ID2].insert(hn[C_ID2].end(), b.n_v.begin(), b.n_v.end());
-    hn[C_T].insert(hn[C_T].end(), b.n_t.begin(), b.n_t.end());
-    for (uint64_t m : b.n_meta) hn[C_META].push_back(restamp(m, i));
-    hm[C_PKH].insert(hm[C_PKH].end(), b.m_pkh.begin(), b.m_pkh.end());
-    hm[C_PKF].insert(hm[C_PKF].end(), b.m_pkf.begin(), b.m_pkf.end());
-    hm[C_ID1].insert(hm[C_ID1].end(), b.m_h.begin(), b.m_h.end());
-    hm[C_ID2].insert(hm[C_ID2].end(), b.m_f.begin(), b.m_f.end());
-    hm[C_T].insert(hm[C_T].end(), b.m_t.begin(), b.m_t.end());
-    for (uint64_t m : b.m_meta) hm[C_META].push_back(restamp(m, i));
-  }
-  auto ptrs = [](std::vector<uint64_t>* v, int nc) {
-    std::vector<const uint64_t*> p(nc);
-    for (int c = 0; c < nc; ++c) p[c] = v[c].data();
-    return p;
-  };
-  DevBlock bk, bn, bm, ok, on, om;
+  // Each batch's columns go straight from its host vectors to their offset in one device
+  // column per field (no host-side concatenation); the fold position is stamped into the meta
+  // words on the device. Input and output blocks are context workspace, reused across calls.
+  const bool timing = std::getenv("CDB_HOST_TIMING") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
   cdb_dev_input din;
   std::memset(&din, 0, sizeof din);
   cdb_dev_output dout;
   std::memset(&dout, 0, sizeof dout);
   din.n_pos = n;
-  cdb_status st;
-  if ((st = upload(ctx, bk, kKeyCols, K, ptrs(hk, kKeyCols), &din.keys)) != CDB_OK) return st;
-  if ((st = upload(ctx, bn, kNodeCols, N, ptrs(hn, kNodeCols), &din.nodes)) != CDB_OK) return st;
-  if ((st = upload(ctx, bm, kMemberCols, M, ptrs(hm, kMemberCols), &din.members)) != CDB_OK) return st;
-  if ((st = upload(ctx, ok, kKeyOutCols, K, {}, &dout.keys)) != CDB_OK) return st;
-  if ((st = upload(ctx, on, kNodeCols, N, {}, &dout.nodes)) != CDB_OK) return st;
-  if ((st = upload(ctx, om, kMemberCols, M, {}, &dout.members)) != CDB_OK) return st;
+  cdb_status st = CDB_OK;
+  auto block = [&](int slot, int ncol, uint64_t rows, cdb_dev_rows* r) -> cdb_status {
+    const uint64_t cap = std::max<uint64_t>(rows, 1);
+    auto* p = static_cast<uint64_t*>(ws_get(ctx, slot, ncol * cap * 8, &st));
+    if (!p) return st;
+    std::memset(r, 0, sizeof *r);
+    for (int c = 0; c < ncol; ++c) r->col[c] = p + c * cap;
+    r->n = rows;
+    return CDB_OK;
+  };
+  if ((st = block(WS_HOST_IN_K, kKeyCols, K, &din.keys)) != CDB_OK ||
+      (st = block(WS_HOST_IN_N, kNodeCols, N, &din.nodes)) != CDB_OK ||
+      (st = block(WS_HOST_IN_M, kMemberCols, M, &din.members)) != CDB_OK ||
+      (st = block(WS_HOST_OUT_K, kKeyOutCols, K, &dout.keys)) != CDB_OK ||
+      (st = block(WS_HOST_OUT_N, kNodeCols, N, &dout.nodes)) != CDB_OK ||
+      (st = block(WS_HOST_OUT_M, kMemberCols, M, &dout.members)) != CDB_OK)
+    return st;
+  auto put = [&](const cdb_dev_rows& r, int c, uint64_t off, const std::vector<uint64_t>& v) -> cdb_status {
+    if (v.empty()) return CDB_OK;
+    return hip_check(ctx, hipMemcpyAsync(r.col[c] + off, v.data(), v.size() * 8, hipMemcpyHostToDevice, ctx->stream),
+                     "h2d");
+  };
+  uint64_t ok = 0, on = 0, om = 0;
+  for (uint32_t i = 0; i < n && st == CDB_OK; ++i) {
+    const Batch& b = *inputs[i]->b;
+    const cdb_dev_rows &rk = din.keys, &rn = din.nodes, &rm = din.members;
+    if ((st = put(rk, K_KH, ok, b.kh)) || (st = put(rk, K_KF, ok, b.kf)) || (st = put(rk, K_CT, ok, b.ct)) ||
+        (st = put(rk, K_UT, ok, b.ut)) || (st = put(rk, K_DT, ok, b.dt)) || (st = put(rk, K_AUX, ok, b.aux)) ||
+        (st = put(rk, K_META, ok, b.meta)) || (st = stamp_pos(ctx, rk.col[K_META] + ok, b.n_keys(), i, ctx->stream)))
+      break;
+    if ((st = put(rn, C_PKH, on, b.n_pkh)) || (st = put(rn, C_PKF, on, b.n_pkf)) ||
+        (st = put(rn, C_ID1, on, b.n_node)) || (st = put(rn, C_ID2, on, b.n_v)) || (st = put(rn, C_T, on, b.n_t)) ||
+        (st = put(rn, C_META, on, b.n_meta)) ||
+        (st = stamp_pos(ctx, rn.col[C_META] + on, b.n_nodes(), i, ctx->stream)))
+      break;
+    if ((st = put(rm, C_PKH, om, b.m_pkh)) || (st = put(rm, C_PKF, om, b.m_pkf)) || (st = put(rm, C_ID1, om, b.m_h)) ||
+        (st = put(rm, C_ID2, om, b.m_f)) || (st = put(rm, C_T, om, b.m_t)) || (st = put(rm, C_META, om, b.m_meta)) ||
+        (st = stamp_pos(ctx, rm.col[C_META] + om, b.n_members(), i, ctx->stream)))
+      break;
+    ok += b.n_keys();
+    on += b.n_nodes();
+    om += b.n_members();
+  }
+  if (st != CDB_OK) return st;
+  const auto t1 = std::chrono::steady_clock::now();
   dout.compact = 1;
   cdb_merge_stats local;
   st = merge_device_impl(ctx, &din, opts, &dout, stats ? stats : &local, ctx->stream);
   if (st != CDB_OK && st != CDB_DICT_MERGE_UNIMPLEMENTED) return st;
   const cdb_status merge_st = st;
+  const auto t2 = std::chrono::steady_clock::now();
   auto* m = new cdb_merged();
   for (uint32_t i = 0; i < n; ++i) m->inputs.push_back(inputs[i]->b);
   auto down = [&](std::vector<uint64_t>* dst, int nc, const cdb_dev_rows& r) -> cdb_status {
     for (int c = 0; c < nc; ++c) {
       dst[c].resize(r.n);
       if (r.n) {
-        cdb_status s2 = hip_check(ctx, hipMemcpy(dst[c].data(), r.col[c], r.n * 8, hipMemcpyDeviceToHost), "d2h");
+        cdb_status s2 = hip_check(
+            ctx, hipMemcpyAsync(dst[c].data(), r.col[c], r.n * 8, hipMemcpyDeviceToHost, ctx->stream), "d2h");
         if (s2 != CDB_OK) return s2;
       }
     }
@@ -220,6 +209,16 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, const c
       (st = down(m->mb, kMemberCols, dout.members)) != CDB_OK) {
     delete m;
     return st;
+  }
+  if ((st = hip_check(ctx, hipStreamSynchronize(ctx->stream), "d2h sync")) != CDB_OK) {
+    delete m;
+    return st;
+  }
+  if (timing) {
+    const auto t3 = std::chrono::steady_clock::now();
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    std::fprintf(stderr, "cdb_merge host timing: upload %.1f ms, merge %.1f ms, download %.1f ms\n", ms(t0, t1),
+                 ms(t1, t2), ms(t2, t3));
   }
   *out = m;
   return merge_st;

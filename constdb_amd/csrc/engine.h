@@ -36,6 +36,8 @@ enum WsSlot {
   WS_STATS,                                             // statistic shards
   WS_KHCOL,                                             // key-hash column of the row level
   WS_LOOKBACK,                                          // output look-back status words
+  WS_HOST_IN_K, WS_HOST_IN_N, WS_HOST_IN_M,             // cdb_merge: uploaded batches
+  WS_HOST_OUT_K, WS_HOST_OUT_N, WS_HOST_OUT_M,          // cdb_merge: device-side result
   WS_COUNT
 };
 
@@ -47,5 +49,6 @@ cdb_status fail(cdb_ctx* ctx, cdb_status st, const std::string& msg);
 cdb_status hip_check(cdb_ctx* ctx, hipError_t e, const char* what);
 cdb_status launch_check(cdb_ctx* ctx, hipStream_t s, const char* what);
 void* ws_get(cdb_ctx* ctx, int slot, size_t bytes, cdb_status* st);
+cdb_status stamp_pos(cdb_ctx* ctx, uint64_t* meta, uint64_t n, uint32_t pos, hipStream_t s);
 
 }  // namespace cdb

@@ -68,6 +68,14 @@ __global__ void set_dir_kernel(uint32_t* base, uint32_t* cnt, uint32_t n) {
   cnt[0] = n;
 }
 
+// pos stamp of the host boundary: batch i's rows carry fold position i (meta bits 48..55)
+__global__ void stamp_pos_kernel(uint64_t* __restrict__ meta, uint64_t n, uint32_t pos) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t m = meta[i];
+    meta[i] = meta_pack(meta_tag(m), pos, meta_src(m));
+  }
+}
+
 __global__ void iota_kernel(uint32_t* p, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     p[i] = (uint32_t)i;
@@ -409,6 +417,13 @@ uint32_t wave_grid(cdb_ctx* ctx, uint64_t nb) {
 }
 
 }  // namespace
+
+cdb_status stamp_pos(cdb_ctx* ctx, uint64_t* meta, uint64_t n, uint32_t pos, hipStream_t s) {
+  if (n == 0) return CDB_OK;
+  const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 4096);
+  stamp_pos_kernel<<<(uint32_t)blocks, 256, 0, s>>>(meta, n, pos);
+  return launch_check(ctx, s, "stamp_pos");
+}
 
 cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts,
                              cdb_dev_output* out, cdb_merge_stats* stats, hipStream_t s) {
