@@ -3,6 +3,7 @@
 #include <stdint.h>
 
 #include <memory>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -10,6 +11,22 @@
 #include "common.h"
 
 namespace cdb {
+
+// Allocator whose resize() leaves new elements uninitialised: result columns are overwritten
+// whole by device downloads, so zero-filling them first only costs a sequential pass.
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind { using other = DefaultInitAlloc<U>; };
+  DefaultInitAlloc() = default;
+  template <class U>
+  DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept { ::new (static_cast<void*>(p)) U; }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) { ::new (static_cast<void*>(p)) U(std::forward<A>(a)...); }
+};
+using ColVec = std::vector<uint64_t, DefaultInitAlloc<uint64_t>>;
 
 struct ByteRef {  // a byte range inside Batch::raw
   uint64_t off, len;
@@ -70,7 +87,7 @@ bool decode_entry_children(const Batch& b, uint64_t off, uint64_t kh, uint64_t k
 // A merge (or op-apply) result, host-resident; bytes resolve through inputs[pos].
 struct cdb_merged {
   std::vector<std::shared_ptr<cdb::Batch>> inputs;  // pos -> decoded batch (byte arenas)
-  std::vector<uint64_t> k[cdb::kKeyOutCols], nd[cdb::kNodeCols], mb[cdb::kMemberCols];
+  cdb::ColVec k[cdb::kKeyOutCols], nd[cdb::kNodeCols], mb[cdb::kMemberCols];
   // replica-metadata merge, computed on first request
   bool replicas_done = false;
   std::vector<std::string> rep_str;          // addr / alias storage (stable: reserved up front)

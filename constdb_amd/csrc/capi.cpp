@@ -1,6 +1,7 @@
 // Host-level C-ABI: decoded batches, the high-level merge (upload, device pipeline,
 // download) and the canonical dump of a merge result.
 #include <hip/hip_runtime_api.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <chrono>
@@ -10,6 +11,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "batch.h"
@@ -32,6 +34,134 @@ struct cdb_ops {  // a decoded replicate stream (op rows + byte arena)
   std::shared_ptr<cdb::Batch> b;
   cdb_ops_info info;
 };
+
+namespace cdb {
+namespace {
+
+constexpr size_t kStageChunk = size_t(32) << 20;  // bytes per pinned slot
+constexpr int kStageSlots = 4;                     // = the size of cdb_ctx::pin_ev
+
+int copy_threads() {
+  static const int t = [] {
+    const char* e = std::getenv("CDB_COPY_THREADS");
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    const int v = e ? std::atoi(e) : std::min(8, hw);
+    return std::max(1, std::min(64, v));
+  }();
+  return t;
+}
+
+// Asks for transparent huge pages on a fresh result column: its first touch (the staged
+// download) then takes one fault per 2 MB instead of one per 4 KB.
+void advise_huge(void* p, size_t bytes) {
+  constexpr uintptr_t kHuge = uintptr_t(2) << 20;
+  const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(kHuge - 1);
+  const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(kHuge - 1);
+  if (b > a) madvise(reinterpret_cast<void*>(a), b - a, MADV_HUGEPAGE);
+}
+
+struct Piece {
+  char* host;
+  char* pin;
+  char* dev;
+  size_t bytes;
+};
+
+// Copies every piece between pageable and pinned memory; the bytes are split in equal ranges
+// over the copy threads (page faults of fresh destination pages are taken in parallel too).
+void par_copy(const std::vector<Piece>& ps, bool to_pin) {
+  size_t total = 0;
+  for (const Piece& p : ps) total += p.bytes;
+  const int T = (int)std::min<size_t>((size_t)copy_threads(), std::max<size_t>(1, total >> 20));
+  auto run = [&](size_t lo, size_t hi) {
+    size_t base = 0;
+    for (const Piece& p : ps) {
+      const size_t a = std::max(lo, base), b = std::min(hi, base + p.bytes);
+      if (a < b) {
+        if (to_pin) std::memcpy(p.pin + (a - base), p.host + (a - base), b - a);
+        else std::memcpy(p.host + (a - base), p.pin + (a - base), b - a);
+      }
+      base += p.bytes;
+    }
+  };
+  if (T <= 1) {
+    run(0, total);
+    return;
+  }
+  const size_t per = (total + T - 1) / T;
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back(run, std::min(total, t * per), std::min(total, (t + 1) * per));
+  run(0, std::min(total, per));
+  for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+cdb_status staged_copy(cdb_ctx* ctx, const HostSeg* segs, size_t nseg, bool h2d) {
+  cdb_status st;
+  if (!ctx->pin) {
+    if ((st = hip_check(ctx, hipHostMalloc(&ctx->pin, kStageSlots * kStageChunk, hipHostMallocDefault),
+                        "hipHostMalloc(staging)")) != CDB_OK) {
+      ctx->pin = nullptr;
+      return st;
+    }
+    for (hipEvent_t& e : ctx->pin_ev) {  // created recorded, so the first waits return at once
+      if ((st = hip_check(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "event")) != CDB_OK) return st;
+      if ((st = hip_check(ctx, hipEventRecord(e, ctx->stream), "event")) != CDB_OK) return st;
+    }
+  }
+  // chunk jobs: job j fills pinned slot j % kStageSlots with pieces of one or more segments
+  std::vector<std::vector<Piece>> jobs;
+  std::vector<Piece> cur;
+  size_t fill = 0;
+  for (size_t i = 0; i < nseg; ++i) {
+    for (size_t off = 0; off < segs[i].bytes;) {
+      const size_t take = std::min(segs[i].bytes - off, kStageChunk - fill);
+      char* slot = static_cast<char*>(ctx->pin) + (jobs.size() % kStageSlots) * kStageChunk;
+      cur.push_back({static_cast<char*>(segs[i].host) + off, slot + fill, static_cast<char*>(segs[i].dev) + off, take});
+      fill += take;
+      off += take;
+      if (fill == kStageChunk) {
+        jobs.push_back(std::move(cur));
+        cur.clear();
+        fill = 0;
+      }
+    }
+  }
+  if (!cur.empty()) jobs.push_back(std::move(cur));
+  const hipMemcpyKind kind = h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+  // a slot is reused only after the copy recorded on its event (this call's or an earlier one's)
+  auto dma = [&](size_t j) -> cdb_status {
+    hipEvent_t ev = ctx->pin_ev[j % kStageSlots];
+    for (const Piece& p : jobs[j]) {
+      void* dst = h2d ? (void*)p.dev : (void*)p.pin;
+      const void* src = h2d ? (const void*)p.pin : (const void*)p.dev;
+      cdb_status s2 = hip_check(ctx, hipMemcpyAsync(dst, src, p.bytes, kind, ctx->stream), "staged copy");
+      if (s2 != CDB_OK) return s2;
+    }
+    return hip_check(ctx, hipEventRecord(ev, ctx->stream), "event");
+  };
+  if (h2d) {
+    for (size_t j = 0; j < jobs.size(); ++j) {
+      if ((st = hip_check(ctx, hipEventSynchronize(ctx->pin_ev[j % kStageSlots]), "staging wait")) != CDB_OK) return st;
+      par_copy(jobs[j], true);
+      if ((st = dma(j)) != CDB_OK) return st;
+    }
+    return CDB_OK;
+  }
+  for (size_t j = 0; j < jobs.size() && j < (size_t)kStageSlots; ++j) {
+    if ((st = hip_check(ctx, hipEventSynchronize(ctx->pin_ev[j % kStageSlots]), "staging wait")) != CDB_OK) return st;
+    if ((st = dma(j)) != CDB_OK) return st;
+  }
+  for (size_t j = 0; j < jobs.size(); ++j) {
+    if ((st = hip_check(ctx, hipEventSynchronize(ctx->pin_ev[j % kStageSlots]), "staging wait")) != CDB_OK) return st;
+    par_copy(jobs[j], false);
+    if (j + kStageSlots < jobs.size() && (st = dma(j + kStageSlots)) != CDB_OK) return st;
+  }
+  return CDB_OK;
+}
+
+}  // namespace cdb
 
 
 using namespace cdb;
@@ -158,27 +288,31 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, const c
       (st = block(WS_HOST_OUT_N, kNodeCols, N, &dout.nodes)) != CDB_OK ||
       (st = block(WS_HOST_OUT_M, kMemberCols, M, &dout.members)) != CDB_OK)
     return st;
-  auto put = [&](const cdb_dev_rows& r, int c, uint64_t off, const std::vector<uint64_t>& v) -> cdb_status {
-    if (v.empty()) return CDB_OK;
-    return hip_check(ctx, hipMemcpyAsync(r.col[c] + off, v.data(), v.size() * 8, hipMemcpyHostToDevice, ctx->stream),
-                     "h2d");
+  std::vector<HostSeg> segs;
+  auto put = [&](const cdb_dev_rows& r, int c, uint64_t off, const std::vector<uint64_t>& v) {
+    if (!v.empty()) segs.push_back({const_cast<uint64_t*>(v.data()), r.col[c] + off, v.size() * 8});
   };
   uint64_t ok = 0, on = 0, om = 0;
-  for (uint32_t i = 0; i < n && st == CDB_OK; ++i) {
+  for (uint32_t i = 0; i < n; ++i) {
     const Batch& b = *inputs[i]->b;
     const cdb_dev_rows &rk = din.keys, &rn = din.nodes, &rm = din.members;
-    if ((st = put(rk, K_KH, ok, b.kh)) || (st = put(rk, K_KF, ok, b.kf)) || (st = put(rk, K_CT, ok, b.ct)) ||
-        (st = put(rk, K_UT, ok, b.ut)) || (st = put(rk, K_DT, ok, b.dt)) || (st = put(rk, K_AUX, ok, b.aux)) ||
-        (st = put(rk, K_META, ok, b.meta)) || (st = stamp_pos(ctx, rk.col[K_META] + ok, b.n_keys(), i, ctx->stream)))
-      break;
-    if ((st = put(rn, C_PKH, on, b.n_pkh)) || (st = put(rn, C_PKF, on, b.n_pkf)) ||
-        (st = put(rn, C_ID1, on, b.n_node)) || (st = put(rn, C_ID2, on, b.n_v)) || (st = put(rn, C_T, on, b.n_t)) ||
-        (st = put(rn, C_META, on, b.n_meta)) ||
-        (st = stamp_pos(ctx, rn.col[C_META] + on, b.n_nodes(), i, ctx->stream)))
-      break;
-    if ((st = put(rm, C_PKH, om, b.m_pkh)) || (st = put(rm, C_PKF, om, b.m_pkf)) || (st = put(rm, C_ID1, om, b.m_h)) ||
-        (st = put(rm, C_ID2, om, b.m_f)) || (st = put(rm, C_T, om, b.m_t)) || (st = put(rm, C_META, om, b.m_meta)) ||
-        (st = stamp_pos(ctx, rm.col[C_META] + om, b.n_members(), i, ctx->stream)))
+    const std::vector<uint64_t>* kc[kKeyCols] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
+    const std::vector<uint64_t>* nc[kNodeCols] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
+    const std::vector<uint64_t>* mc[kMemberCols] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
+    for (int c = 0; c < kKeyCols; ++c) put(rk, c, ok, *kc[c]);
+    for (int c = 0; c < kNodeCols; ++c) put(rn, c, on, *nc[c]);
+    for (int c = 0; c < kMemberCols; ++c) put(rm, c, om, *mc[c]);
+    ok += b.n_keys();
+    on += b.n_nodes();
+    om += b.n_members();
+  }
+  if ((st = staged_copy(ctx, segs.data(), segs.size(), true)) != CDB_OK) return st;
+  ok = on = om = 0;
+  for (uint32_t i = 0; i < n && st == CDB_OK; ++i) {
+    const Batch& b = *inputs[i]->b;
+    if ((st = stamp_pos(ctx, din.keys.col[K_META] + ok, b.n_keys(), i, ctx->stream)) != CDB_OK ||
+        (st = stamp_pos(ctx, din.nodes.col[C_META] + on, b.n_nodes(), i, ctx->stream)) != CDB_OK ||
+        (st = stamp_pos(ctx, din.members.col[C_META] + om, b.n_members(), i, ctx->stream)) != CDB_OK)
       break;
     ok += b.n_keys();
     on += b.n_nodes();
@@ -194,23 +328,18 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, const c
   const auto t2 = std::chrono::steady_clock::now();
   auto* m = new cdb_merged();
   for (uint32_t i = 0; i < n; ++i) m->inputs.push_back(inputs[i]->b);
-  auto down = [&](std::vector<uint64_t>* dst, int nc, const cdb_dev_rows& r) -> cdb_status {
+  std::vector<HostSeg> dsegs;
+  auto down = [&](ColVec* dst, int nc, const cdb_dev_rows& r) {
     for (int c = 0; c < nc; ++c) {
-      dst[c].resize(r.n);
-      if (r.n) {
-        cdb_status s2 = hip_check(
-            ctx, hipMemcpyAsync(dst[c].data(), r.col[c], r.n * 8, hipMemcpyDeviceToHost, ctx->stream), "d2h");
-        if (s2 != CDB_OK) return s2;
-      }
+      dst[c].resize(r.n);  // default-initialised: no zero fill
+      advise_huge(dst[c].data(), r.n * 8);
+      if (r.n) dsegs.push_back({dst[c].data(), r.col[c], r.n * 8});
     }
-    return CDB_OK;
   };
-  if ((st = down(m->k, kKeyOutCols, dout.keys)) != CDB_OK || (st = down(m->nd, kNodeCols, dout.nodes)) != CDB_OK ||
-      (st = down(m->mb, kMemberCols, dout.members)) != CDB_OK) {
-    delete m;
-    return st;
-  }
-  if ((st = hip_check(ctx, hipStreamSynchronize(ctx->stream), "d2h sync")) != CDB_OK) {
+  down(m->k, kKeyOutCols, dout.keys);
+  down(m->nd, kNodeCols, dout.nodes);
+  down(m->mb, kMemberCols, dout.members);
+  if ((st = staged_copy(ctx, dsegs.data(), dsegs.size(), false)) != CDB_OK) {
     delete m;
     return st;
   }

@@ -19,7 +19,9 @@ struct cdb_ctx {
   std::string last_error;
   struct Buf { void* p = nullptr; size_t bytes = 0; };
   Buf ws[32];  // named workspace slots, grown on demand, reused across calls
-  uint32_t wave_slots[2] = {0, 0};  // resident streaming-wave-kernel workgroups per variant (0 = not queried)
+  uint32_t wave_slots[2] = {0, 0};
+  void* pin = nullptr;                                // pinned staging ring of host<->device copies
+  hipEvent_t pin_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // resident streaming-wave-kernel workgroups per variant (0 = not queried)
 };
 
 namespace cdb {
@@ -49,6 +51,16 @@ cdb_status fail(cdb_ctx* ctx, cdb_status st, const std::string& msg);
 cdb_status hip_check(cdb_ctx* ctx, hipError_t e, const char* what);
 cdb_status launch_check(cdb_ctx* ctx, hipStream_t s, const char* what);
 void* ws_get(cdb_ctx* ctx, int slot, size_t bytes, cdb_status* st);
+// One host<->device copy of pageable memory (a column or a piece of one).
+struct HostSeg {
+  void* host;
+  void* dev;
+  size_t bytes;
+};
+// Moves `segs` through the context's pinned staging ring: host threads copy chunk k into (out
+// of) a pinned slot while the DMA engine moves chunk k-1 on ctx->stream. Returns with every
+// copy complete (the stream's earlier work included).
+cdb_status staged_copy(cdb_ctx* ctx, const HostSeg* segs, size_t nseg, bool h2d);
 cdb_status stamp_pos(cdb_ctx* ctx, uint64_t* meta, uint64_t n, uint32_t pos, hipStream_t s);
 
 }  // namespace cdb

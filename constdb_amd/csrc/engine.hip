@@ -779,6 +779,9 @@ void cdb_ctx_destroy(cdb_ctx* ctx) {
   if (ctx->ev_join) hipEventDestroy(ctx->ev_join);
   for (hipEvent_t e : {ctx->ev_pfork, ctx->ev_pn, ctx->ev_pm})
     if (e) hipEventDestroy(e);
+  for (hipEvent_t e : ctx->pin_ev)
+    if (e) hipEventDestroy(e);
+  if (ctx->pin) hipHostFree(ctx->pin);
   if (ctx->side) hipStreamDestroy(ctx->side);
   if (ctx->side2) hipStreamDestroy(ctx->side2);
   if (ctx->stream) hipStreamDestroy(ctx->stream);

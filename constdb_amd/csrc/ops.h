@@ -37,9 +37,8 @@ int decode_ops(const uint8_t* buf, size_t len, uint64_t uuid_he_sent, Batch* out
 
 // Device apply (ops_apply.hip): state = merge-result columns (host), ops = the op batch at fold
 // position pos_ops; out = merge-result columns (host).
-cdb_status apply_ops_impl(cdb_ctx* ctx, const std::vector<uint64_t>* sk, const std::vector<uint64_t>* sn,
-                          const std::vector<uint64_t>* sm, const Batch& ops, uint32_t pos_ops,
-                          std::vector<uint64_t>* ok, std::vector<uint64_t>* on, std::vector<uint64_t>* om,
+cdb_status apply_ops_impl(cdb_ctx* ctx, const ColVec* sk, const ColVec* sn, const ColVec* sm, const Batch& ops, uint32_t pos_ops,
+                          ColVec* ok, ColVec* on, ColVec* om,
                           cdb_apply_stats* stats);
 
 }  // namespace cdb

@@ -648,9 +648,8 @@ __global__ void key_emit_kernel(KeyEmit E, uint32_t nseg, cdb_dev_rows out) {
 
 // Applies `ops` (pos = pos_ops in their meta words) to the state rows. Host vectors in, host
 // vectors out (the cdb_merged layout); device time of the pipeline in stats.
-cdb_status apply_ops_impl(cdb_ctx* ctx, const std::vector<uint64_t>* sk, const std::vector<uint64_t>* sn,
-                          const std::vector<uint64_t>* sm, const Batch& B, uint32_t pos_ops,
-                          std::vector<uint64_t>* ok, std::vector<uint64_t>* on, std::vector<uint64_t>* om,
+cdb_status apply_ops_impl(cdb_ctx* ctx, const ColVec* sk, const ColVec* sn, const ColVec* sm, const Batch& B, uint32_t pos_ops,
+                          ColVec* ok, ColVec* on, ColVec* om,
                           cdb_apply_stats* stats) {
   hipStream_t s = ctx->stream;
   const uint64_t Ks = sk[O_KH].size(), Ns = sn[0].size(), Ms = sm[0].size();
@@ -659,7 +658,7 @@ cdb_status apply_ops_impl(cdb_ctx* ctx, const std::vector<uint64_t>* sk, const s
   if (E >= (1ull << 31) || Cn >= (1ull << 31) || Cm >= (1ull << 31))
     return fail(ctx, CDB_BAD_ARGUMENT, "op apply: row counts must be < 2^31 per family");
   Dev D{{}, ctx};
-  auto up = [&](const std::vector<uint64_t>& v, uint64_t** p) -> cdb_status {
+  auto up = [&](const auto& v, uint64_t** p) -> cdb_status {
     OPS_TRY(D.alloc(p, v.size()));
     if (!v.empty())
       OPS_TRY(hip_check(ctx, hipMemcpyAsync(*p, v.data(), v.size() * 8, hipMemcpyHostToDevice, s), "h2d(ops)"));
@@ -885,7 +884,7 @@ cdb_status apply_ops_impl(cdb_ctx* ctx, const std::vector<uint64_t>* sk, const s
   float ms = 0;
   hipEventElapsedTime(&ms, e0, e1);
   // ---- download
-  auto down = [&](std::vector<uint64_t>* dst, int nc, uint64_t* const* src, uint64_t n) -> cdb_status {
+  auto down = [&](ColVec* dst, int nc, uint64_t* const* src, uint64_t n) -> cdb_status {
     for (int c = 0; c < nc; ++c) {
       dst[c].resize(n);
       if (n) OPS_TRY(hip_check(ctx, hipMemcpy(dst[c].data(), src[c], n * 8, hipMemcpyDeviceToHost), "d2h(ops)"));
