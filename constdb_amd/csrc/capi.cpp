@@ -51,15 +51,6 @@ int copy_threads() {
   return t;
 }
 
-// Asks for transparent huge pages on a fresh result column: its first touch (the staged
-// download) then takes one fault per 2 MB instead of one per 4 KB.
-void advise_huge(void* p, size_t bytes) {
-  constexpr uintptr_t kHuge = uintptr_t(2) << 20;
-  const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(kHuge - 1);
-  const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(kHuge - 1);
-  if (b > a) madvise(reinterpret_cast<void*>(a), b - a, MADV_HUGEPAGE);
-}
-
 struct Piece {
   char* host;
   char* pin;
@@ -97,7 +88,33 @@ void par_copy(const std::vector<Piece>& ps, bool to_pin) {
 
 }  // namespace
 
-cdb_status staged_copy(cdb_ctx* ctx, const HostSeg* segs, size_t nseg, bool h2d) {
+// The first touch of a fresh result buffer (the staged download) then takes one fault per 2 MB
+// instead of one per 4 KB.
+void advise_huge(void* p, size_t bytes) {
+  constexpr uintptr_t kHuge = uintptr_t(2) << 20;
+  const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(kHuge - 1);
+  const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(kHuge - 1);
+  if (b > a) madvise(reinterpret_cast<void*>(a), b - a, MADV_HUGEPAGE);
+}
+
+cdb_status staged_h2d(cdb_ctx* ctx, void* dev, const void* host, size_t bytes, hipStream_t s) {
+  if (!bytes) return CDB_OK;
+  if (bytes < (size_t(1) << 20)) return hip_check(ctx, hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, s), "h2d");
+  const HostSeg g{const_cast<void*>(host), dev, bytes};
+  return staged_copy(ctx, &g, 1, true, s);
+}
+
+cdb_status staged_d2h(cdb_ctx* ctx, void* host, const void* dev, size_t bytes, hipStream_t s) {
+  if (!bytes) return CDB_OK;
+  if (bytes < (size_t(1) << 20)) {
+    cdb_status st = hip_check(ctx, hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, s), "d2h");
+    return st != CDB_OK ? st : hip_check(ctx, hipStreamSynchronize(s), "d2h sync");
+  }
+  const HostSeg g{host, const_cast<void*>(dev), bytes};
+  return staged_copy(ctx, &g, 1, false, s);
+}
+
+cdb_status staged_copy(cdb_ctx* ctx, const HostSeg* segs, size_t nseg, bool h2d, hipStream_t stream) {
   cdb_status st;
   if (!ctx->pin) {
     if ((st = hip_check(ctx, hipHostMalloc(&ctx->pin, kStageSlots * kStageChunk, hipHostMallocDefault),
@@ -107,17 +124,19 @@ cdb_status staged_copy(cdb_ctx* ctx, const HostSeg* segs, size_t nseg, bool h2d)
     }
     for (hipEvent_t& e : ctx->pin_ev) {  // created recorded, so the first waits return at once
       if ((st = hip_check(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming), "event")) != CDB_OK) return st;
-      if ((st = hip_check(ctx, hipEventRecord(e, ctx->stream), "event")) != CDB_OK) return st;
+      if ((st = hip_check(ctx, hipEventRecord(e, stream), "event")) != CDB_OK) return st;
     }
   }
-  // chunk jobs: job j fills pinned slot j % kStageSlots with pieces of one or more segments
+  // chunk jobs: job j fills pinned slot (base + j) % kStageSlots with pieces of one or more
+  // segments; the ring continues where the previous call left it
+  const uint64_t base = ctx->pin_next;
   std::vector<std::vector<Piece>> jobs;
   std::vector<Piece> cur;
   size_t fill = 0;
   for (size_t i = 0; i < nseg; ++i) {
     for (size_t off = 0; off < segs[i].bytes;) {
       const size_t take = std::min(segs[i].bytes - off, kStageChunk - fill);
-      char* slot = static_cast<char*>(ctx->pin) + (jobs.size() % kStageSlots) * kStageChunk;
+      char* slot = static_cast<char*>(ctx->pin) + ((base + jobs.size()) % kStageSlots) * kStageChunk;
       cur.push_back({static_cast<char*>(segs[i].host) + off, slot + fill, static_cast<char*>(segs[i].dev) + off, take});
       fill += take;
       off += take;
@@ -129,32 +148,34 @@ cdb_status staged_copy(cdb_ctx* ctx, const HostSeg* segs, size_t nseg, bool h2d)
     }
   }
   if (!cur.empty()) jobs.push_back(std::move(cur));
+  ctx->pin_next = base + jobs.size();
+  auto ev_of = [&](size_t j) { return ctx->pin_ev[(base + j) % kStageSlots]; };
   const hipMemcpyKind kind = h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
   // a slot is reused only after the copy recorded on its event (this call's or an earlier one's)
   auto dma = [&](size_t j) -> cdb_status {
-    hipEvent_t ev = ctx->pin_ev[j % kStageSlots];
+    hipEvent_t ev = ev_of(j);
     for (const Piece& p : jobs[j]) {
       void* dst = h2d ? (void*)p.dev : (void*)p.pin;
       const void* src = h2d ? (const void*)p.pin : (const void*)p.dev;
-      cdb_status s2 = hip_check(ctx, hipMemcpyAsync(dst, src, p.bytes, kind, ctx->stream), "staged copy");
+      cdb_status s2 = hip_check(ctx, hipMemcpyAsync(dst, src, p.bytes, kind, stream), "staged copy");
       if (s2 != CDB_OK) return s2;
     }
-    return hip_check(ctx, hipEventRecord(ev, ctx->stream), "event");
+    return hip_check(ctx, hipEventRecord(ev, stream), "event");
   };
   if (h2d) {
     for (size_t j = 0; j < jobs.size(); ++j) {
-      if ((st = hip_check(ctx, hipEventSynchronize(ctx->pin_ev[j % kStageSlots]), "staging wait")) != CDB_OK) return st;
+      if ((st = hip_check(ctx, hipEventSynchronize(ev_of(j)), "staging wait")) != CDB_OK) return st;
       par_copy(jobs[j], true);
       if ((st = dma(j)) != CDB_OK) return st;
     }
     return CDB_OK;
   }
   for (size_t j = 0; j < jobs.size() && j < (size_t)kStageSlots; ++j) {
-    if ((st = hip_check(ctx, hipEventSynchronize(ctx->pin_ev[j % kStageSlots]), "staging wait")) != CDB_OK) return st;
+    if ((st = hip_check(ctx, hipEventSynchronize(ev_of(j)), "staging wait")) != CDB_OK) return st;
     if ((st = dma(j)) != CDB_OK) return st;
   }
   for (size_t j = 0; j < jobs.size(); ++j) {
-    if ((st = hip_check(ctx, hipEventSynchronize(ctx->pin_ev[j % kStageSlots]), "staging wait")) != CDB_OK) return st;
+    if ((st = hip_check(ctx, hipEventSynchronize(ev_of(j)), "staging wait")) != CDB_OK) return st;
     par_copy(jobs[j], false);
     if (j + kStageSlots < jobs.size() && (st = dma(j + kStageSlots)) != CDB_OK) return st;
   }
@@ -306,7 +327,7 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, const c
     on += b.n_nodes();
     om += b.n_members();
   }
-  if ((st = staged_copy(ctx, segs.data(), segs.size(), true)) != CDB_OK) return st;
+  if ((st = staged_copy(ctx, segs.data(), segs.size(), true, ctx->stream)) != CDB_OK) return st;
   ok = on = om = 0;
   for (uint32_t i = 0; i < n && st == CDB_OK; ++i) {
     const Batch& b = *inputs[i]->b;
@@ -339,7 +360,7 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, const c
   down(m->k, kKeyOutCols, dout.keys);
   down(m->nd, kNodeCols, dout.nodes);
   down(m->mb, kMemberCols, dout.members);
-  if ((st = staged_copy(ctx, dsegs.data(), dsegs.size(), false)) != CDB_OK) {
+  if ((st = staged_copy(ctx, dsegs.data(), dsegs.size(), false, ctx->stream)) != CDB_OK) {
     delete m;
     return st;
   }

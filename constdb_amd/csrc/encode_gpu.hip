@@ -618,8 +618,7 @@ cdb_status dalloc(cdb_ctx* ctx, DevMem& m, size_t bytes) {
   return hip_check(ctx, hipMalloc(&m.p, std::max<size_t>(bytes, 16)), "hipMalloc(encode)");
 }
 cdb_status h2d(cdb_ctx* ctx, void* dst, const void* src, size_t bytes, hipStream_t s) {
-  if (!bytes) return CDB_OK;
-  return hip_check(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s), "h2d(encode)");
+  return staged_h2d(ctx, dst, src, bytes, s);
 }
 
 template <class Tr>
@@ -887,7 +886,8 @@ cdb_status encode_snapshot_impl(cdb_ctx* ctx, const cdb_merged& m, const cdb_enc
   uint8_t* host = (uint8_t*)std::malloc(L + 8);
   if (!host) return fail(ctx, CDB_OUT_OF_MEMORY, "encode: host buffer");
   uint64_t crc = 0;
-  if ((st = hip_check(ctx, hipMemcpyAsync(host, dev, L + 8, hipMemcpyDeviceToHost, s), "d2h stream")) != CDB_OK ||
+  advise_huge(host, L + 8);
+  if ((st = staged_d2h(ctx, host, dev, L + 8, s)) != CDB_OK ||
       (st = hip_check(ctx, hipMemcpyAsync(&crc, dcrc.p, 8, hipMemcpyDeviceToHost, s), "d2h crc")) != CDB_OK ||
       (st = hip_check(ctx, hipStreamSynchronize(s), "sync")) != CDB_OK) {
     std::free(host);

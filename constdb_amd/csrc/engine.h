@@ -21,7 +21,8 @@ struct cdb_ctx {
   Buf ws[32];  // named workspace slots, grown on demand, reused across calls
   uint32_t wave_slots[2] = {0, 0};
   void* pin = nullptr;                                // pinned staging ring of host<->device copies
-  hipEvent_t pin_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // resident streaming-wave-kernel workgroups per variant (0 = not queried)
+  hipEvent_t pin_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint64_t pin_next = 0;                              // next slot of the ring (continues across calls)  // resident streaming-wave-kernel workgroups per variant (0 = not queried)
 };
 
 namespace cdb {
@@ -58,9 +59,14 @@ struct HostSeg {
   size_t bytes;
 };
 // Moves `segs` through the context's pinned staging ring: host threads copy chunk k into (out
-// of) a pinned slot while the DMA engine moves chunk k-1 on ctx->stream. Returns with every
-// copy complete (the stream's earlier work included).
-cdb_status staged_copy(cdb_ctx* ctx, const HostSeg* segs, size_t nseg, bool h2d);
+// of) a pinned slot while the DMA engine moves chunk k-1 on stream s. H2D returns once every
+// chunk is queued (the sources may be freed); D2H returns with every copy complete.
+cdb_status staged_copy(cdb_ctx* ctx, const HostSeg* segs, size_t nseg, bool h2d, hipStream_t s);
+// Single-segment forms; copies under 1 MB go straight through hipMemcpyAsync.
+cdb_status staged_h2d(cdb_ctx* ctx, void* dev, const void* host, size_t bytes, hipStream_t s);
+cdb_status staged_d2h(cdb_ctx* ctx, void* host, const void* dev, size_t bytes, hipStream_t s);
+// Asks for transparent huge pages on a fresh host buffer about to be filled by a download.
+void advise_huge(void* p, size_t bytes);
 cdb_status stamp_pos(cdb_ctx* ctx, uint64_t* meta, uint64_t n, uint32_t pos, hipStream_t s);
 
 }  // namespace cdb

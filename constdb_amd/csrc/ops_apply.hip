@@ -661,7 +661,7 @@ cdb_status apply_ops_impl(cdb_ctx* ctx, const ColVec* sk, const ColVec* sn, cons
   auto up = [&](const auto& v, uint64_t** p) -> cdb_status {
     OPS_TRY(D.alloc(p, v.size()));
     if (!v.empty())
-      OPS_TRY(hip_check(ctx, hipMemcpyAsync(*p, v.data(), v.size() * 8, hipMemcpyHostToDevice, s), "h2d(ops)"));
+      OPS_TRY(staged_h2d(ctx, *p, v.data(), v.size() * 8, s));
     return CDB_OK;
   };
   uint64_t *sk_d[kKeyOutCols], *sn_d[kNodeCols], *sm_d[kMemberCols];
@@ -886,8 +886,9 @@ cdb_status apply_ops_impl(cdb_ctx* ctx, const ColVec* sk, const ColVec* sn, cons
   // ---- download
   auto down = [&](ColVec* dst, int nc, uint64_t* const* src, uint64_t n) -> cdb_status {
     for (int c = 0; c < nc; ++c) {
-      dst[c].resize(n);
-      if (n) OPS_TRY(hip_check(ctx, hipMemcpy(dst[c].data(), src[c], n * 8, hipMemcpyDeviceToHost), "d2h(ops)"));
+      dst[c].resize(n);  // default-initialised
+      advise_huge(dst[c].data(), n * 8);
+      OPS_TRY(staged_d2h(ctx, dst[c].data(), src[c], n * 8, s));
     }
     return CDB_OK;
   };
