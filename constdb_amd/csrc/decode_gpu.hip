@@ -312,8 +312,13 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) return rc;
   const uint64_t n = idx.offset.size();
   if (n == 0) return rc;
-  hipSetDevice(ctx->device);
+  if (hipSetDevice(ctx->device) != hipSuccess) return CDB_DEVICE_ERROR;
   hipStream_t s = ctx->stream;
+  // every runtime call is checked; the first failure is reported (hip_check keeps its message)
+  cdb_status st = CDB_OK;
+  auto ck = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess && st == CDB_OK) st = hip_check(ctx, e, what);
+  };
   // one device block: raw | off | kind | counts | offsets | key cols | refs | node cols | member cols
   std::vector<uint64_t> noff(n), moff(n);
   std::vector<uint32_t> ncnt(n), mcnt(n);
@@ -329,10 +334,11 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   uint32_t* d_mcnt = d_ncnt + n;
   uint8_t* d_kind = (uint8_t*)(d_mcnt + n);
   EvPair ev;
-  hipEventRecord(ev.a, s);
-  hipMemcpyAsync(d_raw.p, out->raw.data(), len, hipMemcpyHostToDevice, s);
-  hipMemcpyAsync(d_off, idx.offset.data(), n * 8, hipMemcpyHostToDevice, s);
-  hipMemcpyAsync(d_kind, idx.kind.data(), n, hipMemcpyHostToDevice, s);
+  ck(hipEventRecord(ev.a, s), "event");
+  if (st == CDB_OK) st = staged_h2d(ctx, d_raw.p, out->raw.data(), len, s);
+  if (st == CDB_OK) st = staged_h2d(ctx, d_off, idx.offset.data(), n * 8, s);
+  ck(hipMemcpyAsync(d_kind, idx.kind.data(), n, hipMemcpyHostToDevice, s), "h2d(decode)");
+  if (st != CDB_OK) return st;
   DecArgs A;
   std::memset(&A, 0, sizeof A);
   A.raw = (const uint8_t*)d_raw.p;
@@ -343,9 +349,11 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   A.mcount = d_mcnt;
   const uint32_t grid = (uint32_t)((n + kDecThreads - 1) / kDecThreads);
   count_kernel<<<grid, kDecThreads, 0, s>>>(A);
-  hipMemcpyAsync(ncnt.data(), d_ncnt, n * 4, hipMemcpyDeviceToHost, s);
-  hipMemcpyAsync(mcnt.data(), d_mcnt, n * 4, hipMemcpyDeviceToHost, s);
-  if (hipStreamSynchronize(s) != hipSuccess) return CDB_DEVICE_ERROR;
+  ck(hipGetLastError(), "count_kernel");
+  ck(hipMemcpyAsync(ncnt.data(), d_ncnt, n * 4, hipMemcpyDeviceToHost, s), "d2h(decode)");
+  ck(hipMemcpyAsync(mcnt.data(), d_mcnt, n * 4, hipMemcpyDeviceToHost, s), "d2h(decode)");
+  ck(hipStreamSynchronize(s), "sync(decode)");
+  if (st != CDB_OK) return st;
   // entries past the per-thread dedup limits: decoded here, into slots reserved by the scan
   struct HostEntry { uint64_t i; Batch rows; uint64_t total; };
   std::vector<HostEntry> hosted;
@@ -397,39 +405,40 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   A.mvref_len = w; w += nm;
   A.noff = d_noff;
   A.moff = d_moff;
-  hipMemcpyAsync(d_noff, noff.data(), n * 8, hipMemcpyHostToDevice, s);
-  hipMemcpyAsync(d_moff, moff.data(), n * 8, hipMemcpyHostToDevice, s);
+  if (st == CDB_OK) st = staged_h2d(ctx, d_noff, noff.data(), n * 8, s);
+  if (st == CDB_OK) st = staged_h2d(ctx, d_moff, moff.data(), n * 8, s);
+  if (st != CDB_OK) return st;
   emit_kernel<<<grid, kDecThreads, 0, s>>>(A);
   if (hipGetLastError() != hipSuccess) return CDB_DEVICE_ERROR;
-  // rows back into the host batch
+  // rows back into the host batch: one staged download of every column
   Batch& b = *out;
+  std::vector<HostSeg> segs;
+  auto down = [&](std::vector<uint64_t>* v, const uint64_t* dev, uint64_t rows) {
+    v->resize(rows);
+    if (rows) segs.push_back({v->data(), const_cast<uint64_t*>(dev), rows * 8});
+  };
   std::vector<uint64_t>* kc[7] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
-  for (int c = 0; c < 7; ++c) {
-    kc[c]->resize(n);
-    hipMemcpyAsync(kc[c]->data(), A.k[c], n * 8, hipMemcpyDeviceToHost, s);
-  }
-  std::vector<uint64_t> ko(n), kl(n), vo(n), vl(n);
-  hipMemcpyAsync(ko.data(), A.kref_off, n * 8, hipMemcpyDeviceToHost, s);
-  hipMemcpyAsync(kl.data(), A.kref_len, n * 8, hipMemcpyDeviceToHost, s);
-  hipMemcpyAsync(vo.data(), A.vref_off, n * 8, hipMemcpyDeviceToHost, s);
-  hipMemcpyAsync(vl.data(), A.vref_len, n * 8, hipMemcpyDeviceToHost, s);
+  for (int c = 0; c < 7; ++c) down(kc[c], A.k[c], n);
+  std::vector<uint64_t> ko, kl, vo, vl;
+  down(&ko, A.kref_off, n);
+  down(&kl, A.kref_len, n);
+  down(&vo, A.vref_off, n);
+  down(&vl, A.vref_len, n);
   std::vector<uint64_t>* nc[6] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
   std::vector<uint64_t>* mc[6] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
   for (int c = 0; c < 6; ++c) {
-    nc[c]->resize(nn);
-    mc[c]->resize(nm);
-    if (nn) hipMemcpyAsync(nc[c]->data(), A.nd[c], nn * 8, hipMemcpyDeviceToHost, s);
-    if (nm) hipMemcpyAsync(mc[c]->data(), A.mb[c], nm * 8, hipMemcpyDeviceToHost, s);
+    down(nc[c], A.nd[c], nn);
+    down(mc[c], A.mb[c], nm);
   }
-  std::vector<uint64_t> mo(nm), ml(nm), mvo(nm), mvl(nm);
-  if (nm) {
-    hipMemcpyAsync(mo.data(), A.mref_off, nm * 8, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(ml.data(), A.mref_len, nm * 8, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(mvo.data(), A.mvref_off, nm * 8, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(mvl.data(), A.mvref_len, nm * 8, hipMemcpyDeviceToHost, s);
-  }
-  hipEventRecord(ev.b, s);
-  if (hipStreamSynchronize(s) != hipSuccess) return CDB_DEVICE_ERROR;
+  std::vector<uint64_t> mo, ml, mvo, mvl;
+  down(&mo, A.mref_off, nm);
+  down(&ml, A.mref_len, nm);
+  down(&mvo, A.mvref_off, nm);
+  down(&mvl, A.mvref_len, nm);
+  if ((st = staged_copy(ctx, segs.data(), segs.size(), false, s)) != CDB_OK) return st;
+  ck(hipEventRecord(ev.b, s), "event");
+  ck(hipStreamSynchronize(s), "sync(decode)");
+  if (st != CDB_OK) return st;
   if (tm) {
     float ms = 0;
     hipEventElapsedTime(&ms, ev.a, ev.b);
