@@ -74,7 +74,17 @@ struct EntryIndex {
   std::vector<uint8_t> kind;       // 0 DATAS, 1 EXPIRES, 2 DELETES (stream order)
   std::vector<uint64_t> children;  // raw child count: counter nodes or set/dict tags
 };
-int index_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, EntryIndex* idx, size_t* err_off);
+// The stream checksum, left for the GPU: CRC-64/Jones of raw[0, len) must equal `got`
+// (otherwise CDB_INVALID_SNAPSHOT_CHECKSUM at err_off).
+struct DeferredCrc {
+  bool pending = false;
+  uint64_t len = 0, got = 0;
+  size_t err_off = 0;
+};
+// With `crc` non-null and at least one entry indexed, the checksum is not computed here but
+// described in *crc for the caller to check.
+int index_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, EntryIndex* idx, size_t* err_off,
+                   DeferredCrc* crc = nullptr);
 struct DecodeTiming {
   double index_ms = 0;   // host pass
   double device_ms = 0;  // uploads, both kernels, downloads (HIP events)

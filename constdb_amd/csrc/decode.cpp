@@ -138,6 +138,7 @@ struct Decoder {
   Batch* b;
   const uint8_t* base;
   EntryIndex* idx = nullptr;  // index mode (GPU decode): validate and record, no rows
+  DeferredCrc* dcrc = nullptr;  // index mode: leave the checksum to the GPU
 
   bool str(std::string* s) {
     ByteRef r;
@@ -382,6 +383,21 @@ struct Decoder {
         else if (flag == 6) b->n_expires += cnt;
         else b->n_deletes += cnt;
       } else if (flag == 8) {  // SNAPSHOT_FLAG_CHECKSUM
+        const bool defer = dcrc && idx && !idx->offset.empty();
+        if (defer) {  // same prefix, value and error offset as below, checked by the caller
+          int64_t got;
+          if (flags & CDB_DECODE_REFERENCE_CHECKSUM) {
+            if (!c.integer(&got)) return fail();
+            *dcrc = DeferredCrc{true, (uint64_t)c.off, (uint64_t)got, c.off};
+            return CDB_OK;
+          }
+          if (!c.need(8)) return fail();
+          uint64_t w = 0;
+          for (int i = 7; i >= 0; --i) w = (w << 8) | base[c.off + i];
+          *dcrc = DeferredCrc{true, (uint64_t)c.off, w, c.off + 8};
+          c.off += 8;
+          return CDB_OK;
+        }
         const uint64_t crc = crc_tables().update(0, base, c.off);
         if (flags & CDB_DECODE_REFERENCE_CHECKSUM) {
           // snapshot.rs:207-213: read the checksum as a varint, CRC those bytes too
@@ -416,10 +432,12 @@ int decode_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, 
   return d.run(flags, err_off);
 }
 
-int index_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, EntryIndex* idx, size_t* err_off) {
+int index_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, EntryIndex* idx, size_t* err_off,
+                   DeferredCrc* crc) {
   out->raw.assign(buf, buf + len);
   Decoder d{Cursor{out->raw.data(), out->raw.size()}, out, out->raw.data()};
   d.idx = idx;
+  d.dcrc = crc;
   *err_off = 0;
   return d.run(flags, err_off);
 }

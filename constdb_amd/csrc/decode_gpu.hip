@@ -306,8 +306,9 @@ struct EvPair {
 int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off,
                         DecodeTiming* tm) {
   EntryIndex idx;
+  DeferredCrc dcrc;
   const auto t0 = std::chrono::steady_clock::now();
-  const int rc = index_snapshot(buf, len, flags, out, &idx, err_off);
+  int rc = index_snapshot(buf, len, flags, out, &idx, err_off, &dcrc);
   if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) return rc;
   const uint64_t n = idx.offset.size();
@@ -322,8 +323,12 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   // one device block: raw | off | kind | counts | offsets | key cols | refs | node cols | member cols
   std::vector<uint64_t> noff(n), moff(n);
   std::vector<uint32_t> ncnt(n), mcnt(n);
-  DevBuf d_raw, d_meta;
-  if (hipMalloc(&d_raw.p, len + 16) != hipSuccess) return CDB_OUT_OF_MEMORY;
+  DevBuf d_raw, d_meta, d_crc;
+  // the raw stream sits after `pad` zero bytes, so the checksummed prefix ends on a CRC tile
+  const uint64_t tile = crc_tile_bytes();
+  const uint64_t pad = dcrc.pending ? (tile - dcrc.len % tile) % tile : 0;
+  if (hipMalloc(&d_raw.p, pad + len + 16) != hipSuccess) return CDB_OUT_OF_MEMORY;
+  if (hipMalloc(&d_crc.p, 8) != hipSuccess) return CDB_OUT_OF_MEMORY;
   const size_t head = n * (8 + 1 + 4 + 4 + 8 + 8) + 64;
   if (hipMalloc(&d_meta.p, head) != hipSuccess) return CDB_OUT_OF_MEMORY;
   uint8_t* hm = (uint8_t*)d_meta.p;
@@ -335,13 +340,15 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   uint8_t* d_kind = (uint8_t*)(d_mcnt + n);
   EvPair ev;
   ck(hipEventRecord(ev.a, s), "event");
-  if (st == CDB_OK) st = staged_h2d(ctx, d_raw.p, out->raw.data(), len, s);
+  if (pad) ck(hipMemsetAsync(d_raw.p, 0, pad, s), "memset(decode)");
+  const uint8_t* raw_dev = (const uint8_t*)d_raw.p + pad;
+  if (st == CDB_OK) st = staged_h2d(ctx, (void*)raw_dev, out->raw.data(), len, s);
   if (st == CDB_OK) st = staged_h2d(ctx, d_off, idx.offset.data(), n * 8, s);
   ck(hipMemcpyAsync(d_kind, idx.kind.data(), n, hipMemcpyHostToDevice, s), "h2d(decode)");
   if (st != CDB_OK) return st;
   DecArgs A;
   std::memset(&A, 0, sizeof A);
-  A.raw = (const uint8_t*)d_raw.p;
+  A.raw = raw_dev;
   A.off = d_off;
   A.kind = d_kind;
   A.n = n;
@@ -354,6 +361,16 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   ck(hipMemcpyAsync(mcnt.data(), d_mcnt, n * 4, hipMemcpyDeviceToHost, s), "d2h(decode)");
   ck(hipStreamSynchronize(s), "sync(decode)");
   if (st != CDB_OK) return st;
+  if (dcrc.pending) {  // the index pass left the stream checksum to the GPU
+    uint64_t crc = 0;
+    if ((st = crc64_device(ctx, (const uint8_t*)d_raw.p, pad + dcrc.len, (uint64_t*)d_crc.p, s)) != CDB_OK) return st;
+    ck(hipMemcpy(&crc, d_crc.p, 8, hipMemcpyDeviceToHost), "d2h(crc)");
+    if (st != CDB_OK) return st;
+    if (crc != dcrc.got) {
+      rc = CDB_INVALID_SNAPSHOT_CHECKSUM;
+      *err_off = dcrc.err_off;
+    }
+  }
   // entries past the per-thread dedup limits: decoded here, into slots reserved by the scan
   struct HostEntry { uint64_t i; Batch rows; uint64_t total; };
   std::vector<HostEntry> hosted;

@@ -911,4 +911,11 @@ cdb_status encode_snapshot_impl(cdb_ctx* ctx, const cdb_merged& m, const cdb_enc
   return CDB_OK;
 }
 
+// CRC-64/Jones of a device buffer whose length is a multiple of crc_tile_bytes() (leading
+// zero bytes do not change it); the result lands in d_crc. Synchronises the stream.
+uint64_t crc_tile_bytes() { return kCrcTile; }
+cdb_status crc64_device(cdb_ctx* ctx, const uint8_t* dev, uint64_t padded, uint64_t* d_crc, hipStream_t s) {
+  return crc_device(ctx, dev, padded, nullptr, d_crc, s);
+}
+
 }  // namespace cdb

@@ -67,6 +67,8 @@ cdb_status staged_h2d(cdb_ctx* ctx, void* dev, const void* host, size_t bytes, h
 cdb_status staged_d2h(cdb_ctx* ctx, void* host, const void* dev, size_t bytes, hipStream_t s);
 // Asks for transparent huge pages on a fresh host buffer about to be filled by a download.
 void advise_huge(void* p, size_t bytes);
+uint64_t crc_tile_bytes();
+cdb_status crc64_device(cdb_ctx* ctx, const uint8_t* dev, uint64_t padded, uint64_t* d_crc, hipStream_t s);
 cdb_status stamp_pos(cdb_ctx* ctx, uint64_t* meta, uint64_t n, uint32_t pos, hipStream_t s);
 
 }  // namespace cdb

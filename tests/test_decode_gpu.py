@@ -129,6 +129,26 @@ def test_decode_gpu_errors_mirror_host(ctx):
     _same_batch(cdb.decode_snapshot(bytes(bad), allow_bad_checksum=True), b)
 
 
+def test_decode_gpu_checksum_modes_mirror_host(ctx):
+    """The GPU path checks the stream CRC on the device (the index pass defers it): outcome and
+    error offset equal the host decoder's in both checksum layouts, good and corrupted."""
+    s = gen_replicas(5, n_replicas=1)[0]
+    bad = bytearray(s)
+    bad[len(bad) // 3] ^= 0x01  # inside an entry's bytes: parses, CRC differs
+    for case in (s, bytes(bad)):
+        for ref in (False, True):
+            want = got = None
+            try:
+                cdb.decode_snapshot(case, reference_checksum=ref)
+            except cdb.CstError as e:
+                want = (type(e), getattr(e, "offset", None))
+            try:
+                cdb.decode_snapshot_gpu(ctx, case, reference_checksum=ref)
+            except cdb.CstError as e:
+                got = (type(e), getattr(e, "offset", None))
+            assert got == want, (ref, case is s)
+
+
 def test_decode_gpu_c4_replica_speed(ctx):
     """One C4-config replica snapshot of a 1M-key universe (~540K entries): identical batch;
     the host index pass and the device time are reported beside the host decoder's time."""
