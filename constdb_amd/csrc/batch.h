@@ -28,9 +28,11 @@ struct DefaultInitAlloc : std::allocator<T> {
 };
 using ColVec = std::vector<uint64_t, DefaultInitAlloc<uint64_t>>;
 
+
 struct ByteRef {  // a byte range inside Batch::raw
   uint64_t off, len;
 };
+using RefVec = std::vector<ByteRef, DefaultInitAlloc<ByteRef>>;
 
 struct ReplicaAdd { uint64_t add_time, node_id; std::string alias, addr; uint64_t uuid; uint32_t seq; };
 struct ReplicaDel { std::string addr; uint64_t t; uint32_t seq; };  // seq: order among the replica entries
@@ -40,16 +42,16 @@ struct Batch {
 
   // Key rows in stream order: DATAS entries, then EXPIRES, then DELETES (db.rs:122-136).
   // The GPU sees kh kf ct ut dt aux meta; key_ref/val_ref stay on the host.
-  std::vector<uint64_t> kh, kf, ct, ut, dt, aux, meta;
-  std::vector<ByteRef> key_ref, val_ref;
+  ColVec kh, kf, ct, ut, dt, aux, meta;
+  RefVec key_ref, val_ref;
   uint64_t n_data = 0, n_expires = 0, n_deletes = 0;
 
   // Counter children (type_counter.rs:21): pkh pkf node v t meta.
-  std::vector<uint64_t> n_pkh, n_pkf, n_node, n_v, n_t, n_meta;
+  ColVec n_pkh, n_pkf, n_node, n_v, n_t, n_meta;
 
   // Set/Dict member tags after load-time reconstruction: pkh pkf mh mf t meta (+ refs).
-  std::vector<uint64_t> m_pkh, m_pkf, m_h, m_f, m_t, m_meta;
-  std::vector<ByteRef> m_ref, m_vref;
+  ColVec m_pkh, m_pkf, m_h, m_f, m_t, m_meta;
+  RefVec m_ref, m_vref;
 
   // Node header and replica metadata (snapshot.rs:140-179).
   std::string version;

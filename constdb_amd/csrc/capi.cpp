@@ -254,10 +254,10 @@ cdb_status cdb_batch_info_get(const cdb_batch* cb, cdb_batch_info* info) {
 cdb_status cdb_batch_column(const cdb_batch* cb, int family, int col, const uint64_t** data, uint64_t* n) {
   if (!cb || !data || !n) return CDB_BAD_ARGUMENT;
   const Batch& b = *cb->b;
-  const std::vector<uint64_t>* k[] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
-  const std::vector<uint64_t>* nd[] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
-  const std::vector<uint64_t>* mb[] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
-  const std::vector<uint64_t>* v = nullptr;
+  const ColVec* k[] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
+  const ColVec* nd[] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
+  const ColVec* mb[] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
+  const ColVec* v = nullptr;
   if (family == 0 && col >= 0 && col < kKeyCols) v = k[col];
   else if (family == 1 && col >= 0 && col < kNodeCols) v = nd[col];
   else if (family == 2 && col >= 0 && col < kMemberCols) v = mb[col];
@@ -310,16 +310,16 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, const c
       (st = block(WS_HOST_OUT_M, kMemberCols, M, &dout.members)) != CDB_OK)
     return st;
   std::vector<HostSeg> segs;
-  auto put = [&](const cdb_dev_rows& r, int c, uint64_t off, const std::vector<uint64_t>& v) {
+  auto put = [&](const cdb_dev_rows& r, int c, uint64_t off, const ColVec& v) {
     if (!v.empty()) segs.push_back({const_cast<uint64_t*>(v.data()), r.col[c] + off, v.size() * 8});
   };
   uint64_t ok = 0, on = 0, om = 0;
   for (uint32_t i = 0; i < n; ++i) {
     const Batch& b = *inputs[i]->b;
     const cdb_dev_rows &rk = din.keys, &rn = din.nodes, &rm = din.members;
-    const std::vector<uint64_t>* kc[kKeyCols] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
-    const std::vector<uint64_t>* nc[kNodeCols] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
-    const std::vector<uint64_t>* mc[kMemberCols] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
+    const ColVec* kc[kKeyCols] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
+    const ColVec* nc[kNodeCols] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
+    const ColVec* mc[kMemberCols] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
     for (int c = 0; c < kKeyCols; ++c) put(rk, c, ok, *kc[c]);
     for (int c = 0; c < kNodeCols; ++c) put(rn, c, on, *nc[c]);
     for (int c = 0; c < kMemberCols; ++c) put(rm, c, om, *mc[c]);

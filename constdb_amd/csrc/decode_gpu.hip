@@ -430,24 +430,25 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   // rows back into the host batch: one staged download of every column
   Batch& b = *out;
   std::vector<HostSeg> segs;
-  auto down = [&](std::vector<uint64_t>* v, const uint64_t* dev, uint64_t rows) {
-    v->resize(rows);
+  auto down = [&](ColVec* v, const uint64_t* dev, uint64_t rows) {
+    v->resize(rows);  // default-initialised: the download overwrites every word
+    advise_huge(v->data(), rows * 8);
     if (rows) segs.push_back({v->data(), const_cast<uint64_t*>(dev), rows * 8});
   };
-  std::vector<uint64_t>* kc[7] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
+  ColVec* kc[7] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
   for (int c = 0; c < 7; ++c) down(kc[c], A.k[c], n);
-  std::vector<uint64_t> ko, kl, vo, vl;
+  ColVec ko, kl, vo, vl;
   down(&ko, A.kref_off, n);
   down(&kl, A.kref_len, n);
   down(&vo, A.vref_off, n);
   down(&vl, A.vref_len, n);
-  std::vector<uint64_t>* nc[6] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
-  std::vector<uint64_t>* mc[6] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
+  ColVec* nc[6] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
+  ColVec* mc[6] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
   for (int c = 0; c < 6; ++c) {
     down(nc[c], A.nd[c], nn);
     down(mc[c], A.mb[c], nm);
   }
-  std::vector<uint64_t> mo, ml, mvo, mvl;
+  ColVec mo, ml, mvo, mvl;
   down(&mo, A.mref_off, nm);
   down(&ml, A.mref_len, nm);
   down(&mvo, A.mvref_off, nm);

@@ -668,7 +668,7 @@ cdb_status apply_ops_impl(cdb_ctx* ctx, const ColVec* sk, const ColVec* sn, cons
   for (int c = 0; c < kKeyOutCols; ++c) OPS_TRY(up(sk[c], &sk_d[c]));
   for (int c = 0; c < kNodeCols; ++c) OPS_TRY(up(sn[c], &sn_d[c]));
   for (int c = 0; c < kMemberCols; ++c) OPS_TRY(up(sm[c], &sm_d[c]));
-  std::vector<uint64_t> ometa(B.meta);
+  ColVec ometa(B.meta);
   for (auto& m : ometa) m = meta_pack(meta_tag(m), pos_ops, meta_src(m));
   uint64_t *o_kh, *o_kf, *o_uuid, *o_meta, *n_node, *n_v, *n_op, *m_h, *m_f, *m_op;
   OPS_TRY(up(B.kh, &o_kh));
