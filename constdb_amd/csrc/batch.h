@@ -38,7 +38,7 @@ struct ReplicaAdd { uint64_t add_time, node_id; std::string alias, addr; uint64_
 struct ReplicaDel { std::string addr; uint64_t t; uint32_t seq; };  // seq: order among the replica entries
 
 struct Batch {
-  std::vector<uint8_t> raw;  // the snapshot bytes: arena for keys, values, members
+  std::vector<uint8_t, DefaultInitAlloc<uint8_t>> raw;  // the snapshot bytes: arena for keys, values, members
 
   // Key rows in stream order: DATAS entries, then EXPIRES, then DELETES (db.rs:122-136).
   // The GPU sees kh kf ct ut dt aux meta; key_ref/val_ref stay on the host.
@@ -64,6 +64,11 @@ struct Batch {
   uint64_t n_nodes() const { return n_pkh.size(); }
   uint64_t n_members() const { return m_pkh.size(); }
 };
+
+// Copies a large host buffer with the staging ring's copy threads (capi.cpp).
+void parallel_copy(void* dst, const void* src, size_t bytes);
+// Fills b->raw with the caller's snapshot bytes (uninitialised storage, huge pages, parallel copy).
+void adopt_raw(Batch* b, const uint8_t* buf, size_t len);
 
 // Decoder (decode.cpp). Returns a cdb_status value.
 int decode_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off);

@@ -4,6 +4,7 @@
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -95,6 +96,24 @@ void advise_huge(void* p, size_t bytes) {
   const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + kHuge - 1) & ~(kHuge - 1);
   const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(kHuge - 1);
   if (b > a) madvise(reinterpret_cast<void*>(a), b - a, MADV_HUGEPAGE);
+}
+
+void parallel_copy(void* dst, const void* src, size_t bytes) {
+  // callers that already decode in parallel (one thread per snapshot) copy on their own thread
+  static std::atomic<int> active{0};
+  if (bytes < (size_t(8) << 20) || active.fetch_add(1) > 0) {
+    if (bytes >= (size_t(8) << 20)) active.fetch_sub(1);
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  par_copy({Piece{static_cast<char*>(dst), const_cast<char*>(static_cast<const char*>(src)), nullptr, bytes}}, false);
+  active.fetch_sub(1);
+}
+
+void adopt_raw(Batch* b, const uint8_t* buf, size_t len) {
+  b->raw.resize(len);  // default-initialised
+  advise_huge(b->raw.data(), len);
+  parallel_copy(b->raw.data(), buf, len);
 }
 
 cdb_status staged_h2d(cdb_ctx* ctx, void* dev, const void* host, size_t bytes, hipStream_t s) {

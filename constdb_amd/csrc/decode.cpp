@@ -426,7 +426,7 @@ struct Decoder {
 }  // namespace
 
 int decode_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off) {
-  out->raw.assign(buf, buf + len);
+  adopt_raw(out, buf, len);
   Decoder d{Cursor{out->raw.data(), out->raw.size()}, out, out->raw.data()};
   *err_off = 0;
   return d.run(flags, err_off);
@@ -434,7 +434,7 @@ int decode_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, 
 
 int index_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, EntryIndex* idx, size_t* err_off,
                    DeferredCrc* crc) {
-  out->raw.assign(buf, buf + len);
+  adopt_raw(out, buf, len);
   Decoder d{Cursor{out->raw.data(), out->raw.size()}, out, out->raw.data()};
   d.idx = idx;
   d.dcrc = crc;

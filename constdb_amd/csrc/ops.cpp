@@ -182,7 +182,7 @@ bool name_is(const uint8_t* raw, const ByteRef& r, const char* lower) {
 int decode_ops(const uint8_t* buf, size_t len, uint64_t uuid_he_sent, Batch* out, cdb_ops_info* info,
                size_t* err_off) {
   Batch& b = *out;
-  b.raw.assign(buf, buf + len);
+  adopt_raw(&b, buf, len);
   cdb_ops_info& st = *info;
   std::memset(&st, 0, sizeof st);
   st.uuid_he_sent = uuid_he_sent;
