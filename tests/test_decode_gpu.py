@@ -167,3 +167,15 @@ def test_decode_gpu_c4_replica_speed(ctx):
     _same_batch(host, g)
     print(f"\ndecode {len(snap) / 1e6:.1f} MB: host {t_host:.1f} ms; gpu path {t_gpu:.1f} ms "
           f"(index {tm['index_ms']:.1f} ms, device {tm['device_ms']:.1f} ms)")
+
+
+def test_decode_gpu_staging_ring_wraps(ctx):
+    """A ~125 MB snapshot: the upload and the row download each span several 32 MB slots of the
+    context's pinned staging ring, which wraps; the batch equals the host decoder's, twice in a
+    row on one context (the ring continues across calls)."""
+    cfg = cdb.gen_config(seed=11, universe=4_000_000, n_replicas=8, replica_hi=8)
+    snap = cdb.gen_snapshot(cfg, 3)
+    assert len(snap) > 4 * (32 << 20) // 2
+    host = cdb.decode_snapshot(snap)
+    for _ in range(2):
+        _same_batch(host, cdb.decode_snapshot_gpu(ctx, snap))
