@@ -79,7 +79,6 @@ int decode_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, 
 struct EntryIndex {
   std::vector<uint64_t> offset;    // byte offset of the entry (its key's length varint)
   std::vector<uint8_t> kind;       // 0 DATAS, 1 EXPIRES, 2 DELETES (stream order)
-  std::vector<uint64_t> children;  // raw child count: counter nodes or set/dict tags
 };
 // The stream checksum, left for the GPU: CRC-64/Jones of raw[0, len) must equal `got`
 // (otherwise CDB_INVALID_SNAPSHOT_CHECKSUM at err_off).

@@ -162,7 +162,6 @@ struct Decoder {
         int64_t v;
         if (!c.u64(&x) || !c.integer(&v) || !c.u64(&x)) return false;
       }
-      idx->children.back() = cnt;
       return true;
     }
     struct N { uint64_t node, v, t; };
@@ -218,7 +217,6 @@ struct Decoder {
       if (!c.length(&nd)) return false;
       for (uint64_t i = 0; i < nd; ++i)
         if (!c.span(&r) || !c.u64(&t)) return false;
-      idx->children.back() = na + nd;
       return true;
     }
     ops.reserve(na);
@@ -286,7 +284,6 @@ struct Decoder {
     if (idx) {
       idx->offset.push_back(c.off);
       idx->kind.push_back(0);
-      idx->children.push_back(0);
     }
     ByteRef k;
     if (!c.span(&k)) return false;
@@ -334,7 +331,6 @@ struct Decoder {
     if (idx) {
       idx->offset.push_back(c.off);
       idx->kind.push_back(tag == TAG_EXPIRE ? 1 : 2);
-      idx->children.push_back(0);
     }
     ByteRef k;
     uint64_t t;
@@ -438,6 +434,8 @@ int index_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, E
   Decoder d{Cursor{out->raw.data(), out->raw.size()}, out, out->raw.data()};
   d.idx = idx;
   d.dcrc = crc;
+  idx->offset.reserve(len / 48 + 16);  // generator-shaped streams run ~58 bytes per entry
+  idx->kind.reserve(len / 48 + 16);
   *err_off = 0;
   return d.run(flags, err_off);
 }
