@@ -2,15 +2,19 @@
 """Benchmark: ConstDB snapshot merge on MI355X (BASELINE.json metric:
 "merged CRDT entries/sec + achieved HBM GB/s, snapshot merge at 1/2/4/8 GPUs").
 
-One step = one full merge of R=8 replica snapshots already resident in HBM as columnar
-rows (anti-entropy): bucket partition -> fused bucket merge ->
-dense compaction, i.e. everything DB::merge_entry/Object::merge would do for those
-entries. Weak scaling: every GPU owns a fixed 1/8-of-C4 key universe (62.5M keys); at
-N=8 the job is exactly C4 (500M keys x 8 replicas). For N>1 replica r lives on GPU
-r*N/8 and rows are routed to the GPU owning their key hash by an RCCL all-to-all
-(torch.distributed "nccl" backend) inside the timed step.
+One step = one full merge of R replica states already resident in HBM as columnar rows:
+bucket partition -> fused bucket merge -> dense compaction, i.e. everything
+DB::merge_entry / Object::merge / DB::delete / DB::expire_at (and DB::gc for C3) would do for
+those entries. Configs (constdb_amd/configs.py):
+  c4 (default)  8-replica anti-entropy. Weak scaling: every GPU owns a 62.5M-key universe; at
+                N=8 the job is exactly C4 (500M keys x 8 replicas). For N>1 replica r lives on
+                GPU r*N/8 and rows go to the GPU owning their key hash by an RCCL all-to-all
+                (torch.distributed "nccl") inside the timed step.
+  c1            2-node MEET, 1M Bytes + 1M counters per node, 50 % overlap (C1/C2).
+  c3            4 replicas built by replaying 10M sadd/srem/hset/hdel each, merge + DB::gc.
+  c5            Zipf hot keys: 10M keys, 80M node/member rows over 8 replicas.
 
-Prints ONE JSON line (rank 0).
+Prints ONE JSON line (rank 0) per config run.
 """
 import argparse
 import ctypes
@@ -25,6 +29,10 @@ sys.path.insert(0, ROOT)
 # SURVEY.md §8d algorithmic row widths (bytes): compulsory read + write per row
 W_KEY, W_NODE, W_SET, W_DICT = 50, 33, 34, 42
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
+# the merge pipeline's kernels (everything cdb_merge_device launches; not the generator)
+MERGE_KERNEL_PREFIXES = ("part_", "bucket_", "compact", "scan_", "stats_reduce", "gc_lastbad", "set_dir",
+                         "stamp_pos", "iota", "hot_", "sorted_", "seg_")
 
 
 def parse():
@@ -32,60 +40,213 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c4", choices=["c1", "c3", "c4", "c5"])
     ap.add_argument("--universe-per-gpu", type=int, default=62_500_000)
     ap.add_argument("--replicas", type=int, default=8)
     ap.add_argument("--seed", type=int, default=4)
-    ap.add_argument("--cpu-universe", type=int, default=1_000_000,
-                    help="key universe of the bounded CPU-baseline sample (same generator config)")
+    ap.add_argument("--cpu-universe", type=int, default=2_000_000,
+                    help="key universe of the bounded C4 CPU-baseline sample (same generator config)")
+    ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the multi-GPU (RCCL all-to-all) path even when WORLD_SIZE == 1")
+    ap.add_argument("--c3-ops", type=int, default=10_000_000, help="ops per replica of config c3")
     return ap.parse_args()
 
 
 def c4_config(cdb, universe, replicas, seed, lo, hi, shard=0, n_shards=1):
-    # C4: type mix 60/30/5/5, counters 1-8 nodes (mean 2), sets/dicts mean 4 members,
-    # 0.1 % cross-replica type conflicts, ~2 % forced time ties, p(key in replica) = 0.5
-    return cdb.gen_config(seed=seed, universe=universe, n_replicas=replicas, key_permille=500,
-                          mix_bytes=60, mix_counter=30, mix_set=5, mix_dict=5, conflict_ppm=1000,
-                          tie_permille=20, max_nodes=8, mean_members=4, member_universe=16,
-                          del_permille=200, side_permille=20, value_min=8, value_max=32,
-                          shard=shard, n_shards=n_shards, replica_lo=lo, replica_hi=hi)
+    from constdb_amd import configs
+    return configs.c4(cdb, universe, replicas, seed, lo, hi, shard, n_shards)
 
 
-def alg_bytes(st, set_frac=0.5):
+def alg_bytes(st, dict_share=0.5):
     """Compulsory bytes of one merge: inputs + outputs at the survey's row
-    widths. Member rows are priced half set (34 B) half dict (42 B) as in C4's 5/5 mix."""
-    wm = set_frac * W_SET + (1 - set_frac) * W_DICT
+    widths (member rows priced at the config's set/dict share)."""
+    wm = (1 - dict_share) * W_SET + dict_share * W_DICT
     return ((st.key_rows_in + st.key_rows_out) * W_KEY + (st.node_rows_in + st.node_rows_out) * W_NODE
             + (st.member_rows_in + st.member_rows_out) * wm)
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the bucket phase, from the committed rocprofv3 FETCH_SIZE /
-    WRITE_SIZE passes of this same bench command (scripts/gpu_round.sh -> pmc_traffic.py);
-    None when no such measurement is committed."""
-    f = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+def pmc_traffic(config):
+    """HBM bytes per merge step, from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes of
+    this same bench command (scripts/gpu_round.sh -> scripts/pmc_traffic.py): every merge-pipeline
+    kernel, and the bucket phase alone. None when no such measurement is committed."""
+    f = os.path.join(PROFILE_DIR, f"pmc_traffic_{config}.json")
     try:
         with open(f) as fh:
-            return float(json.load(fh)["bucket_phase_bytes"])
-    except (OSError, KeyError, ValueError):
+            d = json.load(fh)
+    except (OSError, ValueError):
         return None
+    total = bucket = 0.0
+    per = {}
+    for k, v in d.get("kernels", {}).items():
+        if not k.startswith(MERGE_KERNEL_PREFIXES):
+            continue
+        b = (v["fetch_bytes"] + v["write_bytes"]) * v.get("per_step", 1)
+        per[k] = b
+        total += b
+        if k.startswith("bucket_"):
+            bucket += b
+    return {"total": total, "bucket_phase": bucket, "per_kernel": per, "source": os.path.relpath(f, ROOT)}
 
 
-def cpu_baseline(cdb, args):
+def host_info():
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "host_cpus": os.cpu_count()}
+
+
+def cpu_baseline(cdb, args, snaps, sample):
     """The oracle's single-thread C++ fold (kind "port": the Rust reference cannot be built
-    here) on a bounded sample of the same generator config; decode is excluded."""
+    here) over already-decoded entries, best of --cpu-reps; decode excluded."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cdb_oracle
-    cfg = c4_config(cdb, args.cpu_universe, args.replicas, args.seed, 0, args.replicas)
-    snaps = [cdb.gen_snapshot(cfg, r) for r in range(args.replicas)]
-    ns, entries = cdb_oracle.time_fold(snaps, reps=2)
-    return {"value": entries / (ns * 1e-9), "unit": "entries/s", "cores": 1, "kind": "port",
-            "sample": f"C4 generator config, {args.cpu_universe} keys x {args.replicas} replicas "
-                      f"({entries} entries, decode excluded, best of 2), oracle/cdb_oracle.cpp "
-                      f"std::unordered_map fold",
-            "host_cpus": os.cpu_count()}
+    ns, entries = cdb_oracle.time_fold(snaps, reps=args.cpu_reps)
+    out = {"value": entries / (ns * 1e-9), "unit": "entries/s", "cores": 1, "kind": "port",
+           "sample": f"{sample} ({entries} entries, decode excluded, best of {args.cpu_reps}), "
+                     f"oracle/cdb_oracle.cpp std::unordered_map fold",
+           **host_info()}
+    ref = os.path.join(PROFILE_DIR, f"cpu_baseline_{args.config}_10m.json")
+    if os.path.exists(ref):
+        with open(ref) as fh:
+            out["larger_sample"] = json.load(fh)
+    return out
+
+
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def setup(cdb, ctx, args):
+    """Device-resident inputs of the chosen config. Returns (din, opts, info) where info holds
+    the workload description and a callable producing the CPU-baseline sample."""
+    from constdb_amd import configs
+    L = cdb.lib()
+    din = cdb.DevInput()
+    opts = cdb.MergeOpts()
+    c = args.config
+    if c == "c4":
+        cfg = configs.c4(cdb, args.universe_per_gpu, args.replicas, args.seed)
+        ctx.check(L.cdb_gen_device(ctx.handle, ctypes.byref(cfg), ctypes.byref(din)))
+        work = (f"C4 anti-entropy shard: {args.universe_per_gpu} keys/GPU x {args.replicas} replicas "
+                f"(N=8 -> exactly C4's 500M keys)")
+
+        def sample():
+            scfg = configs.c4(cdb, args.cpu_universe, args.replicas, args.seed)
+            return ([cdb.gen_snapshot(scfg, r) for r in range(args.replicas)],
+                    f"C4 generator config, {args.cpu_universe} keys x {args.replicas} replicas")
+    elif c == "c1":
+        cfg = configs.c1(cdb)
+        ctx.check(L.cdb_gen_device(ctx.handle, ctypes.byref(cfg), ctypes.byref(din)))
+        work = "C1/C2 2-node MEET: 1M Bytes + 1M counters per node, 50 % key overlap, B merged into A"
+
+        def sample():
+            return [cdb.gen_snapshot(cfg, r) for r in range(2)], "C1 at full size"
+    elif c == "c5":
+        cfg = configs.c5(cdb)
+        ctx.check(L.cdb_gen_device(ctx.handle, ctypes.byref(cfg), ctypes.byref(din)))
+        work = "C5 Zipf hot keys: 10M keys, children ~ rank^-1.1, 80M node/member rows over 8 replicas"
+
+        def sample():
+            scfg = configs.c5(cdb, universe=1_000_000, events=8_000_000)
+            return [cdb.gen_snapshot(scfg, r) for r in range(8)], "C5 generator at 1M keys / 8M children"
+    else:  # c3
+        log("building C3 replica states through the device op apply")
+        snaps = configs.c3_snapshots(cdb, ctx, ops_per_replica=args.c3_ops, log=log)
+        batches = [cdb.decode_snapshot(s) for s in snaps]
+        arr = (ctypes.c_void_p * len(batches))(*[b.handle for b in batches])
+        ctx.check(L.cdb_upload_batches(ctx.handle, arr, len(batches), ctypes.byref(din)))
+        opts.flags = cdb.MERGE_GC_DELETES
+        opts.gc_watermark = configs.median_member_time(cdb, batches)
+        work = (f"C3 set/dict add-win merge: 4 replicas x {args.c3_ops} sadd/srem/hset/hdel replayed over "
+                f"100K keys (Zipf members), merge + DB::gc at the median member time")
+
+        def sample():
+            return snaps, "C3 at full size (the same 4 snapshots)"
+    return din, opts, {"workload": work, "sample": sample}
+
+
+def run_single(cdb, args):
+    ctx = cdb.Context(0)
+    L = cdb.lib()
+    din, opts, info = setup(cdb, ctx, args)
+    dout = cdb.DevOutput()
+    ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.keys), din.keys.n, 8))
+    ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.nodes), din.nodes.n, 6))
+    ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.members), din.members.n, 6))
+    dout.compact = 1
+    st = cdb.MergeStats()
+
+    def step():
+        ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(din), ctypes.byref(opts), ctypes.byref(dout),
+                                     ctypes.byref(st), None))
+
+    for _ in range(args.warmup):
+        step()
+    acc = dict(partition=0.0, bucket=0.0, finish=0.0, device=0.0)
+    t0 = time.perf_counter()  # cdb_merge_device synchronises its stream before returning
+    for _ in range(args.steps):
+        step()
+        acc["bucket"] += st.bucket_ms
+        acc["partition"] += st.partition_ms
+        acc["finish"] += st.finish_ms
+        acc["device"] += st.device_ms
+    t1 = time.perf_counter()
+    ms = (t1 - t0) * 1e3 / args.steps
+    per = {k: v / args.steps for k, v in acc.items()}
+    from constdb_amd import configs
+    B = alg_bytes(st, configs.DICT_MEMBER_SHARE[args.config])
+    tr = pmc_traffic(args.config)
+    res = {
+        "metric": "merged CRDT entries/sec (snapshot merge)",
+        "value": st.key_rows_in / (ms * 1e-3),
+        "unit": "entries/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic: seeded GenModel replica states resident in HBM (keys 'key:<i>')",
+        "config": {"workload": info["workload"], "config": args.config, "replicas": din.n_pos,
+                   "key_rows_in": st.key_rows_in, "node_rows_in": st.node_rows_in,
+                   "member_rows_in": st.member_rows_in, "key_rows_out": st.key_rows_out,
+                   "node_rows_out": st.node_rows_out, "member_rows_out": st.member_rows_out,
+                   "gc_watermark": opts.gc_watermark, "parallelism": "single GPU"},
+        "child_rows_per_s": (st.node_rows_in + st.member_rows_in) / (ms * 1e-3),
+        "phases_ms": {"partition": per["partition"], "bucket_merge": per["bucket"], "finish": per["finish"],
+                      "device_total": per["device"]},
+        # SURVEY §8d: achieved = B_alg / t_merge over the WHOLE merge (HIP events on the merge
+        # stream around partition -> bucket merge -> compaction)
+        "roofline": {"bound": "hbm",
+                     "kernel": "whole merge pipeline (partition + bucket merge + compaction), HIP events",
+                     "achieved": B / (per["device"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": B / (per["device"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "alg_bytes": B,
+                     "traffic": tr["total"] if tr else None,
+                     "traffic_over_alg": tr["total"] / B if tr else None,
+                     "traffic_source": tr["source"] if tr else None,
+                     "phase_frac": {"bucket_merge": B / (per["bucket"] * 1e-3) / 1e9 / HBM_PEAK_GBS}},
+        "stats": {"type_conflicts": st.type_conflicts, "dict_merges": st.dict_merges,
+                  "deletes_gced": st.deletes_gced, "hot_buckets": st.hot_buckets,
+                  "wide_buckets": st.wide_buckets, "mid_buckets": st.mid_buckets,
+                  "orphans": st.orphan_children},
+    }
+    if tr:
+        res["roofline"]["traffic_per_kernel"] = tr["per_kernel"]
+    for fam in (dout.keys, dout.nodes, dout.members, din.keys, din.nodes, din.members):
+        L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
+    res["_sample"] = info["sample"]
+    return res
 
 
 def main():
@@ -104,85 +265,24 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1 or args.force_dist:
+        if args.config != "c4":
+            raise SystemExit("the multi-GPU bench runs config c4")
         from constdb_amd import dist
         res = dist.run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes)
+        sample = None
     else:
         res = run_single(cdb, args)
+        sample = res.pop("_sample")
     if rank != 0:
         os.close(json_fd)
         return
-    if not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(cdb, args)
+    if not args.no_cpu_baseline and sample is not None:
+        snaps, desc = sample()
+        res["cpu_baseline"] = cpu_baseline(cdb, args, snaps, desc)
+    elif not args.no_cpu_baseline and world > 1:
+        pass  # rank 0 at N=1 only (the driver's N=1 line carries it)
     with os.fdopen(json_fd, "w") as out:
         out.write(json.dumps(res) + "\n")
-
-
-def run_single(cdb, args):
-    ctx = cdb.Context(0)
-    L = cdb.lib()
-    cfg = c4_config(cdb, args.universe_per_gpu, args.replicas, args.seed, 0, args.replicas)
-    din = cdb.DevInput()
-    ctx.check(L.cdb_gen_device(ctx.handle, ctypes.byref(cfg), ctypes.byref(din)))
-    dout = cdb.DevOutput()
-    ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.keys), din.keys.n, 8))
-    ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.nodes), din.nodes.n, 6))
-    ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.members), din.members.n, 6))
-    dout.compact = 1
-    opts = cdb.MergeOpts()
-    st = cdb.MergeStats()
-
-    def step():
-        ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(din), ctypes.byref(opts), ctypes.byref(dout),
-                                     ctypes.byref(st), None))
-
-    for _ in range(args.warmup):
-        step()
-    bucket_ms = part_ms = fin_ms = dev_ms = 0.0
-    t0 = time.perf_counter()  # cdb_merge_device synchronises its stream before returning
-    for _ in range(args.steps):
-        step()
-        bucket_ms += st.bucket_ms
-        part_ms += st.partition_ms
-        fin_ms += st.finish_ms
-        dev_ms += st.device_ms
-    t1 = time.perf_counter()
-    ms = (t1 - t0) * 1e3 / args.steps
-    entries = st.key_rows_in
-    B = alg_bytes(st)
-    bk = bucket_ms / args.steps
-    res = {
-        "metric": "merged CRDT entries/sec (snapshot merge)",
-        "value": entries / (ms * 1e-3),
-        "unit": "entries/s",
-        "n_gpus": 1,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": ms,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u64",
-        "data": "synthetic: seeded GenModel replica states generated in HBM (keys 'key:<i>')",
-        "config": {"workload": f"C4 anti-entropy shard: {args.universe_per_gpu} keys/GPU x {args.replicas} "
-                               f"replicas (N=8 -> exactly C4's 500M keys)",
-                   "replicas": args.replicas, "key_rows_in": st.key_rows_in, "node_rows_in": st.node_rows_in,
-                   "member_rows_in": st.member_rows_in, "key_rows_out": st.key_rows_out,
-                   "parallelism": "single GPU"},
-        "hbm_gbs_alg": B / (ms * 1e-3) / 1e9,
-        "phases_ms": {"partition": part_ms / args.steps, "bucket_merge": bk, "finish": fin_ms / args.steps,
-                      "device_total": dev_ms / args.steps},
-        "roofline": {"bound": "hbm",
-                     "kernel": "bucket phase = bucket_wave_kernel + bucket_wide_kernel + bucket_mid_kernel",
-                     "achieved": B / (bk * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": B / (bk * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "alg_bytes": B, "traffic": pmc_traffic()},
-        "stats": {"type_conflicts": st.type_conflicts, "dict_merges": st.dict_merges,
-                  "hot_buckets": st.hot_buckets, "wide_buckets": st.wide_buckets,
-                  "mid_buckets": st.mid_buckets, "orphans": st.orphan_children},
-    }
-    for fam in (dout.keys, dout.nodes, dout.members, din.keys, din.nodes, din.members):
-        L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
-    return res
 
 
 if __name__ == "__main__":

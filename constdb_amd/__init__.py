@@ -38,6 +38,10 @@ MERGE_STRICT_DICT_PANIC = 1
 MERGE_GC_DELETES = 2
 MERGE_GC_MEMBERS = 4
 
+GEN_NODE_PER_REPLICA = 1
+GEN_OPS_ZIPF_MEMBERS = 2
+GEN_OPS_TAGS_ONLY = 4
+
 
 class CstError(Exception):
     status = -1
@@ -181,7 +185,8 @@ class GenConfig(ctypes.Structure):
     _fields_ = [("seed", ctypes.c_uint64), ("universe", ctypes.c_uint64)] + [(n, ctypes.c_uint32) for n in (
         "n_replicas", "key_permille", "mix_bytes", "mix_counter", "mix_set", "mix_dict", "conflict_ppm",
         "tie_permille", "max_nodes", "mean_members", "member_universe", "del_permille", "side_permille",
-        "value_min", "value_max", "shard", "n_shards", "replica_lo", "replica_hi")]
+        "value_min", "value_max", "shard", "n_shards", "replica_lo", "replica_hi", "flags", "hot_zipf_milli",
+        "reserved")] + [("hot_events", ctypes.c_uint64)]
 
 
 # exported C-ABI function names (tests check the .so exports every one of them)
@@ -192,7 +197,7 @@ ABI_FUNCTIONS = (
     "cdb_merged_free", "cdb_free",
     "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_partition_owner", "cdb_gen_default",
     "cdb_gen_snapshot", "cdb_gen_device", "cdb_decode_ops", "cdb_ops_info_get", "cdb_ops_free", "cdb_apply_ops", "cdb_gen_ops",
-    "cdb_encode_snapshot", "cdb_crc64_gpu")
+    "cdb_encode_snapshot", "cdb_crc64_gpu", "cdb_upload_batches")
 
 _lib = None
 
@@ -246,6 +251,7 @@ def lib():
         "cdb_apply_ops": (c_st, [vp, vp, vp, P(vp), P(ApplyStats)]),
         "cdb_encode_snapshot": (c_st, [vp, vp, P(EncodeHeader), P(vp), P(ctypes.c_size_t), P(EncodeStats)]),
         "cdb_crc64_gpu": (c_st, [vp, ctypes.c_char_p, ctypes.c_size_t, P(ctypes.c_uint64)]),
+        "cdb_upload_batches": (c_st, [vp, P(vp), ctypes.c_uint32, P(DevInput)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

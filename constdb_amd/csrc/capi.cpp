@@ -220,6 +220,42 @@ std::string hex(const uint8_t* p, uint64_t n) {
 
 }  // namespace
 
+// Copies batches [0, n) into the device columns of `din` (sized for their sum, batch i's rows
+// after batch i-1's) through the pinned staging ring and stamps fold position i into batch i's
+// meta words on the device.
+static cdb_status upload_batches(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, cdb_dev_input* din) {
+  std::vector<HostSeg> segs;
+  auto put = [&](const cdb_dev_rows& r, int c, uint64_t off, const ColVec& v) {
+    if (!v.empty()) segs.push_back({const_cast<uint64_t*>(v.data()), r.col[c] + off, v.size() * 8});
+  };
+  uint64_t ok = 0, on = 0, om = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const Batch& b = *inputs[i]->b;
+    const ColVec* kc[kKeyCols] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
+    const ColVec* nc[kNodeCols] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
+    const ColVec* mc[kMemberCols] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
+    for (int c = 0; c < kKeyCols; ++c) put(din->keys, c, ok, *kc[c]);
+    for (int c = 0; c < kNodeCols; ++c) put(din->nodes, c, on, *nc[c]);
+    for (int c = 0; c < kMemberCols; ++c) put(din->members, c, om, *mc[c]);
+    ok += b.n_keys();
+    on += b.n_nodes();
+    om += b.n_members();
+  }
+  cdb_status st = staged_copy(ctx, segs.data(), segs.size(), true, ctx->stream);
+  ok = on = om = 0;
+  for (uint32_t i = 0; i < n && st == CDB_OK; ++i) {
+    const Batch& b = *inputs[i]->b;
+    if ((st = stamp_pos(ctx, din->keys.col[K_META] + ok, b.n_keys(), i, ctx->stream)) != CDB_OK ||
+        (st = stamp_pos(ctx, din->nodes.col[C_META] + on, b.n_nodes(), i, ctx->stream)) != CDB_OK ||
+        (st = stamp_pos(ctx, din->members.col[C_META] + om, b.n_members(), i, ctx->stream)) != CDB_OK)
+      break;
+    ok += b.n_keys();
+    on += b.n_nodes();
+    om += b.n_members();
+  }
+  return st;
+}
+
 extern "C" {
 
 cdb_status cdb_decode_snapshot(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags, cdb_batch** out,
@@ -328,37 +364,7 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, const c
       (st = block(WS_HOST_OUT_N, kNodeCols, N, &dout.nodes)) != CDB_OK ||
       (st = block(WS_HOST_OUT_M, kMemberCols, M, &dout.members)) != CDB_OK)
     return st;
-  std::vector<HostSeg> segs;
-  auto put = [&](const cdb_dev_rows& r, int c, uint64_t off, const ColVec& v) {
-    if (!v.empty()) segs.push_back({const_cast<uint64_t*>(v.data()), r.col[c] + off, v.size() * 8});
-  };
-  uint64_t ok = 0, on = 0, om = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    const Batch& b = *inputs[i]->b;
-    const cdb_dev_rows &rk = din.keys, &rn = din.nodes, &rm = din.members;
-    const ColVec* kc[kKeyCols] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
-    const ColVec* nc[kNodeCols] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
-    const ColVec* mc[kMemberCols] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
-    for (int c = 0; c < kKeyCols; ++c) put(rk, c, ok, *kc[c]);
-    for (int c = 0; c < kNodeCols; ++c) put(rn, c, on, *nc[c]);
-    for (int c = 0; c < kMemberCols; ++c) put(rm, c, om, *mc[c]);
-    ok += b.n_keys();
-    on += b.n_nodes();
-    om += b.n_members();
-  }
-  if ((st = staged_copy(ctx, segs.data(), segs.size(), true, ctx->stream)) != CDB_OK) return st;
-  ok = on = om = 0;
-  for (uint32_t i = 0; i < n && st == CDB_OK; ++i) {
-    const Batch& b = *inputs[i]->b;
-    if ((st = stamp_pos(ctx, din.keys.col[K_META] + ok, b.n_keys(), i, ctx->stream)) != CDB_OK ||
-        (st = stamp_pos(ctx, din.nodes.col[C_META] + on, b.n_nodes(), i, ctx->stream)) != CDB_OK ||
-        (st = stamp_pos(ctx, din.members.col[C_META] + om, b.n_members(), i, ctx->stream)) != CDB_OK)
-      break;
-    ok += b.n_keys();
-    on += b.n_nodes();
-    om += b.n_members();
-  }
-  if (st != CDB_OK) return st;
+  if ((st = upload_batches(ctx, inputs, n, &din)) != CDB_OK) return st;
   const auto t1 = std::chrono::steady_clock::now();
   dout.compact = 1;
   cdb_merge_stats local;
@@ -391,6 +397,32 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, const c
   }
   *out = m;
   return merge_st;
+}
+
+cdb_status cdb_upload_batches(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, cdb_dev_input* out) {
+  if (!ctx || !out || (n && !inputs)) return CDB_BAD_ARGUMENT;
+  std::memset(out, 0, sizeof *out);
+  if (n > (uint32_t)kMaxPos) return fail(ctx, CDB_BAD_ARGUMENT, "at most 63 batches per merge");
+  hipSetDevice(ctx->device);
+  uint64_t K = 0, N = 0, M = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    K += inputs[i]->b->n_keys();
+    N += inputs[i]->b->n_nodes();
+    M += inputs[i]->b->n_members();
+  }
+  cdb_status st;
+  if ((st = cdb_dev_rows_alloc(ctx, &out->keys, K, kKeyCols)) != CDB_OK ||
+      (st = cdb_dev_rows_alloc(ctx, &out->nodes, N, kNodeCols)) != CDB_OK ||
+      (st = cdb_dev_rows_alloc(ctx, &out->members, M, kMemberCols)) != CDB_OK ||
+      (st = upload_batches(ctx, inputs, n, out)) != CDB_OK ||
+      (st = hip_check(ctx, hipStreamSynchronize(ctx->stream), "upload")) != CDB_OK) {
+    cdb_dev_rows_release(ctx, &out->keys);
+    cdb_dev_rows_release(ctx, &out->nodes);
+    cdb_dev_rows_release(ctx, &out->members);
+    return st;
+  }
+  out->n_pos = n;
+  return CDB_OK;
 }
 
 cdb_status cdb_merged_canonical_dump(cdb_ctx* ctx, cdb_merged* m, char** out, size_t* len) {

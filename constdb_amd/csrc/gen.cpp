@@ -80,6 +80,39 @@ GenModel model_of(const cdb_gen_config& c) {
   g.value_max = c.value_max;
   g.shard = c.shard;
   g.n_shards = c.n_shards;
+  g.flags = c.flags;
+  g.hot_n = 0;
+  for (int j = 0; j < kHotTab; ++j) g.hot_rank[j] = 0, g.hot_lam[j] = 0;
+  if (c.hot_zipf_milli && c.hot_events && c.universe) {
+    // popularity rank k = i + 1 draws lam(k) = E k^-s / (H R p f) children per present
+    // (key, replica): E = hot_events over all replicas, H = sum_k k^-s (exact up to 4096, the
+    // integral beyond), p = presence probability, f = share of child-bearing types
+    const double s = c.hot_zipf_milli / 1000.0;
+    const double U = (double)c.universe;
+    double H = 0;
+    const uint64_t head = std::min<uint64_t>(c.universe, 4096);
+    for (uint64_t k = 1; k <= head; ++k) H += std::pow((double)k, -s);
+    if (c.universe > head) {
+      H += std::fabs(s - 1.0) < 1e-9 ? std::log((U + 0.5) / (head + 0.5))
+                                     : (std::pow(U + 0.5, 1 - s) - std::pow(head + 0.5, 1 - s)) / (1 - s);
+    }
+    const double tot = (double)c.mix_bytes + c.mix_counter + c.mix_set + c.mix_dict;
+    const double f = tot > 0 ? (c.mix_counter + c.mix_set + c.mix_dict) / tot : 0;
+    const double p = c.key_permille / 1000.0;
+    const double R = c.n_replicas ? (double)c.n_replicas : 1.0;
+    const double scale = (f > 0 && p > 0) ? (double)c.hot_events / (H * R * p * f) : 0.0;
+    uint64_t prev = 0;
+    for (int j = 0; j < kHotTab; ++j) {
+      uint64_t k = j < 16 ? (uint64_t)j + 1 : (uint64_t)std::llround(16.0 * std::pow(2.0, (j - 15) / 4.0));
+      if (k <= prev) k = prev + 1;
+      if (k > 0xFFFFFFFFull) break;
+      g.hot_rank[j] = (uint32_t)k;
+      g.hot_lam[j] = (uint64_t)std::llround(scale * std::pow((double)k, -s) * 65536.0);
+      g.hot_n = (uint32_t)j + 1;
+      prev = k;
+      if (k >= c.universe) break;
+    }
+  }
   return g;
 }
 
@@ -138,7 +171,7 @@ cdb_status cdb_gen_snapshot(const cdb_gen_config* cfg, uint32_t r, uint8_t** out
       } else if (k.tag == TAG_COUNTER) {
         data.integer(k.n_nodes);
         for (uint32_t j = 0; j < k.n_nodes; ++j) {
-          data.integer((int64_t)gen_node_id(g, k, j));
+          data.integer((int64_t)gen_node_id(g, k, j, r));
           data.integer((int64_t)gen_node_v(g, i, r, j));
           data.integer((int64_t)gen_node_t(g, i, r, j));
         }
@@ -204,6 +237,16 @@ cdb_status cdb_gen_snapshot(const cdb_gen_config* cfg, uint32_t r, uint8_t** out
 
 // ---------------------------------------------------------------- op streams
 namespace {
+// An index in [0, n) from the random word u: uniform (s <= 0) or power-law skewed, rank ~
+// x^(1/(1-s)) for x uniform in (0, 1] (s < 1); `spread` scatters the hot ranks over [0, n).
+uint64_t skewed(uint64_t u, double s, uint64_t n, bool spread) {
+  if (s <= 0) return u % n;
+  const double x = ((u >> 11) + 1) * (1.0 / 9007199254740992.0);
+  const double r = std::pow(x, 1.0 / (1.0 - std::min(s, 0.99))) * (double)n;
+  const uint64_t i = std::min<uint64_t>((uint64_t)r, n - 1);
+  return spread ? (i * 0x9E3779B97F4A7C15ull) % n : i;
+}
+
 struct RespWriter {  // WriteBuf::write_msg (conn/buf_write.rs:127-150)
   std::vector<uint8_t> b;
   void lit(const char* s) { b.insert(b.end(), s, s + std::strlen(s)); }
@@ -237,18 +280,11 @@ extern "C" cdb_status cdb_gen_ops(const cdb_gen_config* cfg, uint64_t n_ops, uin
   for (uint64_t q = 0; q < n_ops; ++q) {
     const uint64_t u0 = grnd(g, q, 0xFFFE, 1), u1 = grnd(g, q, 0xFFFE, 2), u2 = grnd(g, q, 0xFFFE, 3);
     // key index: uniform, or a power-law skew (rank ~ x^(1/(1-s)) for x uniform in (0,1])
-    uint64_t i;
-    if (s <= 0) {
-      i = u0 % g.universe;
-    } else {
-      const double x = ((u0 >> 11) + 1) * (1.0 / 9007199254740992.0);
-      double r = std::pow(x, 1.0 / (1.0 - std::min(s, 0.99))) * (double)g.universe;
-      i = std::min<uint64_t>((uint64_t)r, g.universe - 1);
-      i = (i * 0x9E3779B97F4A7C15ull) % g.universe;  // hot keys spread over the key space
-    }
+    const bool zmem = (g.flags & kGenOpsZipfMembers) != 0, tags_only = (g.flags & kGenOpsTagsOnly) != 0;
+    const uint64_t i = zmem ? u0 % g.universe : skewed(u0, zmem ? 0 : s, g.universe, true);
     const Hash128 h = gen_key_hash(i);
     if (!gen_in_shard(g, h.h)) continue;
-    const uint8_t tag = (u1 % 1000 < 2) ? gen_pick_type(g, u2) : gen_type(g, i, kAllReplicas);
+    const uint8_t tag = (!tags_only && u1 % 1000 < 2) ? gen_pick_type(g, u2) : gen_type(g, i, kAllReplicas);
     // ~2^20 ms past the state's times, with 5 % of the ops older than the state
     const uint64_t ms = (u1 >> 20) % 1000 < 50 ? kT0Ms + (u2 >> 24) % (1u << 20) : kT0Ms + (1u << 20) + q / 64;
     const uint64_t uuid = (ms << 22) | (q & 0x3FFFFF);
@@ -265,11 +301,11 @@ extern "C" cdb_status cdb_gen_ops(const cdb_gen_config* cfg, uint64_t n_ops, uin
       name = pick < 60 ? "incr" : pick < 97 ? "decr" : "delcnt";
       if (pick >= 97) nargs += 2;
     } else if (tag == TAG_SET) {
-      name = pick < 70 ? "sadd" : pick < 99 ? "srem" : "delset";
-      if (pick < 99) nargs += nm;
+      name = pick < 70 ? "sadd" : (pick < 99 || tags_only) ? "srem" : "delset";
+      if (pick < 99 || tags_only) nargs += nm;
     } else {
-      name = pick < 70 ? "hset" : pick < 99 ? "hdel" : "deldict";
-      if (pick < 99) nargs += pick < 70 ? 2 * nm : nm;
+      name = pick < 70 ? "hset" : (pick < 99 || tags_only) ? "hdel" : "deldict";
+      if (pick < 99 || tags_only) nargs += pick < 70 ? 2 * nm : nm;
     }
     w.arr(5 + nargs);
     w.bulk("replicate");
@@ -289,7 +325,8 @@ extern "C" cdb_status cdb_gen_ops(const cdb_gen_config* cfg, uint64_t n_ops, uin
       w.integer(-(int64_t)(u1 % 100));
     } else if (nargs > 1) {
       for (uint32_t j = 0; j < nm; ++j) {
-        const int ml = member_bytes((u0 >> 16) % mu + j, mb);
+        const uint64_t mj = zmem ? skewed(grnd(g, q, 0xFFFE, 20 + j), s, mu, false) : (u0 >> 16) % mu + j;
+        const int ml = member_bytes(mj, mb);
         w.bulk(mb, ml);
         if (!std::strcmp(name, "hset")) w.bulk("v", 1);
       }

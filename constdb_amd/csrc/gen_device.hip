@@ -76,10 +76,10 @@ __global__ void gen_fill_kernel(GenArgs a, const uint32_t* __restrict__ ok, cons
             aux += v;
             a.nd[C_PKH][pn] = h.h;
             a.nd[C_PKF][pn] = h.f;
-            a.nd[C_ID1][pn] = gen_node_id(a.g, k, j);
+            a.nd[C_ID1][pn] = gen_node_id(a.g, k, j, r);
             a.nd[C_ID2][pn] = v;
             a.nd[C_T][pn] = gen_node_t(a.g, i, r, j);
-            a.nd[C_META][pn] = meta_pack(0, r, i * a.g.max_nodes + j);
+            a.nd[C_META][pn] = meta_pack(0, r, gen_node_src(a.g, i, j));
             ++pn;
           }
         } else if (k.tag == TAG_SET || k.tag == TAG_DICT) {
@@ -92,7 +92,7 @@ __global__ void gen_fill_kernel(GenArgs a, const uint32_t* __restrict__ ok, cons
             a.mb[C_ID2][pm] = mh.f;
             a.mb[C_T][pm] = gen_member_t(a.g, i, r, j);
             a.mb[C_META][pm] =
-                meta_pack(gen_member_is_del(a.g, i, r, j) ? KIND_DEL : KIND_ADD, r, i * a.g.member_universe + mi);
+                meta_pack(gen_member_is_del(a.g, i, r, j) ? KIND_DEL : KIND_ADD, r, gen_member_src(a.g, i, mi));
             ++pm;
           }
         }

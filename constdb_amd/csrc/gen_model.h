@@ -9,13 +9,28 @@
 
 namespace cdb {
 
+// Hot-key skew (config C5): expected children per present (key, replica) as a function of the
+// key's popularity rank k = i + 1, tabulated on the host (model_of) at ranks 1..16 and then every
+// quarter octave, in 2^16 fixed point; looked up with integer interpolation so that the host
+// writer and the device generator draw identical rows.
+constexpr int kHotTab = 128;
+
 struct GenModel {
   uint64_t seed, universe;
   uint32_t n_replicas, key_permille;
   uint32_t mix[4];  // bytes, counter, set, dict weights
   uint32_t conflict_ppm, tie_permille, max_nodes, mean_members, member_universe, del_permille,
       side_permille, value_min, value_max, shard, n_shards;
+  uint32_t flags;   // CDB_GEN_* (cdb_merge.h)
+  uint32_t hot_n;   // hot-mode table entries (0 = hot mode off)
+  uint32_t hot_rank[kHotTab];  // strictly increasing ranks
+  uint64_t hot_lam[kHotTab];   // expected children x 2^16 at hot_rank[j]
 };
+
+constexpr uint32_t kGenNodePerReplica = 1u;  // CDB_GEN_NODE_PER_REPLICA
+constexpr uint32_t kGenOpsZipfMembers = 2u;  // CDB_GEN_OPS_ZIPF_MEMBERS
+constexpr uint32_t kGenOpsTagsOnly = 4u;     // CDB_GEN_OPS_TAGS_ONLY
+constexpr uint64_t kHotSrcStride = 1ull << 22;  // hot-mode child src = i * stride + slot
 
 constexpr uint64_t kT0Ms = 1700000000000ull;  // uuid = ms << 22 | seq (server.rs:159-173)
 constexpr uint32_t kAllReplicas = 0xFFFFu;
@@ -98,7 +113,35 @@ struct GenKey {  // the data entry of key i in replica r
   uint32_t node_start;
   uint32_t n_members;    // Set / Dict
   uint32_t member_start;
+  uint32_t child_universe;  // node ids / member indices are drawn modulo this
 };
+
+// Hot mode: expected children (x 2^16) of key i in a replica that holds it.
+CDB_HD uint64_t gen_hot_lam(const GenModel& g, uint64_t i) {
+  const uint64_t k = i + 1;
+  uint32_t lo = 0, hi = g.hot_n;  // largest j with hot_rank[j] <= k (hot_rank[0] = 1)
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (g.hot_rank[mid] <= k) lo = mid;
+    else hi = mid;
+  }
+  if (lo + 1 >= g.hot_n) return g.hot_lam[lo];
+  const uint64_t r0 = g.hot_rank[lo], r1 = g.hot_rank[lo + 1];
+  const uint64_t l0 = g.hot_lam[lo], l1 = g.hot_lam[lo + 1];  // l0 >= l1
+  const uint64_t f = ((k - r0) << 16) / (r1 - r0);
+  return l0 - (((l0 - l1) * f) >> 16);
+}
+
+// Hot mode: child count of (i, r) = floor(lam) or floor(lam) + 1 (by the fraction), and the
+// universe the children are drawn from (2 ceil(lam): a child is in about half of the replicas
+// holding the key, so (key, child) segments run up to R rows).
+CDB_HD uint32_t gen_hot_count(const GenModel& g, uint64_t i, uint32_t r, uint32_t* universe) {
+  const uint64_t lam = gen_hot_lam(g, i);
+  const uint64_t whole = lam >> 16;
+  *universe = (uint32_t)(2 * ((lam + 0xFFFF) >> 16));
+  if (*universe == 0) *universe = 1;
+  return (uint32_t)whole + ((lam & 0xFFFF) > (grnd(g, i, r, 13) & 0xFFFF) ? 1u : 0u);
+}
 
 CDB_HD GenKey gen_key(const GenModel& g, uint64_t i, uint32_t r) {
   GenKey k;
@@ -108,20 +151,34 @@ CDB_HD GenKey gen_key(const GenModel& g, uint64_t i, uint32_t r) {
   k.dt = grnd(g, i, r, 5) % 8 == 0 ? gen_time(g, i, r, 2) : 0;
   const uint32_t span = g.value_max >= g.value_min ? g.value_max - g.value_min + 1 : 1;
   k.value_len = g.value_min + (uint32_t)(grnd(g, i, r, 6) % span);
+  if (g.hot_n) {  // C5: one popularity-driven child count for counters and sets / dicts alike
+    uint32_t cu = 1;
+    const uint32_t c = gen_hot_count(g, i, r, &cu);
+    k.child_universe = cu;
+    k.n_nodes = k.n_members = c;
+    k.node_start = (uint32_t)(grnd(g, i, r, 8) % cu);
+    k.member_start = (uint32_t)(grnd(g, i, r, 10) % cu);
+    return k;
+  }
   uint64_t u = grnd(g, i, r, 7);
   uint32_t c = 1;
   const uint32_t mn = g.max_nodes ? g.max_nodes : 1;
   while (c < mn && ((u >> (c - 1)) & 1)) ++c;  // geometric(1/2): mean ~2
-  k.n_nodes = c;
+  k.n_nodes = (g.flags & kGenNodePerReplica) ? 1 : c;
   k.node_start = (uint32_t)(grnd(g, i, kAllReplicas, 8) % mn);
   const uint32_t mu = g.member_universe ? g.member_universe : 1;
   uint32_t m = (uint32_t)(grnd(g, i, r, 9) % (2 * g.mean_members + 1));
   k.n_members = m > mu ? mu : m;
   k.member_start = (uint32_t)(grnd(g, i, r, 10) % mu);
+  k.child_universe = 0;
   return k;
 }
 
-CDB_HD uint64_t gen_node_id(const GenModel& g, const GenKey& k, uint32_t j) {
+// Counter node id of child j. MEET shape (CDB_GEN_NODE_PER_REPLICA): the one node is the
+// replica's own node id r + 1 (bin/test.rs:85-106 snapshots counters written by each node).
+CDB_HD uint64_t gen_node_id(const GenModel& g, const GenKey& k, uint32_t j, uint32_t r) {
+  if (g.flags & kGenNodePerReplica) return r + 1;
+  if (k.child_universe) return 1 + (k.node_start + j) % k.child_universe;
   const uint32_t mn = g.max_nodes ? g.max_nodes : 1;
   return 1 + (k.node_start + j) % mn;
 }
@@ -132,8 +189,15 @@ CDB_HD uint64_t gen_node_t(const GenModel& g, uint64_t i, uint32_t r, uint32_t j
   return gen_time(g, i, r, 8 + j);
 }
 CDB_HD uint64_t gen_member_index(const GenModel& g, const GenKey& k, uint32_t j) {
-  const uint32_t mu = g.member_universe ? g.member_universe : 1;
+  const uint32_t mu = k.child_universe ? k.child_universe : (g.member_universe ? g.member_universe : 1);
   return (k.member_start + j) % mu;
+}
+// src coordinates of the device generator's child rows (unique per key and replica)
+CDB_HD uint64_t gen_node_src(const GenModel& g, uint64_t i, uint32_t j) {
+  return g.hot_n ? i * kHotSrcStride + j : i * (g.max_nodes ? g.max_nodes : 1) + j;
+}
+CDB_HD uint64_t gen_member_src(const GenModel& g, uint64_t i, uint64_t mi) {
+  return g.hot_n ? i * kHotSrcStride + mi : i * (g.member_universe ? g.member_universe : 1) + mi;
 }
 CDB_HD bool gen_member_is_del(const GenModel& g, uint64_t i, uint32_t r, uint32_t j) {
   return grnd(g, i, r, 300 + j) % 1000 < g.del_permille;

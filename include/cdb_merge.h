@@ -299,6 +299,11 @@ typedef struct cdb_dev_output {
 cdb_status cdb_partition_owner(cdb_ctx* ctx, const cdb_dev_rows* in, int ncols, int owner_bits,
                                cdb_dev_rows* out, uint64_t* counts, void* stream);
 
+/* Uploads decoded batches [0, n) into freshly allocated device rows (*out; release each family
+ * with cdb_dev_rows_release), batch i at fold position i, so that a caller can keep a decoded
+ * replica set resident in HBM and merge it with cdb_merge_device (what cdb_merge does per call). */
+cdb_status cdb_upload_batches(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, cdb_dev_input* out);
+
 /* Allocates device columns for `rows` rows of a family (8 u64 columns) in *r. */
 cdb_status cdb_dev_rows_alloc(cdb_ctx* ctx, cdb_dev_rows* r, uint64_t rows, int ncols);
 void cdb_dev_rows_release(cdb_ctx* ctx, cdb_dev_rows* r);
@@ -326,7 +331,19 @@ typedef struct cdb_gen_config {
   uint32_t value_min, value_max; /* Bytes value length range */
   uint32_t shard, n_shards;      /* generate only keys with owner(kh) == shard (multi-GPU) */
   uint32_t replica_lo, replica_hi; /* generate replicas [lo, hi) */
+  uint32_t flags;                /* CDB_GEN_* below */
+  uint32_t hot_zipf_milli;       /* config C5: children per key follow rank^-(s/1000) over key index
+                                    rank i + 1 (0 = off; then max_nodes / mean_members apply) */
+  uint32_t reserved;
+  uint64_t hot_events;           /* config C5: expected node/member rows over all replicas */
 } cdb_gen_config;
+enum {
+  CDB_GEN_NODE_PER_REPLICA = 1u << 0, /* counters carry one node, the replica's own id r + 1 (the
+                                         2-node MEET shape of config C1, bin/test.rs:85-106) */
+  CDB_GEN_OPS_ZIPF_MEMBERS = 1u << 1, /* cdb_gen_ops: zipf_milli skews member choice, keys uniform */
+  CDB_GEN_OPS_TAGS_ONLY = 1u << 2     /* cdb_gen_ops: only sadd/srem/hset/hdel (config C3): no
+                                         whole-key deletes, no other types */
+};
 void cdb_gen_default(cdb_gen_config* cfg);
 /* Snapshot bytes of replica r (writer layout). *out released with cdb_free. */
 cdb_status cdb_gen_snapshot(const cdb_gen_config* cfg, uint32_t replica, uint8_t** out, size_t* len);

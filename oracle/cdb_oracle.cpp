@@ -441,21 +441,42 @@ int cdbo_fold(const uint8_t* const* bufs, const size_t* lens, int n, int flags, 
 
 void cdbo_free(void* p) { std::free(p); }
 
-// CPU baseline: decodes (untimed), then times ONLY the sequential fold into a fresh DB
-// (the reference's merge loop minus its per-entry DEBUG formatting), best of `reps`.
-// Returns the best fold time in ns; *entries = entries (Data/Expires/Deletes) folded per run.
+static Entry clone_entry(const Entry& e) {  // deep copy (Entry owns its object through unique_ptrs)
+  Entry c;
+  c.kind = e.kind;
+  c.key = e.key;
+  c.t = e.t;
+  if (e.obj) {
+    c.obj.reset(new Object());
+    Object& o = *c.obj;
+    o.ct = e.obj->ct; o.ut = e.obj->ut; o.dt = e.obj->dt; o.tag = e.obj->tag; o.bytes = e.obj->bytes;
+    if (e.obj->counter) o.counter.reset(new Counter(*e.obj->counter));
+    if (e.obj->hash) o.hash.reset(new LWWHash(*e.obj->hash));
+  }
+  return c;
+}
+
+// CPU baseline: decodes once (untimed), then times ONLY the sequential fold into a fresh DB
+// (the reference's merge loop minus its per-entry DEBUG formatting), best of `reps`; every rep
+// folds its own untimed copy of the decoded entries. Returns the best fold time in ns;
+// *entries = entries (Data/Expires/Deletes) folded per run.
 int64_t cdbo_time_fold(const uint8_t* const* bufs, const size_t* lens, int n, int reps,
                        uint64_t* entries) {
+  std::vector<std::vector<Entry>> base(n);
+  size_t eo;
+  uint64_t cnt = 0;
+  for (int i = 0; i < n; ++i) {
+    if (decode(bufs[i], lens[i], 0, &base[i], &eo) != OK) return -1;
+    cnt += base[i].size();  // Data + Expires + Deletes entries
+  }
+  *entries = cnt;
   int64_t best = -1;
   for (int r = 0; r < reps; ++r) {
     std::vector<std::vector<Entry>> snaps(n);
-    size_t eo;
-    uint64_t cnt = 0;
     for (int i = 0; i < n; ++i) {
-      if (decode(bufs[i], lens[i], 0, &snaps[i], &eo) != OK) return -1;
-      cnt += snaps[i].size();  // Data + Expires + Deletes entries
+      snaps[i].reserve(base[i].size());
+      for (const Entry& e : base[i]) snaps[i].push_back(clone_entry(e));
     }
-    *entries = cnt;
     DB db;
     db.data.reserve(1024);
     auto t0 = std::chrono::steady_clock::now();

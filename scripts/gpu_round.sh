@@ -1,19 +1,25 @@
 #!/bin/bash
 # One GPU verification round: parity tests, full bench (with CPU baseline), kernel-trace
 # stats of the same bench command, FETCH/WRITE PMC passes for the HBM traffic figure.
-# Usage (from gpurun): TAG=r1e bash scripts/gpu_round.sh
+# Usage (from gpurun): TAG=r2b CONFIG=c4 bash scripts/gpu_round.sh
 set -o pipefail
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-T=${TAG:-r1e}
+T=${TAG:-r2}
+C=${CONFIG:-c4}
 O=gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_$T.log 2>&1 || { echo "pytest failed"; exit 1; }
-timeout -k 10 400 python bench.py --steps 5 --warmup 2 > $O/bench_full_$T.json 2> $O/bench_full_$T.err || { echo "bench failed"; exit 2; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$T -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_$T.log 2>&1 || { echo "prof failed"; exit 3; }
+KRE="part_|bucket_|compact|scan_|stats_reduce|gc_lastbad|hot_|sorted_|seg_"
+if [ -z "$NO_TESTS" ]; then
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_$T.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest_$T.log; exit 1; }
+tail -2 $O/pytest_$T.log
+fi
+timeout -k 10 500 python bench.py --config $C --steps 5 --warmup 2 > $O/bench_${C}_$T.json 2> $O/bench_${C}_$T.err || { echo "bench failed"; tail -20 $O/bench_${C}_$T.err; exit 2; }
+cat $O/bench_${C}_$T.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_${C}_$T -o run -- python bench.py --config $C --steps 5 --warmup 2 --no-cpu-baseline > $O/prof_${C}_$T.log 2>&1 || { echo "prof failed"; exit 3; }
 if [ -z "$NO_PMC" ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 200 rocprofv3 --pmc $c --kernel-include-regex "${KREGEX:-bucket_|part_|compact}" --output-format csv -d $O/pmc_${T}_$c -o run -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_${T}_$c.log 2>&1 || { echo "pmc $c failed"; exit 4; }
+    timeout -s KILL 200 rocprofv3 --pmc $c --kernel-include-regex "$KRE" --output-format csv -d $O/pmc_${C}_${T}_$c -o run -- python bench.py --config $C --steps 1 --warmup 0 --no-cpu-baseline > $O/pmc_${C}_${T}_$c.log 2>&1 || { echo "pmc $c failed"; exit 4; }
   done
-python3 scripts/pmc_traffic.py $O/pmc_${T}_FETCH_SIZE $O/pmc_${T}_WRITE_SIZE $O/pmc_traffic_$T.json || exit 5
+  python3 scripts/pmc_traffic.py $O/pmc_${C}_${T}_FETCH_SIZE $O/pmc_${C}_${T}_WRITE_SIZE $O/pmc_traffic_${C}_$T.json || exit 5
 fi
 echo "round ok"

@@ -28,10 +28,18 @@ out = {"note": "bytes per launch (mean over launches); fetch_bytes = 2 x FETCH_S
 for k in sorted(set(fetch) | set(write)):
     f = 2.0 * sum(fetch.get(k, [0])) / max(1, len(fetch.get(k, [])))
     w = sum(write.get(k, [0])) / max(1, len(write.get(k, [])))
-    out["kernels"][k] = {"fetch_bytes": f, "write_bytes": w, "launches": len(fetch.get(k, []))}
-bucket = [k for k in out["kernels"] if k.startswith("bucket_")]
-out["bucket_phase_bytes"] = sum(out["kernels"][k]["fetch_bytes"] + out["kernels"][k]["write_bytes"] for k in bucket)
+    # the PMC runs are `bench.py --steps 1 --warmup 0`: every launch belongs to the one merge step
+    out["kernels"][k] = {"fetch_bytes": f, "write_bytes": w, "launches": len(fetch.get(k, [])),
+                         "per_step": len(fetch.get(k, []))}
+def step_bytes(names):
+    return sum((out["kernels"][k]["fetch_bytes"] + out["kernels"][k]["write_bytes"]) * out["kernels"][k]["per_step"]
+               for k in names)
+
+
+merge = [k for k in out["kernels"] if not k.startswith("gen_")]
+out["bucket_phase_bytes"] = step_bytes([k for k in merge if k.startswith("bucket_")])
+out["merge_step_bytes"] = step_bytes(merge)
 json.dump(out, open(sys.argv[3], "w"), indent=1)
 for k, v in out["kernels"].items():
     print(f"{k:40s} fetch {v['fetch_bytes'] / 1e9:8.2f} GB  write {v['write_bytes'] / 1e9:8.2f} GB  x{v['launches']}")
-print("bucket phase traffic", out["bucket_phase_bytes"] / 1e9, "GB")
+print("bucket phase traffic", out["bucket_phase_bytes"] / 1e9, "GB; whole merge step", out["merge_step_bytes"] / 1e9, "GB")

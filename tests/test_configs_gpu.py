@@ -1,0 +1,132 @@
+"""BASELINE.json configs C1/C2, C3 and C5 on the GPU, bit-exact against the C++
+oracle's sequential fold (oracle/cdb_oracle.cpp, restating db.rs:31-119, object.rs:63-83,
+type_counter.rs:59-91, crdt/lwwhash.rs:87-128,319-323):
+  * C1/C2 at full size (1M Bytes + 1M counters per node, 50 % overlap) through cdb_merge, the
+    host-boundary FFI call a Rust puller would make (pull.rs:120-128);
+  * C3 at full size: 4 replica states, each left by replaying 10M sadd/srem/hset/hdel through the
+    device op apply, merged with DB::gc at the median member time;
+  * C5 (Zipf hot keys) at sizes the oracle folds in seconds, whose hottest keys own 10^4-10^5
+    children (the over-capacity bucket tiers).
+The device generator (the bench's inputs) is checked row for row against the host writer
+(the oracle's inputs) on every config."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch  # noqa: F401  -- before libcdbmerge loads (one HIP runtime per process)
+
+import cdb_oracle
+import constdb_amd as cdb
+from constdb_amd import configs
+
+pytestmark = pytest.mark.gpu
+
+NCOLS = (7, 6, 6)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from constdb_amd import build
+    build.build()
+    return cdb.Context(0)
+
+
+def _check(ctx, snaps, gc=None):
+    flags = cdb_oracle.FLAG_GC if gc is not None else 0
+    rc, want, ost = cdb_oracle.fold(snaps, flags=flags, gc_watermark=gc or 0)
+    assert rc == 0
+    m = cdb.DB(ctx).merge_snapshots(snaps, gc_watermark=gc)
+    got = m.canonical_dump()
+    if got != want:
+        gl, wl = got.split(b"\n"), want.split(b"\n")
+        i = next((i for i, (a, b) in enumerate(zip(gl, wl)) if a != b), min(len(gl), len(wl)))
+        raise AssertionError(f"first diff at line {i}: gpu {gl[i][:200] if i < len(gl) else None!r} "
+                             f"oracle {wl[i][:200] if i < len(wl) else None!r} ({len(gl)} vs {len(wl)} lines)")
+    assert m.stats.type_conflicts == ost.type_conflicts
+    assert m.stats.dict_merges == ost.dict_merges
+    return m
+
+
+def _rows_multiset(cols, fam):
+    """Rows of one family as a sorted structured array, src stripped from meta (the device
+    generator's src are model coordinates, a decoded batch's are row indices)."""
+    arr = np.stack(cols, axis=1).astype(np.uint64)
+    meta = NCOLS[fam] - 1
+    arr[:, meta] &= np.uint64(0xFFFF000000000000)
+    v = arr.view([(f"c{i}", np.uint64) for i in range(arr.shape[1])]).ravel()
+    return np.sort(v)
+
+
+def _device_matches_host(ctx, cfg, replicas):
+    L = cdb.lib()
+    din = cdb.DevInput()
+    ctx.check(L.cdb_gen_device(ctx.handle, ctypes.byref(cfg), ctypes.byref(din)))
+    try:
+        batches = [cdb.decode_snapshot(cdb.gen_snapshot(cfg, r)) for r in range(replicas)]
+        for fam, rows in enumerate((din.keys, din.nodes, din.members)):
+            dev = [(_wrap(rows.col[c], rows.n).cpu().numpy().view(np.uint64) if rows.n else np.zeros(0, np.uint64))
+                   for c in range(NCOLS[fam])]
+            host = []
+            for c in range(NCOLS[fam]):
+                parts = []
+                for r, b in enumerate(batches):
+                    col = b.column_array(fam, c)
+                    if c == NCOLS[fam] - 1:  # the decoder leaves pos 0: the fold position is the batch index
+                        col = (col & np.uint64(0xFF00FFFFFFFFFFFF)) | np.uint64(r << 48)
+                    parts.append(col)
+                host.append(np.concatenate(parts) if parts else np.zeros(0, np.uint64))
+            assert len(dev[0]) == len(host[0]), (fam, len(dev[0]), len(host[0]))
+            if len(dev[0]):
+                assert (_rows_multiset(dev, fam) == _rows_multiset(host, fam)).all(), fam
+    finally:
+        for fam in (din.keys, din.nodes, din.members):
+            L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
+
+
+def _wrap(ptr, n):
+    """A torch view of n int64 at device address ptr (owned by the library)."""
+    class _Cai:
+        __cuda_array_interface__ = {"shape": (n,), "typestr": "<i8", "data": (ptr, False), "version": 2}
+    return torch.as_tensor(_Cai(), device="cuda")
+
+
+# ------------------------------------------------------------------ C1 / C2
+def test_c1_device_generator_matches_host(ctx):
+    _device_matches_host(ctx, configs.c1(cdb, per_node=20_000), 2)
+
+
+def test_c1_full_size_bit_exact(ctx):
+    """C1/C2: the 2-node MEET at its stated size through the host-boundary cdb_merge."""
+    cfg = configs.c1(cdb)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(2)]
+    m = _check(ctx, snaps)
+    st = m.stats
+    assert 3_900_000 < st.key_rows_in < 4_100_000          # 4M key rows in
+    assert 2_900_000 < st.key_rows_out < 3_100_000         # 3M out (50 % overlap)
+    assert 1_900_000 < st.node_rows_in < 2_100_000        # one node per counter
+
+
+# ------------------------------------------------------------------ C3
+def test_c3_full_size_bit_exact(ctx):
+    """C3: 4 replica states from 10M sadd/srem/hset/hdel each (device op apply), merged with
+    DB::gc at the median member time; bit-exact against the oracle's fold + gc."""
+    snaps = configs.c3_snapshots(cdb, ctx)
+    batches = [cdb.decode_snapshot(s) for s in snaps]
+    wm = configs.median_member_time(cdb, batches)
+    assert wm > 0
+    m = _check(ctx, snaps)
+    assert m.stats.member_rows_in > 1_000_000
+    _check(ctx, snaps, gc=wm)
+
+
+# ------------------------------------------------------------------ C5
+def test_c5_device_generator_matches_host(ctx):
+    _device_matches_host(ctx, configs.c5(cdb, universe=50_000, events=400_000), 8)
+
+
+@pytest.mark.parametrize("universe,events", [(100_000, 800_000), (300_000, 3_000_000)])
+def test_c5_scaled_bit_exact(ctx, universe, events):
+    cfg = configs.c5(cdb, universe=universe, events=events)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(8)]
+    m = _check(ctx, snaps)
+    assert m.stats.hot_buckets + m.stats.mid_buckets > 0
