@@ -51,6 +51,10 @@ def parse():
     ap.add_argument("--force-dist", action="store_true",
                     help="use the multi-GPU (RCCL all-to-all) path even when WORLD_SIZE == 1")
     ap.add_argument("--c3-ops", type=int, default=10_000_000, help="ops per replica of config c3")
+    ap.add_argument("--input-order", default="sorted", choices=["sorted", "hash-random"],
+                    help="sorted: every replica's rows form one run in key-hash order (as this engine's merge "
+                         "output and snapshots encoded from it are; the sorted-run path); hash-random: rows "
+                         "in generator (key-index) order, i.e. random in hash (the partition path)")
     return ap.parse_args()
 
 
@@ -173,10 +177,60 @@ def setup(cdb, ctx, args):
     return din, opts, {"workload": work, "sample": sample}
 
 
+SIGN = -(1 << 63)
+
+
+def sort_into_runs(cdb, ctx, din):
+    """Reorders every family's device rows by (fold position, key hash) in place -- one run per
+    replica, as a replica state produced by this engine arrives -- and records the runs in
+    din.n_runs / din.run_start. Setup only (torch on the library's device columns)."""
+    import torch
+
+    def wrap(ptr, n):
+        class Cai:
+            __cuda_array_interface__ = {"shape": (n,), "typestr": "<i8", "data": (ptr, False), "version": 2}
+        return torch.as_tensor(Cai(), device="cuda")
+
+    R = din.n_pos
+    din.n_runs = R
+    for f, (rows, ncol) in enumerate(((din.keys, 7), (din.nodes, 6), (din.members, 6))):
+        n = rows.n
+        if n == 0:
+            for r in range(R + 1):
+                din.run_start[f][r] = 0
+            continue
+        kh = wrap(rows.col[0], n)
+        meta = wrap(rows.col[ncol - 1], n)
+        o = torch.sort(kh ^ SIGN, stable=True).indices
+        pos = (meta >> 48) & 0xFF
+        o = o[torch.sort(pos[o], stable=True).indices]
+        counts = torch.bincount(pos, minlength=R).tolist()
+        del pos
+        for c in range(ncol):
+            col = wrap(rows.col[c], n)
+            col.copy_(col[o])
+        del o
+        st = 0
+        for r in range(R):
+            din.run_start[f][r] = st
+            st += counts[r]
+        din.run_start[f][R] = st
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+
+
 def run_single(cdb, args):
+    if args.input_order == "sorted":
+        import torch  # noqa: F401 -- before libcdbmerge: one HIP runtime per process
     ctx = cdb.Context(0)
     L = cdb.lib()
     din, opts, info = setup(cdb, ctx, args)
+    if args.input_order == "sorted":
+        sort_into_runs(cdb, ctx, din)
+        info["workload"] += ("; input: one key-hash-ordered run per replica (as this engine's merge output and "
+                             "snapshots encoded from it arrive): the sorted-run path")
+    else:
+        info["workload"] += "; input: rows in generator order, random in key hash: the partition path"
     dout = cdb.DevOutput()
     ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.keys), din.keys.n, 8))
     ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.nodes), din.nodes.n, 6))
@@ -221,7 +275,8 @@ def run_single(cdb, args):
                    "key_rows_in": st.key_rows_in, "node_rows_in": st.node_rows_in,
                    "member_rows_in": st.member_rows_in, "key_rows_out": st.key_rows_out,
                    "node_rows_out": st.node_rows_out, "member_rows_out": st.member_rows_out,
-                   "gc_watermark": opts.gc_watermark, "parallelism": "single GPU"},
+                   "gc_watermark": opts.gc_watermark, "input_order": args.input_order,
+                   "merge_path": "sorted runs" if st.sorted_runs else "partition", "parallelism": "single GPU"},
         "child_rows_per_s": (st.node_rows_in + st.member_rows_in) / (ms * 1e-3),
         "phases_ms": {"partition": per["partition"], "bucket_merge": per["bucket"], "finish": per["finish"],
                       "device_total": per["device"]},

@@ -123,7 +123,8 @@ class MergeStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "key_rows_in", "node_rows_in", "member_rows_in", "key_rows_out", "node_rows_out", "member_rows_out",
         "type_conflicts", "dict_merges", "deletes_gced", "members_gced", "duplicate_rows", "orphan_children",
-        "hot_buckets", "wide_buckets", "mid_buckets")] + [(n, ctypes.c_double) for n in ("device_ms", "partition_ms", "bucket_ms", "finish_ms")]
+        "hot_buckets", "wide_buckets", "mid_buckets")] + [(n, ctypes.c_double) for n in (
+        "device_ms", "partition_ms", "bucket_ms", "finish_ms")] + [("sorted_runs", ctypes.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -171,9 +172,12 @@ class DevRows(ctypes.Structure):
     _fields_ = [("col", ctypes.c_void_p * 8), ("n", ctypes.c_uint64)]
 
 
+MAX_RUNS = 64
+
+
 class DevInput(ctypes.Structure):
     _fields_ = [("keys", DevRows), ("nodes", DevRows), ("members", DevRows), ("n_pos", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("n_runs", ctypes.c_uint32), ("run_start", (ctypes.c_uint64 * (MAX_RUNS + 1)) * 3)]
 
 
 class DevOutput(ctypes.Structure):

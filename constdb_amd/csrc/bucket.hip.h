@@ -62,6 +62,11 @@ struct BucketArgs {
   uint32_t flags;
   uint32_t force_tier;
   int key_shift;
+  // bucket b's smallest hash is >= b * bw (bw = floor((2^64 - 1) / nbuckets)) and its hashes span
+  // less than 2^(44 + rel_shift): the wave kernels order a bucket's keys by the 44 leading bits of
+  // (h << key_shift) - b * bw (exact key-hash order when rel_shift == 0, i.e. nbuckets > ~2^21)
+  uint64_t bw;
+  int rel_shift;
   uint64_t gc_wm;
   const uint64_t* last_bad;   // (pos,src)+1 of the newest garbage entry with t > wm; 0 = none
   unsigned long long* stats;

@@ -89,6 +89,16 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x)
   for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
   return x;
 }
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x = max(x, (uint64_t)__shfl_xor((unsigned long long)x, d, 64));
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) x = min(x, (uint64_t)__shfl_xor((unsigned long long)x, d, 64));
+  return x;
+}
 
 // rk[e] = #{j < n : sw[j] < w[e]} for the first EA of my words; sw[n] must be ~0 when n is
 // odd (the loop reads pairs). Words are distinct, so ranks are a permutation of [0, n).
@@ -106,11 +116,27 @@ __device__ __forceinline__ void rank_count(const uint64_t* sw, uint32_t n, const
   }
 }
 
+// Sorted-run input (cdb_dev_input.n_runs > 0): the rows of every family are nr runs, each
+// non-decreasing in (parent) key hash, left where the caller put them (SoA columns). Bucket b's
+// rows in run r of family f are run rows [rdir[f][r * (nb + 1) + b], rdir[f][r * (nb + 1) + b + 1])
+// (run-relative), i.e. a few consecutive rows per run: the wave kernels read them column by
+// column with no partition pass and no row permutation (runs.hip.h).
+struct RunView {
+  const uint32_t* rdir[3];
+  const uint64_t* rbase;      // absolute first row of run r of family f at rbase[f * 65 + r]
+  uint32_t nr;
+  uint32_t nbp1;              // nb + 1: one run's directory row
+  const uint64_t* kin[kKeyCols];
+  const uint64_t* nin[kNodeCols];
+  const uint64_t* min[kMemberCols];
+};
+
 struct WaveArgs {
   BucketArgs A;
   uint32_t nbuckets;
   uint32_t* big_list;   // buckets for the workgroup tier
   uint32_t* big_count;
+  RunView V;            // sorted-run path only
 };
 
 // A bucket's directory entry (row counts and first row of each family).
@@ -413,13 +439,19 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   }
 
   // ------------------------------------------------------------ 1. keys: rank + scatter
-  // word = kh[43:0] << 20 | family << 18 | pos << 12 | slot   (pos < 64, slot < 4096)
+  // word = rel << 20 | family << 18 | pos << 12 | slot   (pos < 64, slot < 4096), where rel is
+  // the 44 leading bits of (kh << shift) - b * bw (BucketArgs): monotone in the key hash, so the
+  // output keys leave in exact key-hash order whenever rel_shift == 0 (a merge result is then a
+  // sorted run for the next merge, runs.hip.h); two hashes that share rel go to the exact tier
+  const int ks = A.key_shift, rsh = A.rel_shift;
+  const uint64_t lo = (uint64_t)b * A.bw;
+  auto rel44 = [&](uint64_t h) { return (((h << ks) - lo) >> rsh) & kM44; };
   uint64_t w[KE];
   uint32_t rk[KE];
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
     const uint32_t c = lane + 64 * e;
-    w[e] = ((kh[e] & kM44) << 20) | ((uint64_t)tag_family(meta_tag(kmeta[e])) << 18) |
+    w[e] = (rel44(kh[e]) << 20) | ((uint64_t)tag_family(meta_tag(kmeta[e])) << 18) |
            ((uint64_t)meta_pos(kmeta[e]) << 12) | c;
     if (c < K) L.sw[c] = w[e];
   }
@@ -573,21 +605,31 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     ckey[e] = 0;
     if (c < C) {
       const bool isn = c < N;
-      uint32_t lo = 0, hi = kout;  // lower bound on kh[43:0] (output keys are in word order)
-      const uint64_t t44 = cpkh[e] & kM44;
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        const bool less = (L.okh[mid] & kM44) < t44;
-        lo = less ? mid + 1 : lo;
-        hi = less ? hi : mid;
+      uint32_t ql = 0, qh = kout;  // lower bound (output keys are in word order)
+      if (rsh == 0) {   // word order is (hash << shift) order: compare those directly
+        const uint64_t t = cpkh[e] << ks;
+        while (ql < qh) {
+          const uint32_t mid = (ql + qh) >> 1;
+          const bool less = (L.okh[mid] << ks) < t;
+          ql = less ? mid + 1 : ql;
+          qh = less ? qh : mid;
+        }
+      } else {
+        const uint64_t t44 = rel44(cpkh[e]);
+        while (ql < qh) {
+          const uint32_t mid = (ql + qh) >> 1;
+          const bool less = rel44(L.okh[mid]) < t44;
+          ql = less ? mid + 1 : ql;
+          qh = less ? qh : mid;
+        }
       }
-      if (lo < kout && L.okh[lo] == cpkh[e] && L.okf[lo] == cpkf[e] && (L.otp[lo] & 0xFF) <= TAG_SET) {
-        const uint32_t KT = L.otp[lo] & 0xFF, khp = L.otp[lo] >> 8, p = meta_pos(cm[e]);
+      if (ql < kout && L.okh[ql] == cpkh[e] && L.okf[ql] == cpkf[e] && (L.otp[ql] & 0xFF) <= TAG_SET) {
+        const uint32_t KT = L.otp[ql] & 0xFF, khp = L.otp[ql] >> 8, p = meta_pos(cm[e]);
         const bool type_ok = isn ? KT == TAG_COUNTER : (KT == TAG_SET || KT == TAG_DICT);
-        const bool elem_ok = (L.ovm[lo] >> p) & 1;
+        const bool elem_ok = (L.ovm[ql] >> p) & 1;
         const bool cand = isn || meta_tag(cm[e]) == KIND_ADD || p == khp;  // remote dels ignored
         clive[e] = type_ok && elem_ok && cand;
-        ckey[e] = lo;
+        ckey[e] = ql;
       } else {
         ++orph;
       }
@@ -601,9 +643,11 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   for (int e = 0; e < CE; ++e) {
     const uint32_t c = lane + 64 * e;
     const bool isn = c < N;
-    const uint64_t ih = isn ? mix64(cid1[e]) : cid1[e];
-    cw[e] = clive[e] ? (((uint64_t)ckey[e] << 56) | ((ih & kM42) << 14) | ((uint64_t)meta_pos(cm[e]) << 8) | c)
-                     : ~0ull;
+    cw[e] = ~0ull;
+    if (clive[e]) {
+      const uint64_t ih = isn ? mix64(cid1[e]) : cid1[e];
+      cw[e] = ((uint64_t)ckey[e] << 56) | ((ih & kM42) << 14) | ((uint64_t)meta_pos(cm[e]) << 8) | c;
+    }
     const uint64_t Lm = __ballot(clive[e]);
     if (clive[e]) L.sw[nlive + lane_rank(Lm)] = cw[e];
     nlive += __popcll(Lm);

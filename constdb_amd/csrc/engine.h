@@ -22,7 +22,9 @@ struct cdb_ctx {
   uint32_t wave_slots[2] = {0, 0};
   void* pin = nullptr;                                // pinned staging ring of host<->device copies
   hipEvent_t pin_ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  uint64_t pin_next = 0;                              // next slot of the ring (continues across calls)  // resident streaming-wave-kernel workgroups per variant (0 = not queried)
+  uint64_t pin_next = 0;                              // next slot of the ring (continues across calls)
+  uint64_t runs_host[3 * 65] = {};                    // sorted-run path: run starts staged for the device
+  uint32_t runs_err = 0;                              // sorted-run path: run_mark_kernel's verdict
 };
 
 namespace cdb {
@@ -41,6 +43,7 @@ enum WsSlot {
   WS_LOOKBACK,                                          // output look-back status words
   WS_HOST_IN_K, WS_HOST_IN_N, WS_HOST_IN_M,             // cdb_merge: uploaded batches
   WS_HOST_OUT_K, WS_HOST_OUT_N, WS_HOST_OUT_M,          // cdb_merge: device-side result
+  WS_RUNDIR, WS_RUNMISC,                                // sorted-run path: run directories, gap lists
   WS_COUNT
 };
 

@@ -11,6 +11,7 @@
 #include "bucket_wave.hip.h"
 #include "engine.h"
 #include "partition.hip.h"
+#include "runs.hip.h"
 
 namespace cdb {
 
@@ -425,6 +426,85 @@ cdb_status stamp_pos(cdb_ctx* ctx, uint64_t* meta, uint64_t n, uint32_t pos, hip
   return launch_check(ctx, s, "stamp_pos");
 }
 
+namespace {
+// Sorted-run input: checks the caller's run bounds, builds the run directories (run_mark_kernel)
+// and, when every run really is ordered, the bucket directories of the three families. *ok =
+// false sends the merge to the partition path (a run that decreases somewhere).
+cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, uint64_t nb, int shift, const Dir* dirs,
+                          RunView* V, bool* ok, hipStream_t s) {
+  *ok = false;
+  const uint32_t nr = in->n_runs;
+  if (nr > (uint32_t)kMaxRuns) return fail(ctx, CDB_BAD_ARGUMENT, "n_runs > 64");
+  if (nr > (uint32_t)kMaxRuns / 2) return CDB_OK;  // a wave maps 2 nr child slices: partition path
+  const cdb_dev_rows* fam[3] = {&in->keys, &in->nodes, &in->members};
+  for (int f = 0; f < 3; ++f) {
+    if (in->run_start[f][0] != 0 || in->run_start[f][nr] != fam[f]->n)
+      return fail(ctx, CDB_BAD_ARGUMENT, "run_start must run from 0 to the family's row count");
+    for (uint32_t r = 0; r < nr; ++r)
+      if (in->run_start[f][r + 1] < in->run_start[f][r]) return fail(ctx, CDB_BAD_ARGUMENT, "run_start decreases");
+  }
+  cdb_status st = CDB_OK;
+  const uint64_t row = nb + 1, per_fam = (uint64_t)nr * row;
+  uint32_t* rdir = (uint32_t*)ws_get(ctx, WS_RUNDIR, 3 * per_fam * sizeof(uint32_t), &st);
+  if (!rdir) return st;
+  const uint32_t gap_cap = (uint32_t)std::min<uint64_t>(nr * (nb / kGapInline + 2), 1u << 30);
+  uint8_t* rm = (uint8_t*)ws_get(ctx, WS_RUNMISC, 64 + 3 * (kMaxRuns + 1) * 8 + 3 * (uint64_t)gap_cap * 16, &st);
+  if (!rm) return st;
+  uint32_t* d_err = (uint32_t*)rm;            // err | gap_count[3]
+  uint64_t* d_rbase = (uint64_t*)(rm + 64);   // 3 x 65 run starts
+  uint32_t* d_gaps = (uint32_t*)(rm + 64 + 3 * (kMaxRuns + 1) * 8);
+  for (int f = 0; f < 3; ++f)
+    for (uint32_t r = 0; r <= (uint32_t)kMaxRuns; ++r)
+      ctx->runs_host[f * (kMaxRuns + 1) + r] = r <= nr ? in->run_start[f][r] : in->run_start[f][nr];
+  CDB_HIP(hipMemcpyAsync(d_rbase, ctx->runs_host, sizeof ctx->runs_host, hipMemcpyHostToDevice, s), "h2d runs");
+  CDB_HIP(hipMemsetAsync(d_err, 0, 16, s), "memset");
+  for (int f = 0; f < 3; ++f) {
+    uint32_t* rd = rdir + f * per_fam;
+    for (uint32_t r = 0; r < nr; ++r)  // empty runs: every bucket starts at row 0
+      if (in->run_start[f][r + 1] == in->run_start[f][r])
+        CDB_HIP(hipMemsetAsync(rd + r * row, 0, row * sizeof(uint32_t), s), "memset run");
+    const uint64_t n = fam[f]->n;
+    if (n) {
+      RunMarkArgs a;
+      a.kh = fam[f]->col[0];
+      a.rs = d_rbase + f * (kMaxRuns + 1);
+      a.nr = nr;
+      a.nb = nb;
+      a.shift = shift;
+      a.rdir = rd;
+      a.gaps = d_gaps + (uint64_t)f * gap_cap * 4;
+      a.gap_count = d_err + 1 + f;
+      a.gap_cap = gap_cap;
+      a.err = d_err;
+      const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 16384);
+      run_mark_kernel<<<(uint32_t)blocks, 256, 0, s>>>(a, n);
+      CDB_TRY(launch_check(ctx, s, "run_mark_kernel"));
+      run_gap_kernel<<<1024, 256, 0, s>>>(a.gaps, a.gap_count, gap_cap, rd, nb);
+      CDB_TRY(launch_check(ctx, s, "run_gap_kernel"));
+    }
+    V->rdir[f] = rd;
+  }
+  CDB_HIP(hipMemcpyAsync(&ctx->runs_err, d_err, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");
+  CDB_HIP(hipStreamSynchronize(s), "sync");
+  if (ctx->runs_err) return CDB_OK;  // a run is not ordered (or the gap list overflowed)
+  for (int f = 0; f < 3; ++f) {
+    const uint64_t blocks = std::min<uint64_t>((nb + 255) / 256, 8192);
+    run_reduce_kernel<<<(uint32_t)blocks, 256, 0, s>>>(V->rdir[f], nr, nb, dirs[f].base, dirs[f].hist);
+    CDB_TRY(launch_check(ctx, s, "run_reduce_kernel"));
+  }
+  V->rbase = d_rbase;
+  V->nr = nr;
+  V->nbp1 = (uint32_t)row;
+  for (int c = 0; c < kKeyCols; ++c) V->kin[c] = in->keys.col[c];
+  for (int c = 0; c < kNodeCols; ++c) {
+    V->nin[c] = in->nodes.col[c];
+    V->min[c] = in->members.col[c];
+  }
+  *ok = true;
+  return CDB_OK;
+}
+}  // namespace
+
 cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts,
                              cdb_dev_output* out, cdb_merge_stats* stats, hipStream_t s) {
   const uint64_t K = in->keys.n, N = in->nodes.n, M = in->members.n;
@@ -478,7 +558,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   CDB_HIP(hipMemsetAsync(d_shards, 0, kStatShards * kStatStride * sizeof(unsigned long long), s), "memset stats");
 
   CDB_HIP(hipEventRecord(ctx->ev0, s), "event");
-  // ---- 1. bucket partition of each family by (parent) key hash
+  // ---- 1. bucket partition of each family by (parent) key hash, or, for sorted runs, the
+  //         run directories (runs.hip.h)
   uint64_t *krows = nullptr, *nrows = nullptr, *mrows = nullptr;
   uint64_t *ksp[8], *nsp[6], *msp[6];
   uint64_t* kin[8];
@@ -491,9 +572,27 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   }
   uint32_t* perm = (uint32_t*)ws_get(ctx, WS_PERM, (K + N + M + 3) * sizeof(uint32_t), &st);
   if (!perm) return st;
+  uint32_t *kperm = perm, *nperm = perm + K, *mperm = perm + K + N;
+  RunView RV;
+  std::memset(&RV, 0, sizeof RV);
+  bool use_runs = false;
+  static const bool no_runs = std::getenv("CDB_NO_RUNS") != nullptr;
+  if (in->n_runs && !no_runs) {
+    const Dir dirs[3] = {dk, dnd, dm};
+    CDB_TRY(runs_directory(ctx, in, nb, shift, dirs, &RV, &use_runs, s));
+  }
+  if (use_runs) {  // rows stay in the runs; KA/NA/MA take the rows of the workgroup tiers
+    krows = KA[0];
+    nrows = NA[0];
+    mrows = MA[0];
+    for (int c = 0; c < 8; ++c) ksp[c] = KB[c];
+    for (int c = 0; c < 6; ++c) {
+      nsp[c] = NB[c];
+      msp[c] = MBf[c];
+    }
+  } else {
   uint64_t* khcol = (uint64_t*)ws_get(ctx, WS_KHCOL, (K + N + M + 3) * sizeof(uint64_t), &st);
   if (!khcol) return st;
-  uint32_t *kperm = perm, *nperm = perm + K, *mperm = perm + K + N;
   // the three families partition independently (own buffers, directories, scan scratch):
   // nodes and members run on side streams beside the keys
   static const bool part_serial = std::getenv("CDB_PART_SERIAL") != nullptr;
@@ -519,8 +618,9 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     uint64_t* const* free_k = (krows == KA[0]) ? KB : KA;
     for (int c = 0; c < 8; ++c) ksp[c] = free_k[c];
   }
+  }  // partition path
 
-  if (std::getenv("CDB_VERIFY_PARTITION")) {  // debugging aid: perm must be a permutation
+  if (!use_runs && std::getenv("CDB_VERIFY_PARTITION")) {  // debugging aid: perm must be a permutation
     CDB_HIP(hipStreamSynchronize(s), "sync");
     const uint64_t fam_n[3] = {K, N, M};
     const uint32_t* fam_p[3] = {kperm, nperm, mperm};
@@ -574,6 +674,14 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   A.gc_wm = wm;
   A.force_tier = opts ? opts->force_tier : 0;
   A.key_shift = shift;
+  A.bw = ~0ull / nb;
+  {
+    const uint64_t span = A.bw + 2 * nb + 2;  // > the hash span of any bucket measured from b * bw
+    int bits = 0;
+    while (bits < 64 && (span >> bits)) ++bits;
+    if (span < A.bw) bits = 64;  // (wrapped: a handful of buckets)
+    A.rel_shift = bits > 44 ? bits - 44 : 0;
+  }
   A.last_bad = (const uint64_t*)d_last_bad;
   A.stats = d_shards;
   A.hot_list = d_hot_list;
@@ -609,13 +717,40 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   WA.nbuckets = (uint32_t)nb;
   WA.big_list = d_big_list;
   WA.big_count = d_big_count;
+  WA.V = RV;
   CDB_HIP(hipEventRecord(ctx->ev_fork, s), "event");  // inputs of both bucket tiers are ready
-  if (wave_pf() == 0)
+  if (use_runs) {
+    bucket_wave_runs_kernel<<<(uint32_t)((nb + kWavesPerWG - 1) / kWavesPerWG), kWavesPerWG * 64, 0, s>>>(WA);
+    CDB_TRY(launch_check(ctx, s, "bucket_wave_runs_kernel"));
+    static const bool serial = std::getenv("CDB_WIDE_SERIAL") != nullptr;
+    hipStream_t ws = serial ? s : ctx->side;
+    const uint32_t g = (uint32_t)std::min<uint64_t>((nb + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024);
+    if (!serial) CDB_HIP(hipStreamWaitEvent(ws, ctx->ev_fork, 0), "wait");
+    bucket_wide_runs_kernel<<<g, kWavesPerWG * 64, 0, ws>>>(WA);
+    CDB_TRY(launch_check(ctx, ws, "bucket_wide_runs_kernel"));
+    if (!serial) {
+      CDB_HIP(hipEventRecord(ctx->ev_join, ws), "event");
+      CDB_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0), "wait");
+    }
+    // the workgroup tiers' buckets: copied out of the runs into AoS rows + row indices
+    MatArgs MA_;
+    MA_.kr = krows;
+    MA_.nr = nrows;
+    MA_.mr = mrows;
+    MA_.kp = kperm;
+    MA_.np = nperm;
+    MA_.mp = mperm;
+    MA_.cursor = (unsigned long long*)(misc + 104);
+    CDB_HIP(hipMemsetAsync(MA_.cursor, 0, 3 * sizeof(unsigned long long), s), "memset");
+    materialize_kernel<<<std::min<uint64_t>(nb, 2048), 256, 0, s>>>(WA, MA_, d_big_list, d_big_count);
+    CDB_TRY(launch_check(ctx, s, "materialize_kernel"));
+  } else if (wave_pf() == 0)
     bucket_wave_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA);
   else if (wave_pf() == 1)
     bucket_wave_pf1_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
   else
     bucket_wave_pf2_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
+  if (!use_runs) {
   CDB_TRY(launch_check(ctx, s, "bucket_wave_kernel"));
   {  // the wide tier's buckets are disjoint from the wave tier's: it runs on a side stream
      // and fills the wave kernel's tail (CDB_WIDE_SERIAL=1 runs it after the wave kernel)
@@ -630,6 +765,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
       CDB_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0), "wait");
     }
   }
+  }  // partition path tiers
   bucket_mid_kernel<<<std::min<uint64_t>(nb, 2048), kBktThreads, 0, s>>>(A, d_big_list, d_big_count);
   CDB_TRY(launch_check(ctx, s, "bucket_mid_kernel"));
   CDB_HIP(hipEventRecord(ctx->ev_bucket, s), "event");
@@ -728,6 +864,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     stats->bucket_ms = ms;
     hipEventElapsedTime(&ms, ctx->ev_bucket, ctx->ev1);
     stats->finish_ms = ms;
+    stats->sorted_runs = use_runs ? 1 : 0;
   }
   if ((flags & CDB_MERGE_STRICT_DICT_PANIC) && hs[ST_DICT_MERGES])
     return fail(ctx, CDB_DICT_MERGE_UNIMPLEMENTED, "Dict::merge reached (lwwhash.rs:180 unimplemented!())");

@@ -1,0 +1,309 @@
+// Sorted-run merge path (gfx950): inputs whose rows are already grouped into runs ordered by key
+// hash -- one run per replica, as this engine's own merge output is (bucket order, then exact
+// key-hash order inside a bucket) and as a snapshot written from it and decoded again is.
+//
+// The partition pass disappears: a bucket's rows are a few consecutive rows of every run.
+//   1. run_mark_kernel: one streaming read of column 0 (the key hash; 8 B of each row) finds,
+//      for every run and bucket, the run-relative first row of the bucket (the run directory,
+//      run-major: rdir[r * (nb + 1) + b]), and verifies that every run is non-decreasing in
+//      (hash << key_shift) -- a violation sends the merge to the partition path;
+//   2. run_reduce_kernel: per bucket, the row count and the exclusive prefix over buckets (the
+//      same bucket directory the partition path builds; the other tiers and the compaction
+//      read it unchanged);
+//   3. the wave / wide kernels read each bucket's rows straight from the caller's SoA columns,
+//      lane by lane, consecutive rows of each run on consecutive lanes; buckets beyond a wave
+//      are materialised as AoS rows + row indices (materialize_kernel), the layout the
+//      workgroup tiers (bucket.hip.h) read.
+// Bucket function, folds and outputs are those of the partition path, so both paths produce the
+// same result row for row (tests/test_sorted_runs_gpu.py).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bucket_wave.hip.h"
+#include "common.h"
+
+namespace cdb {
+
+constexpr int kMaxRuns = 64;          // runs per family (cdb_dev_input.run_start rows)
+constexpr uint32_t kGapInline = 32;  // longer directory gaps go to the gap list
+
+struct RunMarkArgs {
+  const uint64_t* kh;        // column 0 of the family
+  const uint64_t* rs;        // device copy of run_start[f][0 .. nr]
+  uint32_t nr;
+  uint64_t nb;
+  int shift;
+  uint32_t* rdir;            // nr x (nb + 1)
+  uint32_t* gaps;            // 4 u32 per entry: run, first bucket, last bucket, value
+  uint32_t* gap_count;
+  uint32_t gap_cap;
+  uint32_t* err;             // bit 0: a run decreases; bit 1: gap list overflow
+};
+
+__device__ __forceinline__ void run_fill(const RunMarkArgs& a, uint32_t r, uint64_t c0, uint64_t c1, uint32_t v) {
+  // buckets c0 .. c1 (inclusive) of run r start at run row v
+  if (c0 > c1) return;
+  if (c1 - c0 < kGapInline) {
+    uint32_t* row = a.rdir + (uint64_t)r * (a.nb + 1);
+    for (uint64_t c = c0; c <= c1; ++c) row[c] = v;
+    return;
+  }
+  const uint32_t k = atomicAdd(a.gap_count, 1u);
+  if (k >= a.gap_cap) {
+    atomicOr(a.err, 2u);
+    return;
+  }
+  uint4* g = reinterpret_cast<uint4*>(a.gaps) + k;
+  *g = make_uint4(r, (uint32_t)c0, (uint32_t)c1, v);
+}
+
+// One thread per row: the first row of each (run, bucket) writes the directory entries of every
+// bucket from its predecessor's bucket + 1 up to its own (empty buckets start where the next
+// non-empty one does); the last row of a run closes the run's remaining buckets.
+__global__ void __launch_bounds__(256) run_mark_kernel(RunMarkArgs a, uint64_t n) {
+  __shared__ uint64_t rs[kMaxRuns + 1];
+  for (uint32_t i = threadIdx.x; i <= a.nr; i += blockDim.x) rs[i] = a.rs[i];
+  __syncthreads();
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t lo = 0, hi = a.nr;  // run r: rs[r] <= i < rs[r + 1]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (rs[mid] <= i) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t r = lo;
+    const uint64_t rel = i - rs[r], len = rs[r + 1] - rs[r];
+    const uint64_t h = a.kh[i] << a.shift;
+    const uint64_t b = __umul64hi(h, a.nb);
+    uint64_t c0 = 0;
+    if (rel) {
+      const uint64_t hp = a.kh[i - 1] << a.shift;
+      if (hp > h) atomicOr(a.err, 1u);
+      c0 = __umul64hi(hp, a.nb) + 1;
+    }
+    run_fill(a, r, c0, b, (uint32_t)rel);
+    if (rel + 1 == len) run_fill(a, r, b + 1, a.nb, (uint32_t)len);
+  }
+}
+
+// The long gaps, one workgroup per entry.
+__global__ void __launch_bounds__(256) run_gap_kernel(const uint32_t* __restrict__ gaps, const uint32_t* gap_count,
+                                                      uint32_t gap_cap, uint32_t* __restrict__ rdir, uint64_t nb) {
+  const uint32_t n = min(*gap_count, gap_cap);
+  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) {
+    const uint4 g = reinterpret_cast<const uint4*>(gaps)[k];
+    uint32_t* row = rdir + (uint64_t)g.x * (nb + 1);
+    for (uint64_t c = (uint64_t)g.y + threadIdx.x; c <= g.z; c += blockDim.x) row[c] = g.w;
+  }
+}
+
+// Bucket directory of the family from its run directory: count[b] and the exclusive prefix
+// base[b] = sum over runs of the run-relative first row of b.
+__global__ void __launch_bounds__(256) run_reduce_kernel(const uint32_t* __restrict__ rdir, uint32_t nr, uint64_t nb,
+                                                         uint32_t* __restrict__ base, uint32_t* __restrict__ cnt) {
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t s0 = 0, s1 = 0;
+    for (uint32_t r = 0; r < nr; ++r) {
+      s0 += rdir[(uint64_t)r * (nb + 1) + b];
+      s1 += rdir[(uint64_t)r * (nb + 1) + b + 1];
+    }
+    base[b] = s0;
+    cnt[b] = s1 - s0;
+  }
+}
+
+// A bucket's slices of the runs, one per lane: lane j < L holds slice j of the family group --
+// keys: the nr key runs; children: the nr node runs, then the nr member runs (child slots are
+// node rows first, then member rows). incl = inclusive prefix of the slice lengths over lanes;
+// off = absolute row of the slice's first row minus its first slot (row of slot c = off + c).
+struct RunMap {
+  uint32_t incl, L;
+  uint64_t off;
+};
+
+__device__ __forceinline__ RunMap run_map(const RunView& V, uint32_t b, int lane, bool children) {
+  RunMap q;
+  q.L = children ? 2 * V.nr : V.nr;
+  uint32_t s = 0, n = 0;
+  uint64_t rb = 0;
+  if ((uint32_t)lane < q.L) {
+    const int f = children ? 1 + (lane >= (int)V.nr) : 0;
+    const uint32_t r = (uint32_t)lane - (f == 2 ? V.nr : 0);
+    const uint32_t* row = V.rdir[f] + (uint64_t)r * V.nbp1;
+    s = row[b];
+    n = row[b + 1] - s;
+    rb = V.rbase[f * (kMaxRuns + 1) + r];
+  }
+  uint32_t incl = n;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  q.incl = incl;
+  q.off = rb + s - (incl - n);
+  return q;
+}
+
+// Absolute row of slot c: its slice is the number of slices that end at or before c (incl is
+// non-decreasing over the lanes), found by a binary search over the lanes' incl.
+__device__ __forceinline__ uint64_t run_row(const RunMap& q, uint32_t c) {
+  uint32_t r = 0;
+  uint32_t k = 1;
+  while (2 * k <= q.L) k <<= 1;
+  for (; k; k >>= 1) {
+    const uint32_t v = (uint32_t)__shfl((int)q.incl, (int)min(r + k - 1, q.L - 1), 64);
+    if (r + k <= q.L && v <= c) r += k;
+  }
+  r = min(r, q.L - 1);
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)q.off, (int)r, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(q.off >> 32), (int)r, 64);
+  return (((uint64_t)hi << 32) | lo) + c;
+}
+
+// The columns of bucket b (KE key rows and 2 KE child rows per lane) from the runs.
+template <int KE>
+__device__ __forceinline__ void load_runs(const WaveArgs& W, const WaveDir& d, uint32_t b, int lane,
+                                          WaveIn<KE>& in) {
+  const RunView& V = W.V;
+  const RunMap qk = run_map(V, b, lane, false), qc = run_map(V, b, lane, true);
+  in.d = d;
+  const uint32_t C = d.N + d.M;
+#pragma unroll
+  for (int e = 0; e < KE; ++e) {
+    const uint32_t c = lane + 64 * e;
+    in.kh[e] = in.kf[e] = in.kct[e] = in.kut[e] = in.kdt[e] = in.kaux[e] = in.kmeta[e] = 0;
+    const uint64_t row = run_row(qk, c);
+    if (c < d.K) {
+      in.kh[e] = V.kin[K_KH][row];
+      in.kf[e] = V.kin[K_KF][row];
+      in.kct[e] = V.kin[K_CT][row];
+      in.kut[e] = V.kin[K_UT][row];
+      in.kdt[e] = V.kin[K_DT][row];
+      in.kaux[e] = V.kin[K_AUX][row];
+      in.kmeta[e] = V.kin[K_META][row];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 2 * KE; ++e) {
+    const uint32_t c = lane + 64 * e;
+    in.cpkh[e] = in.cpkf[e] = in.cid1[e] = in.cid2[e] = in.ct[e] = in.cm[e] = 0;
+    if (__ballot(c < C) == 0) continue;  // (uniform) no child in this slot group
+    const uint64_t row = run_row(qc, c);
+    if (c < C) {
+      const uint64_t* const* col = c < d.N ? V.nin : V.min;
+      in.cpkh[e] = col[C_PKH][row];
+      in.cpkf[e] = col[C_PKF][row];
+      in.cid1[e] = col[C_ID1][row];
+      in.cid2[e] = col[C_ID2][row];
+      in.ct[e] = col[C_T][row];
+      in.cm[e] = col[C_META][row];
+    }
+  }
+}
+
+// Workgroups are dispatched round-robin over the 8 XCDs; XCD x takes one contiguous range of
+// buckets, so neighbouring buckets (which share the runs' cache lines) meet in one L2.
+__device__ __forceinline__ uint32_t xcd_bucket(uint32_t blk, uint32_t G, int wv) {
+  const uint32_t q = G / kXcds, r = G % kXcds, x = blk % kXcds, j = blk / kXcds;
+  return (x * q + min(x, r) + j) * kWavesPerWG + wv;
+}
+
+__global__ void __launch_bounds__(kWavesPerWG * 64, 5) bucket_wave_runs_kernel(WaveArgs W) {
+  __shared__ WaveLds<1> lds_all[kWavesPerWG];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t b = xcd_bucket(blockIdx.x, gridDim.x, wv);
+  if (b >= W.nbuckets) return;
+  const WaveDir d = load_dir(W.A, b);
+  WaveIn<1> in;
+  load_runs<1>(W, d, b, lane, in);
+  wave_bucket<1>(W, lds_all[wv], b, lane, in, []() {});
+}
+
+// The wide tier (65..128 key rows or 129..256 child rows) on the runs: as bucket_wide_kernel.
+__global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_runs_kernel(WaveArgs W) {
+  __shared__ WaveLds<2> lds_all[kWavesPerWG];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t groups = (W.nbuckets + 63) / 64;
+  unsigned long long found = 0;
+  for (uint32_t g = blockIdx.x * kWavesPerWG + wv; g < groups; g += gridDim.x * kWavesPerWG) {
+    const uint32_t b = g * 64 + lane;
+    uint64_t m = __ballot(b < W.nbuckets && wide_bucket_candidate(W.A, b));
+    found += __popcll(m);
+    while (m) {
+      const int i = __builtin_ctzll(m);
+      m &= m - 1;
+      const uint32_t bb = g * 64 + i;
+      const WaveDir d = load_dir(W.A, bb);
+      WaveIn<2> in;
+      load_runs<2>(W, d, bb, lane, in);
+      wave_bucket<2>(W, lds_all[wv], bb, lane, in, []() {});
+    }
+  }
+  if (lane == 0 && found) atomicAdd(&stat_shard(W.A.stats)[ST_WIDE], found);
+}
+
+// Buckets handed to the workgroup tiers: their rows are copied out of the runs into AoS rows
+// (8-word key rows, 6-word child rows, at a place reserved with one atomic per bucket and
+// family) and the row indices of the bucket are written to the permutation, so that
+// bucket.hip.h reads them as it reads partitioned rows.
+struct MatArgs {
+  uint64_t *kr, *nr, *mr;        // AoS scratch rows
+  uint32_t *kp, *np, *mp;        // permutations (indexed by the bucket's base + slot)
+  unsigned long long* cursor;    // 3 scratch cursors
+};
+
+__global__ void __launch_bounds__(256) materialize_kernel(WaveArgs W, MatArgs M, const uint32_t* __restrict__ list,
+                                                          const uint32_t* __restrict__ count) {
+  const RunView& V = W.V;
+  const BucketArgs& A = W.A;
+  __shared__ uint64_t rb[3][kMaxRuns + 1];
+  __shared__ uint32_t rs[3][kMaxRuns + 1], pre[3][kMaxRuns + 2];
+  __shared__ unsigned long long base[3];
+  const uint32_t total = *count;
+  for (uint32_t li = blockIdx.x; li < total; li += gridDim.x) {
+    const uint32_t b = list[li];
+    __syncthreads();
+    if (threadIdx.x < 3 * V.nr) {
+      const uint32_t f = threadIdx.x / V.nr, r = threadIdx.x % V.nr;
+      const uint32_t* row = V.rdir[f] + (uint64_t)r * V.nbp1;
+      rs[f][r] = row[b];
+      pre[f][r + 1] = row[b + 1] - row[b];
+      rb[f][r] = V.rbase[f * (kMaxRuns + 1) + r];
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+      const uint32_t f = threadIdx.x;
+      pre[f][0] = 0;
+      for (uint32_t r = 0; r < V.nr; ++r) pre[f][r + 1] += pre[f][r];
+      base[f] = atomicAdd(&M.cursor[f], (unsigned long long)pre[f][V.nr]);
+    }
+    __syncthreads();
+    const uint32_t kb[3] = {A.kbase[b], A.nbase[b], A.mbase[b]};
+    for (int f = 0; f < 3; ++f) {
+      const uint32_t n = pre[f][V.nr];
+      for (uint32_t c = threadIdx.x; c < n; c += blockDim.x) {
+        uint32_t r = 0;
+        while (r + 1 < V.nr && pre[f][r + 1] <= c) ++r;
+        const uint64_t src = rb[f][r] + rs[f][r] + (c - pre[f][r]);
+        const uint64_t dst = base[f] + c;
+        if (f == 0) {
+          uint64_t* o = M.kr + dst * kKeyStride;
+#pragma unroll
+          for (int k = 0; k < kKeyCols; ++k) o[k] = V.kin[k][src];
+          o[kKeyCols] = 0;
+          M.kp[kb[0] + c] = (uint32_t)dst;
+        } else {
+          const uint64_t* const* in = f == 1 ? V.nin : V.min;
+          uint64_t* o = (f == 1 ? M.nr : M.mr) + dst * kChildStride;
+#pragma unroll
+          for (int k = 0; k < kChildStride; ++k) o[k] = in[k][src];
+          (f == 1 ? M.np : M.mp)[kb[f] + c] = (uint32_t)dst;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace cdb

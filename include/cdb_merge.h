@@ -145,6 +145,7 @@ typedef struct cdb_merge_stats {
   double   partition_ms;     /* bucket partition of the three row families */
   double   bucket_ms;        /* fused bucket-merge kernel (the dominant kernel) */
   double   finish_ms;        /* over-capacity buckets + dense compaction */
+  uint64_t sorted_runs;      /* 1 when the sorted-run path ran (partition_ms = its run directories) */
 } cdb_merge_stats;
 
 cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n,
@@ -276,10 +277,19 @@ typedef struct cdb_dev_rows {
                        members: pkh pkf mh mf t meta */
   uint64_t n;
 } cdb_dev_rows;
+#define CDB_MAX_RUNS 64
 typedef struct cdb_dev_input {
   cdb_dev_rows keys, nodes, members;
   uint32_t n_pos;
-  uint32_t reserved;
+  uint32_t n_runs;  /* 0: rows in any order (the partition path). 1..64: the rows of every family
+                       are n_runs consecutive runs, run r = rows [run_start[f][r], run_start[f][r+1])
+                       of family f (0 keys, 1 nodes, 2 members), each non-decreasing in column 0
+                       (the key hash; children: the parent key hash) -- one run per replica, as
+                       this engine's merge output and snapshots encoded from it are. Then the
+                       merge reads the runs in place (no partition pass). A run found out of
+                       order, or more than 32 runs, send the merge to the partition path; the
+                       result is the same. */
+  uint64_t run_start[3][CDB_MAX_RUNS + 1];
 } cdb_dev_input;
 /* Outputs are written sparse-by-bucket: bucket b's rows start at the bucket's input
  * offset; dense compaction into *_dense happens when cdb_dev_output.compact != 0. */
