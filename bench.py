@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--force-dist", action="store_true",
                     help="use the multi-GPU (RCCL all-to-all) path even when WORLD_SIZE == 1")
     ap.add_argument("--c3-ops", type=int, default=10_000_000, help="ops per replica of config c3")
+    ap.add_argument("--force-tier", type=int, default=0, help="testing: cdb_merge_opts.force_tier")
     ap.add_argument("--input-order", default="sorted", choices=["sorted", "hash-random"],
                     help="sorted: every replica's rows form one run in key-hash order (as this engine's merge "
                          "output and snapshots encoded from it are; the sorted-run path); hash-random: rows "
@@ -237,6 +238,7 @@ def run_single(cdb, args):
     ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.members), din.members.n, 6))
     dout.compact = 1
     st = cdb.MergeStats()
+    opts.force_tier = args.force_tier
 
     def step():
         ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(din), ctypes.byref(opts), ctypes.byref(dout),

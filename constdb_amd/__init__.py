@@ -17,7 +17,7 @@ import os
 from typing import List, Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "libcdbmerge.so")
+_LIB_PATH = os.environ.get("CDB_LIB", os.path.join(_HERE, "libcdbmerge.so"))  # CDB_LIB: profiling builds
 
 # ----------------------------------------------------------------- errors (lib.rs:146-175)
 OK = 0

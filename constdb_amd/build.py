@@ -25,12 +25,21 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, out=None, defines=()):
+    """Builds the library (out/defines: profiling variants, e.g. scripts/wave_phases.sh)."""
+    if out is not None:
+        hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+        cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-w",
+               *[f"-D{d}" for d in defines], "-o", out] + [os.path.join(CSRC, f) for f in SOURCES]
+        subprocess.check_call(cmd)
+        return out
+    if os.environ.get("CDB_LIB"):
+        return os.environ["CDB_LIB"]
     if not force and not _stale():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+           "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unused-value",
            "-o", OUT + ".tmp"] + [os.path.join(CSRC, f) for f in SOURCES]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

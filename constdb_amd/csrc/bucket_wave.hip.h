@@ -37,6 +37,11 @@
 namespace cdb {
 
 constexpr int kWavesPerWG = 4;
+// Profiling builds only (-DCDB_WAVE_STOP=n, scripts/wave_phases.sh): stop a bucket after phase n
+// and sink what it computed into a spare statistics word, to time the phases of the wave kernel.
+#ifndef CDB_WAVE_STOP
+#define CDB_WAVE_STOP 99
+#endif
 // Cooperative row loads (load_cols_coop) cut the vector-memory accesses per row 3-4x but were
 // measured slower on MI355X (wave kernel 16.2 -> 17.2 ms, wide 5.0 -> 8.8 ms on the C4 shard:
 // the LDS transpose and its syncs cost more than the saved accesses). Off by default.
@@ -438,6 +443,14 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     cm[e] = in.cm[e];
   }
 
+  if (CDB_WAVE_STOP <= 0) {
+    const unsigned long long sk = wave_sum_u64((unsigned long long)(in.kh[0] ^ in.kf[0] ^ in.kct[0] ^ in.kut[0] ^ in.kdt[0] ^ in.kaux[0] ^ in.kmeta[0] ^ in.cpkh[0] ^ in.cpkf[0] ^ in.cid1[0] ^ in.cid2[0] ^ in.ct[0] ^ in.cm[0] ^ in.cpkh[CE-1] ^ in.cm[CE-1]));
+    if (lane == 0) {
+      A.kout[b] = A.nout[b] = A.mout[b] = 0;
+      atomicAdd(&stat_shard(A.stats)[kStatStride - 1], sk);
+    }
+    return;
+  }
   // ------------------------------------------------------------ 1. keys: rank + scatter
   // word = rel << 20 | family << 18 | pos << 12 | slot   (pos < 64, slot < 4096), where rel is
   // the 44 leading bits of (kh << shift) - b * bw (BucketArgs): monotone in the key hash, so the
@@ -500,6 +513,14 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     return;
   }
 
+  if (CDB_WAVE_STOP <= 1) {
+    const unsigned long long sk = wave_sum_u64((unsigned long long)(w[0] ^ kh[0] ^ (uint64_t)Hk[0]));
+    if (lane == 0) {
+      A.kout[b] = A.nout[b] = A.mout[b] = 0;
+      atomicAdd(&stat_shard(A.stats)[kStatStride - 1], sk);
+    }
+    return;
+  }
   // ------------------------------------------------------------ 2. key folds (tail slots)
   const uint64_t last_bad = (A.flags & F_GC_DELETES) ? *A.last_bad : 0;
   uint64_t o_ct[KE], o_ut[KE], o_dt[KE], o_meta[KE], o_win[KE];
@@ -593,6 +614,14 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   }
   wave_sync();
 
+  if (CDB_WAVE_STOP <= 2) {
+    const unsigned long long sk = wave_sum_u64((unsigned long long)((uint64_t)kout ^ o_ct[0] ^ o_win[0]));
+    if (lane == 0) {
+      A.kout[b] = A.nout[b] = A.mout[b] = 0;
+      atomicAdd(&stat_shard(A.stats)[kStatStride - 1], sk);
+    }
+    return;
+  }
   // ------------------------------------------------------------ 3. children: key lookup
   // word = key rank << 56 | id hash[41:0] << 14 | pos << 8 | slot   (rank < 128, slot < 256)
   unsigned long long orph = 0, gcm = 0;
@@ -679,6 +708,14 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   wave_sync();
   next();  // this bucket's input registers are dead from here on
 
+  if (CDB_WAVE_STOP <= 3) {
+    const unsigned long long sk = wave_sum_u64((unsigned long long)((uint64_t)nlive ^ cw[0] ^ orph));
+    if (lane == 0) {
+      A.kout[b] = A.nout[b] = A.mout[b] = 0;
+      atomicAdd(&stat_shard(A.stats)[kStatStride - 1], sk);
+    }
+    return;
+  }
   // ------------------------------------------------------------ 4. child folds + outputs
   bool live[CE], knode[CE], coll2 = false;
   uint64_t H[CE], Lv[CE], sw_[CE], sid1[CE], sid2[CE];

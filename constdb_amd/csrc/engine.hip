@@ -250,7 +250,7 @@ Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
   // A wave holds 64 key rows (128 in the wide kernel) and 128 child rows, so only the
   // far tail of the bucket-size distribution reaches the workgroup tier.
   uint64_t target = 40;
-  if (const char* e = std::getenv("CDB_PLAN_TARGET")) target = (uint64_t)std::max(8, std::min(60, std::atoi(e)));
+  if (const char* e = std::getenv("CDB_PLAN_TARGET")) target = (uint64_t)std::max(8, std::min(120, std::atoi(e)));
   const uint64_t want = std::max<uint64_t>({(K + target - 1) / target, (N + M + target - 1) / target, 1});
   Plan p;
   // The last level moves only a row index, so it takes a large fan-out (segments of
