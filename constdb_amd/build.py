@@ -12,7 +12,7 @@ OUT = os.path.join(HERE, "libcdbmerge.so")
 SOURCES = ["engine.hip", "gen_device.hip", "decode_gpu.hip", "ops_apply.hip", "encode_gpu.hip", "capi.cpp", "decode.cpp", "gen.cpp",
            "ops.cpp"]
 HEADERS = ["common.h", "batch.h", "engine.h", "partition.hip.h", "bucket.hip.h", "bucket_wave.hip.h",
-           "gen_model.h", "ops.h", "runs.hip.h"]
+           "gen_model.h", "ops.h", "runs.hip.h", "hot.hip.h", "radix.hip.h"]
 
 
 def _stale():

@@ -227,10 +227,11 @@ __device__ void wg_sort(uint32_t* idx, uint32_t* rk, uint32_t* cnt, uint32_t n, 
 
 __device__ __forceinline__ uint64_t imax64(uint64_t a, uint64_t b) { return (int64_t)a > (int64_t)b ? a : b; }
 
-__device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S) {
+// Key phase of one bucket by one workgroup: sorts the key rows, folds every (key, family)
+// segment, writes the key output rows (win of counters and cref are completed by the caller)
+// and leaves the sorted output keys in S.okh / okf / ovm / osum / otp / ocb / occ. Returns kout.
+__device__ uint32_t bucket_keys(const BucketArgs& A, uint32_t b, const Scratch& S) {
   const uint32_t K = A.kcnt[b], kb = A.kbase[b];
-  const uint32_t N = A.ncnt[b], nb = A.nbase[b];
-  const uint32_t M = A.mcnt[b], mb = A.mbase[b];
   uint32_t* tmp = S.misc + 4;  // 16 words for wg_scan
   for (int i = threadIdx.x; i < ST_COUNT; i += blockDim.x) S.st[i] = 0;
 
@@ -341,6 +342,16 @@ __device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S
     S.occ[o] = 0;
   }
   __syncthreads();
+  return kout;
+}
+
+__device__ void process_bucket(const BucketArgs& A, uint32_t b, const Scratch& S) {
+  const uint32_t kb = A.kbase[b];
+  const uint32_t N = A.ncnt[b], nb = A.nbase[b];
+  const uint32_t M = A.mcnt[b], mb = A.mbase[b];
+  uint32_t* tmp = S.misc + 4;  // 16 words for wg_scan
+  const uint32_t kout = bucket_keys(A, b, S);
+  const int ks = A.key_shift;
 
   // ------------------------------------------------------------ child phases
   uint32_t outs[2] = {0, 0};
@@ -505,7 +516,7 @@ __global__ void __launch_bounds__(kBktThreads) bucket_mid_kernel(BucketArgs A, c
   const uint32_t total = *count;
   for (uint32_t i = blockIdx.x; i < total; i += gridDim.x) {
     const uint32_t b = list[i];
-    if (A.kcnt[b] > kCapK || A.ncnt[b] > kCapC || A.mcnt[b] > kCapC || A.force_tier == 2) {
+    if (A.kcnt[b] > kCapK || A.ncnt[b] > kCapC || A.mcnt[b] > kCapC || A.force_tier == 2 || A.force_tier == 4) {
       if (threadIdx.x == 0) {
         const uint32_t s = atomicAdd(A.hot_count, 1u);
         A.hot_list[s] = b;

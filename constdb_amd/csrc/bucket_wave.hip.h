@@ -406,7 +406,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     if (lane == 0) list[atomicAdd(count, 1u)] = b;
   };
   if (KE == 1) {  // the wide kernel finds its buckets itself (wide_bucket_candidate)
-    if (A.force_tier == 1 || A.force_tier == 2 || N + M > WaveLds<2>::CC || K > WaveLds<2>::KC) {
+    if (A.force_tier == 1 || A.force_tier == 2 || A.force_tier == 4 || N + M > WaveLds<2>::CC || K > WaveLds<2>::KC) {
       next();
       push(W.big_list, W.big_count);
       return;
@@ -1019,7 +1019,7 @@ __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_pf1_kernel(WaveA
 // Buckets over bucket_wave_kernel's capacity but within this kernel's.
 __device__ __forceinline__ bool wide_bucket_candidate(const BucketArgs& A, uint32_t b) {
   const uint32_t K = A.kcnt[b], C = A.ncnt[b] + A.mcnt[b];
-  if (A.force_tier == 1 || A.force_tier == 2 || C > WaveLds<2>::CC || K > WaveLds<2>::KC) return false;
+  if (A.force_tier == 1 || A.force_tier == 2 || A.force_tier == 4 || C > WaveLds<2>::CC || K > WaveLds<2>::KC) return false;
   return K > WaveLds<1>::KC || C > WaveLds<1>::CC || A.force_tier == 3;
 }
 

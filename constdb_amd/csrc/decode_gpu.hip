@@ -5,8 +5,8 @@
 // is known only after its predecessor is parsed. Two passes:
 //   1. host: index_snapshot() walks the stream once with the reference loader's checks (same
 //      status codes and offsets as decode_snapshot), decodes the header, replica entries and
-//      checksum, and records each entry's byte offset and raw child count. It hashes nothing
-//      and builds no rows;
+//      checksum, and records each entry's byte offset and kind. It hashes nothing and builds
+//      no rows;
 //   2. GPU, one thread per entry, over the bytes in HBM:
 //      count_kernel   parses the entry and counts the children the loader keeps after its
 //                     load-time dedup (type_counter.rs:111-126: the last of a repeated node id;
@@ -327,10 +327,17 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   // the raw stream sits after `pad` zero bytes, so the checksummed prefix ends on a CRC tile
   const uint64_t tile = crc_tile_bytes();
   const uint64_t pad = dcrc.pending ? (tile - dcrc.len % tile) % tile : 0;
-  if (hipMalloc(&d_raw.p, pad + len + 16) != hipSuccess) return CDB_OUT_OF_MEMORY;
-  if (hipMalloc(&d_crc.p, 8) != hipSuccess) return CDB_OUT_OF_MEMORY;
+  // a failed allocation is reported with its own message and leaves no pending HIP error
+  auto alloc = [&](void** p, size_t bytes, const char* what) {
+    if (hipMalloc(p, bytes) == hipSuccess) return CDB_OK;
+    (void)hipGetLastError();
+    *p = nullptr;
+    return fail(ctx, CDB_OUT_OF_MEMORY, what);
+  };
+  if ((st = alloc(&d_raw.p, pad + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK) return st;
+  if ((st = alloc(&d_crc.p, 8, "decode: device checksum word")) != CDB_OK) return st;
   const size_t head = n * (8 + 1 + 4 + 4 + 8 + 8) + 64;
-  if (hipMalloc(&d_meta.p, head) != hipSuccess) return CDB_OUT_OF_MEMORY;
+  if ((st = alloc(&d_meta.p, head, "decode: device entry index")) != CDB_OK) return st;
   uint8_t* hm = (uint8_t*)d_meta.p;
   uint64_t* d_off = (uint64_t*)hm;
   uint64_t* d_noff = d_off + n;
@@ -392,7 +399,8 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
     uint64_t q = o;
     const uint64_t klen = rint(q);
     const Hash128 h = hash_bytes(p + q, klen, kDomainKey);
-    if (!decode_entry_children(*out, o, h.h, h.f, &he.rows, &he.total)) return CDB_DEVICE_ERROR;
+    if (!decode_entry_children(*out, o, h.h, h.f, &he.rows, &he.total))
+      return fail(ctx, CDB_DEVICE_ERROR, "decode: host tier could not re-parse an indexed entry");
     if (ncnt[i] == kHostTier) ncnt[i] = (uint32_t)he.rows.n_pkh.size();
     if (mcnt[i] == kHostTier) mcnt[i] = (uint32_t)he.rows.m_pkh.size();
     hosted.push_back(std::move(he));
@@ -407,7 +415,7 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   // (the emit pass still sees the host tier's markers in the device copies of the counts)
   DevBuf d_rows;
   const size_t rows_words = n * 11 + nn * 6 + nm * 10 + 8;
-  if (hipMalloc(&d_rows.p, rows_words * 8) != hipSuccess) return CDB_OUT_OF_MEMORY;
+  if ((st = alloc(&d_rows.p, rows_words * 8, "decode: device row columns")) != CDB_OK) return st;
   uint64_t* w = (uint64_t*)d_rows.p;
   for (int c = 0; c < 7; ++c, w += n) A.k[c] = w;
   A.kref_off = w; w += n;
@@ -426,7 +434,8 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   if (st == CDB_OK) st = staged_h2d(ctx, d_moff, moff.data(), n * 8, s);
   if (st != CDB_OK) return st;
   emit_kernel<<<grid, kDecThreads, 0, s>>>(A);
-  if (hipGetLastError() != hipSuccess) return CDB_DEVICE_ERROR;
+  ck(hipGetLastError(), "emit_kernel");
+  if (st != CDB_OK) return st;
   // rows back into the host batch: one staged download of every column
   Batch& b = *out;
   std::vector<HostSeg> segs;

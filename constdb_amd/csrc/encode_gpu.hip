@@ -647,12 +647,14 @@ struct Varints {
 
 // CRC over dev[0, padded) where padded is a whole number of tiles (zero prefix).
 cdb_status crc_device(cdb_ctx* ctx, const uint8_t* dev, uint64_t padded, uint8_t* dst, uint64_t* d_crc, hipStream_t s) {
-  static uint64_t tables[8 * 256];
-  static bool init = false;
-  if (!init) {
-    crc_tables(tables);
-    init = true;
-  }
+  // built once; a function-local static's initialisation is thread-safe (contexts may run on
+  // different threads at the same time, cdb_merge.h)
+  struct CrcTables {
+    uint64_t t[8 * 256];
+    CrcTables() { crc_tables(t); }
+  };
+  static const CrcTables tab;
+  const uint64_t* tables = tab.t;
   const uint64_t tiles = padded / kCrcTile;
   const uint64_t run = std::max<uint64_t>(1, (tiles + kCrcThreads - 1) / kCrcThreads);
   CrcConsts K;
@@ -661,9 +663,9 @@ cdb_status crc_device(cdb_ctx* ctx, const uint8_t* dev, uint64_t padded, uint8_t
   for (int k = 0; k < 8; ++k) K.run_lvl[k] = x8n_mod((kCrcTile * run) << k);
   DevMem dt, dtc;
   cdb_status st;
-  if ((st = dalloc(ctx, dt, sizeof tables)) != CDB_OK) return st;
+  if ((st = dalloc(ctx, dt, sizeof tab.t)) != CDB_OK) return st;
   if ((st = dalloc(ctx, dtc, std::max<uint64_t>(tiles, 1) * 8)) != CDB_OK) return st;
-  if ((st = h2d(ctx, dt.p, tables, sizeof tables, s)) != CDB_OK) return st;
+  if ((st = h2d(ctx, dt.p, tables, sizeof tab.t, s)) != CDB_OK) return st;
   if (tiles) crc_tile_kernel<<<tiles, kCrcThreads, 0, s>>>(dev, (const uint64_t*)dt.p, K, (uint64_t*)dtc.p);
   crc_final_kernel<<<1, kCrcThreads, 0, s>>>((const uint64_t*)dtc.p, tiles, run, run * kCrcThreads - tiles, K, d_crc,
                                             dst);

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -11,6 +12,8 @@
 #include "bucket_wave.hip.h"
 #include "engine.h"
 #include "partition.hip.h"
+#include "hot.hip.h"
+#include "radix.hip.h"
 #include "runs.hip.h"
 
 namespace cdb {
@@ -505,6 +508,166 @@ cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, uint64_t nb, in
 }
 }  // namespace
 
+namespace {
+// Stable LSD radix sort of n (u64 key, u32 value) pairs on bits [0, bits) (rounded up to whole
+// bytes); returns the buffers holding the result (the inputs or the spare pair).
+cdb_status radix_sort_pairs(cdb_ctx* ctx, uint64_t** k, uint32_t** v, uint64_t* k2, uint32_t* v2, uint64_t n,
+                            int bits, hipStream_t s) {
+  if (n == 0) return CDB_OK;
+  const uint32_t tiles = (uint32_t)((n + kRadixTile - 1) / kRadixTile);
+  cdb_status st = CDB_OK;
+  uint32_t* hist = (uint32_t*)ws_get(ctx, WS_RADIX, 2ull * 256 * tiles * sizeof(uint32_t), &st);
+  if (!hist) return st;
+  uint32_t* base = hist + 256ull * tiles;
+  uint64_t *ka = *k, *kb = k2;
+  uint32_t *va = *v, *vb = v2;
+  for (int sh = 0; sh < bits; sh += 8) {
+    radix_hist_kernel<<<tiles, kRadixThreads, 0, s>>>(ka, n, sh, hist, tiles);
+    CDB_TRY(launch_check(ctx, s, "radix_hist_kernel"));
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, hist, 256ull * tiles, base, (uint32_t*)nullptr, nullptr, s));
+    radix_scatter_kernel<<<tiles, kRadixThreads, 0, s>>>(ka, va, n, sh, base, tiles, kb, vb);
+    CDB_TRY(launch_check(ctx, s, "radix_scatter_kernel"));
+    std::swap(ka, kb);
+    std::swap(va, vb);
+  }
+  *k = ka;
+  *v = va;
+  return CDB_OK;
+}
+
+// Buckets beyond the workgroup tier's LDS pool (the mid kernel lists them). Buckets whose keys fit
+// the pool take the chip-wide child path (hot.hip.h); any other (more than kCapK key rows in one
+// bucket, or CDB_HOT_LEGACY set) runs the whole bucket algorithm on one workgroup over a global
+// scratch slab (bucket_hot_kernel).
+cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list, uint32_t hot, hipStream_t s) {
+  cdb_status st = CDB_OK;
+  uint32_t* d_cnt3 = (uint32_t*)ws_get(ctx, WS_HOTC3, 4ull * hot * sizeof(uint32_t), &st);
+  if (!d_cnt3) return st;
+  hot_counts_kernel<<<(hot + 255) / 256, 256, 0, s>>>(A, d_hot_list, hot, d_cnt3);
+  CDB_TRY(launch_check(ctx, s, "hot_counts_kernel"));
+  std::vector<uint32_t> ids(hot), cnt3(3ull * hot);
+  CDB_HIP(hipMemcpyAsync(ids.data(), d_hot_list, hot * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");
+  CDB_HIP(hipMemcpyAsync(cnt3.data(), d_cnt3, 3ull * hot * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");
+  CDB_HIP(hipStreamSynchronize(s), "sync");
+  std::vector<uint32_t> order(hot);
+  for (uint32_t i = 0; i < hot; ++i) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return ids[a] < ids[b]; });
+  static const bool legacy_env = std::getenv("CDB_HOT_LEGACY") != nullptr;
+  const bool legacy_all = legacy_env || A.force_tier == 4;
+  std::vector<uint32_t> wide_ids, legacy;  // wide: the chip-wide child path
+  std::vector<uint32_t> hk_off(1, 0), c_off(1, 0);
+  std::vector<uint32_t> lk, ln, lm;
+  uint64_t tk = 0, tc = 0;
+  for (uint32_t i : order) {
+    const uint32_t K = cnt3[3 * i], N = cnt3[3 * i + 1], M = cnt3[3 * i + 2];
+    if (!legacy_all && K <= (uint32_t)kCapK && tk + K < (1ull << 23) && tc + N + M < (1ull << 32)) {
+      wide_ids.push_back(ids[i]);
+      tk += K;
+      tc += N + M;
+      hk_off.push_back((uint32_t)tk);
+      c_off.push_back((uint32_t)tc);
+    } else {
+      legacy.push_back(ids[i]);
+      lk.push_back(K);
+      ln.push_back(N);
+      lm.push_back(M);
+    }
+  }
+  if (!legacy.empty()) {
+    const uint32_t nl = (uint32_t)legacy.size();
+    std::vector<uint64_t> off(nl);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < nl; ++i) {
+      off[i] = total;
+      total += hot_scratch_words(lk[i], std::max(ln[i], lm[i]));
+      total = (total + 15) & ~uint64_t(15);
+    }
+    uint8_t* slab = (uint8_t*)ws_get(ctx, WS_HOT, total * 8 + nl * 12 + 64, &st);
+    if (!slab) return st;
+    uint64_t* d_off = (uint64_t*)(slab + total * 8);
+    uint32_t* d_ids = (uint32_t*)(d_off + nl);
+    CDB_HIP(hipMemcpyAsync(d_off, off.data(), nl * 8, hipMemcpyHostToDevice, s), "h2d");
+    CDB_HIP(hipMemcpyAsync(d_ids, legacy.data(), nl * 4, hipMemcpyHostToDevice, s), "h2d");
+    A.hot_in = d_ids;
+    A.hot_scratch = (uint64_t*)slab;
+    A.hot_scratch_off = d_off;
+    bucket_hot_kernel<<<nl, kBktThreads, 0, s>>>(A);
+    CDB_TRY(launch_check(ctx, s, "bucket_hot_kernel"));
+    CDB_HIP(hipStreamSynchronize(s), "sync");  // the host vectors above are copy sources
+  }
+  if (wide_ids.empty()) return CDB_OK;
+  const uint32_t H = (uint32_t)wide_ids.size();
+  // device: ids[H] | hk_off[H + 1] | c_off[H + 1] | hk_kout[H] | h_first[H]
+  uint32_t* meta = (uint32_t*)ws_get(ctx, WS_HOTMETA, (5ull * H + 2) * sizeof(uint32_t), &st);
+  if (!meta) return st;
+  HotArgs HA;
+  std::memset(&HA, 0, sizeof HA);
+  uint32_t* d_ids = meta;
+  uint32_t* d_hk_off = meta + H;
+  uint32_t* d_c_off = d_hk_off + H + 1;
+  HA.ids = d_ids;
+  HA.hk_off = d_hk_off;
+  HA.c_off = d_c_off;
+  HA.hk_kout = d_c_off + H + 1;
+  HA.h_first = HA.hk_kout + H;
+  HA.H = H;
+  HA.n_children = tc;
+  CDB_HIP(hipMemcpyAsync(d_ids, wide_ids.data(), H * 4, hipMemcpyHostToDevice, s), "h2d");
+  CDB_HIP(hipMemcpyAsync(d_hk_off, hk_off.data(), (H + 1) * 4, hipMemcpyHostToDevice, s), "h2d");
+  CDB_HIP(hipMemcpyAsync(d_c_off, c_off.data(), (H + 1) * 4, hipMemcpyHostToDevice, s), "h2d");
+  const uint64_t nk = std::max<uint64_t>(tk, 1), nc = std::max<uint64_t>(tc, 1);
+  uint8_t* kt = (uint8_t*)ws_get(ctx, WS_HOTK, nk * (4 * 8 + 3 * 4) + 64, &st);
+  if (!kt) return st;
+  HA.hk_h = (uint64_t*)kt;
+  HA.hk_f = HA.hk_h + nk;
+  HA.hk_vm = HA.hk_f + nk;
+  HA.hk_sum = (unsigned long long*)(HA.hk_vm + nk);
+  HA.hk_tp = (uint32_t*)(HA.hk_sum + nk);
+  HA.hk_cnt = HA.hk_tp + nk;
+  HA.hk_cb = HA.hk_cnt + nk;
+  uint8_t* ct = (uint8_t*)ws_get(ctx, WS_HOTCH, nc * (2 * 8 + 2 * 4 + 2 * 4 + 4 * 4) + 64, &st);
+  if (!ct) return st;
+  uint64_t* w = (uint64_t*)ct;
+  uint64_t* w2 = w + nc;
+  uint32_t* v = (uint32_t*)(w2 + nc);
+  uint32_t* v2 = v + nc;
+  HA.c_row = v2 + nc;
+  HA.c_h = HA.c_row + nc;
+  HA.emit_n = HA.c_h + nc;
+  HA.emit_m = HA.emit_n + nc;
+  uint32_t* rank_n = HA.emit_m + nc;
+  uint32_t* rank_m = rank_n + nc;
+  HA.rank_n = rank_n;
+  HA.rank_m = rank_m;
+  HA.w = w;
+  HA.v = v;
+  hot_keys_kernel<<<H, kBktThreads, 0, s>>>(A, HA);
+  CDB_TRY(launch_check(ctx, s, "hot_keys_kernel"));
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((tc + 255) / 256, 16384);
+  if (tc) {
+    hot_tag_kernel<<<grid, 256, 0, s>>>(A, HA);
+    CDB_TRY(launch_check(ctx, s, "hot_tag_kernel"));
+    int gbits = 0;
+    while (gbits < 32 && (tk >> gbits)) ++gbits;
+    CDB_TRY(radix_sort_pairs(ctx, &HA.w, &HA.v, w2, v2, tc, kHotIdBits + gbits, s));
+  }
+  hot_first_kernel<<<(H + 255) / 256, 256, 0, s>>>(HA);
+  CDB_TRY(launch_check(ctx, s, "hot_first_kernel"));
+  if (tc) {
+    hot_fold_kernel<<<grid, 256, 0, s>>>(A, HA, 0);
+    CDB_TRY(launch_check(ctx, s, "hot_fold_kernel"));
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, HA.emit_n, tc, rank_n, (uint32_t*)nullptr, nullptr, s));
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, HA.emit_m, tc, rank_m, (uint32_t*)nullptr, nullptr, s));
+    hot_fold_kernel<<<grid, 256, 0, s>>>(A, HA, 1);
+    CDB_TRY(launch_check(ctx, s, "hot_fold_kernel"));
+  }
+  hot_finish_kernel<<<H, 256, 0, s>>>(A, HA);
+  CDB_TRY(launch_check(ctx, s, "hot_finish_kernel"));
+  CDB_HIP(hipStreamSynchronize(s), "sync");  // the host vectors above are copy sources
+  return CDB_OK;
+}
+}  // namespace
+
 cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts,
                              cdb_dev_output* out, cdb_merge_stats* stats, hipStream_t s) {
   const uint64_t K = in->keys.n, N = in->nodes.n, M = in->members.n;
@@ -775,32 +938,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   CDB_HIP(hipMemcpyAsync(counts, d_hot_count, sizeof counts, hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipStreamSynchronize(s), "sync");
   const uint32_t hot = counts[0];
-  if (hot) {
-    std::vector<uint32_t> ids(hot), kc(hot), nc(hot), mc(hot);
-    CDB_HIP(hipMemcpy(ids.data(), d_hot_list, hot * sizeof(uint32_t), hipMemcpyDeviceToHost), "d2h");
-    std::sort(ids.begin(), ids.end());
-    std::vector<uint64_t> off(hot);
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < hot; ++i) {
-      CDB_HIP(hipMemcpy(&kc[i], dk.hist + ids[i], 4, hipMemcpyDeviceToHost), "d2h");
-      CDB_HIP(hipMemcpy(&nc[i], dnd.hist + ids[i], 4, hipMemcpyDeviceToHost), "d2h");
-      CDB_HIP(hipMemcpy(&mc[i], dm.hist + ids[i], 4, hipMemcpyDeviceToHost), "d2h");
-      off[i] = total;
-      total += hot_scratch_words(kc[i], std::max(nc[i], mc[i]));
-      total = (total + 15) & ~uint64_t(15);
-    }
-    uint8_t* slab = (uint8_t*)ws_get(ctx, WS_HOT, total * 8 + hot * 12 + 64, &st);
-    if (!slab) return st;
-    uint64_t* d_off = (uint64_t*)(slab + total * 8);
-    uint32_t* d_ids = (uint32_t*)(d_off + hot);
-    CDB_HIP(hipMemcpyAsync(d_off, off.data(), hot * 8, hipMemcpyHostToDevice, s), "h2d");
-    CDB_HIP(hipMemcpyAsync(d_ids, ids.data(), hot * 4, hipMemcpyHostToDevice, s), "h2d");
-    A.hot_in = d_ids;
-    A.hot_scratch = (uint64_t*)slab;
-    A.hot_scratch_off = d_off;
-    bucket_hot_kernel<<<hot, kBktThreads, 0, s>>>(A);
-    CDB_TRY(launch_check(ctx, s, "bucket_hot_kernel"));
-  }
+  if (hot) CDB_TRY(over_capacity(ctx, A, d_hot_list, hot, s));
 
   // ---- 5. dense compaction into the caller's output columns
   CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dk.out, nb, dk.doff, (uint32_t*)nullptr, d_totals + 0, s));

@@ -1,0 +1,322 @@
+// Over-capacity buckets whose keys fit the workgroup tier but whose children do not (config C5:
+// a few keys own up to millions of counter nodes or set/dict members; the per-key loops of
+// type_counter.rs:59-87 and lwwhash.rs:319-323 are then the whole cost). The keys of such a
+// bucket are sorted and folded by one workgroup (bucket_keys), and its children are spread over
+// the whole chip instead:
+//   hot_keys_kernel : one workgroup per hot bucket: the key phase; the bucket's output keys go to
+//                     a global key table at hk_off[h] (G = hk_off[h] + rank is a chip-wide key id);
+//   hot_tag_kernel  : one thread per child: finds its key (binary search of the bucket's table),
+//                     decides whether it takes part (head type, element type, remote dels
+//                     ignored, exactly as the wave tier) and tags it with W = G << 40 | id-hash[63:24];
+//   radix sort of (W, child) pairs (radix.hip.h), stable, so equal W keep (bucket, row) order;
+//   hot_fold_kernel : one thread per W-run (a (key, child id) group, ~ one row per replica):
+//                     folds every exact child id of the run in (pos, src) order -- Counter::merge's
+//                     head-t rule or LWWHash::set's later-wins rule -- counting outputs (pass 0)
+//                     or writing them at their rank inside the bucket (pass 1, after a scan);
+//   hot_finish_kernel: counter sums (cal_sum) and child ranges into the key rows, bucket counts.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bucket.hip.h"
+#include "common.h"
+
+namespace cdb {
+
+constexpr int kHotIdBits = 40;
+  // W = G << 40 | child-id hash >> 24
+
+struct HotArgs {
+  const uint32_t* ids;       // hot bucket of h
+  const uint32_t* hk_off;    // first key-table slot of h (prefix of the key rows)
+  const uint32_t* c_off;     // first flat child of h (prefix of nodes + members), H + 1 entries
+  uint32_t H;
+  // key table (G)
+  uint64_t *hk_h, *hk_f, *hk_vm;
+  unsigned long long* hk_sum;
+  uint32_t *hk_tp, *hk_cnt, *hk_cb;
+  uint32_t* hk_kout;         // per h
+  // children
+  uint64_t* w;               // W per flat child (then sorted)
+  uint32_t* v;               // flat child index (then sorted)
+  uint32_t* c_row;           // physical row of flat child j
+  uint32_t* c_h;             // bucket h of flat child j, bit 31 = member
+  uint32_t *emit_n, *emit_m; // per sorted position: outputs of the run starting there
+  const uint32_t *rank_n, *rank_m;  // exclusive scans of emit_n / emit_m
+  uint32_t* h_first;         // per h: first sorted position of its children
+  uint64_t n_children;
+};
+
+__device__ __forceinline__ uint32_t hot_bucket_of(const HotArgs& H, uint64_t j) {  // last h: c_off[h] <= j
+  uint32_t lo = 0, hi = H.H;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (H.c_off[mid] <= j) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(kBktThreads) hot_keys_kernel(BucketArgs A, HotArgs H) {
+  __shared__ LdsPool L;
+  Scratch S;
+  S.kh = L.kh; S.kf = L.kf; S.meta = L.meta;
+  S.idx = L.idx; S.rk = L.rk; S.flag = L.flag; S.rank = L.rank; S.cnt = L.cnt;
+  S.okh = L.okh; S.okf = L.okf; S.ovm = L.ovm; S.osum = L.osum;
+  S.otp = L.otp; S.ocb = L.ocb; S.occ = L.occ;
+  S.c1 = L.c1; S.c2 = L.c2; S.cm = L.cm; S.rt = L.rt; S.rm = L.rm;
+  S.ck = L.ck; S.cidx = L.cidx; S.crk = L.crk; S.cflag = L.cflag; S.crank = L.crank;
+  S.st = L.st; S.misc = L.misc;
+  const uint32_t h = blockIdx.x, b = H.ids[h];
+  const uint32_t kout = bucket_keys(A, b, S);
+  const uint32_t g0 = H.hk_off[h];
+  for (uint32_t o = threadIdx.x; o < kout; o += blockDim.x) {
+    H.hk_h[g0 + o] = S.okh[o];
+    H.hk_f[g0 + o] = S.okf[o];
+    H.hk_vm[g0 + o] = S.ovm[o];
+    H.hk_sum[g0 + o] = S.osum[o];
+    H.hk_tp[g0 + o] = S.otp[o];
+    H.hk_cnt[g0 + o] = 0;
+    H.hk_cb[g0 + o] = kNone;
+  }
+  if (threadIdx.x == 0) H.hk_kout[h] = kout;
+  __syncthreads();
+  for (int i = threadIdx.x; i < ST_COUNT; i += blockDim.x)
+    if (S.st[i]) atomicAdd(&stat_shard(A.stats)[i], S.st[i]);
+}
+
+__global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
+  const int ks = A.key_shift;
+  unsigned long long orph = 0;
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < H.n_children;
+       j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t h = hot_bucket_of(H, j), b = H.ids[h];
+    const uint32_t i = (uint32_t)(j - H.c_off[h]), N = A.ncnt[b];
+    const bool isn = i < N;
+    const uint32_t row = isn ? A.np[A.nbase[b] + i] : A.mp[A.mbase[b] + (i - N)];
+    const uint64_t* C = (isn ? A.nr : A.mr) + (uint64_t)row * kChildStride;
+    const uint64_t pkh = C[C_PKH], pkf = C[C_PKF], id1 = C[C_ID1], m = C[C_META];
+    // lower bound over the bucket's sorted output keys on (kh << shift, kh, kf)
+    const uint32_t g0 = H.hk_off[h], kout = H.hk_kout[h];
+    uint32_t lo = 0, hi = kout;
+    const uint64_t sp = pkh << ks;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const uint64_t kh = H.hk_h[g0 + mid], sm = kh << ks;
+      const bool less = sm < sp || (sm == sp && (kh < pkh || (kh == pkh && H.hk_f[g0 + mid] < pkf)));
+      lo = less ? mid + 1 : lo;
+      hi = less ? hi : mid;
+    }
+    uint64_t w = ~0ull;
+    if (lo < kout && H.hk_h[g0 + lo] == pkh && H.hk_f[g0 + lo] == pkf && (H.hk_tp[g0 + lo] & 0xFF) <= TAG_SET) {
+      const uint32_t T = H.hk_tp[g0 + lo] & 0xFF, hp = H.hk_tp[g0 + lo] >> 8, p = meta_pos(m);
+      const bool type_ok = isn ? T == TAG_COUNTER : (T == TAG_SET || T == TAG_DICT);
+      const bool elem_ok = (H.hk_vm[g0 + lo] >> p) & 1;
+      const bool cand = isn || meta_tag(m) == KIND_ADD || p == hp;  // remote dels ignored
+      if (type_ok && elem_ok && cand) {
+        const uint64_t ih = isn ? mix64(id1) : id1;
+        w = ((uint64_t)(g0 + lo) << kHotIdBits) | (ih >> (64 - kHotIdBits));
+      }
+    } else {
+      ++orph;
+    }
+    H.w[j] = w;
+    H.v[j] = (uint32_t)j;
+    H.c_row[j] = row;
+    H.c_h[j] = h | (isn ? 0u : 0x80000000u);
+  }
+  if (orph) atomicAdd(&stat_shard(A.stats)[ST_ORPHANS], orph);
+}
+
+// One child of a W-run, by sorted position q (j: its flat index, the last tie-break).
+struct HotChild {
+  uint64_t id1, id2, t, meta;
+  uint32_t j;
+};
+__device__ __forceinline__ HotChild hot_child(const BucketArgs& A, const HotArgs& H, uint64_t q, bool isn) {
+  const uint32_t j = H.v[q];
+  const uint64_t* C = (isn ? A.nr : A.mr) + (uint64_t)H.c_row[j] * kChildStride;
+  HotChild c;
+  c.id1 = C[C_ID1];
+  c.id2 = C[C_ID2];
+  c.t = C[C_T];
+  c.meta = C[C_META];
+  c.j = j;
+  return c;
+}
+// Total order of a run's rows: exact id (nodes: the node id alone), fold position (pos, src),
+// flat index. The fold visits the rows in this order.
+__device__ __forceinline__ bool hot_before(const HotChild& a, const HotChild& b, bool isn) {
+  if (a.id1 != b.id1) return a.id1 < b.id1;
+  if (!isn && a.id2 != b.id2) return a.id2 < b.id2;
+  const uint64_t oa = meta_order(a.meta), ob = meta_order(b.meta);
+  if (oa != ob) return oa < ob;
+  return a.j < b.j;
+}
+
+// pass 0: emit counts per run (emit_n / emit_m at the run's first position); pass 1: outputs.
+// A run holds ~ one row per replica; each step selects the successor of the last visited row
+// (an O(run^2) selection over rows in L2, no per-thread arrays), so rows are folded in order
+// whatever order the sort left them in. Every loop has a wave-uniform trip count (the longest
+// run in the wave) with per-lane predicates: the selection's loop-carried row must not be a
+// live-out of a loop with divergent exits (gfx950 compilers have produced the first candidate
+// instead of the smallest there).
+__global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, int pass) {
+  unsigned long long gcm = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < H.n_children; base += stride) {
+    const uint64_t p = base + threadIdx.x;
+    uint64_t W = ~0ull;
+    bool start = false;
+    if (p < H.n_children) {
+      W = H.w[p];
+      if (pass == 0) {
+        H.emit_n[p] = 0;
+        H.emit_m[p] = 0;
+      }
+      start = W != ~0ull && !(p > 0 && H.w[p - 1] == W);
+    }
+    uint32_t nrows = 0;
+    if (start) {
+      uint64_t e = p + 1;
+      while (e < H.n_children && H.w[e] == W) ++e;
+      nrows = (uint32_t)(e - p);
+    }
+    uint32_t kmax = nrows;
+    for (int off = 32; off > 0; off >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off));
+    if (kmax == 0) continue;  // wave-uniform
+    uint32_t hc = 0, h = 0, b = 0, G = 0;
+    bool isn = false;
+    uint64_t obase = 0;
+    if (start) {
+      hc = H.c_h[H.v[p]];
+      h = hc & 0x7FFFFFFFu;
+      isn = (hc >> 31) == 0;
+      b = H.ids[h];
+      G = (uint32_t)(W >> kHotIdBits);
+      if (pass == 1) obase = (isn ? H.rank_n[p] - H.rank_n[H.h_first[h]] : H.rank_m[p] - H.rank_m[H.h_first[h]]);
+    }
+    uint32_t nout = 0;
+    HotChild last, head;  // last visited row; first row of the id being folded
+    last.id1 = last.id2 = last.t = last.meta = 0;
+    last.j = 0;
+    head = last;
+    uint64_t v = 0, tw = 0, wmeta = 0;  // the fold of head's id so far
+    bool open = false;                  // head's id has rows not yet emitted
+    for (uint32_t step = 0; step <= kmax; ++step) {
+      HotChild c = last;
+      bool have = false;
+      for (uint32_t k = 0; k < kmax; ++k) {
+        if (k < nrows && step < nrows) {
+          const HotChild x = hot_child(A, H, p + k, isn);
+          const bool after = step == 0 || hot_before(last, x, isn);
+          const bool take = after && (!have || hot_before(x, c, isn));
+          c.id1 = take ? x.id1 : c.id1;
+          c.id2 = take ? x.id2 : c.id2;
+          c.t = take ? x.t : c.t;
+          c.meta = take ? x.meta : c.meta;
+          c.j = take ? x.j : c.j;
+          have = have || take;
+        }
+      }
+      const bool new_id = !have || !open || c.id1 != head.id1 || (!isn && c.id2 != head.id2);
+      if (open && new_id) {  // head's id is complete: emit it
+        bool emit = true;
+        if (!isn && (A.flags & F_GC_MEMBERS) && meta_tag(wmeta) == KIND_DEL && tw < A.gc_wm) {
+          emit = false;
+          ++gcm;
+        }
+        if (emit) {
+          if (pass == 1) {
+            const uint32_t o = (uint32_t)(obase + nout);
+            uint64_t* row = (isn ? A.nos + (uint64_t)(A.nbase[b] + o) * kChildStride
+                                 : A.mos + (uint64_t)(A.mbase[b] + o) * kChildStride);
+            row[C_PKH] = H.hk_h[G];
+            row[C_PKF] = H.hk_f[G];
+            row[C_ID1] = head.id1;
+            row[C_ID2] = isn ? v : head.id2;
+            row[C_T] = isn ? head.t : tw;
+            row[C_META] = isn ? meta_pack(0, meta_pos(head.meta), meta_src(head.meta)) : wmeta;
+            atomicMin(&H.hk_cb[G], o);
+            atomicAdd(&H.hk_cnt[G], 1u);
+            if (isn && (H.hk_vm[G] & kVmaskMerged)) atomicAdd(&H.hk_sum[G], (unsigned long long)v);
+          }
+          ++nout;
+        }
+        open = false;
+      }
+      if (have) {
+        if (new_id) {  // c opens an id
+          head = c;
+          v = c.id2;
+          tw = c.t;
+          wmeta = c.meta;
+          open = true;
+        } else if (isn) {  // Counter::merge (type_counter.rs:60-84): the head's t is kept
+          v = c.t > head.t ? c.id2 : (c.t == head.t ? imax64(v, c.id2) : v);
+        } else if (!(tw > c.t)) {  // LWWHash::set (lwwhash.rs:87-107): later wins ties
+          tw = c.t;
+          wmeta = c.meta;
+        }
+        last = c;
+      }
+    }
+    if (pass == 0 && start) (isn ? H.emit_n : H.emit_m)[p] = nout;
+  }
+  if (pass == 1 && gcm) atomicAdd(&stat_shard(A.stats)[ST_MEMBERS_GCED], gcm);
+}
+
+// First sorted position of each hot bucket's children (sorted by W, whose top bits are G).
+__global__ void hot_first_kernel(HotArgs H) {
+  const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H.H) return;
+  const uint64_t key = (uint64_t)H.hk_off[h] << kHotIdBits;
+  uint64_t lo = 0, hi = H.n_children;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (H.w[mid] < key) lo = mid + 1;
+    else hi = mid;
+  }
+  H.h_first[h] = (uint32_t)lo;
+}
+
+// Key rows: counter sums and child ranges (bucket-relative, as every tier leaves them for the
+// compaction); the bucket's output counts.
+__global__ void __launch_bounds__(256) hot_finish_kernel(BucketArgs A, HotArgs H) {
+  const uint32_t h = blockIdx.x, b = H.ids[h];
+  const uint32_t g0 = H.hk_off[h], kout = H.hk_kout[h], kb = A.kbase[b];
+  uint32_t nn = 0, nm = 0;
+  for (uint32_t o = threadIdx.x; o < kout; o += blockDim.x) {
+    const uint32_t G = g0 + o, T = H.hk_tp[G] & 0xFF, cnt = H.hk_cnt[G];
+    if (T == TAG_COUNTER) {
+      A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_WIN] = H.hk_sum[G];
+      nn += cnt;
+    } else if (T == TAG_SET || T == TAG_DICT) {
+      nm += cnt;
+    }
+    A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_CREF] = cref_pack(cnt ? H.hk_cb[G] : 0, cnt);
+  }
+  __shared__ uint32_t tot[2];
+  if (threadIdx.x == 0) tot[0] = tot[1] = 0;
+  __syncthreads();
+  if (nn) atomicAdd(&tot[0], nn);
+  if (nm) atomicAdd(&tot[1], nm);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    A.kout[b] = kout;
+    A.nout[b] = tot[0];
+    A.mout[b] = tot[1];
+  }
+}
+
+// Row counts of the listed buckets, for the host's plan of the over-capacity path.
+__global__ void hot_counts_kernel(BucketArgs A, const uint32_t* __restrict__ list, uint32_t n, uint32_t* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t b = list[i];
+  out[3 * i] = A.kcnt[b];
+  out[3 * i + 1] = A.ncnt[b];
+  out[3 * i + 2] = A.mcnt[b];
+}
+
+}  // namespace cdb

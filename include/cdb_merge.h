@@ -122,7 +122,9 @@ typedef struct cdb_merge_opts {
   uint32_t flags;
   uint32_t force_tier;   /* testing only: 0 = automatic; 1 = every bucket through the LDS
                             workgroup tier; 2 = every bucket through the global-scratch tier;
-                            3 = every bucket through the wide (128-key-row) wave kernel */
+                            3 = every bucket through the wide (128-key-row) wave kernel;
+                            4 = every bucket through the one-workgroup global-scratch kernel
+                            (tier 2 sends children through the chip-wide child path) */
   uint64_t gc_watermark; /* ReplicaManager::min_uuid (replica/replica.rs:87-89) */
   uint32_t key_shift;    /* multi-GPU: the top `key_shift` bits of every key hash are the owner
                             rank (all equal on one device), so local buckets use the bits below */

@@ -1,0 +1,45 @@
+"""The C ABI from C: tests/abi/abi_check.c is compiled with the system C compiler against
+include/cdb_merge.h and linked to libcdbmerge.so. Compiling it pins sizeof/offsetof of every
+public struct a binding mirrors by hand (INTEGRATION.md's Rust structs); running it walks the
+boundary a host takes: gen -> decode -> ctx -> merge -> canonical dump."""
+import os
+import subprocess
+
+import pytest
+
+import constdb_amd as cdb
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _compile(tmp_path):
+    from constdb_amd import build
+    build.build()
+    exe = str(tmp_path / "abi_check")
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                           "-o", exe, os.path.join(ROOT, "tests", "abi", "abi_check.c"),
+                           "-L", os.path.join(ROOT, "constdb_amd"), "-lcdbmerge",
+                           "-Wl,-rpath," + os.path.join(ROOT, "constdb_amd")])
+    return exe
+
+
+def test_abi_layout_and_decode_from_c(tmp_path):
+    """Compiles (the layout pins) and runs the decode half; without a device cdb_ctx_create must
+    answer CDB_NO_DEVICE (no CPU fallback)."""
+    exe = _compile(tmp_path)
+    out = subprocess.run([exe, str(tmp_path / "dump.txt")], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    assert "no device" in out.stdout or "merged" in out.stdout
+
+
+@pytest.mark.gpu
+def test_abi_merge_from_c(tmp_path):
+    import cdb_oracle
+    exe = _compile(tmp_path)
+    out = subprocess.run([exe, str(tmp_path / "dump.txt")], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    assert "merged" in out.stdout
+    cfg = cdb.gen_config(seed=17, universe=3000, n_replicas=3, replica_hi=3)
+    rc, want, _ = cdb_oracle.fold([cdb.gen_snapshot(cfg, r) for r in range(3)])
+    assert rc == 0
+    assert (tmp_path / "dump.txt").read_bytes() == want

@@ -129,11 +129,11 @@ def test_random_small(db, seed):
     _check(db, snaps)
 
 
-@pytest.mark.parametrize("tier", [1, 2, 3])
+@pytest.mark.parametrize("tier", [1, 2, 3, 4])
 @pytest.mark.parametrize("seed", range(12))
 def test_random_forced_tier(db, seed, tier):
-    """The LDS workgroup tier, the global-scratch tier and the wide wave kernel on every
-    bucket."""
+    """The LDS workgroup tier (1), the chip-wide child path of over-capacity buckets (2), the
+    wide wave kernel (3) and the one-workgroup global-scratch kernel (4) on every bucket."""
     snaps = gen_replicas(900 + seed, n_replicas=1 + seed % 5, n_keys=40, p_conflict=0.1, p_side=0.3)
     _check(db, snaps, gc=(seed % 7) if seed % 2 else None, members=bool(seed % 4 == 1), tier=tier)
 
@@ -221,6 +221,7 @@ def test_hot_bucket_path(db):
     objs2 = {b"big": o.Object(2, 0, 0, o.OBJECT_ENC_SET, big2), b"cnt": o.Object(2, 0, 0, o.OBJECT_ENC_COUNTER, c2)}
     m = _check(db, [_snap(objs1), _snap(objs2)])
     assert m.stats.hot_buckets >= 1
+    _check(db, [_snap(objs1), _snap(objs2)], tier=4)  # the one-workgroup global-scratch kernel
 
 
 def test_deterministic(db):

@@ -141,7 +141,7 @@ def test_runs_equal_partition_random(ctx, seed):
                       side_permille=200, mean_members=5))
 
 
-@pytest.mark.parametrize("tier", [1, 2, 3])
+@pytest.mark.parametrize("tier", [1, 2, 3, 4])
 def test_runs_forced_tiers(ctx, tier):
     """Every bucket through the materialised workgroup tiers (1, 2) or the wide runs kernel (3)."""
     _both(ctx, _small(40 + tier, 3000, 5, conflict_ppm=20000, side_permille=200), force_tier=tier)
