@@ -45,6 +45,7 @@ enum WsSlot {
   WS_HOST_OUT_K, WS_HOST_OUT_N, WS_HOST_OUT_M,          // cdb_merge: device-side result
   WS_RUNDIR, WS_RUNMISC,                                // sorted-run path: run directories, gap lists
   WS_HOTC3, WS_HOTMETA, WS_HOTK, WS_HOTCH, WS_RADIX,    // over-capacity child path (hot.hip.h)
+  WS_MAT,                                               // sorted-run path: materialisation counts
   WS_COUNT
 };
 static_assert(WS_COUNT <= 32, "cdb_ctx::ws has 32 slots");

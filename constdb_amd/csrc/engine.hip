@@ -612,6 +612,11 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   HA.h_first = HA.hk_kout + H;
   HA.H = H;
   HA.n_children = tc;
+  HA.id_shift = 30;
+  if (const char* e = std::getenv("CDB_HOT_ID_BITS")) {  // tests: fewer id bits force the collision path
+    const int bits = std::atoi(e);
+    if (bits >= 1 && bits <= 34) HA.id_shift = 64 - bits;
+  }
   CDB_HIP(hipMemcpyAsync(d_ids, wide_ids.data(), H * 4, hipMemcpyHostToDevice, s), "h2d");
   CDB_HIP(hipMemcpyAsync(d_hk_off, hk_off.data(), (H + 1) * 4, hipMemcpyHostToDevice, s), "h2d");
   CDB_HIP(hipMemcpyAsync(d_c_off, c_off.data(), (H + 1) * 4, hipMemcpyHostToDevice, s), "h2d");
@@ -903,10 +908,24 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     MA_.kp = kperm;
     MA_.np = nperm;
     MA_.mp = mperm;
-    MA_.cursor = (unsigned long long*)(misc + 104);
-    CDB_HIP(hipMemsetAsync(MA_.cursor, 0, 3 * sizeof(unsigned long long), s), "memset");
-    materialize_kernel<<<std::min<uint64_t>(nb, 2048), 256, 0, s>>>(WA, MA_, d_big_list, d_big_count);
-    CDB_TRY(launch_check(ctx, s, "materialize_kernel"));
+    uint32_t* mw = (uint32_t*)ws_get(ctx, WS_MAT, (8 * nb + 4) * sizeof(uint32_t) + 64, &st);
+    if (!mw) return st;
+    MA_.cnt = mw;
+    MA_.base = mw + 3 * nb;
+    MA_.chunks = mw + 6 * nb;
+    MA_.chunk0 = mw + 7 * nb;
+    uint64_t* d_nchunks = (uint64_t*)(((uintptr_t)(mw + 8 * nb) + 15) & ~(uintptr_t)15);
+    MA_.n_chunks = d_nchunks;
+    MA_.nb = (uint32_t)nb;
+    mat_count_kernel<<<(uint32_t)std::min<uint64_t>((nb + 255) / 256, 4096), 256, 0, s>>>(WA, MA_, d_big_list,
+                                                                                          d_big_count);
+    CDB_TRY(launch_check(ctx, s, "mat_count_kernel"));
+    for (int f = 0; f < 3; ++f)
+      CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, MA_.cnt + f * nb, nb, MA_.base + f * nb, (uint32_t*)nullptr,
+                                                 nullptr, s));
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, MA_.chunks, nb, MA_.chunk0, (uint32_t*)nullptr, d_nchunks, s));
+    mat_copy_kernel<<<4096, 256, 0, s>>>(WA, MA_, d_big_list);
+    CDB_TRY(launch_check(ctx, s, "mat_copy_kernel"));
   } else if (wave_pf() == 0)
     bucket_wave_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA);
   else if (wave_pf() == 1)

@@ -17,10 +17,21 @@ GenModel model_of(const cdb_gen_config& c);
 
 namespace {
 
+// (key, replica) entries with more children than this are filled by gen_big_kernel, one
+// workgroup each (C5's hottest keys hold millions of children: one thread per key would
+// serialise the whole generator behind them).
+constexpr uint32_t kGenBig = 1024;
+
+struct GenBig {  // one large (key, replica) entry
+  uint64_t i, r, child0, key_row;
+};
+
 struct GenArgs {
   GenModel g;
   uint32_t lo, hi;
   uint32_t *ck, *cn, *cm;  // per key index counts
+  unsigned long long* n_big;
+  GenBig* big;             // capacity: the count kernel's n_big
   uint64_t* k[kKeyCols];
   uint64_t* nd[kNodeCols];
   uint64_t* mb[kMemberCols];
@@ -29,15 +40,20 @@ struct GenArgs {
 __global__ void gen_count_kernel(GenArgs a) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.g.universe;
        i += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t nk = 0, nn = 0, nm = 0;
+    uint32_t nk = 0, nn = 0, nm = 0, nbig = 0;
     const Hash128 h = gen_key_hash(i);
     if (gen_in_shard(a.g, h.h)) {
       for (uint32_t r = a.lo; r < a.hi; ++r) {
         if (gen_present(a.g, i, r)) {
           const GenKey k = gen_key(a.g, i, r);
           ++nk;
-          if (k.tag == TAG_COUNTER) nn += k.n_nodes;
-          else if (k.tag == TAG_SET || k.tag == TAG_DICT) nm += k.n_members;
+          if (k.tag == TAG_COUNTER) {
+            nn += k.n_nodes;
+            nbig += k.n_nodes > kGenBig;
+          } else if (k.tag == TAG_SET || k.tag == TAG_DICT) {
+            nm += k.n_members;
+            nbig += k.n_members > kGenBig;
+          }
         }
         nk += gen_has_expire(a.g, i, r);
         nk += gen_has_delete(a.g, i, r);
@@ -46,7 +62,29 @@ __global__ void gen_count_kernel(GenArgs a) {
     a.ck[i] = nk;
     a.cn[i] = nn;
     a.cm[i] = nm;
+    if (nbig) atomicAdd(a.n_big, (unsigned long long)nbig);
   }
+}
+
+__device__ __forceinline__ void gen_node_row(const GenArgs& a, const Hash128& h, const GenKey& k, uint64_t i,
+                                             uint32_t r, uint32_t j, uint64_t pn, uint64_t v) {
+  a.nd[C_PKH][pn] = h.h;
+  a.nd[C_PKF][pn] = h.f;
+  a.nd[C_ID1][pn] = gen_node_id(a.g, k, j, r);
+  a.nd[C_ID2][pn] = v;
+  a.nd[C_T][pn] = gen_node_t(a.g, i, r, j);
+  a.nd[C_META][pn] = meta_pack(0, r, gen_node_src(a.g, i, j));
+}
+__device__ __forceinline__ void gen_member_row(const GenArgs& a, const Hash128& h, const GenKey& k, uint64_t i,
+                                               uint32_t r, uint32_t j, uint64_t pm) {
+  const uint64_t mi = gen_member_index(a.g, k, j);
+  const Hash128 mh = gen_member_hash(mi);
+  a.mb[C_PKH][pm] = h.h;
+  a.mb[C_PKF][pm] = h.f;
+  a.mb[C_ID1][pm] = mh.h;
+  a.mb[C_ID2][pm] = mh.f;
+  a.mb[C_T][pm] = gen_member_t(a.g, i, r, j);
+  a.mb[C_META][pm] = meta_pack(gen_member_is_del(a.g, i, r, j) ? KIND_DEL : KIND_ADD, r, gen_member_src(a.g, i, mi));
 }
 
 __global__ void gen_fill_kernel(GenArgs a, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ on,
@@ -70,37 +108,52 @@ __global__ void gen_fill_kernel(GenArgs a, const uint32_t* __restrict__ ok, cons
       if (gen_present(a.g, i, r)) {
         const GenKey k = gen_key(a.g, i, r);
         uint64_t aux = 0;
-        if (k.tag == TAG_COUNTER) {
-          for (uint32_t j = 0; j < k.n_nodes; ++j) {
+        const uint32_t nc = k.tag == TAG_COUNTER ? k.n_nodes : (k.tag == TAG_SET || k.tag == TAG_DICT) ? k.n_members : 0;
+        if (nc > kGenBig) {  // filled by gen_big_kernel (a counter's total added there)
+          const unsigned long long e = atomicAdd(a.n_big, 1ull);
+          a.big[e] = GenBig{i, r, k.tag == TAG_COUNTER ? pn : pm, pk};
+          (k.tag == TAG_COUNTER ? pn : pm) += nc;
+        } else if (k.tag == TAG_COUNTER) {
+          for (uint32_t j = 0; j < k.n_nodes; ++j, ++pn) {
             const uint64_t v = gen_node_v(a.g, i, r, j);
             aux += v;
-            a.nd[C_PKH][pn] = h.h;
-            a.nd[C_PKF][pn] = h.f;
-            a.nd[C_ID1][pn] = gen_node_id(a.g, k, j, r);
-            a.nd[C_ID2][pn] = v;
-            a.nd[C_T][pn] = gen_node_t(a.g, i, r, j);
-            a.nd[C_META][pn] = meta_pack(0, r, gen_node_src(a.g, i, j));
-            ++pn;
+            gen_node_row(a, h, k, i, r, j, pn, v);
           }
         } else if (k.tag == TAG_SET || k.tag == TAG_DICT) {
-          for (uint32_t j = 0; j < k.n_members; ++j) {
-            const uint64_t mi = gen_member_index(a.g, k, j);
-            const Hash128 mh = gen_member_hash(mi);
-            a.mb[C_PKH][pm] = h.h;
-            a.mb[C_PKF][pm] = h.f;
-            a.mb[C_ID1][pm] = mh.h;
-            a.mb[C_ID2][pm] = mh.f;
-            a.mb[C_T][pm] = gen_member_t(a.g, i, r, j);
-            a.mb[C_META][pm] =
-                meta_pack(gen_member_is_del(a.g, i, r, j) ? KIND_DEL : KIND_ADD, r, gen_member_src(a.g, i, mi));
-            ++pm;
-          }
+          for (uint32_t j = 0; j < k.n_members; ++j, ++pm) gen_member_row(a, h, k, i, r, j, pm);
         }
         key_row(k.ct, k.ut, k.dt, aux, meta_pack(k.tag, r, i));
       }
       if (gen_has_expire(a.g, i, r)) key_row(gen_time(a.g, i, r, 3), 0, 0, 0, meta_pack(TAG_EXPIRE, r, U + i));
       if (gen_has_delete(a.g, i, r)) key_row(gen_time(a.g, i, r, 4), 0, 0, 0, meta_pack(TAG_DELETE, r, 2 * U + i));
     }
+  }
+}
+
+// One workgroup per large (key, replica) entry: its children, and a counter's total.
+__global__ void __launch_bounds__(256) gen_big_kernel(GenArgs a, uint64_t n) {
+  __shared__ unsigned long long part;
+  for (uint64_t e = blockIdx.x; e < n; e += gridDim.x) {
+    const GenBig B = a.big[e];
+    const uint32_t r = (uint32_t)B.r;
+    const Hash128 h = gen_key_hash(B.i);
+    const GenKey k = gen_key(a.g, B.i, r);
+    if (threadIdx.x == 0) part = 0;
+    __syncthreads();
+    unsigned long long sum = 0;
+    if (k.tag == TAG_COUNTER) {
+      for (uint32_t j = threadIdx.x; j < k.n_nodes; j += blockDim.x) {
+        const uint64_t v = gen_node_v(a.g, B.i, r, j);
+        sum += v;
+        gen_node_row(a, h, k, B.i, r, j, B.child0 + j, v);
+      }
+      atomicAdd(&part, sum);
+    } else {
+      for (uint32_t j = threadIdx.x; j < k.n_members; j += blockDim.x) gen_member_row(a, h, k, B.i, r, j, B.child0 + j);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && k.tag == TAG_COUNTER) a.k[K_AUX][B.key_row] += part;
+    __syncthreads();
   }
 }
 
@@ -129,8 +182,10 @@ extern "C" cdb_status cdb_gen_device(cdb_ctx* ctx, const cdb_gen_config* cfg, cd
   a.cm = cnt + 2 * U;
   uint32_t *ok = cnt + 3 * U, *on = cnt + 4 * U, *om = cnt + 5 * U;
   uint64_t* tot = nullptr;
-  st = hip_check(ctx, hipMalloc(&tot, 3 * sizeof(uint64_t)), "hipMalloc");
+  st = hip_check(ctx, hipMalloc(&tot, 4 * sizeof(uint64_t)), "hipMalloc");
   if (st != CDB_OK) { hipFree(cnt); return st; }
+  a.n_big = (unsigned long long*)(tot + 3);
+  if ((st = hip_check(ctx, hipMemsetAsync(a.n_big, 0, 8, s), "memset")) != CDB_OK) { hipFree(cnt); hipFree(tot); return st; }
   const int grid = 4096, block = 256;
   gen_count_kernel<<<grid, block, 0, s>>>(a);
   // exclusive scans of the per-key counts
@@ -152,11 +207,19 @@ extern "C" cdb_status cdb_gen_device(cdb_ctx* ctx, const cdb_gen_config* cfg, cd
     hipFree(tot);
     return st;
   }
-  uint64_t t[3];
+  uint64_t t[4];
   hipMemcpy(t, tot, sizeof t, hipMemcpyDeviceToHost);
+  GenBig* big = nullptr;
+  if (t[3] && (st = hip_check(ctx, hipMalloc(&big, t[3] * sizeof(GenBig)), "hipMalloc(gen big)")) != CDB_OK) {
+    hipFree(cnt);
+    hipFree(tot);
+    return st;
+  }
+  a.big = big;
   if (t[0] >= (1ull << 32) || t[1] >= (1ull << 32) || t[2] >= (1ull << 32)) {
     hipFree(cnt);
     hipFree(tot);
+    if (big) hipFree(big);
     return fail(ctx, CDB_BAD_ARGUMENT, "generated rows exceed 2^32 per family");
   }
   std::memset(in, 0, sizeof *in);
@@ -165,6 +228,7 @@ extern "C" cdb_status cdb_gen_device(cdb_ctx* ctx, const cdb_gen_config* cfg, cd
       (st = cdb_dev_rows_alloc(ctx, &in->members, t[2], kMemberCols)) != CDB_OK) {
     hipFree(cnt);
     hipFree(tot);
+    if (big) hipFree(big);
     return st;
   }
   for (int c = 0; c < kKeyCols; ++c) a.k[c] = in->keys.col[c];
@@ -172,10 +236,13 @@ extern "C" cdb_status cdb_gen_device(cdb_ctx* ctx, const cdb_gen_config* cfg, cd
     a.nd[c] = in->nodes.col[c];
     a.mb[c] = in->members.col[c];
   }
+  hipMemsetAsync(a.n_big, 0, 8, s);
   gen_fill_kernel<<<grid, block, 0, s>>>(a, ok, on, om);
+  if (t[3]) gen_big_kernel<<<(uint32_t)std::min<uint64_t>(t[3], 4096), 256, 0, s>>>(a, t[3]);
   st = hip_check(ctx, hipStreamSynchronize(s), "gen fill");
   hipFree(cnt);
   hipFree(tot);
+  if (big) hipFree(big);
   in->n_pos = cfg->replica_hi;
   return st;
 }

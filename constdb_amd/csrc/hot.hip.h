@@ -7,7 +7,9 @@
 //                     a global key table at hk_off[h] (G = hk_off[h] + rank is a chip-wide key id);
 //   hot_tag_kernel  : one thread per child: finds its key (binary search of the bucket's table),
 //                     decides whether it takes part (head type, element type, remote dels
-//                     ignored, exactly as the wave tier) and tags it with W = G << 40 | id-hash[63:24];
+//                     ignored, exactly as the wave tier) and tags it with
+//                     W = G << 40 | id-hash[63:30] << 6 | pos, so that a run's rows arrive in
+//                     fold order unless two ids share 34 hash bits;
 //   radix sort of (W, child) pairs (radix.hip.h), stable, so equal W keep (bucket, row) order;
 //   hot_fold_kernel : one thread per W-run (a (key, child id) group, ~ one row per replica):
 //                     folds every exact child id of the run in (pos, src) order -- Counter::merge's
@@ -45,6 +47,7 @@ struct HotArgs {
   const uint32_t *rank_n, *rank_m;  // exclusive scans of emit_n / emit_m
   uint32_t* h_first;         // per h: first sorted position of its children
   uint64_t n_children;
+  int id_shift;              // W's id bits = id hash >> id_shift (30; larger in tests: collisions)
 };
 
 __device__ __forceinline__ uint32_t hot_bucket_of(const HotArgs& H, uint64_t j) {  // last h: c_off[h] <= j
@@ -115,7 +118,7 @@ __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
       const bool cand = isn || meta_tag(m) == KIND_ADD || p == hp;  // remote dels ignored
       if (type_ok && elem_ok && cand) {
         const uint64_t ih = isn ? mix64(id1) : id1;
-        w = ((uint64_t)(g0 + lo) << kHotIdBits) | (ih >> (64 - kHotIdBits));
+        w = ((uint64_t)(g0 + lo) << kHotIdBits) | ((ih >> H.id_shift) << 6) | p;
       }
     } else {
       ++orph;
@@ -174,12 +177,12 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
         H.emit_n[p] = 0;
         H.emit_m[p] = 0;
       }
-      start = W != ~0ull && !(p > 0 && H.w[p - 1] == W);
+      start = W != ~0ull && !(p > 0 && (H.w[p - 1] >> 6) == (W >> 6));  // a run: equal W but the pos bits
     }
     uint32_t nrows = 0;
     if (start) {
       uint64_t e = p + 1;
-      while (e < H.n_children && H.w[e] == W) ++e;
+      while (e < H.n_children && (H.w[e] >> 6) == (W >> 6)) ++e;
       nrows = (uint32_t)(e - p);
     }
     uint32_t kmax = nrows;
@@ -197,17 +200,70 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
       if (pass == 1) obase = (isn ? H.rank_n[p] - H.rank_n[H.h_first[h]] : H.rank_m[p] - H.rank_m[H.h_first[h]]);
     }
     uint32_t nout = 0;
+    auto emit_id = [&](const HotChild& hd, uint64_t v, uint64_t tw, uint64_t wmeta) {
+      if (!isn && (A.flags & F_GC_MEMBERS) && meta_tag(wmeta) == KIND_DEL && tw < A.gc_wm) {
+        ++gcm;
+        return;
+      }
+      if (pass == 1) {
+        const uint32_t o = (uint32_t)(obase + nout);
+        uint64_t* row = (isn ? A.nos + (uint64_t)(A.nbase[b] + o) * kChildStride
+                             : A.mos + (uint64_t)(A.mbase[b] + o) * kChildStride);
+        row[C_PKH] = H.hk_h[G];
+        row[C_PKF] = H.hk_f[G];
+        row[C_ID1] = hd.id1;
+        row[C_ID2] = isn ? v : hd.id2;
+        row[C_T] = isn ? hd.t : tw;
+        row[C_META] = isn ? meta_pack(0, meta_pos(hd.meta), meta_src(hd.meta)) : wmeta;
+        atomicMin(&H.hk_cb[G], o);
+        atomicAdd(&H.hk_cnt[G], 1u);
+        if (isn && (H.hk_vm[G] & kVmaskMerged)) atomicAdd(&H.hk_sum[G], (unsigned long long)v);
+      }
+      ++nout;
+    };
+    // common case: one exact id whose rows arrive in strictly increasing (pos, src) order (the
+    // tag's low bits are the position): one linear pass
+    bool simple = start;
+    {
+      HotChild hd;
+      hd.id1 = hd.id2 = hd.t = hd.meta = 0;
+      hd.j = 0;
+      uint64_t v = 0, tw = 0, wmeta = 0, lastm = 0;
+      for (uint32_t k = 0; k < kmax; ++k) {
+        if (k < nrows && simple) {
+          const HotChild x = hot_child(A, H, p + k, isn);
+          if (k == 0) {
+            hd = x;
+            v = x.id2;
+            tw = x.t;
+            wmeta = x.meta;
+          } else if (x.id1 != hd.id1 || (!isn && x.id2 != hd.id2) || meta_order(x.meta) <= meta_order(lastm)) {
+            simple = false;
+          } else if (isn) {  // Counter::merge (type_counter.rs:60-84): the head's t is kept
+            v = x.t > hd.t ? x.id2 : (x.t == hd.t ? imax64(v, x.id2) : v);
+          } else if (!(tw > x.t)) {  // LWWHash::set (lwwhash.rs:87-107): later wins ties
+            tw = x.t;
+            wmeta = x.meta;
+          }
+          lastm = x.meta;
+        }
+      }
+      if (simple) emit_id(hd, v, tw, wmeta);
+    }
+    // otherwise (ids sharing 34 hash bits): every exact id, by successor selection
+    const bool slow = start && !simple;
+    const uint32_t kslow = __ballot(slow) ? kmax : 0;  // wave-uniform
     HotChild last, head;  // last visited row; first row of the id being folded
     last.id1 = last.id2 = last.t = last.meta = 0;
     last.j = 0;
     head = last;
     uint64_t v = 0, tw = 0, wmeta = 0;  // the fold of head's id so far
     bool open = false;                  // head's id has rows not yet emitted
-    for (uint32_t step = 0; step <= kmax; ++step) {
+    for (uint32_t step = 0; step < kslow + 1 && kslow; ++step) {
       HotChild c = last;
       bool have = false;
-      for (uint32_t k = 0; k < kmax; ++k) {
-        if (k < nrows && step < nrows) {
+      for (uint32_t k = 0; k < kslow; ++k) {
+        if (slow && k < nrows && step < nrows) {
           const HotChild x = hot_child(A, H, p + k, isn);
           const bool after = step == 0 || hot_before(last, x, isn);
           const bool take = after && (!have || hot_before(x, c, isn));
@@ -220,41 +276,20 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
         }
       }
       const bool new_id = !have || !open || c.id1 != head.id1 || (!isn && c.id2 != head.id2);
-      if (open && new_id) {  // head's id is complete: emit it
-        bool emit = true;
-        if (!isn && (A.flags & F_GC_MEMBERS) && meta_tag(wmeta) == KIND_DEL && tw < A.gc_wm) {
-          emit = false;
-          ++gcm;
-        }
-        if (emit) {
-          if (pass == 1) {
-            const uint32_t o = (uint32_t)(obase + nout);
-            uint64_t* row = (isn ? A.nos + (uint64_t)(A.nbase[b] + o) * kChildStride
-                                 : A.mos + (uint64_t)(A.mbase[b] + o) * kChildStride);
-            row[C_PKH] = H.hk_h[G];
-            row[C_PKF] = H.hk_f[G];
-            row[C_ID1] = head.id1;
-            row[C_ID2] = isn ? v : head.id2;
-            row[C_T] = isn ? head.t : tw;
-            row[C_META] = isn ? meta_pack(0, meta_pos(head.meta), meta_src(head.meta)) : wmeta;
-            atomicMin(&H.hk_cb[G], o);
-            atomicAdd(&H.hk_cnt[G], 1u);
-            if (isn && (H.hk_vm[G] & kVmaskMerged)) atomicAdd(&H.hk_sum[G], (unsigned long long)v);
-          }
-          ++nout;
-        }
+      if (slow && open && new_id) {  // head's id is complete: emit it
+        emit_id(head, v, tw, wmeta);
         open = false;
       }
-      if (have) {
+      if (slow && have) {
         if (new_id) {  // c opens an id
           head = c;
           v = c.id2;
           tw = c.t;
           wmeta = c.meta;
           open = true;
-        } else if (isn) {  // Counter::merge (type_counter.rs:60-84): the head's t is kept
+        } else if (isn) {
           v = c.t > head.t ? c.id2 : (c.t == head.t ? imax64(v, c.id2) : v);
-        } else if (!(tw > c.t)) {  // LWWHash::set (lwwhash.rs:87-107): later wins ties
+        } else if (!(tw > c.t)) {
           tw = c.t;
           wmeta = c.meta;
         }

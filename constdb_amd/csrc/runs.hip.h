@@ -245,62 +245,109 @@ __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_runs_kernel(Wave
 }
 
 // Buckets handed to the workgroup tiers: their rows are copied out of the runs into AoS rows
-// (8-word key rows, 6-word child rows, at a place reserved with one atomic per bucket and
-// family) and the row indices of the bucket are written to the permutation, so that
-// bucket.hip.h reads them as it reads partitioned rows.
+// (8-word key rows, 6-word child rows) and the row indices of the bucket are written to the
+// permutation, so that bucket.hip.h reads them as it reads partitioned rows. Work is split in
+// chunks of kMatChunk rows of one (bucket, family), so one over-capacity bucket (C5's hottest
+// keys: millions of children) spreads over the chip instead of one workgroup:
+//   mat_count_kernel : rows per (listed bucket, family) and chunks per listed bucket;
+//   (exclusive scans: each family's AoS row base per bucket, each bucket's first chunk)
+//   mat_copy_kernel  : one workgroup per chunk (grid-stride over the device-side chunk total).
+constexpr uint32_t kMatChunk = 4096;
+
 struct MatArgs {
   uint64_t *kr, *nr, *mr;        // AoS scratch rows
   uint32_t *kp, *np, *mp;        // permutations (indexed by the bucket's base + slot)
-  unsigned long long* cursor;    // 3 scratch cursors
+  uint32_t* cnt;                 // [3][nb]: rows per listed bucket and family
+  uint32_t* base;                // [3][nb]: exclusive scan of cnt per family (AoS row base)
+  uint32_t* chunks;              // [nb]: chunks per listed bucket
+  uint32_t* chunk0;              // [nb]: exclusive scan of chunks
+  const uint64_t* n_chunks;      // total chunks (device)
+  uint32_t nb;
 };
 
-__global__ void __launch_bounds__(256) materialize_kernel(WaveArgs W, MatArgs M, const uint32_t* __restrict__ list,
-                                                          const uint32_t* __restrict__ count) {
+__global__ void __launch_bounds__(256) mat_count_kernel(WaveArgs W, MatArgs M, const uint32_t* __restrict__ list,
+                                                        const uint32_t* __restrict__ count) {
+  const RunView& V = W.V;
+  const uint32_t total = *count;
+  for (uint32_t li = blockIdx.x * blockDim.x + threadIdx.x; li < M.nb; li += gridDim.x * blockDim.x) {
+    uint32_t ch = 0;
+    for (int f = 0; f < 3; ++f) {
+      uint32_t n = 0;
+      if (li < total) {
+        const uint32_t b = list[li];
+        for (uint32_t r = 0; r < V.nr; ++r) {
+          const uint32_t* row = V.rdir[f] + (uint64_t)r * V.nbp1;
+          n += row[b + 1] - row[b];
+        }
+      }
+      M.cnt[(uint64_t)f * M.nb + li] = n;
+      ch += (n + kMatChunk - 1) / kMatChunk;
+    }
+    M.chunks[li] = ch;
+  }
+}
+
+__global__ void __launch_bounds__(256) mat_copy_kernel(WaveArgs W, MatArgs M, const uint32_t* __restrict__ list) {
   const RunView& V = W.V;
   const BucketArgs& A = W.A;
-  __shared__ uint64_t rb[3][kMaxRuns + 1];
-  __shared__ uint32_t rs[3][kMaxRuns + 1], pre[3][kMaxRuns + 2];
-  __shared__ unsigned long long base[3];
-  const uint32_t total = *count;
-  for (uint32_t li = blockIdx.x; li < total; li += gridDim.x) {
-    const uint32_t b = list[li];
+  __shared__ uint32_t rs[kMaxRuns + 1], pre[kMaxRuns + 1];
+  __shared__ uint64_t rb[kMaxRuns + 1];
+  const uint64_t total = *M.n_chunks;
+  for (uint64_t ci = blockIdx.x; ci < total; ci += gridDim.x) {
+    // the listed bucket holding chunk ci: last li with chunk0[li] <= ci
+    uint32_t lo = 0, hi = M.nb;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (M.chunk0[mid] <= ci) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t li = lo, b = list[li];
+    uint32_t local = (uint32_t)(ci - M.chunk0[li]);
+    int f = 0;
+    uint32_t n = M.cnt[li];
+    while (f < 2 && local >= (n + kMatChunk - 1) / kMatChunk) {
+      local -= (n + kMatChunk - 1) / kMatChunk;
+      ++f;
+      n = M.cnt[(uint64_t)f * M.nb + li];
+    }
     __syncthreads();
-    if (threadIdx.x < 3 * V.nr) {
-      const uint32_t f = threadIdx.x / V.nr, r = threadIdx.x % V.nr;
+    if (threadIdx.x < V.nr) {
+      const uint32_t r = threadIdx.x;
       const uint32_t* row = V.rdir[f] + (uint64_t)r * V.nbp1;
-      rs[f][r] = row[b];
-      pre[f][r + 1] = row[b + 1] - row[b];
-      rb[f][r] = V.rbase[f * (kMaxRuns + 1) + r];
+      rs[r] = row[b];
+      pre[r + 1] = row[b + 1] - row[b];
+      rb[r] = V.rbase[f * (kMaxRuns + 1) + r];
     }
     __syncthreads();
-    if (threadIdx.x < 3) {
-      const uint32_t f = threadIdx.x;
-      pre[f][0] = 0;
-      for (uint32_t r = 0; r < V.nr; ++r) pre[f][r + 1] += pre[f][r];
-      base[f] = atomicAdd(&M.cursor[f], (unsigned long long)pre[f][V.nr]);
+    if (threadIdx.x == 0) {
+      pre[0] = 0;
+      for (uint32_t r = 0; r < V.nr; ++r) pre[r + 1] += pre[r];
     }
     __syncthreads();
-    const uint32_t kb[3] = {A.kbase[b], A.nbase[b], A.mbase[b]};
-    for (int f = 0; f < 3; ++f) {
-      const uint32_t n = pre[f][V.nr];
-      for (uint32_t c = threadIdx.x; c < n; c += blockDim.x) {
-        uint32_t r = 0;
-        while (r + 1 < V.nr && pre[f][r + 1] <= c) ++r;
-        const uint64_t src = rb[f][r] + rs[f][r] + (c - pre[f][r]);
-        const uint64_t dst = base[f] + c;
-        if (f == 0) {
-          uint64_t* o = M.kr + dst * kKeyStride;
+    const uint32_t c0 = local * kMatChunk, c1 = min(n, c0 + kMatChunk);
+    const uint32_t abase = M.base[(uint64_t)f * M.nb + li];
+    const uint32_t pb = f == 0 ? A.kbase[b] : f == 1 ? A.nbase[b] : A.mbase[b];
+    for (uint32_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) {
+      uint32_t r = 0, rhi = V.nr;  // last run with pre[r] <= c
+      while (rhi - r > 1) {
+        const uint32_t mid = (r + rhi) >> 1;
+        if (pre[mid] <= c) r = mid;
+        else rhi = mid;
+      }
+      const uint64_t src = rb[r] + rs[r] + (c - pre[r]);
+      const uint64_t dst = (uint64_t)abase + c;
+      if (f == 0) {
+        uint64_t* o = M.kr + dst * kKeyStride;
 #pragma unroll
-          for (int k = 0; k < kKeyCols; ++k) o[k] = V.kin[k][src];
-          o[kKeyCols] = 0;
-          M.kp[kb[0] + c] = (uint32_t)dst;
-        } else {
-          const uint64_t* const* in = f == 1 ? V.nin : V.min;
-          uint64_t* o = (f == 1 ? M.nr : M.mr) + dst * kChildStride;
+        for (int k = 0; k < kKeyCols; ++k) o[k] = V.kin[k][src];
+        o[kKeyCols] = 0;
+        M.kp[pb + c] = (uint32_t)dst;
+      } else {
+        const uint64_t* const* in = f == 1 ? V.nin : V.min;
+        uint64_t* o = (f == 1 ? M.nr : M.mr) + dst * kChildStride;
 #pragma unroll
-          for (int k = 0; k < kChildStride; ++k) o[k] = in[k][src];
-          (f == 1 ? M.np : M.mp)[kb[f] + c] = (uint32_t)dst;
-        }
+        for (int k = 0; k < kChildStride; ++k) o[k] = in[k][src];
+        (f == 1 ? M.np : M.mp)[pb + c] = (uint32_t)dst;
       }
     }
   }

@@ -31,11 +31,14 @@ def ctx():
     return cdb.Context(0)
 
 
-def _check(ctx, snaps, gc=None):
+def _check(ctx, snaps, gc=None, tier=0, want=None):
     flags = cdb_oracle.FLAG_GC if gc is not None else 0
-    rc, want, ost = cdb_oracle.fold(snaps, flags=flags, gc_watermark=gc or 0)
-    assert rc == 0
-    m = cdb.DB(ctx).merge_snapshots(snaps, gc_watermark=gc)
+    if want is None:
+        rc, want, ost = cdb_oracle.fold(snaps, flags=flags, gc_watermark=gc or 0)
+        assert rc == 0
+    else:
+        want, ost = want
+    m = cdb.DB(ctx).merge_snapshots(snaps, gc_watermark=gc, force_tier=tier)
     got = m.canonical_dump()
     if got != want:
         gl, wl = got.split(b"\n"), want.split(b"\n")
@@ -130,3 +133,24 @@ def test_c5_scaled_bit_exact(ctx, universe, events):
     snaps = [cdb.gen_snapshot(cfg, r) for r in range(8)]
     m = _check(ctx, snaps)
     assert m.stats.hot_buckets + m.stats.mid_buckets > 0
+
+
+def test_c3_chip_wide_child_path_repeatable(ctx):
+    """Every bucket of a C3 merge through the over-capacity tier (force_tier=2: key table, tag
+    sort, per-run fold): bit-exact three times over. The tag sort keeps rows of one (key,
+    child) in input order, which varies from merge to merge, so the fold must not depend on it."""
+    snaps = configs.c3_snapshots(cdb, ctx, ops_per_replica=200_000)
+    rc, want, ost = cdb_oracle.fold(snaps)
+    assert rc == 0
+    for _ in range(3):
+        _check(ctx, snaps, tier=2, want=(want, ost))
+
+
+def test_c5_child_id_collisions(ctx, monkeypatch):
+    """Tags with 6 child-id hash bits: most runs hold several exact ids, folded by successor
+    selection instead of the one-id linear pass."""
+    monkeypatch.setenv("CDB_HOT_ID_BITS", "6")
+    cfg = configs.c5(cdb, universe=50_000, events=400_000)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(8)]
+    m = _check(ctx, snaps, tier=2)
+    assert m.stats.hot_buckets > 0
