@@ -181,45 +181,6 @@ def setup(cdb, ctx, args):
 SIGN = -(1 << 63)
 
 
-def sort_into_runs(cdb, ctx, din):
-    """Reorders every family's device rows by (fold position, key hash) in place -- one run per
-    replica, as a replica state produced by this engine arrives -- and records the runs in
-    din.n_runs / din.run_start. Setup only (torch on the library's device columns)."""
-    import torch
-
-    def wrap(ptr, n):
-        class Cai:
-            __cuda_array_interface__ = {"shape": (n,), "typestr": "<i8", "data": (ptr, False), "version": 2}
-        return torch.as_tensor(Cai(), device="cuda")
-
-    R = din.n_pos
-    din.n_runs = R
-    for f, (rows, ncol) in enumerate(((din.keys, 7), (din.nodes, 6), (din.members, 6))):
-        n = rows.n
-        if n == 0:
-            for r in range(R + 1):
-                din.run_start[f][r] = 0
-            continue
-        kh = wrap(rows.col[0], n)
-        meta = wrap(rows.col[ncol - 1], n)
-        o = torch.sort(kh ^ SIGN, stable=True).indices
-        pos = (meta >> 48) & 0xFF
-        o = o[torch.sort(pos[o], stable=True).indices]
-        counts = torch.bincount(pos, minlength=R).tolist()
-        del pos
-        for c in range(ncol):
-            col = wrap(rows.col[c], n)
-            col.copy_(col[o])
-        del o
-        st = 0
-        for r in range(R):
-            din.run_start[f][r] = st
-            st += counts[r]
-        din.run_start[f][R] = st
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
-
-
 def run_single(cdb, args):
     if args.input_order == "sorted":
         import torch  # noqa: F401 -- before libcdbmerge: one HIP runtime per process
@@ -227,7 +188,8 @@ def run_single(cdb, args):
     L = cdb.lib()
     din, opts, info = setup(cdb, ctx, args)
     if args.input_order == "sorted":
-        sort_into_runs(cdb, ctx, din)
+        from constdb_amd.runs import sort_into_runs
+        sort_into_runs(din)
         info["workload"] += ("; input: one key-hash-ordered run per replica (as this engine's merge output and "
                              "snapshots encoded from it arrive): the sorted-run path")
     else:

@@ -106,10 +106,10 @@ struct CompactArgs {
 };
 
 // Sparse-by-bucket outputs -> dense arrays; child ranges become absolute row indices.
-// One wave per group of 64 consecutive buckets: the group's dense output rows are one
-// contiguous range (doff is an exclusive scan), so lane t of a pass copies dense row
-// doff[b0] + t from its bucket's sparse slot — coalesced stores, nearly coalesced loads.
-// The source bucket of a dense row is a 6-step binary search over the group's offsets.
+// A group of 64 consecutive buckets' dense output rows are one contiguous range (doff is an
+// exclusive scan), so lane t of a pass copies dense row doff[b0] + t from its bucket's sparse
+// slot -- coalesced stores, nearly coalesced loads. The source bucket of a dense row is a
+// 6-step binary search over the group's offsets in LDS.
 constexpr int kCompactWaves = 4;
 
 struct CompactLds {
@@ -173,44 +173,65 @@ __device__ __forceinline__ void compact_row(const CompactArgs& A, const CompactL
   }
 }
 
+// One wave per (family, chunk of kCompactChunk dense rows): the chunk's first bucket by a
+// 64-ary search of the dense offsets, then groups of 64 buckets staged in LDS as above. Work
+// per wave is bounded by the chunk, however the rows spread over buckets (an over-capacity
+// bucket with millions of rows is split over many waves).
+constexpr uint32_t kCompactChunk = 4096;
+
 template <int FAM>
-__device__ __forceinline__ void compact_group(const CompactArgs& A, CompactLds& L, uint32_t g, uint32_t nbuckets) {
+__device__ __forceinline__ void compact_chunk(const CompactArgs& A, CompactLds& L, uint64_t chunk, uint32_t nbuckets) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t b0 = g * 64, nb = min(64u, nbuckets - b0);
-  const uint32_t b = b0 + min(lane, nb - 1);
-  const bool in = lane < nb;
   const uint32_t* out = FAM == 0 ? A.kout : FAM == 1 ? A.nout : A.mout;
   const uint32_t* base = FAM == 0 ? A.kbase : FAM == 1 ? A.nbase : A.mbase;
   const uint32_t* doff = FAM == 0 ? A.kdoff : FAM == 1 ? A.ndoff : A.mdoff;
-  const uint32_t d0 = doff[b0];
-  const uint32_t dl = doff[b0 + nb - 1] + out[b0 + nb - 1];
-  // padding lanes repeat the group end so the search never selects them
-  L.doff[lane] = in ? doff[b] - d0 : dl - d0;
-  L.sbase[lane] = base[b];
-  if (FAM == 0) {
-    L.ndoff[lane] = A.ndoff[b];
-    L.mdoff[lane] = A.mdoff[b];
+  const uint32_t total = doff[nbuckets - 1] + out[nbuckets - 1];
+  if (chunk * kCompactChunk >= total) return;
+  const uint32_t c0 = (uint32_t)(chunk * kCompactChunk), c1 = min(total, c0 + kCompactChunk);
+  // last bucket j with doff[j] <= c0 (doff[0] = 0)
+  uint32_t lo = 0, hi = nbuckets;
+  while (hi - lo > 1) {
+    const uint32_t step = (hi - lo + 63) / 64, idx = lo + lane * step;
+    const uint64_t ok = __ballot(idx < hi && doff[idx] <= c0);
+    const uint32_t k = 63 - __builtin_clzll(ok);  // lane 0 always holds
+    lo += k * step;
+    hi = min(hi, lo + step);
   }
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  const uint32_t total = dl - d0;
-  uint32_t t = lane;
-  for (; t + 64 < total; t += 128) {
-    compact_row<FAM>(A, L, t, d0);
-    compact_row<FAM>(A, L, t + 64, d0);
+  for (uint32_t b0 = lo; b0 < nbuckets; b0 += 64) {
+    const uint32_t nb = min(64u, nbuckets - b0);
+    const uint32_t b = b0 + min(lane, nb - 1);
+    const bool in = lane < nb;
+    const uint32_t d0 = doff[b0];
+    const uint32_t dl = doff[b0 + nb - 1] + out[b0 + nb - 1];
+    __builtin_amdgcn_wave_barrier();
+    // padding lanes repeat the group end so the search never selects them
+    L.doff[lane] = in ? doff[b] - d0 : dl - d0;
+    L.sbase[lane] = base[b];
+    if (FAM == 0) {
+      L.ndoff[lane] = A.ndoff[b];
+      L.mdoff[lane] = A.mdoff[b];
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint32_t tend = min(c1, dl) - d0;
+    uint32_t t = max(c0, d0) - d0 + lane;
+    for (; t + 64 < tend; t += 128) {
+      compact_row<FAM>(A, L, t, d0);
+      compact_row<FAM>(A, L, t + 64, d0);
+    }
+    if (t < tend) compact_row<FAM>(A, L, t, d0);
+    if (dl >= c1) break;
   }
-  if (t < total) compact_row<FAM>(A, L, t, d0);
 }
 
-__global__ void __launch_bounds__(kCompactWaves * 64) compact_kernel(CompactArgs A, uint32_t nbuckets) {
+__global__ void __launch_bounds__(kCompactWaves * 64) compact_kernel(CompactArgs A, uint32_t nbuckets, uint64_t ck,
+                                                                     uint64_t cn) {
   __shared__ CompactLds lds_all[kCompactWaves];
   CompactLds& L = lds_all[threadIdx.x >> 6];
-  const uint32_t task = blockIdx.x * kCompactWaves + (threadIdx.x >> 6);
-  const uint32_t g = task / 3, fam = task - g * 3;
-  if (g * 64 >= nbuckets) return;
-  if (fam == 0) compact_group<0>(A, L, g, nbuckets);
-  else if (fam == 1) compact_group<1>(A, L, g, nbuckets);
-  else compact_group<2>(A, L, g, nbuckets);
+  const uint64_t task = (uint64_t)blockIdx.x * kCompactWaves + (threadIdx.x >> 6);
+  if (task < ck) compact_chunk<0>(A, L, task, nbuckets);
+  else if (task < ck + cn) compact_chunk<1>(A, L, task - ck, nbuckets);
+  else compact_chunk<2>(A, L, task - ck - cn, nbuckets);
 }
 
 template <typename T, typename OutT>
@@ -976,8 +997,13 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   C.kout = dk.out; C.nout = dnd.out; C.mout = dm.out;
   C.kdoff = dk.doff; C.ndoff = dnd.doff; C.mdoff = dm.doff;
   C.base_tot = d_lb_tot;
-  compact_kernel<<<(uint32_t)((3 * ((nb + 63) / 64) + kCompactWaves - 1) / kCompactWaves), 64 * kCompactWaves, 0,
-                   s>>>(C, (uint32_t)nb);
+  {  // chunks per family from the input row counts (outputs never exceed inputs)
+    const uint64_t ck = (K + kCompactChunk - 1) / kCompactChunk, cn = (N + kCompactChunk - 1) / kCompactChunk,
+                   cm = (M + kCompactChunk - 1) / kCompactChunk;
+    const uint64_t tasks = std::max<uint64_t>(ck + cn + cm, 1);
+    compact_kernel<<<(uint32_t)((tasks + kCompactWaves - 1) / kCompactWaves), 64 * kCompactWaves, 0, s>>>(
+        C, (uint32_t)nb, ck, cn);
+  }
   CDB_TRY(launch_check(ctx, s, "compact_kernel"));
   stats_reduce_kernel<<<1, 64, 0, s>>>(d_shards, d_stats);
   CDB_TRY(launch_check(ctx, s, "stats_reduce_kernel"));

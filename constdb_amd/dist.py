@@ -1,23 +1,36 @@
-"""Multi-GPU snapshot merge: key-hash sharding with an RCCL all-to-all.
+"""Multi-GPU snapshot merge: key-hash sharding with RCCL point-to-point over xGMI.
 
-One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI). Replica r lives on
-rank r*N/R. Every key has ONE owner rank: owner = top log2(N) bits of its key hash (children
-use their parent's hash, so a key and its children travel together). A merge step:
-  1. pack   : cdb_partition_owner groups each family's rows by owner (HIP multisplit);
-  2. counts : all_to_all of the per-owner row counts (N x 3 integers);
-  3. rows   : one all_to_all_single per column, split sizes = row counts (RCCL);
-  4. merge  : cdb_merge_device on the received rows with key_shift = log2(N), so the local
-              buckets use the hash bits below the owner bits. Outputs stay sharded.
+One process per GPU (torch.distributed, backend "nccl" = RCCL). Replica r lives on rank
+r*N/R, as one run: its rows in key-hash order (runs.py). Every key has ONE owner rank: the
+top log2(N) bits of its key hash (children use their parent's hash, so a key and its children
+travel together). Because a run is in hash order, the rows a rank owes owner d are ONE
+contiguous slice of every run -- there is no pack pass. A merge step:
+  1. splits : per (family, run), the owner boundaries by binary search (torch.searchsorted);
+  2. counts : one all_to_all of the (family, run) row counts, then ONE host copy of the
+              split table and the received counts (the step's only host synchronisation);
+  3. rows   : one batch of point-to-point transfers (dist.batch_isend_irecv -> one RCCL
+              group): per (peer, family, run, column) a contiguous slice, pieces of at most
+              max_piece_bytes; this rank's own slices are device copies;
+  4. merge  : the received slices are again runs in key-hash order (one per source run), so
+              cdb_merge_device takes the sorted-run path (no partition pass) with
+              key_shift = log2(N). Outputs stay sharded.
 There is no other collective on the data path: merging is per key.
 """
 from __future__ import annotations
 
 import ctypes
 import time
-from typing import List, Sequence
+from typing import Sequence
 
-FAMILY_COLS = (7, 6, 6)     # key rows, counter nodes, set/dict members (input layout)
+from .runs import FAMILY_COLS, SIGN, sort_into_runs, wrap
+
 OUT_COLS = (8, 6, 6)
+
+# Largest single transfer. A 2.2 GB (2.2e9-byte, 2.75e8-element) RCCL transfer never completed
+# on MI355X in round 1 while every transfer below 2^31 bytes did: the limit is a byte count
+# crossing 2^31, so every slice moves in pieces of at most 1 GiB. Both sides of a transfer
+# cut the same pieces from the same row count, so no collective is needed to agree on them.
+MAX_PIECE_BYTES = 1 << 30
 
 
 def owner_bits(world: int) -> int:
@@ -35,76 +48,117 @@ def owner_of(h: int, world: int) -> int:
     return (h >> (64 - b)) if b else 0
 
 
-def exchange_counts(send_counts: Sequence[Sequence[int]], device=None) -> List[List[int]]:
-    """send_counts[f][d] = rows of family f this rank sends to rank d. Returns
-    recv_counts[f][s] = rows of family f received from rank s."""
+def _signed(u: int) -> int:
+    u &= (1 << 64) - 1
+    return u - (1 << 64) if u >= (1 << 63) else u
+
+
+def owner_splits(kh, starts: Sequence[int], world: int):
+    """kh: int64 tensor (key-hash bits) of one family whose rows form runs [starts[r],
+    starts[r+1]), each ascending in unsigned order. Returns an int64 tensor [R, world + 1] of
+    absolute row offsets: rows of run r owned by rank d are [s[r, d], s[r, d + 1])."""
     import torch
-    import torch.distributed as dist
-    world = dist.get_world_size()
-    nf = len(send_counts)
-    t = torch.tensor([[send_counts[f][d] for f in range(nf)] for d in range(world)], dtype=torch.int64,
-                     device=device)
-    r = torch.empty_like(t)
-    dist.all_to_all_single(r, t)
-    r = r.cpu().tolist()
-    return [[r[s][f] for s in range(world)] for f in range(nf)]
-
-
-# Largest piece one (source, destination) pair moves in one collective: RCCL's point-to-point
-# transfers misbehave past 2^31 bytes (a 2.2 GB self-transfer never completed on MI355X), so
-# bigger pairs move in several rounds.
-MAX_PIECE_BYTES = 1 << 30
-
-
-def exchange_columns(send_cols, send_counts: Sequence[int], recv_counts: Sequence[int], recv_cols=None,
-                     max_piece_bytes: int = MAX_PIECE_BYTES):
-    """All-to-all of one family's columns. send_cols: list of 1-D int64 tensors grouped by
-    destination (rows for rank 0 first, ...). Returns the received columns (source-rank
-    order). Works with any torch.distributed backend (RCCL on GPUs, gloo in CPU tests).
-    Each column moves with dist.all_to_all over per-peer views (no staging copies), in as
-    many rounds as the largest (source, destination) piece needs."""
-    import torch
-    import torch.distributed as dist
-    world = len(send_counts)
-    total = int(sum(recv_counts))
-    soff = [0] * (world + 1)
-    roff = [0] * (world + 1)
-    for d in range(world):
-        soff[d + 1] = soff[d] + int(send_counts[d])
-        roff[d + 1] = roff[d] + int(recv_counts[d])
-    out = []
-    for c, col in enumerate(send_cols):
-        dst = recv_cols[c][:total] if recv_cols is not None else torch.empty(total, dtype=col.dtype,
-                                                                             device=col.device)
-        piece = max(1, max_piece_bytes // col.element_size())
-        # every rank runs the same number of rounds: the largest pair anywhere decides
-        most = torch.tensor([max(max(send_counts), max(recv_counts))], dtype=torch.int64, device=col.device)
-        dist.all_reduce(most, op=dist.ReduceOp.MAX)
-        rounds = max(1, -(-int(most.item()) // piece))
-        if rounds == 1:
-            dist.all_to_all_single(dst, col[:soff[world]], output_split_sizes=[int(x) for x in recv_counts],
-                                   input_split_sizes=[int(x) for x in send_counts])
-            out.append(dst)
-            continue
-        lists = dist.get_backend() != "gloo"  # gloo has no list all_to_all: stage each round
-        for r in range(rounds):
-            a = r * piece
-            ins = [col[soff[d] + min(a, int(send_counts[d])): soff[d] + min(a + piece, int(send_counts[d]))]
-                   for d in range(world)]
-            outs = [dst[roff[s] + min(a, int(recv_counts[s])): roff[s] + min(a + piece, int(recv_counts[s]))]
-                    for s in range(world)]
-            if lists:
-                dist.all_to_all(outs, ins)
-            else:
-                got = torch.empty(sum(o.numel() for o in outs), dtype=col.dtype, device=col.device)
-                dist.all_to_all_single(got, torch.cat(ins), output_split_sizes=[o.numel() for o in outs],
-                                       input_split_sizes=[i.numel() for i in ins])
-                k = 0
-                for o in outs:
-                    o.copy_(got[k:k + o.numel()])
-                    k += o.numel()
-        out.append(dst)
+    b = owner_bits(world)
+    R = len(starts) - 1
+    out = torch.empty((R, world + 1), dtype=torch.int64, device=kh.device)
+    bounds = torch.tensor([_signed((d << (64 - b)) ^ (1 << 63)) if b else _signed(1 << 63) for d in range(world)],
+                          dtype=torch.int64, device=kh.device)
+    for r in range(R):
+        a, e = int(starts[r]), int(starts[r + 1])
+        if e > a:
+            out[r, :world] = torch.searchsorted(kh[a:e] ^ SIGN, bounds) + a
+        else:
+            out[r, :world] = a
+        out[r, world] = e
     return out
+
+
+def _pieces(a: int, e: int, piece_rows: int):
+    while a < e:
+        b = min(e, a + piece_rows)
+        yield a, b
+        a = b
+
+
+class Plan:
+    """Who sends what to whom in one step (host integers, from the one synchronised copy)."""
+
+    def __init__(self, splits, recv, world: int, rank: int, n_runs: int):
+        self.world, self.rank, self.R = world, rank, n_runs
+        self.splits = splits      # [3][R][world + 1] absolute offsets in this rank's rows
+        self.recv = recv          # [world(src)][3][R] rows this rank receives
+        # receiver runs: (source run r, source s) pairs that carry rows, in (r, s) order
+        self.runs = [(r, s) for r in range(n_runs) for s in range(world)
+                     if any(recv[s][f][r] for f in range(3))]
+        self.run_start = []       # [3][len(runs) + 1]
+        self.total = []
+        for f in range(3):
+            st, acc = [], 0
+            for r, s in self.runs:
+                st.append(acc)
+                acc += recv[s][f][r]
+            st.append(acc)
+            self.run_start.append(st)
+            self.total.append(acc)
+
+    def dest(self, f: int, r: int, s: int) -> int:
+        """First receive-buffer row of source s's run r in family f."""
+        return self.run_start[f][self.runs.index((r, s))]
+
+
+def make_plan(fams, starts, world: int, rank: int, device=None) -> Plan:
+    """fams: three [ncols, n] int64 tensors (this rank's rows as runs); starts: three lists of
+    R + 1 run offsets. One all_to_all of the counts, one host copy."""
+    import torch
+    import torch.distributed as dist
+    R = len(starts[0]) - 1
+    sp = torch.stack([owner_splits(fams[f][0], starts[f], world) for f in range(3)])  # [3, R, world+1]
+    cnt = (sp[:, :, 1:] - sp[:, :, :-1]).permute(2, 0, 1).contiguous()             # [world(dst), 3, R]
+    if device is not None:
+        cnt = cnt.to(device)
+    got = torch.empty_like(cnt)
+    if world > 1:
+        dist.all_to_all_single(got, cnt)
+    else:
+        got.copy_(cnt)
+    host = torch.cat([sp.reshape(-1).to(got.device), got.reshape(-1)]).cpu().tolist()
+    k = 3 * R * (world + 1)
+    flat_sp, flat_got = host[:k], host[k:]
+    splits = [[flat_sp[(f * R + r) * (world + 1):(f * R + r + 1) * (world + 1)] for r in range(R)] for f in range(3)]
+    recv = [[flat_got[(s * 3 + f) * R:(s * 3 + f + 1) * R] for f in range(3)] for s in range(world)]
+    return Plan(splits, recv, world, rank, R)
+
+
+def exchange_runs(fams, plan: Plan, recv_bufs, max_piece_bytes: int = MAX_PIECE_BYTES) -> int:
+    """Moves every owed slice into recv_bufs (three [ncols, >= total] tensors on the same
+    device as fams) at the plan's run offsets. One batch of point-to-point operations; own
+    slices are local copies. Returns the number of point-to-point operations posted."""
+    import torch.distributed as dist
+    world, me = plan.world, plan.rank
+    ops = []
+    for peer in range(world):
+        for f in range(3):
+            t, buf = fams[f], recv_bufs[f]
+            piece = max(1, max_piece_bytes // t.element_size())
+            for r in range(plan.R):
+                # what I send to peer: my run r's slice owned by peer
+                a, e = plan.splits[f][r][peer], plan.splits[f][r][peer + 1]
+                # what I receive from peer: peer's run r's slice owned by me
+                n_in = plan.recv[peer][f][r]
+                d0 = plan.dest(f, r, peer) if n_in else 0
+                if peer == me:
+                    if e > a:
+                        buf[:, d0:d0 + (e - a)].copy_(t[:, a:e])
+                    continue
+                for c in range(t.shape[0]):
+                    for x, y in _pieces(a, e, piece):
+                        ops.append(dist.P2POp(dist.isend, t[c, x:y], peer))
+                    for x, y in _pieces(d0, d0 + n_in, piece):
+                        ops.append(dist.P2POp(dist.irecv, buf[c, x:y], peer))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    return len(ops)
 
 
 def _rows_from_tensor(cdb, t, n):
@@ -114,6 +168,31 @@ def _rows_from_tensor(cdb, t, n):
         r.col[c] = t[c].data_ptr()
     r.n = n
     return r
+
+
+def _input_tensors(din):
+    """The input families as three [ncols, n] torch tensors (copies: the library's columns
+    are separate allocations; setup, outside any timed step)."""
+    import torch
+    out = []
+    for rows, nc in zip((din.keys, din.nodes, din.members), FAMILY_COLS):
+        if rows.n:
+            out.append(torch.stack([wrap(rows.col[c], rows.n) for c in range(nc)]))
+        else:
+            out.append(torch.zeros((nc, 0), dtype=torch.int64, device="cuda"))
+    return out
+
+
+def _merge_input(cdb, recv, plan: Plan, n_pos: int):
+    d = cdb.DevInput()
+    d.keys, d.nodes, d.members = (_rows_from_tensor(cdb, recv[f], plan.total[f]) for f in range(3))
+    d.n_pos = n_pos
+    if len(plan.runs) <= cdb.MAX_RUNS:
+        d.n_runs = len(plan.runs)
+        for f in range(3):
+            for i, v in enumerate(plan.run_start[f]):
+                d.run_start[f][i] = v
+    return d
 
 
 def _log(rank, msg):
@@ -137,94 +216,80 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
     cfg = c4_config(cdb, universe, R, args.seed, lo, hi)
     din = cdb.DevInput()
     ctx.check(L.cdb_gen_device(ctx.handle, ctypes.byref(cfg), ctypes.byref(din)))
-    _log(rank, f"generated {din.keys.n} key rows")
-    fams_in = [din.keys, din.nodes, din.members]
-    n_in = [f.n for f in fams_in]
-    send = [torch.empty((FAMILY_COLS[f], max(n_in[f], 1)), dtype=torch.int64, device=dev) for f in range(3)]
+    din.n_pos = R
+    sort_into_runs(din, R)  # setup: this rank's replica states as key-hash-ordered runs
+    fams = _input_tensors(din)
+    starts = [[din.run_start[f][r] for r in range(R + 1)] for f in range(3)]
+    n_in = [din.keys.n, din.nodes.n, din.members.n]
+    for fam in (din.keys, din.nodes, din.members):
+        L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
+    _log(rank, f"generated {n_in[0]} key rows as {R} runs")
     opts = cdb.MergeOpts()
     opts.key_shift = ob
     st = cdb.MergeStats()
-    counts = (ctypes.c_uint64 * world)()
     state = {}
-    # One explicit stream for the whole step: torch makes it wait for each RCCL collective, and
+    # One explicit stream for the whole step: torch orders it after each RCCL transfer, and
     # the library's kernels run on it too (the legacy default stream's handle is 0, which the
     # library would read as "use the context's own stream" -- unordered with the exchange).
     cs = torch.cuda.Stream(device=dev)
 
+    def buf(key, ncols, need):
+        b = state.get(key)
+        if b is None or b.shape[1] < need:
+            b = torch.empty((ncols, need + need // 8), dtype=torch.int64, device=dev)
+            state[key] = b
+        return b
+
     def step():
         with torch.cuda.stream(cs):
-            _step()
-
-    def _step():
-        stream = torch.cuda.current_stream().cuda_stream
-        assert stream, "the merge must run on the exchange's (non-default) stream"
-        send_counts = []
-        for f in range(3):
-            out_rows = _rows_from_tensor(cdb, send[f], n_in[f])
-            ctx.check(L.cdb_partition_owner(ctx.handle, ctypes.byref(fams_in[f]), FAMILY_COLS[f], ob,
-                                            ctypes.byref(out_rows), counts, ctypes.c_void_p(stream)))
-            send_counts.append([counts[d] for d in range(world)])
-        _log(rank, "packed") if not state.get("quiet") else None
-        recv_counts = exchange_counts(send_counts, device=dev)
-        _log(rank, f"counts exchanged {recv_counts}") if not state.get("quiet") else None
-        recv = []
-        for f in range(3):
-            total = sum(recv_counts[f])
-            buf = state.get(("recv", f))
-            if buf is None or buf.shape[1] < max(total, 1):
-                buf = torch.empty((FAMILY_COLS[f], max(total, 1) + max(total, 1) // 8), dtype=torch.int64,
-                                  device=dev)
-                state[("recv", f)] = buf
-            cols = [send[f][c][:n_in[f]] for c in range(FAMILY_COLS[f])]
-            exchange_columns(cols, send_counts[f], recv_counts[f], recv_cols=buf)
-            recv.append((buf, total))
-        if not state.get("quiet"):  # first (warmup) step: locate a stall in the log
-            torch.cuda.current_stream().synchronize()
-            _log(rank, "rows exchanged")
-        din2 = cdb.DevInput()
-        din2.keys = _rows_from_tensor(cdb, recv[0][0], recv[0][1])
-        din2.nodes = _rows_from_tensor(cdb, recv[1][0], recv[1][1])
-        din2.members = _rows_from_tensor(cdb, recv[2][0], recv[2][1])
-        din2.n_pos = R
-        dout = cdb.DevOutput()
-        outs = []
-        for f, fam in enumerate((dout.keys, dout.nodes, dout.members)):
-            buf = state.get(("out", f))
-            need = max(recv[f][1], 1)
-            if buf is None or buf.shape[1] < need:
-                buf = torch.empty((OUT_COLS[f], need + need // 8), dtype=torch.int64, device=dev)
-                state[("out", f)] = buf
-            outs.append(buf)
-        dout.keys = _rows_from_tensor(cdb, outs[0], 0)
-        dout.nodes = _rows_from_tensor(cdb, outs[1], 0)
-        dout.members = _rows_from_tensor(cdb, outs[2], 0)
-        dout.compact = 1
-        ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(din2), ctypes.byref(opts), ctypes.byref(dout),
-                                     ctypes.byref(st), ctypes.c_void_p(stream)))
-        _log(rank, "merged") if not state.get("quiet") else None
-        state["quiet"] = True
+            if world == 1:  # every row is this rank's own: the runs are the merge input as they lie
+                d2 = cdb.DevInput()
+                d2.keys, d2.nodes, d2.members = (_rows_from_tensor(cdb, fams[f], n_in[f]) for f in range(3))
+                d2.n_pos = R
+                d2.n_runs = R
+                for f in range(3):
+                    for r in range(R + 1):
+                        d2.run_start[f][r] = starts[f][r]
+                state["ops"], state["runs"] = 0, R
+                total = n_in
+            else:
+                plan = make_plan(fams, starts, world, rank)
+                recv = [buf(("recv", f), FAMILY_COLS[f], max(plan.total[f], 1)) for f in range(3)]
+                state["ops"] = exchange_runs(fams, plan, recv)
+                state["runs"] = len(plan.runs)
+                d2 = _merge_input(cdb, recv, plan, R)
+                total = plan.total
+            dout = cdb.DevOutput()
+            outs = [buf(("out", f), OUT_COLS[f], max(total[f], 1)) for f in range(3)]
+            dout.keys, dout.nodes, dout.members = (_rows_from_tensor(cdb, t, 0) for t in outs)
+            dout.compact = 1
+            stream = torch.cuda.current_stream().cuda_stream
+            assert stream, "the merge must run on the exchange's (non-default) stream"
+            ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(d2), ctypes.byref(opts), ctypes.byref(dout),
+                                         ctypes.byref(st), ctypes.c_void_p(stream)))
 
     for i in range(args.warmup):
         step()
-        _log(rank, f"warmup step {i} done")
-    bucket_ms = 0.0
+        _log(rank, f"warmup step {i} done ({state['ops']} p2p ops, {state['runs']} runs, "
+                   f"sorted-run path {st.sorted_runs})")
+    dev_ms = 0.0
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        bucket_ms += st.bucket_ms
+        dev_ms += st.device_ms
     torch.cuda.synchronize()
     dist.barrier()
     t1 = time.perf_counter()
     el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    tot = torch.tensor([n_in[0], n_in[1], n_in[2]], dtype=torch.int64, device=dev)
+    tot = torch.tensor(n_in, dtype=torch.int64, device=dev)
     dist.all_reduce(tot)
     ms = el.item() * 1e3 / args.steps
     entries = int(tot[0].item())
     B = alg_bytes(st)
-    bk = bucket_ms / args.steps
+    dm = dev_ms / args.steps
     res = {
         "metric": "merged CRDT entries/sec (snapshot merge)",
         "value": entries / (ms * 1e-3),
@@ -237,64 +302,52 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u64",
-        "data": "synthetic: seeded GenModel replica states generated in HBM (keys 'key:<i>')",
+        "data": "synthetic: seeded GenModel replica states generated in HBM (keys 'key:<i>'), "
+                "each replica one key-hash-ordered run",
         "config": {"workload": f"C4 anti-entropy: {universe} keys x {R} replicas, replica r on rank r*N/R, "
-                               f"rows routed to owner = top log2(N) key-hash bits via RCCL all-to-all",
-                   "replicas": R, "key_rows_in_total": entries, "parallelism": f"key-hash sharding x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "bucket_wave_kernel (rank 0)",
-                     "achieved": B / (bk * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-                     "frac": B / (bk * 1e-3) / 1e9 / 8000.0, "traffic": None},
+                               f"owner = top log2(N) key-hash bits; every run's owner slice moves by RCCL "
+                               f"point-to-point, merged on the sorted-run path",
+                   "config": "c4", "replicas": R, "key_rows_in_total": entries,
+                   "parallelism": f"key-hash sharding x{world}", "p2p_ops_per_step": state["ops"],
+                   "merge_path": "sorted runs" if st.sorted_runs else "partition"},
+        "roofline": {"bound": "hbm", "kernel": "whole merge pipeline on rank 0 (cdb_merge_device, HIP events)",
+                     "achieved": B / (dm * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
+                     "frac": B / (dm * 1e-3) / 1e9 / 8000.0, "alg_bytes": B, "traffic": None},
     }
     dist.barrier()
-    for fam in (din.keys, din.nodes, din.members):
-        L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
     dist.destroy_process_group()
     return res
 
 
-def sharded_merge(cdb, ctx, din, n_pos: int, stream=None):
-    """One sharded merge step, outside the bench's timing harness: pack this rank's rows by
-    owner (cdb_partition_owner), exchange them (RCCL on GPU tensors; gloo through host copies),
-    merge the received shard with key_shift = log2(N). Returns ([keys, nodes, members] output
-    column tensors, MergeStats). Used by the multi-process tests; bench.py runs the same steps
-    with persistent buffers."""
+def sharded_merge(cdb, ctx, din, n_pos: int, stream=None, max_piece_bytes: int = MAX_PIECE_BYTES):
+    """One sharded merge step outside the bench's timing harness: this rank's rows as runs
+    (sorted here when din carries none), the owner slices exchanged (RCCL on GPU tensors; gloo
+    through host copies), the received runs merged with key_shift = log2(N). Returns ([keys,
+    nodes, members] output column tensors, MergeStats, Plan). Used by the multi-process tests."""
     import torch
     import torch.distributed as dist
-    world = dist.get_world_size()
+    world, rank = dist.get_world_size(), dist.get_rank()
     ob = owner_bits(world)
     L = cdb.lib()
     dev = torch.device("cuda", torch.cuda.current_device())
     on_host = dist.get_backend() == "gloo"
-    fams = [din.keys, din.nodes, din.members]
-    counts = (ctypes.c_uint64 * world)()
-    send, send_counts = [], []
-    for f, fam in enumerate(fams):
-        t = torch.empty((FAMILY_COLS[f], max(fam.n, 1)), dtype=torch.int64, device=dev)
-        ctx.check(L.cdb_partition_owner(ctx.handle, ctypes.byref(fam), FAMILY_COLS[f], ob,
-                                        ctypes.byref(_rows_from_tensor(cdb, t, fam.n)), counts, stream))
-        send.append(t)
-        send_counts.append([counts[d] for d in range(world)])
-    recv_counts = exchange_counts(send_counts, device=None if on_host else dev)
-    recv = []
-    for f in range(3):
-        cols = [send[f][c][:fams[f].n] for c in range(FAMILY_COLS[f])]
-        if on_host:
-            cols = [c.cpu() for c in cols]
-        got = exchange_columns(cols, send_counts[f], recv_counts[f])
-        total = int(sum(recv_counts[f]))
-        buf = torch.empty((FAMILY_COLS[f], max(total, 1)), dtype=torch.int64, device=dev)
-        for c, g in enumerate(got):
-            buf[c][:total].copy_(g)
-        recv.append((buf, total))
+    din.n_pos = n_pos
+    if din.n_runs == 0:
+        sort_into_runs(din, n_pos)
+    R = din.n_runs
+    starts = [[din.run_start[f][r] for r in range(R + 1)] for f in range(3)]
+    fams = _input_tensors(din)
+    if on_host:
+        fams = [t.cpu() for t in fams]
+    plan = make_plan(fams, starts, world, rank)
+    recv = [torch.empty((FAMILY_COLS[f], max(plan.total[f], 1)), dtype=torch.int64, device=fams[f].device)
+            for f in range(3)]
+    exchange_runs(fams, plan, recv, max_piece_bytes)
+    recv = [t.to(dev) for t in recv]
     torch.cuda.synchronize()
-    d2 = cdb.DevInput()
-    d2.keys, d2.nodes, d2.members = (_rows_from_tensor(cdb, b, n) for b, n in recv)
-    d2.n_pos = n_pos
+    d2 = _merge_input(cdb, recv, plan, n_pos)
     dout = cdb.DevOutput()
-    outs = []
-    for f, (b, n) in enumerate(recv):
-        t = torch.empty((OUT_COLS[f], max(n, 1)), dtype=torch.int64, device=dev)
-        outs.append(t)
+    outs = [torch.empty((OUT_COLS[f], max(plan.total[f], 1)), dtype=torch.int64, device=dev) for f in range(3)]
     dout.keys, dout.nodes, dout.members = (_rows_from_tensor(cdb, t, 0) for t in outs)
     dout.compact = 1
     opts = cdb.MergeOpts()
@@ -303,4 +356,4 @@ def sharded_merge(cdb, ctx, din, n_pos: int, stream=None):
     ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(d2), ctypes.byref(opts), ctypes.byref(dout),
                                  ctypes.byref(st), stream))
     torch.cuda.synchronize()
-    return [outs[0][:, :dout.keys.n], outs[1][:, :dout.nodes.n], outs[2][:, :dout.members.n]], st
+    return [outs[0][:, :dout.keys.n], outs[1][:, :dout.nodes.n], outs[2][:, :dout.members.n]], st, plan

@@ -19,11 +19,24 @@ def _free_port():
     return p
 
 
-def _rows(rank, n=997):
+SIGN = -(1 << 63)
+
+
+def _runs(rank, n_runs, n=997):
+    """Rank `rank`'s rows as n_runs runs (some empty), each ascending in unsigned key hash:
+    [cols, n] with column 0 = key hash, plus the run offsets."""
     rng = np.random.default_rng(1000 + rank)
-    kh = rng.integers(0, 2**63, size=n, dtype=np.int64) * 2 + rng.integers(0, 2, size=n)
-    payload = rng.integers(-2**62, 2**62, size=(5, n), dtype=np.int64)
-    return np.vstack([kh[None, :], payload])  # [cols, n]; column 0 = key hash
+    sizes = rng.multinomial(n, [1 / n_runs] * n_runs)
+    sizes[rank % n_runs] = 0  # an empty run
+    parts = []
+    for r, m in enumerate(sizes):
+        kh = rng.integers(0, 2**63, size=m, dtype=np.int64) * 2 + rng.integers(0, 2, size=m)
+        kh = np.sort(kh.view(np.uint64)).view(np.int64)
+        payload = rng.integers(-2**62, 2**62, size=(5, m), dtype=np.int64)
+        payload[0] = r  # the run a row came from
+        parts.append(np.vstack([kh[None, :], payload]))
+    starts = [0] + np.cumsum(sizes).tolist()
+    return np.hstack(parts), starts
 
 
 def _owner(col0, world):
@@ -38,19 +51,42 @@ def _worker(rank, world, port, q, piece=None):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        rows = _rows(rank)
-        own = _owner(rows[0], world)
-        order = np.argsort(own, kind="stable")          # the pack step (cdb_partition_owner on GPU)
-        packed = rows[:, order]
-        counts = np.bincount(own, minlength=world).tolist()
-        recv_counts = cdist.exchange_counts([counts])
-        cols = [torch.from_numpy(np.ascontiguousarray(packed[c])) for c in range(packed.shape[0])]
+        R = 3
+        # three families of different widths, as key rows / nodes / members
+        data = [_runs(rank + 17 * f, R) for f in range(3)]
+        fams = [torch.from_numpy(np.ascontiguousarray(d[0][: 6 + (f == 0)] if d[0].shape[0] >= 6 else d[0]))
+                for f, d in enumerate(data)]
+        starts = [d[1] for d in data]
+        plan = cdist.make_plan(fams, starts, world, rank)
+        recv = [torch.empty((fams[f].shape[0], max(plan.total[f], 1)), dtype=torch.int64) for f in range(3)]
         kw = {"max_piece_bytes": piece} if piece else {}
-        got = cdist.exchange_columns(cols, counts, recv_counts[0], **kw)
-        got = np.vstack([g.numpy()[None, :] for g in got])
-        want = np.hstack([r[:, _owner(r[0], world) == rank] for r in (_rows(s) for s in range(world))])
-        ok = sorted(map(tuple, got.T.tolist())) == sorted(map(tuple, want.T.tolist()))
-        ok = ok and bool(np.all(_owner(got[0], world) == rank)) and sum(recv_counts[0]) == got.shape[1]
+        ops = cdist.exchange_runs(fams, plan, recv, **kw)
+        ok = True
+        for f in range(3):
+            got = recv[f][:, :plan.total[f]].numpy()
+            allr = [_runs(s + 17 * f, R) for s in range(world)]
+            want = np.hstack([r[:, _owner(r[0], world) == rank] for r, _ in allr])
+            want = want[: fams[f].shape[0]]
+            ok = ok and sorted(map(tuple, got.T.tolist())) == sorted(map(tuple, want.T.tolist()))
+            ok = ok and bool(np.all(_owner(got[0], world) == rank))
+            st = plan.run_start[f]
+            for i, (r, s) in enumerate(plan.runs):  # every receiver run: one source run, sorted
+                seg = got[:, st[i]:st[i + 1]]
+                u = seg[0].view(np.uint64)
+                ok = ok and bool(np.all(u[1:] >= u[:-1])) and bool(np.all(seg[1] == r))
+        # pieces: every transfer is cut at `piece` bytes on both sides
+        p_rows = max(1, (piece or cdist.MAX_PIECE_BYTES) // 8)
+        want_ops = 0
+        for peer in range(world):
+            if peer == rank:
+                continue
+            for f in range(3):
+                nc = fams[f].shape[0]
+                for r in range(R):
+                    a, e = plan.splits[f][r][peer], plan.splits[f][r][peer + 1]
+                    want_ops += nc * (-(-(e - a) // p_rows))
+                    want_ops += nc * (-(-plan.recv[peer][f][r] // p_rows))
+        ok = ok and ops == want_ops
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()
@@ -58,8 +94,9 @@ def _worker(rank, world, port, q, piece=None):
 
 @pytest.mark.parametrize("world,piece", [(2, None), (4, None), (2, 800), (4, 2000)])
 def test_exchange_gloo(world, piece):
-    """The column exchange; a small piece limit forces the multi-round path that keeps every
-    (source, destination) transfer under RCCL's 2^31-byte limit at full size."""
+    """The run-slice exchange: every rank receives exactly the rows it owns, each source run's
+    slice as one receiver run still in key-hash order; a small piece limit cuts every transfer
+    into pieces on both sides (the 1 GiB limit at full size), with the op count pinned."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -71,6 +108,20 @@ def test_exchange_gloo(world, piece):
     for p in procs:
         p.join(timeout=60)
     assert all(res[r] for r in range(world)), res
+
+
+def test_owner_splits_cpu():
+    import torch
+    rows, starts = _runs(5, 4, n=3000)
+    kh = torch.from_numpy(rows[0].copy())
+    for world in (1, 2, 4, 8):
+        sp = cdist.owner_splits(kh, starts, world).tolist()
+        for r in range(4):
+            a, e = starts[r], starts[r + 1]
+            own = _owner(rows[0, a:e], world)
+            assert sp[r][0] == a and sp[r][world] == e
+            for d in range(world):
+                assert np.all(own[sp[r][d] - a:sp[r][d + 1] - a] == d)
 
 
 def _records(dump: bytes):

@@ -1,7 +1,7 @@
 """The sharded merge end to end on the GPU with two ranks: each rank generates
-its replicas in HBM, packs rows by owner (top key-hash bit), exchanges them (gloo through host
-copies: both ranks share this box's one GPU, which RCCL refuses), and merges its shard with
-key_shift = 1. The union of the two shards' outputs must equal the single-GPU merge of all
+its replicas in HBM as key-hash-ordered runs, sends every run's owner slice (top key-hash bit)
+to its owner (gloo through host copies: both ranks share this box's one GPU, which RCCL
+refuses), and merges the received runs on the sorted-run path with key_shift = 1. The union of the two shards' outputs must equal the single-GPU merge of all
 replicas: the same key rows and the same child rows under the same keys."""
 import os
 import socket
@@ -49,7 +49,8 @@ def _worker(rank, world, port, outdir):
         din = cdb2.DevInput()
         lo, hi = rank * REPLICAS // world, (rank + 1) * REPLICAS // world
         ctx.check(L.cdb_gen_device(ctx.handle, ctypes.byref(_cfg(lo, hi)), ctypes.byref(din)))
-        outs, st = cdist.sharded_merge(cdb2, ctx, din, REPLICAS)
+        outs, st, plan = cdist.sharded_merge(cdb2, ctx, din, REPLICAS)
+        assert st.sorted_runs == 1 and len(plan.runs) == REPLICAS  # one receiver run per replica
         k, n, m = _canon(outs)
         np.savez(os.path.join(outdir, f"r{rank}.npz"), k=k, n=n, m=m)
         for fam in (din.keys, din.nodes, din.members):
