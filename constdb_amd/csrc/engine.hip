@@ -618,8 +618,8 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   }
   if (wide_ids.empty()) return CDB_OK;
   const uint32_t H = (uint32_t)wide_ids.size();
-  // device: ids[H] | hk_off[H + 1] | c_off[H + 1] | hk_kout[H] | h_first[H]
-  uint32_t* meta = (uint32_t*)ws_get(ctx, WS_HOTMETA, (5ull * H + 2) * sizeof(uint32_t), &st);
+  // device: ids[H] | hk_off[H + 1] | c_off[H + 1] | hk_kout[H] | h_first[H] | run count
+  uint32_t* meta = (uint32_t*)ws_get(ctx, WS_HOTMETA, (5ull * H + 6) * sizeof(uint32_t), &st);
   if (!meta) return st;
   HotArgs HA;
   std::memset(&HA, 0, sizeof HA);
@@ -651,7 +651,7 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   HA.hk_tp = (uint32_t*)(HA.hk_sum + nk);
   HA.hk_cnt = HA.hk_tp + nk;
   HA.hk_cb = HA.hk_cnt + nk;
-  uint8_t* ct = (uint8_t*)ws_get(ctx, WS_HOTCH, nc * (2 * 8 + 2 * 4 + 2 * 4 + 4 * 4) + 64, &st);
+  uint8_t* ct = (uint8_t*)ws_get(ctx, WS_HOTCH, nc * (2 * 8 + 2 * 4 + 2 * 4 + 5 * 4) + 64, &st);
   if (!ct) return st;
   uint64_t* w = (uint64_t*)ct;
   uint64_t* w2 = w + nc;
@@ -680,6 +680,19 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   hot_first_kernel<<<(H + 255) / 256, 256, 0, s>>>(HA);
   CDB_TRY(launch_check(ctx, s, "hot_first_kernel"));
   if (tc) {
+    // the sort's other buffers are free now: fold results per run start
+    HA.fold_v = HA.w == w ? w2 : w;
+    HA.fold_q = HA.v == v ? v2 : v;
+    uint64_t* d_runs = (uint64_t*)(((uintptr_t)(HA.h_first + H) + 7) & ~(uintptr_t)7);
+    HA.run_count = d_runs;
+    HA.run_list = rank_m + nc;
+    // run starts -> run list (ascending): flags in emit_n, their scan in rank_n
+    hot_runflag_kernel<<<grid, 256, 0, s>>>(HA, HA.emit_n);
+    CDB_TRY(launch_check(ctx, s, "hot_runflag_kernel"));
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, HA.emit_n, tc, rank_n, (uint32_t*)nullptr, d_runs, s));
+    hot_runlist_kernel<<<grid, 256, 0, s>>>(HA, HA.emit_n, rank_n);
+    CDB_TRY(launch_check(ctx, s, "hot_runlist_kernel"));
+    CDB_HIP(hipMemsetAsync(HA.emit_n, 0, 2 * tc * sizeof(uint32_t), s), "memset");  // emit_n | emit_m
     hot_fold_kernel<<<grid, 256, 0, s>>>(A, HA, 0);
     CDB_TRY(launch_check(ctx, s, "hot_fold_kernel"));
     CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, HA.emit_n, tc, rank_n, (uint32_t*)nullptr, nullptr, s));

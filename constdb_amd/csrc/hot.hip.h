@@ -25,8 +25,7 @@
 
 namespace cdb {
 
-constexpr int kHotIdBits = 40;
-  // W = G << 40 | child-id hash >> 24
+constexpr int kHotIdBits = 40;  // W = G << 40 | (child-id hash >> id_shift) << 6 | pos
 
 struct HotArgs {
   const uint32_t* ids;       // hot bucket of h
@@ -48,6 +47,11 @@ struct HotArgs {
   uint32_t* h_first;         // per h: first sorted position of its children
   uint64_t n_children;
   int id_shift;              // W's id bits = id hash >> id_shift (30; larger in tests: collisions)
+  uint32_t* run_list;        // sorted position of every run's first row, ascending
+  const uint64_t* run_count; // runs in run_list (device)
+  uint32_t* fold_q;          // per run start: the sorted position whose row is the output
+                             // (members: the winner; nodes: the head), kNone: selection path
+  uint64_t* fold_v;          // per run start: a counter node's folded value
 };
 
 __device__ __forceinline__ uint32_t hot_bucket_of(const HotArgs& H, uint64_t j) {  // last h: c_off[h] <= j
@@ -157,41 +161,52 @@ __device__ __forceinline__ bool hot_before(const HotChild& a, const HotChild& b,
   return a.j < b.j;
 }
 
-// pass 0: emit counts per run (emit_n / emit_m at the run's first position); pass 1: outputs.
-// A run holds ~ one row per replica; each step selects the successor of the last visited row
-// (an O(run^2) selection over rows in L2, no per-thread arrays), so rows are folded in order
-// whatever order the sort left them in. Every loop has a wave-uniform trip count (the longest
-// run in the wave) with per-lane predicates: the selection's loop-carried row must not be a
-// live-out of a loop with divergent exits (gfx950 compilers have produced the first candidate
-// instead of the smallest there).
+// Run starts: flag per sorted position (then an exclusive scan gives each run its index).
+__global__ void __launch_bounds__(256) hot_runflag_kernel(HotArgs H, uint32_t* __restrict__ flag) {
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < H.n_children;
+       p += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t W = H.w[p];
+    flag[p] = W != ~0ull && !(p > 0 && (H.w[p - 1] >> 6) == (W >> 6));  // a run: equal W but the pos bits
+  }
+}
+__global__ void __launch_bounds__(256) hot_runlist_kernel(HotArgs H, const uint32_t* __restrict__ flag,
+                                                          const uint32_t* __restrict__ idx) {
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < H.n_children;
+       p += (uint64_t)gridDim.x * blockDim.x)
+    if (flag[p]) H.run_list[idx[p]] = (uint32_t)p;
+}
+
+constexpr uint32_t kFoldFast = 8;  // runs up to this many rows: rows in registers, loads overlapped
+
+// One thread per run. Pass 0: the run's output count (emit_n / emit_m at its first position)
+// and, for a run of one exact id whose rows arrive in strictly increasing (pos, src) order (the
+// tag's low bits are the position) and no longer than kFoldFast, the output row's position and
+// value (fold_q / fold_v); pass 1 writes outputs at their rank. Other runs (ids sharing 34 hash
+// bits, long runs) fold by successor selection in both passes: each step selects the successor
+// of the last visited row (O(run^2) over rows in L2, no per-thread arrays), so rows are folded
+// in order whatever order the sort left them in. Loops have wave-uniform trip counts with
+// per-lane predicates: a loop-carried row must not be a live-out of a loop with divergent exits
+// (gfx950 compilers have produced the first candidate instead of the smallest there).
 __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, int pass) {
   unsigned long long gcm = 0;
+  const uint64_t nruns = *H.run_count;
+  const uint32_t lane = threadIdx.x & 63;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < H.n_children; base += stride) {
-    const uint64_t p = base + threadIdx.x;
-    uint64_t W = ~0ull;
-    bool start = false;
-    if (p < H.n_children) {
-      W = H.w[p];
-      if (pass == 0) {
-        H.emit_n[p] = 0;
-        H.emit_m[p] = 0;
-      }
-      start = W != ~0ull && !(p > 0 && (H.w[p - 1] >> 6) == (W >> 6));  // a run: equal W but the pos bits
-    }
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < nruns; base += stride) {  // wave-uniform
+    const uint64_t i = base + threadIdx.x;
+    const bool act = i < nruns;
+    const uint64_t p = act ? H.run_list[i] : 0;
+    const uint64_t W = H.w[p];
     uint32_t nrows = 0;
-    if (start) {
+    if (act) {
       uint64_t e = p + 1;
       while (e < H.n_children && (H.w[e] >> 6) == (W >> 6)) ++e;
       nrows = (uint32_t)(e - p);
     }
-    uint32_t kmax = nrows;
-    for (int off = 32; off > 0; off >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off));
-    if (kmax == 0) continue;  // wave-uniform
     uint32_t hc = 0, h = 0, b = 0, G = 0;
     bool isn = false;
     uint64_t obase = 0;
-    if (start) {
+    if (act) {
       hc = H.c_h[H.v[p]];
       h = hc & 0x7FFFFFFFu;
       isn = (hc >> 31) == 0;
@@ -200,59 +215,99 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
       if (pass == 1) obase = (isn ? H.rank_n[p] - H.rank_n[H.h_first[h]] : H.rank_m[p] - H.rank_m[H.h_first[h]]);
     }
     uint32_t nout = 0;
+    // this run's contribution to its key's row: outputs, first output slot, counter sum (one
+    // atomic per key and wave below, not per output: a hot key owns up to millions of them)
+    uint32_t k_cnt = 0, k_cb = kNone;
+    unsigned long long k_sum = 0;
+    auto put = [&](uint64_t id1, uint64_t id2, uint64_t t, uint64_t meta, uint64_t v) {
+      const uint32_t o = (uint32_t)(obase + nout);
+      uint64_t* row = (isn ? A.nos + (uint64_t)(A.nbase[b] + o) * kChildStride
+                           : A.mos + (uint64_t)(A.mbase[b] + o) * kChildStride);
+      row[C_PKH] = H.hk_h[G];
+      row[C_PKF] = H.hk_f[G];
+      row[C_ID1] = id1;
+      row[C_ID2] = isn ? v : id2;
+      row[C_T] = t;
+      row[C_META] = isn ? meta_pack(0, meta_pos(meta), meta_src(meta)) : meta;
+      k_cb = min(k_cb, o);
+      ++k_cnt;
+      k_sum += isn ? v : 0;
+    };
     auto emit_id = [&](const HotChild& hd, uint64_t v, uint64_t tw, uint64_t wmeta) {
       if (!isn && (A.flags & F_GC_MEMBERS) && meta_tag(wmeta) == KIND_DEL && tw < A.gc_wm) {
         ++gcm;
         return;
       }
-      if (pass == 1) {
-        const uint32_t o = (uint32_t)(obase + nout);
-        uint64_t* row = (isn ? A.nos + (uint64_t)(A.nbase[b] + o) * kChildStride
-                             : A.mos + (uint64_t)(A.mbase[b] + o) * kChildStride);
-        row[C_PKH] = H.hk_h[G];
-        row[C_PKF] = H.hk_f[G];
-        row[C_ID1] = hd.id1;
-        row[C_ID2] = isn ? v : hd.id2;
-        row[C_T] = isn ? hd.t : tw;
-        row[C_META] = isn ? meta_pack(0, meta_pos(hd.meta), meta_src(hd.meta)) : wmeta;
-        atomicMin(&H.hk_cb[G], o);
-        atomicAdd(&H.hk_cnt[G], 1u);
-        if (isn && (H.hk_vm[G] & kVmaskMerged)) atomicAdd(&H.hk_sum[G], (unsigned long long)v);
-      }
+      if (pass == 1) put(hd.id1, hd.id2, isn ? hd.t : tw, isn ? hd.meta : wmeta, v);
       ++nout;
     };
-    // common case: one exact id whose rows arrive in strictly increasing (pos, src) order (the
-    // tag's low bits are the position): one linear pass
-    bool simple = start;
-    {
-      HotChild hd;
-      hd.id1 = hd.id2 = hd.t = hd.meta = 0;
-      hd.j = 0;
-      uint64_t v = 0, tw = 0, wmeta = 0, lastm = 0;
-      for (uint32_t k = 0; k < kmax; ++k) {
-        if (k < nrows && simple) {
-          const HotChild x = hot_child(A, H, p + k, isn);
-          if (k == 0) {
-            hd = x;
-            v = x.id2;
-            tw = x.t;
-            wmeta = x.meta;
-          } else if (x.id1 != hd.id1 || (!isn && x.id2 != hd.id2) || meta_order(x.meta) <= meta_order(lastm)) {
-            simple = false;
-          } else if (isn) {  // Counter::merge (type_counter.rs:60-84): the head's t is kept
-            v = x.t > hd.t ? x.id2 : (x.t == hd.t ? imax64(v, x.id2) : v);
-          } else if (!(tw > x.t)) {  // LWWHash::set (lwwhash.rs:87-107): later wins ties
-            tw = x.t;
-            wmeta = x.meta;
-          }
-          lastm = x.meta;
+    bool slow = act;
+    if (pass == 0) {
+      // fast path: up to kFoldFast rows, their loads issued together
+      const bool fast = act && nrows <= kFoldFast;
+      uint32_t rj[kFoldFast];
+#pragma unroll
+      for (uint32_t k = 0; k < kFoldFast; ++k) rj[k] = (fast && k < nrows) ? H.c_row[H.v[p + k]] : 0;
+      const uint64_t* src = isn ? A.nr : A.mr;
+      uint64_t xi1[kFoldFast], xi2[kFoldFast], xt[kFoldFast], xm[kFoldFast];
+#pragma unroll
+      for (uint32_t k = 0; k < kFoldFast; ++k) {
+        if (fast && k < nrows) {
+          const uint64_t* C = src + (uint64_t)rj[k] * kChildStride;
+          xi1[k] = C[C_ID1];
+          xi2[k] = C[C_ID2];
+          xt[k] = C[C_T];
+          xm[k] = C[C_META];
+        } else {
+          xi1[k] = xi2[k] = xt[k] = xm[k] = 0;
         }
       }
-      if (simple) emit_id(hd, v, tw, wmeta);
+      bool simple = fast;
+      uint64_t v = xi2[0], tw = xt[0];
+      uint32_t qw = 0;  // winner (members)
+#pragma unroll
+      for (uint32_t k = 1; k < kFoldFast; ++k) {
+        if (k < nrows) {
+          simple = simple && xi1[k] == xi1[0] && (isn || xi2[k] == xi2[0]) &&
+                   meta_order(xm[k]) > meta_order(xm[k - 1]);
+          if (isn) {  // Counter::merge (type_counter.rs:60-84): the head's t is kept
+            v = xt[k] > xt[0] ? xi2[k] : (xt[k] == xt[0] ? imax64(v, xi2[k]) : v);
+          } else if (!(tw > xt[k])) {  // LWWHash::set (lwwhash.rs:87-107): later wins ties
+            tw = xt[k];
+            qw = k;
+          }
+        }
+      }
+      if (simple) {
+        uint64_t wm = xm[0];
+#pragma unroll
+        for (uint32_t k = 1; k < kFoldFast; ++k) wm = (k == qw) ? xm[k] : wm;
+        HotChild hd;
+        hd.id1 = xi1[0];
+        hd.id2 = xi2[0];
+        hd.t = xt[0];
+        hd.meta = xm[0];
+        hd.j = 0;
+        emit_id(hd, v, tw, wm);
+        H.fold_q[p] = (uint32_t)(p + (isn ? 0 : qw));
+        H.fold_v[p] = v;
+        slow = false;
+      } else if (act) {
+        H.fold_q[p] = kNone;
+      }
+    } else if (act) {  // pass 1, fold kept by pass 0
+      const uint32_t q = H.fold_q[p];
+      if (q != kNone) {
+        slow = false;
+        if ((isn ? H.emit_n : H.emit_m)[p]) {
+          const HotChild x = hot_child(A, H, q, isn);
+          put(x.id1, x.id2, x.t, x.meta, H.fold_v[p]);
+        }
+      }
     }
-    // otherwise (ids sharing 34 hash bits): every exact id, by successor selection
-    const bool slow = start && !simple;
-    const uint32_t kslow = __ballot(slow) ? kmax : 0;  // wave-uniform
+    // selection path
+    uint32_t kslow = slow ? nrows : 0;
+    for (int off = 32; off > 0; off >>= 1) kslow = max(kslow, (uint32_t)__shfl_xor((int)kslow, off));
     HotChild last, head;  // last visited row; first row of the id being folded
     last.id1 = last.id2 = last.t = last.meta = 0;
     last.j = 0;
@@ -296,9 +351,32 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
         last = c;
       }
     }
-    if (pass == 0 && start) (isn ? H.emit_n : H.emit_m)[p] = nout;
+    if (pass == 0 && act) (isn ? H.emit_n : H.emit_m)[p] = nout;
+    if (pass == 1) {
+      // runs are in sorted order, so the wave's active lanes hold non-decreasing keys G:
+      // a segmented reduction per key, and the segment's last lane does the atomics
+      const uint32_t key = act ? G : kNone;  // inactive lanes only at the tail: segments are contiguous
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t gk = (uint32_t)__shfl_up((int)key, d);
+        const uint32_t c2 = (uint32_t)__shfl_up((int)k_cnt, d);
+        const uint32_t b2 = (uint32_t)__shfl_up((int)k_cb, d);
+        const unsigned long long s2 = __shfl_up(k_sum, d);
+        if (lane >= (uint32_t)d && gk == key) {
+          k_cnt += c2;
+          k_cb = min(k_cb, b2);
+          k_sum += s2;
+        }
+      }
+      const uint32_t next = (uint32_t)__shfl_down((int)key, 1);
+      if (key != kNone && k_cnt && (lane == 63 || next != key)) {
+        atomicMin(&H.hk_cb[G], k_cb);
+        atomicAdd(&H.hk_cnt[G], k_cnt);
+        if (isn && (H.hk_vm[G] & kVmaskMerged)) atomicAdd(&H.hk_sum[G], k_sum);
+      }
+    }
   }
-  if (pass == 1 && gcm) atomicAdd(&stat_shard(A.stats)[ST_MEMBERS_GCED], gcm);
+  if (pass == 0 && gcm) atomicAdd(&stat_shard(A.stats)[ST_MEMBERS_GCED], gcm);
 }
 
 // First sorted position of each hot bucket's children (sorted by W, whose top bits are G).
