@@ -32,7 +32,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
 # the merge pipeline's kernels (everything cdb_merge_device launches; not the generator)
 MERGE_KERNEL_PREFIXES = ("part_", "bucket_", "compact", "scan_", "stats_reduce", "gc_lastbad", "set_dir",
-                         "stamp_pos", "iota", "hot_", "sorted_", "seg_")
+                         "stamp_pos", "iota", "hot_", "sorted_", "seg_", "run_", "mat_", "radix_hist",
+                         "radix_scatter")
 
 
 def parse():
@@ -113,7 +114,11 @@ def cpu_baseline(cdb, args, snaps, sample):
     here) over already-decoded entries, best of --cpu-reps; decode excluded."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cdb_oracle
-    ns, entries = cdb_oracle.time_fold(snaps, reps=args.cpu_reps)
+    ns = None
+    for rep in range(args.cpu_reps):  # one rep per call: progress on stderr between reps
+        t, entries = cdb_oracle.time_fold(snaps, reps=1)
+        ns = t if ns is None else min(ns, t)
+        log(f"cpu baseline rep {rep}: {entries / (t * 1e-9) / 1e6:.2f} M entries/s")
     out = {"value": entries / (ns * 1e-9), "unit": "entries/s", "cores": 1, "kind": "port",
            "sample": f"{sample} ({entries} entries, decode excluded, best of {args.cpu_reps}), "
                      f"oracle/cdb_oracle.cpp std::unordered_map fold",
@@ -145,7 +150,11 @@ def setup(cdb, ctx, args):
 
         def sample():
             scfg = configs.c4(cdb, args.cpu_universe, args.replicas, args.seed)
-            return ([cdb.gen_snapshot(scfg, r) for r in range(args.replicas)],
+            snaps = []
+            for r in range(args.replicas):
+                snaps.append(cdb.gen_snapshot(scfg, r))
+                log(f"cpu baseline sample: replica {r} snapshot {len(snaps[-1])} bytes")
+            return (snaps,
                     f"C4 generator config, {args.cpu_universe} keys x {args.replicas} replicas")
     elif c == "c1":
         cfg = configs.c1(cdb)

@@ -982,15 +982,31 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     }
   }
   }  // partition path tiers
-  bucket_mid_kernel<<<std::min<uint64_t>(nb, 2048), kBktThreads, 0, s>>>(A, d_big_list, d_big_count);
-  CDB_TRY(launch_check(ctx, s, "bucket_mid_kernel"));
-  CDB_HIP(hipEventRecord(ctx->ev_bucket, s), "event");
-
-  // ---- 4. over-capacity buckets (same algorithm, global scratch)
+  // ---- 4. buckets beyond the wave tiers: the mid tier (one workgroup per bucket, LDS), or,
+  //         when there are many of them, the chip-wide child path of the over-capacity
+  //         buckets (hot.hip.h): buckets of a few keys with hundreds of children each (C3's
+  //         sets) sort their children serially inside one workgroup, but spread over the chip
+  //         they fold in parallel; then the over-capacity buckets
   uint32_t counts[2] = {0, 0};  // hot, big (mid tier)
   CDB_HIP(hipMemcpyAsync(counts, d_hot_count, sizeof counts, hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipStreamSynchronize(s), "sync");
-  const uint32_t hot = counts[0];
+  static const uint32_t mid_chip = [] {
+    const char* e = std::getenv("CDB_MID_CHIPWIDE");  // buckets from which the mid tier goes chip-wide
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 4096u;
+  }();
+  const bool mid_wide = A.force_tier == 0 && mid_chip && counts[1] >= mid_chip;
+  if (mid_wide) {
+    CDB_TRY(over_capacity(ctx, A, d_big_list, counts[1], s));
+  } else {
+    bucket_mid_kernel<<<std::min<uint64_t>(nb, 2048), kBktThreads, 0, s>>>(A, d_big_list, d_big_count);
+    CDB_TRY(launch_check(ctx, s, "bucket_mid_kernel"));
+  }
+  CDB_HIP(hipEventRecord(ctx->ev_bucket, s), "event");
+  if (!mid_wide) {  // the mid tier forwards buckets over its capacity
+    CDB_HIP(hipMemcpyAsync(counts, d_hot_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");
+    CDB_HIP(hipStreamSynchronize(s), "sync");
+  }
+  const uint32_t hot = mid_wide ? 0 : counts[0];
   if (hot) CDB_TRY(over_capacity(ctx, A, d_hot_list, hot, s));
 
   // ---- 5. dense compaction into the caller's output columns

@@ -8,7 +8,7 @@ cd $GRAFT_REPO_ROOT
 T=${TAG:-r2}
 C=${CONFIG:-c4}
 O=gpurun_out
-KRE="part_|bucket_|compact|scan_|stats_reduce|gc_lastbad|hot_|sorted_|seg_"
+KRE="part_|bucket_|compact|scan_|stats_reduce|gc_lastbad|hot_|sorted_|seg_|run_|mat_|radix_hist|radix_scatter"
 if [ -z "$NO_TESTS" ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_$T.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest_$T.log; exit 1; }
 tail -2 $O/pytest_$T.log

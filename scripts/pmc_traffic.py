@@ -36,7 +36,9 @@ def step_bytes(names):
                for k in names)
 
 
-merge = [k for k in out["kernels"] if not k.startswith("gen_")]
+# the merge step's kernels: not the generator's, not the input setup's torch sort (rocprim)
+merge = [k for k in out["kernels"] if not k.startswith("gen_") and "rocprim" not in k and "at::" not in k]
+out["merge_kernels"] = merge
 out["bucket_phase_bytes"] = step_bytes([k for k in merge if k.startswith("bucket_")])
 out["merge_step_bytes"] = step_bytes(merge)
 json.dump(out, open(sys.argv[3], "w"), indent=1)
