@@ -201,7 +201,7 @@ ABI_FUNCTIONS = (
     "cdb_merged_free", "cdb_free",
     "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_partition_owner", "cdb_gen_default",
     "cdb_gen_snapshot", "cdb_gen_device", "cdb_decode_ops", "cdb_ops_info_get", "cdb_ops_free", "cdb_apply_ops", "cdb_gen_ops",
-    "cdb_encode_snapshot", "cdb_crc64_gpu", "cdb_upload_batches")
+    "cdb_encode_snapshot", "cdb_crc64_gpu", "cdb_upload_batches", "cdb_decode_snapshots_device")
 
 _lib = None
 
@@ -256,6 +256,9 @@ def lib():
         "cdb_encode_snapshot": (c_st, [vp, vp, P(EncodeHeader), P(vp), P(ctypes.c_size_t), P(EncodeStats)]),
         "cdb_crc64_gpu": (c_st, [vp, ctypes.c_char_p, ctypes.c_size_t, P(ctypes.c_uint64)]),
         "cdb_upload_batches": (c_st, [vp, P(vp), ctypes.c_uint32, P(DevInput)]),
+        "cdb_decode_snapshots_device": (c_st, [vp, P(ctypes.c_char_p), P(ctypes.c_size_t), ctypes.c_uint32,
+                                               ctypes.c_uint32, P(vp), P(DevInput), P(ctypes.c_uint32),
+                                               P(ctypes.c_size_t), P(ctypes.c_double), P(ctypes.c_double)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -387,6 +390,34 @@ def decode_snapshot_gpu(ctx: "Context", data: bytes, reference_checksum: bool = 
             lib().cdb_batch_free(h)
         _raise(st, ctx.last_error(), offset=off.value)
     return Batch(h)
+
+
+def decode_snapshots_device(ctx: "Context", snaps, reference_checksum: bool = False,
+                            timing: Optional[dict] = None):
+    """GPU decode of several snapshots straight into HBM (cdb_decode_snapshots_device):
+    returns (batches, DevInput) -- the rows of snapshot i at fold position i in one set of
+    device columns (release each family with cdb_dev_rows_release), each batch holding the
+    host side (bytes, references, header). Errors are raised for the failing snapshot."""
+    n = len(snaps)
+    datas = [bytes(x) for x in snaps]
+    bufs = (ctypes.c_char_p * max(n, 1))(*datas)
+    lens = (ctypes.c_size_t * max(n, 1))(*[len(x) for x in datas])
+    hs = (ctypes.c_void_p * max(n, 1))()
+    din = DevInput()
+    failed = ctypes.c_uint32()
+    off = ctypes.c_size_t()
+    ims, dms = ctypes.c_double(), ctypes.c_double()
+    flags = DECODE_REFERENCE_CHECKSUM if reference_checksum else 0
+    st = lib().cdb_decode_snapshots_device(ctx.handle, bufs, lens, n, flags, hs, ctypes.byref(din),
+                                           ctypes.byref(failed), ctypes.byref(off), ctypes.byref(ims),
+                                           ctypes.byref(dms))
+    if timing is not None:
+        timing.update(index_ms=ims.value, device_ms=dms.value, failed=failed.value)
+    batches = [Batch(hs[i], checksum_ok=not (st == INVALID_SNAPSHOT_CHECKSUM and i == failed.value))
+               for i in range(n) if hs[i]]
+    if st not in (OK, INVALID_SNAPSHOT_CHECKSUM):
+        _raise(st, ctx.last_error(), offset=off.value)
+    return batches, din
 
 
 # ----------------------------------------------------------------- op stream (SURVEY §8f.2)

@@ -60,6 +60,11 @@ struct Batch {
   std::vector<ReplicaAdd> replica_add;
   std::vector<ReplicaDel> replica_del;
 
+  // cdb_decode_snapshots_device: the row columns above stay empty, the rows live in HBM
+  // (dev_rows = keys, nodes, members there); byte references, header and replicas are here.
+  bool rows_on_device = false;
+  uint64_t dev_rows[3] = {0, 0, 0};
+
   uint64_t n_keys() const { return kh.size(); }
   uint64_t n_nodes() const { return n_pkh.size(); }
   uint64_t n_members() const { return m_pkh.size(); }

@@ -224,6 +224,8 @@ std::string hex(const uint8_t* p, uint64_t n) {
 // after batch i-1's) through the pinned staging ring and stamps fold position i into batch i's
 // meta words on the device.
 static cdb_status upload_batches(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, cdb_dev_input* din) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (inputs[i]->b->rows_on_device) return fail(ctx, CDB_BAD_ARGUMENT, "a batch's rows are already in HBM");
   std::vector<HostSeg> segs;
   auto put = [&](const cdb_dev_rows& r, int c, uint64_t off, const ColVec& v) {
     if (!v.empty()) segs.push_back({const_cast<uint64_t*>(v.data()), r.col[c] + off, v.size() * 8});
@@ -289,6 +291,36 @@ cdb_status cdb_decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len,
   return (cdb_status)rc;
 }
 
+cdb_status cdb_decode_snapshots_device(cdb_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, uint32_t n,
+                                       uint32_t flags, cdb_batch** batches, cdb_dev_input* out, uint32_t* failed,
+                                       size_t* err_offset, double* index_ms, double* device_ms) {
+  if (!batches || !out || (n && (!bufs || !lens))) return CDB_BAD_ARGUMENT;
+  if (!ctx) return CDB_NO_DEVICE;
+  if (n > (uint32_t)kMaxPos) return fail(ctx, CDB_BAD_ARGUMENT, "at most 63 snapshots per merge");
+  for (uint32_t i = 0; i < n; ++i) {
+    batches[i] = nullptr;
+    if (!bufs[i] && lens[i]) return CDB_BAD_ARGUMENT;
+  }
+  std::vector<std::shared_ptr<Batch>> bs(n);
+  std::vector<Batch*> raw(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    bs[i] = std::make_shared<Batch>();
+    raw[i] = bs[i].get();
+  }
+  uint32_t fi = 0;
+  size_t eo = 0;
+  DecodeTiming tm;
+  hipSetDevice(ctx->device);
+  const int rc = decode_snapshots_gpu_device(ctx, bufs, lens, n, flags, raw.data(), out, &fi, &eo, &tm);
+  if (failed) *failed = fi;
+  if (err_offset) *err_offset = eo;
+  if (index_ms) *index_ms = tm.index_ms;
+  if (device_ms) *device_ms = tm.device_ms;
+  if (rc == CDB_OK || rc == CDB_INVALID_SNAPSHOT_CHECKSUM)
+    for (uint32_t i = 0; i < n; ++i) batches[i] = new cdb_batch{bs[i]};
+  return (cdb_status)rc;
+}
+
 cdb_status cdb_batch_info_get(const cdb_batch* cb, cdb_batch_info* info) {
   if (!cb || !info) return CDB_BAD_ARGUMENT;
   const Batch& b = *cb->b;
@@ -296,8 +328,8 @@ cdb_status cdb_batch_info_get(const cdb_batch* cb, cdb_batch_info* info) {
   info->n_data = b.n_data;
   info->n_expires = b.n_expires;
   info->n_deletes = b.n_deletes;
-  info->n_nodes = b.n_nodes();
-  info->n_members = b.n_members();
+  info->n_nodes = b.rows_on_device ? b.dev_rows[1] : b.n_nodes();
+  info->n_members = b.rows_on_device ? b.dev_rows[2] : b.n_members();
   info->node_id = b.node_id;
   info->uuid_he_sent = b.uuid_he_sent;
   info->n_replica_add = (uint32_t)b.replica_add.size();
@@ -309,6 +341,7 @@ cdb_status cdb_batch_info_get(const cdb_batch* cb, cdb_batch_info* info) {
 cdb_status cdb_batch_column(const cdb_batch* cb, int family, int col, const uint64_t** data, uint64_t* n) {
   if (!cb || !data || !n) return CDB_BAD_ARGUMENT;
   const Batch& b = *cb->b;
+  if (b.rows_on_device) return CDB_BAD_ARGUMENT;  // its rows are in HBM (cdb_decode_snapshots_device)
   const ColVec* k[] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
   const ColVec* nd[] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
   const ColVec* mb[] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
@@ -332,6 +365,9 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, const c
   hipSetDevice(ctx->device);
   // batches are folded in array order: pos = array index, stamped into meta below
   uint64_t K = 0, N = 0, M = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (!inputs[i] || inputs[i]->b->rows_on_device)
+      return fail(ctx, CDB_BAD_ARGUMENT, "cdb_merge: a batch's rows are in HBM; merge them with cdb_merge_device");
   for (uint32_t i = 0; i < n; ++i) {
     K += inputs[i]->b->n_keys();
     N += inputs[i]->b->n_nodes();
@@ -405,6 +441,9 @@ cdb_status cdb_upload_batches(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n
   if (n > (uint32_t)kMaxPos) return fail(ctx, CDB_BAD_ARGUMENT, "at most 63 batches per merge");
   hipSetDevice(ctx->device);
   uint64_t K = 0, N = 0, M = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (!inputs[i] || inputs[i]->b->rows_on_device)
+      return fail(ctx, CDB_BAD_ARGUMENT, "cdb_merge: a batch's rows are in HBM; merge them with cdb_merge_device");
   for (uint32_t i = 0; i < n; ++i) {
     K += inputs[i]->b->n_keys();
     N += inputs[i]->b->n_nodes();

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <memory>
 #include <vector>
 
 #include "batch.h"
@@ -80,6 +81,7 @@ struct DecArgs {
   uint64_t* nd[6];                  // pkh pkf node v t meta
   uint64_t* mb[6];                  // pkh pkf mh mf t meta
   uint64_t *mref_off, *mref_len, *mvref_off, *mvref_len;
+  uint32_t pos;                     // fold position stamped into meta (device-resident emit)
 };
 
 struct Head {  // the part of a DATAS entry before the payload
@@ -196,7 +198,7 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
     A.k[1][i] = h.f;
     A.k[2][i] = t;
     A.k[3][i] = A.k[4][i] = A.k[5][i] = 0;
-    A.k[6][i] = meta_pack(A.kind[i] == 1 ? TAG_EXPIRE : TAG_DELETE, 0, i);
+    A.k[6][i] = meta_pack(A.kind[i] == 1 ? TAG_EXPIRE : TAG_DELETE, A.pos, i);
     A.kref_off[i] = key.off;
     A.kref_len[i] = key.len;
     A.vref_off[i] = A.vref_len[i] = 0;
@@ -232,7 +234,7 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
       A.nd[2][row] = id;
       A.nd[3][row] = v;
       A.nd[4][row] = t;
-      A.nd[5][row] = meta_pack(0, 0, row);
+      A.nd[5][row] = meta_pack(0, A.pos, row);
       ++row;
     }
   } else if ((hd.tag == TAG_SET || hd.tag == TAG_DICT) && A.mcount[i] != kHostTier) {
@@ -262,7 +264,7 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
       A.mb[2][row] = mh.h;
       A.mb[3][row] = mh.f;
       A.mb[4][row] = t;
-      A.mb[5][row] = meta_pack(j < na ? KIND_ADD : KIND_DEL, 0, row);
+      A.mb[5][row] = meta_pack(j < na ? KIND_ADD : KIND_DEL, A.pos, row);
       A.mref_off[row] = m.off;
       A.mref_len[row] = m.len;
       A.mvref_off[row] = v.off;
@@ -276,7 +278,7 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
   A.k[3][i] = hd.ut;
   A.k[4][i] = hd.dt;
   A.k[5][i] = aux;
-  A.k[6][i] = meta_pack(hd.tag, 0, i);
+  A.k[6][i] = meta_pack(hd.tag, A.pos, i);
   A.kref_off[i] = hd.key.off;
   A.kref_len[i] = hd.key.len;
   A.vref_off[i] = val.off;
@@ -303,91 +305,126 @@ struct EvPair {
 
 }  // namespace
 
-int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off,
-                        DecodeTiming* tm) {
-  EntryIndex idx;
-  DeferredCrc dcrc;
-  const auto t0 = std::chrono::steady_clock::now();
-  int rc = index_snapshot(buf, len, flags, out, &idx, err_off, &dcrc);
-  if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) return rc;
-  const uint64_t n = idx.offset.size();
-  if (n == 0) return rc;
-  if (hipSetDevice(ctx->device) != hipSuccess) return CDB_DEVICE_ERROR;
-  hipStream_t s = ctx->stream;
-  // every runtime call is checked; the first failure is reported (hip_check keeps its message)
-  cdb_status st = CDB_OK;
-  auto ck = [&](hipError_t e, const char* what) {
-    if (e != hipSuccess && st == CDB_OK) st = hip_check(ctx, e, what);
+// One snapshot through the GPU decode, in two steps so that several snapshots can be sized
+// first and then emitted into one set of device columns (decode_snapshots_gpu_device):
+//   prepare : the host index pass, the bytes to the device, the count pass, the stream
+//             checksum, the host tier (entries past the per-thread dedup limits), child offsets;
+//   emit_*  : the emit pass into the batch's host columns, or into caller device columns.
+class GpuDecode {
+ public:
+  GpuDecode(cdb_ctx* ctx, Batch* out, uint32_t flags) : ctx_(ctx), out_(out), flags_(flags) {}
+  int prepare(const uint8_t* buf, size_t len, size_t* err_off, DecodeTiming* tm);
+  cdb_status emit_host(DecodeTiming* tm);
+  cdb_status emit_device(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t pos,
+                         DecodeTiming* tm);
+  uint64_t keys() const { return n_; }
+  uint64_t nodes() const { return nn_; }
+  uint64_t members() const { return nm_; }
+
+ private:
+  struct HostEntry {
+    uint64_t i;
+    Batch rows;
+    uint64_t total;
   };
-  // one device block: raw | off | kind | counts | offsets | key cols | refs | node cols | member cols
-  std::vector<uint64_t> noff(n), moff(n);
-  std::vector<uint32_t> ncnt(n), mcnt(n);
-  DevBuf d_raw, d_meta, d_crc;
-  // the raw stream sits after `pad` zero bytes, so the checksummed prefix ends on a CRC tile
-  const uint64_t tile = crc_tile_bytes();
-  const uint64_t pad = dcrc.pending ? (tile - dcrc.len % tile) % tile : 0;
-  // a failed allocation is reported with its own message and leaves no pending HIP error
-  auto alloc = [&](void** p, size_t bytes, const char* what) {
+  void ck(hipError_t e, const char* what) {
+    if (e != hipSuccess && st_ == CDB_OK) st_ = hip_check(ctx_, e, what);
+  }
+  cdb_status alloc(void** p, size_t bytes, const char* what) {  // reported, no pending HIP error
     if (hipMalloc(p, bytes) == hipSuccess) return CDB_OK;
     (void)hipGetLastError();
     *p = nullptr;
-    return fail(ctx, CDB_OUT_OF_MEMORY, what);
-  };
-  if ((st = alloc(&d_raw.p, pad + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK) return st;
-  if ((st = alloc(&d_crc.p, 8, "decode: device checksum word")) != CDB_OK) return st;
+    return fail(ctx_, CDB_OUT_OF_MEMORY, what);
+  }
+  cdb_status refs_to_batch(const ColVec& ko, const ColVec& kl, const ColVec& vo, const ColVec& vl, const ColVec& mo,
+                           const ColVec& ml, const ColVec& mvo, const ColVec& mvl);
+
+  cdb_ctx* ctx_;
+  Batch* out_;
+  uint32_t flags_;
+  cdb_status st_ = CDB_OK;
+  int rc_ = CDB_OK;
+  hipStream_t s_ = nullptr;
+  EntryIndex idx_;
+  DeferredCrc dcrc_;
+  uint64_t n_ = 0, nn_ = 0, nm_ = 0;
+  std::vector<uint64_t> noff_, moff_;
+  std::vector<HostEntry> hosted_;
+  DevBuf d_raw_, d_meta_, d_crc_, d_rows_;
+  DecArgs A_;
+  uint32_t grid_ = 0;
+  EvPair ev_;
+};
+
+int GpuDecode::prepare(const uint8_t* buf, size_t len, size_t* err_off, DecodeTiming* tm) {
+  const auto t0 = std::chrono::steady_clock::now();
+  rc_ = index_snapshot(buf, len, flags_, out_, &idx_, err_off, &dcrc_);
+  if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (rc_ != CDB_OK && rc_ != CDB_INVALID_SNAPSHOT_CHECKSUM) return rc_;
+  const uint64_t n = n_ = idx_.offset.size();
+  if (n == 0) return rc_;
+  if (hipSetDevice(ctx_->device) != hipSuccess) return CDB_DEVICE_ERROR;
+  hipStream_t s = s_ = ctx_->stream;
+  noff_.resize(n);
+  moff_.resize(n);
+  std::vector<uint32_t> ncnt(n), mcnt(n);
+  // the raw stream sits after `pad` zero bytes, so the checksummed prefix ends on a CRC tile
+  const uint64_t tile = crc_tile_bytes();
+  const uint64_t pad = dcrc_.pending ? (tile - dcrc_.len % tile) % tile : 0;
+  if ((st_ = alloc(&d_raw_.p, pad + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK) return st_;
+  if ((st_ = alloc(&d_crc_.p, 8, "decode: device checksum word")) != CDB_OK) return st_;
+  // one device block: off | noff | moff | ncount | mcount | kind
   const size_t head = n * (8 + 1 + 4 + 4 + 8 + 8) + 64;
-  if ((st = alloc(&d_meta.p, head, "decode: device entry index")) != CDB_OK) return st;
-  uint8_t* hm = (uint8_t*)d_meta.p;
+  if ((st_ = alloc(&d_meta_.p, head, "decode: device entry index")) != CDB_OK) return st_;
+  uint8_t* hm = (uint8_t*)d_meta_.p;
   uint64_t* d_off = (uint64_t*)hm;
   uint64_t* d_noff = d_off + n;
   uint64_t* d_moff = d_noff + n;
   uint32_t* d_ncnt = (uint32_t*)(d_moff + n);
   uint32_t* d_mcnt = d_ncnt + n;
   uint8_t* d_kind = (uint8_t*)(d_mcnt + n);
-  EvPair ev;
-  ck(hipEventRecord(ev.a, s), "event");
-  if (pad) ck(hipMemsetAsync(d_raw.p, 0, pad, s), "memset(decode)");
-  const uint8_t* raw_dev = (const uint8_t*)d_raw.p + pad;
-  if (st == CDB_OK) st = staged_h2d(ctx, (void*)raw_dev, out->raw.data(), len, s);
-  if (st == CDB_OK) st = staged_h2d(ctx, d_off, idx.offset.data(), n * 8, s);
-  ck(hipMemcpyAsync(d_kind, idx.kind.data(), n, hipMemcpyHostToDevice, s), "h2d(decode)");
-  if (st != CDB_OK) return st;
-  DecArgs A;
-  std::memset(&A, 0, sizeof A);
-  A.raw = raw_dev;
-  A.off = d_off;
-  A.kind = d_kind;
-  A.n = n;
-  A.ncount = d_ncnt;
-  A.mcount = d_mcnt;
-  const uint32_t grid = (uint32_t)((n + kDecThreads - 1) / kDecThreads);
-  count_kernel<<<grid, kDecThreads, 0, s>>>(A);
+  ck(hipEventRecord(ev_.a, s), "event");
+  if (pad) ck(hipMemsetAsync(d_raw_.p, 0, pad, s), "memset(decode)");
+  const uint8_t* raw_dev = (const uint8_t*)d_raw_.p + pad;
+  if (st_ == CDB_OK) st_ = staged_h2d(ctx_, (void*)raw_dev, out_->raw.data(), len, s);
+  if (st_ == CDB_OK) st_ = staged_h2d(ctx_, d_off, idx_.offset.data(), n * 8, s);
+  ck(hipMemcpyAsync(d_kind, idx_.kind.data(), n, hipMemcpyHostToDevice, s), "h2d(decode)");
+  if (st_ != CDB_OK) return st_;
+  std::memset(&A_, 0, sizeof A_);
+  A_.raw = raw_dev;
+  A_.off = d_off;
+  A_.kind = d_kind;
+  A_.n = n;
+  A_.ncount = d_ncnt;
+  A_.mcount = d_mcnt;
+  A_.noff = d_noff;
+  A_.moff = d_moff;
+  grid_ = (uint32_t)((n + kDecThreads - 1) / kDecThreads);
+  count_kernel<<<grid_, kDecThreads, 0, s>>>(A_);
   ck(hipGetLastError(), "count_kernel");
   ck(hipMemcpyAsync(ncnt.data(), d_ncnt, n * 4, hipMemcpyDeviceToHost, s), "d2h(decode)");
   ck(hipMemcpyAsync(mcnt.data(), d_mcnt, n * 4, hipMemcpyDeviceToHost, s), "d2h(decode)");
   ck(hipStreamSynchronize(s), "sync(decode)");
-  if (st != CDB_OK) return st;
-  if (dcrc.pending) {  // the index pass left the stream checksum to the GPU
+  if (st_ != CDB_OK) return st_;
+  if (dcrc_.pending) {  // the index pass left the stream checksum to the GPU
     uint64_t crc = 0;
-    if ((st = crc64_device(ctx, (const uint8_t*)d_raw.p, pad + dcrc.len, (uint64_t*)d_crc.p, s)) != CDB_OK) return st;
-    ck(hipMemcpy(&crc, d_crc.p, 8, hipMemcpyDeviceToHost), "d2h(crc)");
-    if (st != CDB_OK) return st;
-    if (crc != dcrc.got) {
-      rc = CDB_INVALID_SNAPSHOT_CHECKSUM;
-      *err_off = dcrc.err_off;
+    if ((st_ = crc64_device(ctx_, (const uint8_t*)d_raw_.p, pad + dcrc_.len, (uint64_t*)d_crc_.p, s)) != CDB_OK)
+      return st_;
+    ck(hipMemcpy(&crc, d_crc_.p, 8, hipMemcpyDeviceToHost), "d2h(crc)");
+    if (st_ != CDB_OK) return st_;
+    if (crc != dcrc_.got) {
+      rc_ = CDB_INVALID_SNAPSHOT_CHECKSUM;
+      *err_off = dcrc_.err_off;
     }
   }
   // entries past the per-thread dedup limits: decoded here, into slots reserved by the scan
-  struct HostEntry { uint64_t i; Batch rows; uint64_t total; };
-  std::vector<HostEntry> hosted;
   for (uint64_t i = 0; i < n; ++i) {
     if (ncnt[i] != kHostTier && mcnt[i] != kHostTier) continue;
     HostEntry he;
     he.i = i;
-    uint64_t o = idx.offset[i];
+    uint64_t o = idx_.offset[i];
     // the key's hash, as decode.cpp computes it
-    const uint8_t* p = out->raw.data();
+    const uint8_t* p = out_->raw.data();
     auto rint = [&](uint64_t& q) {
       const uint32_t f = p[q++];
       uint64_t v = f & 0x3F;
@@ -399,24 +436,57 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
     uint64_t q = o;
     const uint64_t klen = rint(q);
     const Hash128 h = hash_bytes(p + q, klen, kDomainKey);
-    if (!decode_entry_children(*out, o, h.h, h.f, &he.rows, &he.total))
-      return fail(ctx, CDB_DEVICE_ERROR, "decode: host tier could not re-parse an indexed entry");
+    if (!decode_entry_children(*out_, o, h.h, h.f, &he.rows, &he.total))
+      return st_ = fail(ctx_, CDB_DEVICE_ERROR, "decode: host tier could not re-parse an indexed entry");
     if (ncnt[i] == kHostTier) ncnt[i] = (uint32_t)he.rows.n_pkh.size();
     if (mcnt[i] == kHostTier) mcnt[i] = (uint32_t)he.rows.m_pkh.size();
-    hosted.push_back(std::move(he));
+    hosted_.push_back(std::move(he));
   }
-  uint64_t nn = 0, nm = 0;
   for (uint64_t i = 0; i < n; ++i) {
-    noff[i] = nn;
-    moff[i] = nm;
-    nn += ncnt[i];
-    nm += mcnt[i];
+    noff_[i] = nn_;
+    moff_[i] = nm_;
+    nn_ += ncnt[i];
+    nm_ += mcnt[i];
   }
   // (the emit pass still sees the host tier's markers in the device copies of the counts)
-  DevBuf d_rows;
+  if (st_ == CDB_OK) st_ = staged_h2d(ctx_, d_noff, noff_.data(), n * 8, s);
+  if (st_ == CDB_OK) st_ = staged_h2d(ctx_, d_moff, moff_.data(), n * 8, s);
+  return st_ != CDB_OK ? (int)st_ : rc_;
+}
+
+cdb_status GpuDecode::refs_to_batch(const ColVec& ko, const ColVec& kl, const ColVec& vo, const ColVec& vl,
+                                    const ColVec& mo, const ColVec& ml, const ColVec& mvo, const ColVec& mvl) {
+  Batch& b = *out_;
+  b.key_ref.resize(n_);
+  b.val_ref.resize(n_);
+  for (uint64_t i = 0; i < n_; ++i) {
+    b.key_ref[i] = ByteRef{ko[i], kl[i]};
+    b.val_ref[i] = ByteRef{vo[i], vl[i]};
+  }
+  b.m_ref.resize(nm_);
+  b.m_vref.resize(nm_);
+  for (uint64_t i = 0; i < nm_; ++i) {
+    b.m_ref[i] = ByteRef{mo[i], ml[i]};
+    b.m_vref[i] = ByteRef{mvo[i], mvl[i]};
+  }
+  for (const HostEntry& he : hosted_) {
+    const Batch& r = he.rows;
+    for (size_t j = 0; j < r.m_pkh.size(); ++j) {
+      b.m_ref[moff_[he.i] + j] = r.m_ref[j];
+      b.m_vref[moff_[he.i] + j] = r.m_vref[j];
+    }
+  }
+  return CDB_OK;
+}
+
+cdb_status GpuDecode::emit_host(DecodeTiming* tm) {
+  if (n_ == 0) return CDB_OK;
+  const uint64_t n = n_, nn = nn_, nm = nm_;
+  hipStream_t s = s_;
   const size_t rows_words = n * 11 + nn * 6 + nm * 10 + 8;
-  if ((st = alloc(&d_rows.p, rows_words * 8, "decode: device row columns")) != CDB_OK) return st;
-  uint64_t* w = (uint64_t*)d_rows.p;
+  if ((st_ = alloc(&d_rows_.p, rows_words * 8, "decode: device row columns")) != CDB_OK) return st_;
+  uint64_t* w = (uint64_t*)d_rows_.p;
+  DecArgs& A = A_;
   for (int c = 0; c < 7; ++c, w += n) A.k[c] = w;
   A.kref_off = w; w += n;
   A.kref_len = w; w += n;
@@ -428,16 +498,12 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   A.mref_len = w; w += nm;
   A.mvref_off = w; w += nm;
   A.mvref_len = w; w += nm;
-  A.noff = d_noff;
-  A.moff = d_moff;
-  if (st == CDB_OK) st = staged_h2d(ctx, d_noff, noff.data(), n * 8, s);
-  if (st == CDB_OK) st = staged_h2d(ctx, d_moff, moff.data(), n * 8, s);
-  if (st != CDB_OK) return st;
-  emit_kernel<<<grid, kDecThreads, 0, s>>>(A);
+  A.pos = 0;
+  emit_kernel<<<grid_, kDecThreads, 0, s>>>(A);
   ck(hipGetLastError(), "emit_kernel");
-  if (st != CDB_OK) return st;
+  if (st_ != CDB_OK) return st_;
   // rows back into the host batch: one staged download of every column
-  Batch& b = *out;
+  Batch& b = *out_;
   std::vector<HostSeg> segs;
   auto down = [&](ColVec* v, const uint64_t* dev, uint64_t rows) {
     v->resize(rows);  // default-initialised: the download overwrites every word
@@ -462,32 +528,21 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   down(&ml, A.mref_len, nm);
   down(&mvo, A.mvref_off, nm);
   down(&mvl, A.mvref_len, nm);
-  if ((st = staged_copy(ctx, segs.data(), segs.size(), false, s)) != CDB_OK) return st;
-  ck(hipEventRecord(ev.b, s), "event");
+  if ((st_ = staged_copy(ctx_, segs.data(), segs.size(), false, s)) != CDB_OK) return st_;
+  ck(hipEventRecord(ev_.b, s), "event");
   ck(hipStreamSynchronize(s), "sync(decode)");
-  if (st != CDB_OK) return st;
+  if (st_ != CDB_OK) return st_;
   if (tm) {
     float ms = 0;
-    hipEventElapsedTime(&ms, ev.a, ev.b);
+    hipEventElapsedTime(&ms, ev_.a, ev_.b);
     tm->device_ms = ms;
   }
-  b.key_ref.resize(n);
-  b.val_ref.resize(n);
-  for (uint64_t i = 0; i < n; ++i) {
-    b.key_ref[i] = ByteRef{ko[i], kl[i]};
-    b.val_ref[i] = ByteRef{vo[i], vl[i]};
-  }
-  b.m_ref.resize(nm);
-  b.m_vref.resize(nm);
-  for (uint64_t i = 0; i < nm; ++i) {
-    b.m_ref[i] = ByteRef{mo[i], ml[i]};
-    b.m_vref[i] = ByteRef{mvo[i], mvl[i]};
-  }
+  refs_to_batch(ko, kl, vo, vl, mo, ml, mvo, mvl);
   // the host tier's children, src fields made absolute
-  for (const HostEntry& he : hosted) {
+  for (const HostEntry& he : hosted_) {
     const Batch& r = he.rows;
     for (size_t j = 0; j < r.n_pkh.size(); ++j) {
-      const uint64_t row = noff[he.i] + j;
+      const uint64_t row = noff_[he.i] + j;
       b.n_pkh[row] = r.n_pkh[j];
       b.n_pkf[row] = r.n_pkf[j];
       b.n_node[row] = r.n_node[j];
@@ -496,18 +551,178 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
       b.n_meta[row] = meta_pack(0, 0, row);
     }
     for (size_t j = 0; j < r.m_pkh.size(); ++j) {
-      const uint64_t row = moff[he.i] + j;
+      const uint64_t row = moff_[he.i] + j;
       b.m_pkh[row] = r.m_pkh[j];
       b.m_pkf[row] = r.m_pkf[j];
       b.m_h[row] = r.m_h[j];
       b.m_f[row] = r.m_f[j];
       b.m_t[row] = r.m_t[j];
       b.m_meta[row] = meta_pack(meta_tag(r.m_meta[j]), 0, row);
-      b.m_ref[row] = r.m_ref[j];
-      b.m_vref[row] = r.m_vref[j];
     }
   }
-  return rc;
+  return CDB_OK;
+}
+
+cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t pos,
+                                  DecodeTiming* tm) {
+  out_->rows_on_device = true;
+  out_->dev_rows[0] = n_;
+  out_->dev_rows[1] = nn_;
+  out_->dev_rows[2] = nm_;
+  if (n_ == 0) return CDB_OK;
+  const uint64_t n = n_, nn = nn_, nm = nm_;
+  hipStream_t s = s_;
+  // the byte references only: the rows go to the caller's columns
+  const size_t ref_words = n * 4 + nm * 4 + 8;
+  if ((st_ = alloc(&d_rows_.p, ref_words * 8, "decode: device byte references")) != CDB_OK) return st_;
+  uint64_t* w = (uint64_t*)d_rows_.p;
+  DecArgs& A = A_;
+  for (int c = 0; c < 7; ++c) A.k[c] = k[c];
+  for (int c = 0; c < 6; ++c) {
+    A.nd[c] = nd[c];
+    A.mb[c] = mb[c];
+  }
+  A.kref_off = w; w += n;
+  A.kref_len = w; w += n;
+  A.vref_off = w; w += n;
+  A.vref_len = w; w += n;
+  A.mref_off = w; w += nm;
+  A.mref_len = w; w += nm;
+  A.mvref_off = w; w += nm;
+  A.mvref_len = w; w += nm;
+  A.pos = pos;
+  emit_kernel<<<grid_, kDecThreads, 0, s>>>(A);
+  ck(hipGetLastError(), "emit_kernel");
+  if (st_ != CDB_OK) return st_;
+  // the host tier's children go up into their reserved rows
+  std::vector<ColVec> up;
+  up.reserve(hosted_.size() * 12);
+  std::vector<HostSeg> segs;
+  for (const HostEntry& he : hosted_) {
+    const Batch& r = he.rows;
+    const uint64_t nr = r.n_pkh.size(), mr = r.m_pkh.size();
+    if (nr) {
+      const ColVec* src[6] = {&r.n_pkh, &r.n_pkf, &r.n_node, &r.n_v, &r.n_t, nullptr};
+      for (int c = 0; c < 6; ++c) {
+        up.emplace_back(nr);
+        ColVec& v = up.back();
+        for (uint64_t j = 0; j < nr; ++j) v[j] = c < 5 ? (*src[c])[j] : meta_pack(0, pos, noff_[he.i] + j);
+        segs.push_back({v.data(), nd[c] + noff_[he.i], nr * 8});
+      }
+    }
+    if (mr) {
+      const ColVec* src[6] = {&r.m_pkh, &r.m_pkf, &r.m_h, &r.m_f, &r.m_t, nullptr};
+      for (int c = 0; c < 6; ++c) {
+        up.emplace_back(mr);
+        ColVec& v = up.back();
+        for (uint64_t j = 0; j < mr; ++j)
+          v[j] = c < 5 ? (*src[c])[j] : meta_pack(meta_tag(r.m_meta[j]), pos, moff_[he.i] + j);
+        segs.push_back({v.data(), mb[c] + moff_[he.i], mr * 8});
+      }
+    }
+  }
+  if (!segs.empty() && (st_ = staged_copy(ctx_, segs.data(), segs.size(), true, s)) != CDB_OK) return st_;
+  // the byte references down into the batch
+  ColVec ko, kl, vo, vl, mo, ml, mvo, mvl;
+  std::vector<HostSeg> dsegs;
+  auto down = [&](ColVec* v, const uint64_t* dev, uint64_t rows) {
+    v->resize(rows);
+    if (rows) dsegs.push_back({v->data(), const_cast<uint64_t*>(dev), rows * 8});
+  };
+  down(&ko, A.kref_off, n);
+  down(&kl, A.kref_len, n);
+  down(&vo, A.vref_off, n);
+  down(&vl, A.vref_len, n);
+  down(&mo, A.mref_off, nm);
+  down(&ml, A.mref_len, nm);
+  down(&mvo, A.mvref_off, nm);
+  down(&mvl, A.mvref_len, nm);
+  if ((st_ = staged_copy(ctx_, dsegs.data(), dsegs.size(), false, s)) != CDB_OK) return st_;
+  ck(hipEventRecord(ev_.b, s), "event");
+  ck(hipStreamSynchronize(s), "sync(decode)");
+  if (st_ != CDB_OK) return st_;
+  if (tm) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, ev_.a, ev_.b);
+    tm->device_ms = ms;
+  }
+  (void)nn;
+  return refs_to_batch(ko, kl, vo, vl, mo, ml, mvo, mvl);
+}
+
+int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off,
+                        DecodeTiming* tm) {
+  GpuDecode d(ctx, out, flags);
+  const int rc = d.prepare(buf, len, err_off, tm);
+  if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) return rc;
+  const cdb_status st = d.emit_host(tm);
+  return st != CDB_OK ? (int)st : rc;
+}
+
+int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, uint32_t n,
+                                uint32_t flags, Batch* const* outs, cdb_dev_input* din, uint32_t* failed,
+                                size_t* err_off, DecodeTiming* tm) {
+  const auto t_start = std::chrono::steady_clock::now();
+  std::vector<std::unique_ptr<GpuDecode>> dec;
+  int rc_all = CDB_OK;
+  uint64_t tot[3] = {0, 0, 0};
+  for (uint32_t i = 0; i < n; ++i) {
+    dec.emplace_back(new GpuDecode(ctx, outs[i], flags));
+    size_t eo = 0;
+    DecodeTiming t1;
+    const int rc = dec.back()->prepare(bufs[i], lens[i], &eo, &t1);
+    if (tm) tm->index_ms += t1.index_ms;
+    if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) {
+      *failed = i;
+      *err_off = eo;
+      return rc;
+    }
+    if (rc != CDB_OK && rc_all == CDB_OK) {  // a checksum mismatch: the rows are still merged
+      rc_all = rc;
+      *failed = i;
+      *err_off = eo;
+    }
+    tot[0] += dec.back()->keys();
+    tot[1] += dec.back()->nodes();
+    tot[2] += dec.back()->members();
+  }
+  if (tot[0] >= (1ull << 32) || tot[1] >= (1ull << 32) || tot[2] >= (1ull << 32))
+    return fail(ctx, CDB_BAD_ARGUMENT, "decoded rows exceed 2^32 per family");
+  std::memset(din, 0, sizeof *din);
+  cdb_status st;
+  if ((st = cdb_dev_rows_alloc(ctx, &din->keys, tot[0], kKeyCols)) != CDB_OK ||
+      (st = cdb_dev_rows_alloc(ctx, &din->nodes, tot[1], kNodeCols)) != CDB_OK ||
+      (st = cdb_dev_rows_alloc(ctx, &din->members, tot[2], kMemberCols)) != CDB_OK) {
+    cdb_dev_rows_release(ctx, &din->keys);
+    cdb_dev_rows_release(ctx, &din->nodes);
+    cdb_dev_rows_release(ctx, &din->members);
+    return st;
+  }
+  uint64_t o[3] = {0, 0, 0};
+  for (uint32_t i = 0; i < n; ++i) {
+    uint64_t* k[kKeyCols];
+    uint64_t* nd[kNodeCols];
+    uint64_t* mb[kMemberCols];
+    for (int c = 0; c < kKeyCols; ++c) k[c] = din->keys.col[c] + o[0];
+    for (int c = 0; c < kNodeCols; ++c) nd[c] = din->nodes.col[c] + o[1];
+    for (int c = 0; c < kMemberCols; ++c) mb[c] = din->members.col[c] + o[2];
+    DecodeTiming t1;
+    if ((st = dec[i]->emit_device(k, nd, mb, i, &t1)) != CDB_OK) {
+      cdb_dev_rows_release(ctx, &din->keys);
+      cdb_dev_rows_release(ctx, &din->nodes);
+      cdb_dev_rows_release(ctx, &din->members);
+      *failed = i;
+      return st;
+    }
+    o[0] += dec[i]->keys();
+    o[1] += dec[i]->nodes();
+    o[2] += dec[i]->members();
+  }
+  din->n_pos = n;
+  if (tm)  // everything but the host index passes (the snapshots' device work overlaps)
+    tm->device_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count() - tm->index_ms;
+  return rc_all;
 }
 
 }  // namespace cdb

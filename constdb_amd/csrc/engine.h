@@ -54,6 +54,9 @@ struct Batch;
 struct DecodeTiming;
 int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off,
                         DecodeTiming* tm);
+int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, uint32_t n,
+                                uint32_t flags, Batch* const* outs, cdb_dev_input* din, uint32_t* failed,
+                                size_t* err_off, DecodeTiming* tm);
 cdb_status fail(cdb_ctx* ctx, cdb_status st, const std::string& msg);
 cdb_status hip_check(cdb_ctx* ctx, hipError_t e, const char* what);
 cdb_status launch_check(cdb_ctx* ctx, hipStream_t s, const char* what);

@@ -103,6 +103,8 @@ struct CompactArgs {
   uint64_t* md[kMemberCols];
   const uint32_t *kbase, *nbase, *mbase, *kout, *nout, *mout, *kdoff, *ndoff, *mdoff;
   const unsigned long long* base_tot;  // dense rows already placed by the wave tier, per family
+  uint64_t cap[3];                     // rows of each family's sparse slots and dense output
+  uint32_t* err;                       // set when an index falls outside them
 };
 
 // Sparse-by-bucket outputs -> dense arrays; child ranges become absolute row indices.
@@ -132,6 +134,10 @@ __device__ __forceinline__ void compact_row(const CompactArgs& A, const CompactL
   const int j = group_bucket(L.doff, t);
   const uint32_t src = L.sbase[j] + (t - L.doff[j]);
   const uint64_t dst = A.base_tot[FAM] + d0 + t;
+  if (src >= A.cap[FAM] || dst >= A.cap[FAM]) {  // a broken directory: report, never touch memory
+    atomicOr(A.err, 1u);
+    return;
+  }
   if constexpr (FAM == 0) {
     uint64_t v[kKeyOutCols];
     const ulonglong2* row = (const ulonglong2*)(A.ks + (uint64_t)src * kKeyOutCols);
@@ -742,7 +748,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   Dir dk{dir, dir + dn, dir + 2 * dn, dir + 3 * dn, dir + 4 * dn};
   Dir dnd{dir + 5 * dn, dir + 6 * dn, dir + 7 * dn, dir + 8 * dn, dir + 9 * dn};
   Dir dm{dir + 10 * dn, dir + 11 * dn, dir + 12 * dn, dir + 13 * dn, dir + 14 * dn};
-  // misc: stats[8] u64 | last_bad u64 | totals[3] u64 | hot_count u32 | big_count u32 |
+  // misc: stats[8] u64 | last_bad u64 | totals[3] u64 | hot_count u32 | big_count u32 | compaction error u32 |
   //       hot_list[nb] u32 | big_list[nb] u32
   uint8_t* misc = (uint8_t*)ws_get(ctx, WS_MISC, 128 + 2 * nb * sizeof(uint32_t), &st);
   if (!misc) return st;
@@ -1026,6 +1032,11 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   C.kout = dk.out; C.nout = dnd.out; C.mout = dm.out;
   C.kdoff = dk.doff; C.ndoff = dnd.doff; C.mdoff = dm.doff;
   C.base_tot = d_lb_tot;
+  C.cap[0] = K;
+  C.cap[1] = N;
+  C.cap[2] = M;
+  uint32_t* d_cerr = (uint32_t*)(misc + 104);  // zeroed with the misc header
+  C.err = d_cerr;
   {  // chunks per family from the input row counts (outputs never exceed inputs)
     const uint64_t ck = (K + kCompactChunk - 1) / kCompactChunk, cn = (N + kCompactChunk - 1) / kCompactChunk,
                    cm = (M + kCompactChunk - 1) / kCompactChunk;
@@ -1043,7 +1054,10 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   CDB_HIP(hipMemcpyAsync(totals, d_totals, sizeof totals, hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipMemcpyAsync(hs, d_stats, sizeof hs, hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipMemcpyAsync(wave_tot, d_lb_tot, sizeof wave_tot, hipMemcpyDeviceToHost, s), "d2h");
+  uint32_t cerr = 0;
+  CDB_HIP(hipMemcpyAsync(&cerr, d_cerr, sizeof cerr, hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipStreamSynchronize(s), "sync");
+  if (cerr) return fail(ctx, CDB_DEVICE_ERROR, "compaction: a source or destination row fell outside the family's rows");
   if ((uint32_t)wave_tot[3])
     return fail(ctx, CDB_DEVICE_ERROR, "output look-back did not converge (bucket dispatch order violated)");
   for (int f = 0; f < 3; ++f) totals[f] += wave_tot[f];

@@ -84,6 +84,22 @@ cdb_status cdb_decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len,
                                    cdb_batch** out, size_t* err_offset, double* index_ms,
                                    double* device_ms);
 
+/* GPU decode of n snapshots straight into HBM, for cdb_merge_device (replica/pull.rs:64-79
+ * followed by :120-128 with no host round trip of the rows). Every snapshot is validated and
+ * indexed exactly as by cdb_decode_snapshot_gpu; then all are sized, ONE set of device columns
+ * is allocated (*out; release each family with cdb_dev_rows_release) and snapshot i's rows are
+ * emitted into it at fold position i -- row for row what cdb_upload_batches leaves from the
+ * host-decoded batches. batches[i] receives snapshot i's host side (bytes, byte references,
+ * header, replica entries, cdb_batch_info) to resolve merge outputs by src; its row columns
+ * stay in HBM, so cdb_merge, cdb_upload_batches and cdb_batch_column reject it. Errors: *failed
+ * is the snapshot, *err_offset the byte offset in it, and nothing is allocated; a checksum
+ * mismatch (CDB_INVALID_SNAPSHOT_CHECKSUM) still returns every batch and the rows, as the
+ * reference merges a snapshot's entries before it reaches the checksum. */
+struct cdb_dev_input; /* below, with cdb_merge_device */
+cdb_status cdb_decode_snapshots_device(cdb_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, uint32_t n,
+                                       uint32_t flags, cdb_batch** batches, struct cdb_dev_input* out,
+                                       uint32_t* failed, size_t* err_offset, double* index_ms, double* device_ms);
+
 typedef struct cdb_batch_info {
   uint64_t n_data;        /* SnapshotEntry::Data entries   (snapshot.rs:309) */
   uint64_t n_expires;     /* SnapshotEntry::Expires        (snapshot.rs:310) */

@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--universe", type=int, default=8_000_000)
     ap.add_argument("--replicas", type=int, default=8)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--device-snapshots", type=int, default=4,
+                    help="replica snapshots decoded straight into HBM (0: skip)")
     a = ap.parse_args()
     cfg = cdb.gen_config(seed=4, universe=a.universe, n_replicas=a.replicas, replica_hi=a.replicas)
     snap = cdb.gen_snapshot(cfg, 0)
@@ -44,6 +46,44 @@ def main():
            "host_ms": host * 1e3, "gpu_call_ms": gpu[0] * 1e3, "gpu_index_ms": gpu[1]["index_ms"],
            "gpu_device_ms": gpu[1]["device_ms"], "host_mb_s": len(snap) / host / 1e6,
            "gpu_mb_s": len(snap) / gpu[0] / 1e6}
+    # decode -> merge handoff: R snapshots straight into HBM (cdb_decode_snapshots_device)
+    # against host decode + cdb_upload_batches of the same snapshots
+    import ctypes
+    from constdb_amd.runs import FAMILY_COLS  # noqa: F401
+    R = a.device_snapshots
+    if R:
+        snaps = [snap] + [cdb.gen_snapshot(cfg, r) for r in range(1, R)]
+        L = cdb.lib()
+
+        def release(din):
+            for fam in (din.keys, din.nodes, din.members):
+                L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
+        bs, din = cdb.decode_snapshots_device(ctx, snaps)  # warm-up
+        release(din)
+        del bs
+        dev = up = None
+        for _ in range(a.reps):
+            tm = {}
+            t = time.perf_counter()
+            bs, din = cdb.decode_snapshots_device(ctx, snaps, timing=tm)
+            dt = time.perf_counter() - t
+            if dev is None or dt < dev[0]:
+                dev = (dt, tm)
+            release(din)
+            del bs
+            t = time.perf_counter()
+            hb = [cdb.decode_snapshot(x) for x in snaps]
+            din = cdb.DevInput()
+            arr = (ctypes.c_void_p * R)(*[b.handle for b in hb])
+            ctx.check(L.cdb_upload_batches(ctx.handle, arr, R, ctypes.byref(din)))
+            dt = time.perf_counter() - t
+            up = dt if up is None else min(up, dt)
+            release(din)
+            del hb
+        out["device_resident"] = {"snapshots": R, "bytes": sum(len(x) for x in snaps),
+                                  "decode_to_hbm_ms": dev[0] * 1e3, "index_ms": dev[1]["index_ms"],
+                                  "device_ms": dev[1]["device_ms"],
+                                  "host_decode_plus_upload_ms": up * 1e3}
     print(json.dumps(out))
 
 

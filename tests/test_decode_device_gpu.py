@@ -1,0 +1,154 @@
+"""GPU decode straight into HBM (cdb_decode_snapshots_device, SURVEY §8f.1 / pull.rs:64-79 ->
+:120-128 without a host round trip): the device rows must equal, column for column, what
+cdb_upload_batches leaves from the host decoder's batches (the host decoder is pinned to the
+oracle's loader by tests/test_abi_decode.py, and that upload + merge to the oracle's fold by
+tests/test_gpu_parity.py); the batches carry the same host side; errors name the snapshot
+and the offset the host decoder reports; a bad checksum still returns every row."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch  # noqa: F401  -- before libcdbmerge loads (one HIP runtime per process)
+
+import constdb_amd as cdb
+import constdb_oracle as o
+from constdb_amd import configs
+from snapgen import gen_replicas
+
+pytestmark = pytest.mark.gpu
+
+NCOLS = (7, 6, 6)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from constdb_amd import build
+    build.build()
+    return cdb.Context(0)
+
+
+def _cols(din):
+    from constdb_amd.runs import wrap
+    out = []
+    for f, rows in enumerate((din.keys, din.nodes, din.members)):
+        out.append([wrap(rows.col[c], rows.n).cpu().numpy().view(np.uint64) if rows.n else np.zeros(0, np.uint64)
+                    for c in range(NCOLS[f])])
+    return out
+
+
+def _release(din):
+    L = cdb.lib()
+    for fam in (din.keys, din.nodes, din.members):
+        L.cdb_dev_rows_release(None, ctypes.byref(fam))
+
+
+def _check(ctx, snaps):
+    batches, din = cdb.decode_snapshots_device(ctx, snaps)
+    try:
+        host = [cdb.decode_snapshot(s) for s in snaps]
+        up = cdb.DevInput()
+        arr = (ctypes.c_void_p * len(host))(*[b.handle for b in host])
+        ctx.check(cdb.lib().cdb_upload_batches(ctx.handle, arr, len(host), ctypes.byref(up)))
+        try:
+            assert din.n_pos == len(snaps)
+            for f, (x, y) in enumerate(zip(_cols(din), _cols(up))):
+                for c in range(NCOLS[f]):
+                    assert x[c].shape == y[c].shape and (x[c] == y[c]).all(), (f, c)
+        finally:
+            _release(up)
+        for g, h in zip(batches, host):
+            ig, ih = g.info(), h.info()
+            for fld in ("n_data", "n_expires", "n_deletes", "n_nodes", "n_members", "node_id", "uuid_he_sent",
+                        "n_replica_add", "n_replica_del", "version"):
+                assert getattr(ig, fld) == getattr(ih, fld), fld
+        return batches, din
+    except BaseException:
+        _release(din)
+        raise
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_device_decode_random(ctx, seed):
+    snaps = gen_replicas(seed, n_replicas=1 + seed % 4, n_keys=40 + 7 * seed, p_conflict=0.1, p_side=0.3)
+    _, din = _check(ctx, snaps)
+    _release(din)
+
+
+def test_device_decode_generator_and_merge(ctx):
+    """A C4-shaped replica set (60K keys x 4): equal rows, and a merge of the device rows equals
+    the merge of the uploaded host batches row for row."""
+    cfg = cdb.gen_config(seed=3, universe=60_000, n_replicas=4, replica_hi=4, mix_set=20, mix_dict=20,
+                         mean_members=6, del_permille=300)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(4)]
+    _, din = _check(ctx, snaps)
+    try:
+        from test_gpu_parity import _dev_merge
+        got, st = _dev_merge(ctx, din, torch)
+        host = [cdb.decode_snapshot(s) for s in snaps]
+        up = cdb.DevInput()
+        arr = (ctypes.c_void_p * 4)(*[b.handle for b in host])
+        ctx.check(cdb.lib().cdb_upload_batches(ctx.handle, arr, 4, ctypes.byref(up)))
+        try:
+            want, st2 = _dev_merge(ctx, up, torch)
+        finally:
+            _release(up)
+        for x, y in zip(got, want):
+            assert torch.equal(x, y)
+        assert st.key_rows_out == st2.key_rows_out > 0
+    finally:
+        _release(din)
+
+
+def test_device_decode_host_tier(ctx):
+    """Objects past the per-thread dedup limits (3000 members, 1500 nodes) are decoded on the
+    host and uploaded into their reserved rows at the snapshot's fold position."""
+    big, c = o.Set(), o.Counter()
+    for j in range(3000):
+        big.set(b"m%d" % j, None, j % 17)
+        if j % 5 == 0:
+            big.dele[b"m%d" % j] = (j % 13) + 3
+    for n in range(1500):
+        c.data[n] = (n, n % 5)
+    c.cal_sum()
+    db = o.DB()
+    db.data.update({b"big": o.Object(1, 0, 0, o.OBJECT_ENC_SET, big),
+                    b"cnt": o.Object(1, 0, 0, o.OBJECT_ENC_COUNTER, c)})
+    snap = o.dump_all(db, o.NodeHeader())
+    _, din = _check(ctx, [gen_replicas(4, n_replicas=1)[0], snap, snap])
+    _release(din)
+
+
+def test_device_decode_c3_snapshots(ctx):
+    """C3 replica states (op-stream apply results: ~300-member sets, mostly the host tier)."""
+    snaps = configs.c3_snapshots(cdb, ctx, ops_per_replica=200_000)
+    _, din = _check(ctx, snaps)
+    _release(din)
+
+
+def test_device_decode_errors(ctx):
+    good = gen_replicas(7, n_replicas=2)
+    bad = bytearray(good[1])
+    cut = bytes(bad[: len(bad) // 2])
+    want = None
+    try:
+        cdb.decode_snapshot(cut)
+    except cdb.CstError as e:
+        want = (type(e), getattr(e, "offset", None))
+    tm = {}
+    with pytest.raises(cdb.CstError) as ei:
+        cdb.decode_snapshots_device(ctx, [good[0], cut], timing=tm)
+    assert (type(ei.value), getattr(ei.value, "offset", None)) == want and tm["failed"] == 1
+    # a checksum mismatch in snapshot 1: every row is still returned, that batch flagged
+    bad[-1] ^= 0xFF
+    batches, din = cdb.decode_snapshots_device(ctx, [good[0], bytes(bad)])
+    try:
+        assert [b.checksum_ok for b in batches] == [True, False]
+        host = cdb.decode_snapshot(bytes(bad), allow_bad_checksum=True)
+        assert din.keys.n == cdb.decode_snapshot(good[0]).info().n_data + cdb.decode_snapshot(good[0]).info().n_expires \
+            + cdb.decode_snapshot(good[0]).info().n_deletes + host.info().n_data + host.info().n_expires \
+            + host.info().n_deletes
+    finally:
+        _release(din)
+    # rows in HBM: the host merge and the upload refuse such a batch
+    with pytest.raises((cdb.CstError, ValueError)):
+        cdb.DB(ctx).merge_batches(batches)
