@@ -94,6 +94,14 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x)
   for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
   return x;
 }
+// Sum over the wave of per-lane values below 2^BITS: one ballot + popcount per bit.
+template <int BITS>
+__device__ __forceinline__ uint32_t wave_sum_bits(uint32_t x) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < BITS; ++k) s += (uint32_t)__popcll(__ballot((x >> k) & 1u)) << k;
+  return s;
+}
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
 #pragma unroll
   for (int d = 32; d > 0; d >>= 1) x = max(x, (uint64_t)__shfl_xor((unsigned long long)x, d, 64));
@@ -139,6 +147,7 @@ struct RunView {
 struct WaveArgs {
   BucketArgs A;
   uint32_t nbuckets;
+  uint32_t blo, bhi;    // this launch's bucket range (the bucket phase runs in chunks)
   uint32_t* big_list;   // buckets for the workgroup tier
   uint32_t* big_count;
   RunView V;            // sorted-run path only
@@ -179,12 +188,13 @@ __device__ __forceinline__ void load_perm(const BucketArgs& A, const WaveDir& d,
   }
 }
 
-// Every input column of a bucket, one key row and two child rows per lane and KE.
-template <int KE>
+// Every input column of a bucket: KE key rows and CE child rows per lane (CE = 1 for the
+// buckets of at most 64 child rows, the common case: the child phases then run once per lane).
+template <int KE, int CE = 2 * KE>
 struct WaveIn {
   WaveDir d;
   uint64_t kh[KE], kf[KE], kct[KE], kut[KE], kdt[KE], kaux[KE], kmeta[KE];
-  uint64_t cpkh[2 * KE], cpkf[2 * KE], cid1[2 * KE], cid2[2 * KE], ct[2 * KE], cm[2 * KE];
+  uint64_t cpkh[CE], cpkf[CE], cid1[CE], cid2[CE], ct[CE], cm[CE];
 };
 template <int KE>
 __device__ __forceinline__ void load_cols(const BucketArgs& A, const WaveDir& d, const WavePerm<KE>& p, int lane,
@@ -385,10 +395,10 @@ __device__ __forceinline__ void lookback(const BucketArgs& A, uint32_t b, int la
 // ITS capacity (and forced tiers) for the workgroup tier. `next()` runs exactly once, as
 // soon as `in` is dead (after the children are staged in LDS): the streaming kernel issues
 // the next bucket's loads there, so they are in flight while this bucket's children fold.
-template <int KE, typename Next>
+template <int KE, int CE, typename Next>
 __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, uint32_t b, int lane,
-                                            const WaveIn<KE>& in, Next&& next) {
-  constexpr int CE = 2 * KE;
+                                            const WaveIn<KE, CE>& in, Next&& next) {
+  static_assert(CE <= 2 * KE, "child slots per lane");
   constexpr uint32_t KC = WaveLds<KE>::KC, CC = WaveLds<KE>::CC;
   const BucketArgs& A = W.A;
   const uint32_t K = in.d.K, N = in.d.N, M = in.d.M;
@@ -403,7 +413,10 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   };
   auto push = [&](uint32_t* list, uint32_t* count) {
     pass_on();
-    if (lane == 0) list[atomicAdd(count, 1u)] = b;
+    if (lane == 0) {  // no outputs until the workgroup tier's (a pipelined compaction may read them first)
+      A.kout[b] = A.nout[b] = A.mout[b] = 0;
+      list[atomicAdd(count, 1u)] = b;
+    }
   };
   if (KE == 1) {  // the wide kernel finds its buckets itself (wide_bucket_candidate)
     if (A.force_tier == 1 || A.force_tier == 2 || A.force_tier == 4 || N + M > WaveLds<2>::CC || K > WaveLds<2>::KC) {
@@ -526,7 +539,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   uint64_t o_ct[KE], o_ut[KE], o_dt[KE], o_meta[KE], o_win[KE];
   uint32_t o_T[KE], orank[KE];
   bool emit[KE];
-  unsigned long long st_conf = 0, st_dict = 0, st_gcd = 0;
+  uint32_t st_conf = 0, st_dict = 0, st_gcd = 0;
   uint32_t kout = 0;
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
@@ -624,7 +637,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   }
   // ------------------------------------------------------------ 3. children: key lookup
   // word = key rank << 56 | id hash[41:0] << 14 | pos << 8 | slot   (rank < 128, slot < 256)
-  unsigned long long orph = 0, gcm = 0;
+  uint32_t orph = 0, gcm = 0;
   uint32_t ckey[CE];
   bool clive[CE];
 #pragma unroll
@@ -674,8 +687,9 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     const bool isn = c < N;
     cw[e] = ~0ull;
     if (clive[e]) {
-      const uint64_t ih = isn ? mix64(cid1[e]) : cid1[e];
-      cw[e] = ((uint64_t)ckey[e] << 56) | ((ih & kM42) << 14) | ((uint64_t)meta_pos(cm[e]) << 8) | c;
+      // a node is ranked by its raw id, a member by its hash (ids that share the low 42 bits
+      // are caught below and go to the exact tier)
+      cw[e] = ((uint64_t)ckey[e] << 56) | ((cid1[e] & kM42) << 14) | ((uint64_t)meta_pos(cm[e]) << 8) | c;
     }
     const uint64_t Lm = __ballot(clive[e]);
     if (clive[e]) L.sw[nlive + lane_rank(Lm)] = cw[e];
@@ -688,8 +702,8 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     rank_count<(CE >= 4 ? 4 : CE)>(L.sw, nlive, cw, crk);
   else if (CE >= 3 && C > 128)
     rank_count<(CE >= 3 ? 3 : CE)>(L.sw, nlive, cw, crk);
-  else if (C > 64)
-    rank_count<2>(L.sw, nlive, cw, crk);
+  else if (CE >= 2 && C > 64)
+    rank_count<(CE >= 2 ? 2 : CE)>(L.sw, nlive, cw, crk);
   else
     rank_count<1>(L.sw, nlive, cw, crk);
   wave_sync();
@@ -863,24 +877,25 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     A.mout[b] = dense ? 0 : mbase;
   }
   unsigned long long* st = stat_shard(A.stats);
+  // per-lane counts are small (<= 64 KE segment rows, <= CE children): summed by bit slices
   if (__ballot(st_conf)) {
-    const unsigned long long v = wave_sum_u64(st_conf);
+    const unsigned long long v = wave_sum_bits<8>(st_conf);
     if (lane == 0) atomicAdd(&st[ST_TYPE_CONFLICTS], v);
   }
   if (__ballot(st_dict)) {
-    const unsigned long long v = wave_sum_u64(st_dict);
+    const unsigned long long v = wave_sum_bits<8>(st_dict);
     if (lane == 0) atomicAdd(&st[ST_DICT_MERGES], v);
   }
   if (__ballot(orph)) {
-    const unsigned long long v = wave_sum_u64(orph);
+    const unsigned long long v = wave_sum_bits<3>(orph);
     if (lane == 0) atomicAdd(&st[ST_ORPHANS], v);
   }
   if (__ballot(st_gcd)) {
-    const unsigned long long v = wave_sum_u64(st_gcd);
+    const unsigned long long v = wave_sum_bits<2>(st_gcd);
     if (lane == 0) atomicAdd(&st[ST_DELETES_GCED], v);
   }
   if (__ballot(gcm)) {
-    const unsigned long long v = wave_sum_u64(gcm);
+    const unsigned long long v = wave_sum_bits<3>(gcm);
     if (lane == 0) atomicAdd(&st[ST_MEMBERS_GCED], v);
   }
 }
@@ -996,8 +1011,8 @@ __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_kernel(WaveArgs 
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   // buckets in dispatch order (the look-back relies on it; an XCD remap measured no faster
   // with whole-row reads)
-  const uint32_t b = blockIdx.x * kWavesPerWG + wv;
-  if (b >= W.nbuckets) return;
+  const uint32_t b = W.blo + blockIdx.x * kWavesPerWG + wv;
+  if (b >= W.bhi) return;
   const WaveDir d = load_dir(W.A, b);
   WavePerm<1> p;
   WaveIn<1> in;
@@ -1028,16 +1043,16 @@ __device__ __forceinline__ bool wide_bucket_candidate(const BucketArgs& A, uint3
 __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_kernel(WaveArgs W) {
   __shared__ WaveLds<2> lds_all[kWavesPerWG];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t groups = (W.nbuckets + 63) / 64;
+  const uint32_t groups = (W.bhi - W.blo + 63) / 64;
   unsigned long long found = 0;
   for (uint32_t g = blockIdx.x * kWavesPerWG + wv; g < groups; g += gridDim.x * kWavesPerWG) {
-    const uint32_t b = g * 64 + lane;
-    uint64_t m = __ballot(b < W.nbuckets && wide_bucket_candidate(W.A, b));
+    const uint32_t b = W.blo + g * 64 + lane;
+    uint64_t m = __ballot(b < W.bhi && wide_bucket_candidate(W.A, b));
     found += __popcll(m);
     while (m) {
       const int i = __builtin_ctzll(m);
       m &= m - 1;
-      const uint32_t bb = g * 64 + i;
+      const uint32_t bb = W.blo + g * 64 + i;
       const WaveDir d = load_dir(W.A, bb);
       WavePerm<2> p;
       WaveIn<2> in;

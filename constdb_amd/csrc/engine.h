@@ -16,6 +16,7 @@ struct cdb_ctx {
   hipStream_t side2 = nullptr;                        // node / member partitions beside the keys'
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;    // (timing disabled)
   hipEvent_t ev_pfork = nullptr, ev_pn = nullptr, ev_pm = nullptr;
+  hipEvent_t ev_cs = nullptr, ev_cw = nullptr, ev_cdone = nullptr;  // pipelined compaction (side2)
   std::string last_error;
   struct Buf { void* p = nullptr; size_t bytes = 0; };
   Buf ws[32];  // named workspace slots, grown on demand, reused across calls
@@ -46,6 +47,7 @@ enum WsSlot {
   WS_RUNDIR, WS_RUNMISC,                                // sorted-run path: run directories, gap lists
   WS_HOTC3, WS_HOTMETA, WS_HOTK, WS_HOTCH, WS_RADIX,    // over-capacity child path (hot.hip.h)
   WS_MAT,                                               // sorted-run path: materialisation counts
+  WS_PIPE,                                              // pipelined bucket phase: range bases, totals
   WS_COUNT
 };
 static_assert(WS_COUNT <= 32, "cdb_ctx::ws has 32 slots");

@@ -230,14 +230,28 @@ __device__ __forceinline__ void compact_chunk(const CompactArgs& A, CompactLds& 
   }
 }
 
-__global__ void __launch_bounds__(kCompactWaves * 64) compact_kernel(CompactArgs A, uint32_t nbuckets, uint64_t ck,
-                                                                     uint64_t cn) {
+// Grid-stride over the (family, chunk) tasks; the task counts follow from the dense totals on
+// the device, so one launch of any size covers a bucket range whose output size the host does
+// not know (the pipelined bucket phase compacts each range while the next one merges).
+__global__ void __launch_bounds__(kCompactWaves * 64) compact_kernel(CompactArgs A, uint32_t nbuckets) {
   __shared__ CompactLds lds_all[kCompactWaves];
   CompactLds& L = lds_all[threadIdx.x >> 6];
-  const uint64_t task = (uint64_t)blockIdx.x * kCompactWaves + (threadIdx.x >> 6);
-  if (task < ck) compact_chunk<0>(A, L, task, nbuckets);
-  else if (task < ck + cn) compact_chunk<1>(A, L, task - ck, nbuckets);
-  else compact_chunk<2>(A, L, task - ck - cn, nbuckets);
+  if (nbuckets == 0) return;
+  const uint32_t n1 = nbuckets - 1;
+  const uint64_t ck = (A.kdoff[n1] + A.kout[n1] + kCompactChunk - 1) / kCompactChunk;
+  const uint64_t cn = (A.ndoff[n1] + A.nout[n1] + kCompactChunk - 1) / kCompactChunk;
+  const uint64_t cm = (A.mdoff[n1] + A.mout[n1] + kCompactChunk - 1) / kCompactChunk;
+  for (uint64_t task = (uint64_t)blockIdx.x * kCompactWaves + (threadIdx.x >> 6); task < ck + cn + cm;
+       task += (uint64_t)gridDim.x * kCompactWaves) {
+    if (task < ck) compact_chunk<0>(A, L, task, nbuckets);
+    else if (task < ck + cn) compact_chunk<1>(A, L, task - ck, nbuckets);
+    else compact_chunk<2>(A, L, task - ck - cn, nbuckets);
+  }
+}
+
+// Dense base of the next bucket range: base[p + 1] = base[p] + the range's totals (3 families).
+__global__ void pipe_base_kernel(uint64_t* base, const uint64_t* tot) {
+  if (threadIdx.x < 3) base[3 + threadIdx.x] = base[threadIdx.x] + tot[threadIdx.x];
 }
 
 template <typename T, typename OutT>
@@ -923,23 +937,126 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   WaveArgs WA;
   WA.A = A;
   WA.nbuckets = (uint32_t)nb;
+  WA.blo = 0;
+  WA.bhi = (uint32_t)nb;
   WA.big_list = d_big_list;
   WA.big_count = d_big_count;
   WA.V = RV;
   CDB_HIP(hipEventRecord(ctx->ev_fork, s), "event");  // inputs of both bucket tiers are ready
-  if (use_runs) {
-    bucket_wave_runs_kernel<<<(uint32_t)((nb + kWavesPerWG - 1) / kWavesPerWG), kWavesPerWG * 64, 0, s>>>(WA);
-    CDB_TRY(launch_check(ctx, s, "bucket_wave_runs_kernel"));
-    static const bool serial = std::getenv("CDB_WIDE_SERIAL") != nullptr;
-    hipStream_t ws = serial ? s : ctx->side;
-    const uint32_t g = (uint32_t)std::min<uint64_t>((nb + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024);
-    if (!serial) CDB_HIP(hipStreamWaitEvent(ws, ctx->ev_fork, 0), "wait");
-    bucket_wide_runs_kernel<<<g, kWavesPerWG * 64, 0, ws>>>(WA);
-    CDB_TRY(launch_check(ctx, ws, "bucket_wide_runs_kernel"));
-    if (!serial) {
-      CDB_HIP(hipEventRecord(ctx->ev_join, ws), "event");
-      CDB_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0), "wait");
+  // The wave and wide tiers run over P consecutive bucket ranges. Range p is scanned and compacted
+  // into the dense outputs on stream cs while range p + 1 merges: the tiers are VALU-bound and
+  // the compaction HBM-bound, so the two overlap. Only valid when no bucket goes to a workgroup
+  // tier (those add outputs after every range): then everything is compacted again at the end.
+  static const uint32_t pipe_env = [] {
+    const char* e = std::getenv("CDB_PIPE");
+    return e ? (uint32_t)std::max(1, std::atoi(e)) : 8u;
+  }();
+  const uint32_t P = (dense || wave_pf() != 0 || nb < 64ull * pipe_env) ? 1 : pipe_env;
+  const bool pipelined = P > 1;
+  CompactArgs C;
+  C.ks = ksp[0];
+  C.ns = nsp[0];
+  C.ms = msp[0];
+  for (int c = 0; c < kKeyOutCols; ++c) C.kd[c] = out->keys.col[c];
+  for (int c = 0; c < kNodeCols; ++c) {
+    C.nd[c] = out->nodes.col[c];
+    C.md[c] = out->members.col[c];
+  }
+  C.kbase = dk.base; C.nbase = dnd.base; C.mbase = dm.base;
+  C.kout = dk.out; C.nout = dnd.out; C.mout = dm.out;
+  C.kdoff = dk.doff; C.ndoff = dnd.doff; C.mdoff = dm.doff;
+  C.base_tot = d_lb_tot;
+  C.cap[0] = K;
+  C.cap[1] = N;
+  C.cap[2] = M;
+  uint32_t* d_cerr = (uint32_t*)(misc + 104);   // zeroed with the misc header
+  uint32_t* d_cerr_p = (uint32_t*)(misc + 108);  // the pipelined compaction's
+  C.err = d_cerr;
+  uint64_t* d_pipe = nullptr;  // [P + 1][3] dense bases | [P][3] range totals
+  static const bool wide_serial = std::getenv("CDB_WIDE_SERIAL") != nullptr;
+  hipStream_t ws = wide_serial ? s : ctx->side;
+  hipStream_t cs = ctx->side2;
+  if (!wide_serial) CDB_HIP(hipStreamWaitEvent(ws, ctx->ev_fork, 0), "wait");
+  if (pipelined) {
+    d_pipe = (uint64_t*)ws_get(ctx, WS_PIPE, (6 * P + 3) * sizeof(uint64_t), &st);
+    if (!d_pipe) return st;
+    CDB_HIP(hipStreamWaitEvent(cs, ctx->ev_fork, 0), "wait");
+    CDB_HIP(hipMemsetAsync(d_pipe, 0, 3 * sizeof(uint64_t), cs), "memset pipe");
+  }
+  static const int tile_nw = [] {  // staged tiles of NW buckets on the sorted-run path (0: off)
+    const char* e = std::getenv("CDB_TILE_NW");
+    return e ? std::atoi(e) : 0;
+  }();
+  // extra (unused) LDS per wave-tier workgroup: caps how many share a CU, leaving room for the
+  // pipelined compaction's waves beside them
+  static const uint32_t wave_dyn_lds = [] {
+    const char* e = std::getenv("CDB_WAVE_DYN_LDS");
+    return e ? (uint32_t)std::atoi(e) : 0u;
+  }();
+  for (uint32_t p = 0; p < P; ++p) {
+    const uint32_t lo = (uint32_t)(nb * p / P), hi = (uint32_t)(nb * (p + 1) / P), nr_b = hi - lo;
+    WA.blo = lo;
+    WA.bhi = hi;
+    if (nr_b == 0) continue;
+    const uint32_t gw = (uint32_t)std::min<uint64_t>((nr_b + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024);
+    if (use_runs) {
+      if (tile_nw == 4)
+        bucket_tile_runs_kernel<4><<<(nr_b + 3) / 4, 4 * 64, 0, s>>>(WA);
+      else if (tile_nw == 8)
+        bucket_tile_runs_kernel<8><<<(nr_b + 7) / 8, 8 * 64, 0, s>>>(WA);
+      else if (tile_nw == 16)
+        bucket_tile_runs_kernel<16><<<(nr_b + 15) / 16, 16 * 64, 0, s>>>(WA);
+      else
+        bucket_wave_runs_kernel<<<(nr_b + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, wave_dyn_lds, s>>>(WA);
+      CDB_TRY(launch_check(ctx, s, "bucket_wave_runs_kernel"));
+      // the wide tier's buckets are disjoint from the wave tier's: beside it on a side stream
+      bucket_wide_runs_kernel<<<gw, kWavesPerWG * 64, 0, ws>>>(WA);
+      CDB_TRY(launch_check(ctx, ws, "bucket_wide_runs_kernel"));
+    } else {
+      if (wave_pf() == 0)
+        bucket_wave_kernel<<<(nr_b + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, 0, s>>>(WA);
+      else if (wave_pf() == 1)
+        bucket_wave_pf1_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
+      else
+        bucket_wave_pf2_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
+      CDB_TRY(launch_check(ctx, s, "bucket_wave_kernel"));
+      bucket_wide_kernel<<<gw, kWavesPerWG * 64, 0, ws>>>(WA);
+      CDB_TRY(launch_check(ctx, ws, "bucket_wide_kernel"));
     }
+    if (pipelined) {  // range p: scans and compaction on cs once both tiers are through it
+      CDB_HIP(hipEventRecord(ctx->ev_cs, s), "event");
+      CDB_HIP(hipStreamWaitEvent(cs, ctx->ev_cs, 0), "wait");
+      if (!wide_serial) {
+        CDB_HIP(hipEventRecord(ctx->ev_cw, ws), "event");
+        CDB_HIP(hipStreamWaitEvent(cs, ctx->ev_cw, 0), "wait");
+      }
+      uint64_t* base = d_pipe + 3 * p;
+      uint64_t* tot = d_pipe + 3 * (P + 1) + 3 * p;
+      CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dk.out + lo, nr_b, dk.doff + lo, (uint32_t*)nullptr, tot + 0, cs,
+                                                 WS_SCAN2));
+      CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dnd.out + lo, nr_b, dnd.doff + lo, (uint32_t*)nullptr, tot + 1,
+                                                 cs, WS_SCAN2));
+      CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dm.out + lo, nr_b, dm.doff + lo, (uint32_t*)nullptr, tot + 2, cs,
+                                                 WS_SCAN2));
+      pipe_base_kernel<<<1, 64, 0, cs>>>(base, tot);
+      CDB_TRY(launch_check(ctx, cs, "pipe_base_kernel"));
+      CompactArgs Cp = C;
+      Cp.kbase += lo; Cp.nbase += lo; Cp.mbase += lo;
+      Cp.kout += lo; Cp.nout += lo; Cp.mout += lo;
+      Cp.kdoff += lo; Cp.ndoff += lo; Cp.mdoff += lo;
+      Cp.base_tot = (const unsigned long long*)base;
+      Cp.err = d_cerr_p;
+      compact_kernel<<<1024, 64 * kCompactWaves, 0, cs>>>(Cp, nr_b);
+      CDB_TRY(launch_check(ctx, cs, "compact_kernel"));
+    }
+  }
+  if (!wide_serial) {
+    CDB_HIP(hipEventRecord(ctx->ev_join, ws), "event");
+    CDB_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0), "wait");
+  }
+  WA.blo = 0;
+  WA.bhi = (uint32_t)nb;
+  if (use_runs) {
     // the workgroup tiers' buckets: copied out of the runs into AoS rows + row indices
     MatArgs MA_;
     MA_.kr = krows;
@@ -966,28 +1083,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, MA_.chunks, nb, MA_.chunk0, (uint32_t*)nullptr, d_nchunks, s));
     mat_copy_kernel<<<4096, 256, 0, s>>>(WA, MA_, d_big_list);
     CDB_TRY(launch_check(ctx, s, "mat_copy_kernel"));
-  } else if (wave_pf() == 0)
-    bucket_wave_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA);
-  else if (wave_pf() == 1)
-    bucket_wave_pf1_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
-  else
-    bucket_wave_pf2_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
-  if (!use_runs) {
-  CDB_TRY(launch_check(ctx, s, "bucket_wave_kernel"));
-  {  // the wide tier's buckets are disjoint from the wave tier's: it runs on a side stream
-     // and fills the wave kernel's tail (CDB_WIDE_SERIAL=1 runs it after the wave kernel)
-    static const bool serial = std::getenv("CDB_WIDE_SERIAL") != nullptr;
-    hipStream_t ws = serial ? s : ctx->side;
-    const uint32_t g = (uint32_t)std::min<uint64_t>((nb + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024);
-    if (!serial) CDB_HIP(hipStreamWaitEvent(ws, ctx->ev_fork, 0), "wait");
-    bucket_wide_kernel<<<g, kWavesPerWG * 64, 0, ws>>>(WA);
-    CDB_TRY(launch_check(ctx, ws, "bucket_wide_kernel"));
-    if (!serial) {
-      CDB_HIP(hipEventRecord(ctx->ev_join, ws), "event");
-      CDB_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0), "wait");
-    }
   }
-  }  // partition path tiers
   // ---- 4. buckets beyond the wave tiers: the mid tier (one workgroup per bucket, LDS), or,
   //         when there are many of them, the chip-wide child path of the over-capacity
   //         buckets (hot.hip.h): buckets of a few keys with hundreds of children each (C3's
@@ -1015,36 +1111,26 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   const uint32_t hot = mid_wide ? 0 : counts[0];
   if (hot) CDB_TRY(over_capacity(ctx, A, d_hot_list, hot, s));
 
-  // ---- 5. dense compaction into the caller's output columns
-  CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dk.out, nb, dk.doff, (uint32_t*)nullptr, d_totals + 0, s));
-  CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dnd.out, nb, dnd.doff, (uint32_t*)nullptr, d_totals + 1, s));
-  CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dm.out, nb, dm.doff, (uint32_t*)nullptr, d_totals + 2, s));
-  CompactArgs C;
-  C.ks = ksp[0];
-  C.ns = nsp[0];
-  C.ms = msp[0];
-  for (int c = 0; c < kKeyOutCols; ++c) C.kd[c] = out->keys.col[c];
-  for (int c = 0; c < kNodeCols; ++c) {
-    C.nd[c] = out->nodes.col[c];
-    C.md[c] = out->members.col[c];
+  // ---- 5. dense compaction into the caller's output columns (already done range by range when
+  //         the bucket phase was pipelined and no workgroup tier added outputs)
+  const bool recompact = !pipelined || counts[1] > 0;
+  if (pipelined) {
+    CDB_HIP(hipEventRecord(ctx->ev_cdone, cs), "event");
+    CDB_HIP(hipStreamWaitEvent(s, ctx->ev_cdone, 0), "wait");
   }
-  C.kbase = dk.base; C.nbase = dnd.base; C.mbase = dm.base;
-  C.kout = dk.out; C.nout = dnd.out; C.mout = dm.out;
-  C.kdoff = dk.doff; C.ndoff = dnd.doff; C.mdoff = dm.doff;
-  C.base_tot = d_lb_tot;
-  C.cap[0] = K;
-  C.cap[1] = N;
-  C.cap[2] = M;
-  uint32_t* d_cerr = (uint32_t*)(misc + 104);  // zeroed with the misc header
-  C.err = d_cerr;
-  {  // chunks per family from the input row counts (outputs never exceed inputs)
-    const uint64_t ck = (K + kCompactChunk - 1) / kCompactChunk, cn = (N + kCompactChunk - 1) / kCompactChunk,
-                   cm = (M + kCompactChunk - 1) / kCompactChunk;
-    const uint64_t tasks = std::max<uint64_t>(ck + cn + cm, 1);
-    compact_kernel<<<(uint32_t)((tasks + kCompactWaves - 1) / kCompactWaves), 64 * kCompactWaves, 0, s>>>(
-        C, (uint32_t)nb, ck, cn);
+  if (recompact) {
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dk.out, nb, dk.doff, (uint32_t*)nullptr, d_totals + 0, s));
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dnd.out, nb, dnd.doff, (uint32_t*)nullptr, d_totals + 1, s));
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dm.out, nb, dm.doff, (uint32_t*)nullptr, d_totals + 2, s));
+    // one wave per 4096 output rows of a family (the kernel strides over any excess)
+    const uint64_t tasks = (K + N + M) / kCompactChunk + 3;
+    compact_kernel<<<(uint32_t)std::min<uint64_t>((tasks + kCompactWaves - 1) / kCompactWaves, 65536),
+                     64 * kCompactWaves, 0, s>>>(C, (uint32_t)nb);
+    CDB_TRY(launch_check(ctx, s, "compact_kernel"));
+  } else {
+    CDB_HIP(hipMemcpyAsync(d_totals, d_pipe + 3 * P, 3 * sizeof(uint64_t), hipMemcpyDeviceToDevice, s), "d2d");
+    CDB_HIP(hipMemcpyAsync(d_cerr, d_cerr_p, sizeof(uint32_t), hipMemcpyDeviceToDevice, s), "d2d");
   }
-  CDB_TRY(launch_check(ctx, s, "compact_kernel"));
   stats_reduce_kernel<<<1, 64, 0, s>>>(d_shards, d_stats);
   CDB_TRY(launch_check(ctx, s, "stats_reduce_kernel"));
   CDB_HIP(hipEventRecord(ctx->ev1, s), "event");
@@ -1113,7 +1199,7 @@ cdb_status cdb_ctx_create(cdb_ctx** out, int device) {
   if (st == CDB_OK) st = hip_check(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking), "stream");
   if (st == CDB_OK) st = hip_check(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking), "stream");
   if (st == CDB_OK) st = hip_check(ctx, hipStreamCreateWithFlags(&ctx->side2, hipStreamNonBlocking), "stream");
-  for (hipEvent_t* e : {&ctx->ev_pfork, &ctx->ev_pn, &ctx->ev_pm})
+  for (hipEvent_t* e : {&ctx->ev_pfork, &ctx->ev_pn, &ctx->ev_pm, &ctx->ev_cs, &ctx->ev_cw, &ctx->ev_cdone})
     if (st == CDB_OK) st = hip_check(ctx, hipEventCreateWithFlags(e, hipEventDisableTiming), "event");
   if (st == CDB_OK) st = hip_check(ctx, hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming), "event");
   if (st == CDB_OK) st = hip_check(ctx, hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming), "event");
@@ -1140,7 +1226,7 @@ void cdb_ctx_destroy(cdb_ctx* ctx) {
   if (ctx->ev_bucket) hipEventDestroy(ctx->ev_bucket);
   if (ctx->ev_fork) hipEventDestroy(ctx->ev_fork);
   if (ctx->ev_join) hipEventDestroy(ctx->ev_join);
-  for (hipEvent_t e : {ctx->ev_pfork, ctx->ev_pn, ctx->ev_pm})
+  for (hipEvent_t e : {ctx->ev_pfork, ctx->ev_pn, ctx->ev_pm, ctx->ev_cs, ctx->ev_cw, ctx->ev_cdone})
     if (e) hipEventDestroy(e);
   for (hipEvent_t e : ctx->pin_ev)
     if (e) hipEventDestroy(e);

@@ -44,18 +44,19 @@ struct SnapWriter {  // SnapshotWriter (snapshot.rs:9-69) without the CRC (done 
 };
 
 uint64_t crc64_jones(const uint8_t* p, size_t n) {
-  static uint64_t t[256];
-  static bool init = false;
-  if (!init) {
-    for (int i = 0; i < 256; ++i) {
-      uint64_t c = (uint64_t)i;
-      for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x95AC9329AC4BC9B5ull : c >> 1;
-      t[i] = c;
+  struct Table {  // function-local static: initialised once, thread-safe (C++11)
+    uint64_t t[256];
+    Table() {
+      for (int i = 0; i < 256; ++i) {
+        uint64_t c = (uint64_t)i;
+        for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ 0x95AC9329AC4BC9B5ull : c >> 1;
+        t[i] = c;
+      }
     }
-    init = true;
-  }
+  };
+  static const Table tab;
   uint64_t crc = 0;
-  for (size_t i = 0; i < n; ++i) crc = t[(crc ^ p[i]) & 0xFF] ^ (crc >> 8);
+  for (size_t i = 0; i < n; ++i) crc = tab.t[(crc ^ p[i]) & 0xFF] ^ (crc >> 8);
   return crc;
 }
 
