@@ -19,13 +19,16 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <cstring>
 #include <memory>
 #include <vector>
 
 #include "batch.h"
 #include "engine.h"
+#include "partition.hip.h"
 
 namespace cdb {
 namespace {
@@ -77,10 +80,10 @@ struct DecArgs {
   uint32_t *ncount, *mcount;        // count pass: kept children per entry (kHostTier: host decodes)
   const uint64_t *noff, *moff;      // emit pass: first child row of each entry
   uint64_t* k[7];                   // kh kf ct ut dt aux meta
-  uint64_t *kref_off, *kref_len, *vref_off, *vref_len;
+  ulonglong2 *kref, *vref;           // byte references as (offset, length): Batch::key_ref / val_ref
   uint64_t* nd[6];                  // pkh pkf node v t meta
   uint64_t* mb[6];                  // pkh pkf mh mf t meta
-  uint64_t *mref_off, *mref_len, *mvref_off, *mvref_len;
+  ulonglong2 *mref, *mvref;          // Batch::m_ref / m_vref
   uint32_t pos;                     // fold position stamped into meta (device-resident emit)
 };
 
@@ -199,9 +202,8 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
     A.k[2][i] = t;
     A.k[3][i] = A.k[4][i] = A.k[5][i] = 0;
     A.k[6][i] = meta_pack(A.kind[i] == 1 ? TAG_EXPIRE : TAG_DELETE, A.pos, i);
-    A.kref_off[i] = key.off;
-    A.kref_len[i] = key.len;
-    A.vref_off[i] = A.vref_len[i] = 0;
+    A.kref[i] = make_ulonglong2(key.off, key.len);
+    A.vref[i] = make_ulonglong2(0, 0);
     return;
   }
   const Head hd = rd_head(p, o);
@@ -265,10 +267,8 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
       A.mb[3][row] = mh.f;
       A.mb[4][row] = t;
       A.mb[5][row] = meta_pack(j < na ? KIND_ADD : KIND_DEL, A.pos, row);
-      A.mref_off[row] = m.off;
-      A.mref_len[row] = m.len;
-      A.mvref_off[row] = v.off;
-      A.mvref_len[row] = v.len;
+      A.mref[row] = make_ulonglong2(m.off, m.len);
+      A.mvref[row] = make_ulonglong2(v.off, v.len);
       ++row;
     }
   }
@@ -279,10 +279,17 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
   A.k[4][i] = hd.dt;
   A.k[5][i] = aux;
   A.k[6][i] = meta_pack(hd.tag, A.pos, i);
-  A.kref_off[i] = hd.key.off;
-  A.kref_len[i] = hd.key.len;
-  A.vref_off[i] = val.off;
-  A.vref_len[i] = val.len;
+  A.kref[i] = make_ulonglong2(hd.key.off, hd.key.len);
+  A.vref[i] = make_ulonglong2(val.off, val.len);
+}
+
+// Any entry left to the host tier (its count is the kHostTier marker)?
+__global__ void host_tier_flag_kernel(const uint32_t* __restrict__ nc, const uint32_t* __restrict__ mc, uint64_t n,
+                                      unsigned long long* flag) {
+  bool any = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    any |= nc[i] == kHostTier || mc[i] == kHostTier;
+  if (__ballot(any) && (threadIdx.x & 63) == 0) atomicOr(flag, 1ull);
 }
 
 struct DevBuf {
@@ -313,7 +320,14 @@ struct EvPair {
 class GpuDecode {
  public:
   GpuDecode(cdb_ctx* ctx, Batch* out, uint32_t flags) : ctx_(ctx), out_(out), flags_(flags) {}
-  int prepare(const uint8_t* buf, size_t len, size_t* err_off, DecodeTiming* tm);
+  int prepare(const uint8_t* buf, size_t len, size_t* err_off, DecodeTiming* tm) {
+    const int rc = index(buf, len, err_off, tm);
+    return rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM ? rc : prepare_device(err_off);
+  }
+  // the host index pass alone (no HIP call: several snapshots are indexed on parallel threads)
+  int index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTiming* tm);
+  // everything after it (returns the index pass's status when the device part succeeds)
+  int prepare_device(size_t* err_off);
   cdb_status emit_host(DecodeTiming* tm);
   cdb_status emit_device(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t pos,
                          DecodeTiming* tm);
@@ -336,8 +350,9 @@ class GpuDecode {
     *p = nullptr;
     return fail(ctx_, CDB_OUT_OF_MEMORY, what);
   }
-  cdb_status refs_to_batch(const ColVec& ko, const ColVec& kl, const ColVec& vo, const ColVec& vl, const ColVec& mo,
-                           const ColVec& ml, const ColVec& mvo, const ColVec& mvl);
+  // byte references straight into the batch (pairs as written by the emit pass), then the host
+  // tier's member references
+  cdb_status refs_to_batch(const DecArgs& A);
 
   cdb_ctx* ctx_;
   Batch* out_;
@@ -356,35 +371,41 @@ class GpuDecode {
   EvPair ev_;
 };
 
-int GpuDecode::prepare(const uint8_t* buf, size_t len, size_t* err_off, DecodeTiming* tm) {
+int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTiming* tm) {
   const auto t0 = std::chrono::steady_clock::now();
   rc_ = index_snapshot(buf, len, flags_, out_, &idx_, err_off, &dcrc_);
   if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  if (rc_ != CDB_OK && rc_ != CDB_INVALID_SNAPSHOT_CHECKSUM) return rc_;
+  return rc_;
+}
+
+int GpuDecode::prepare_device(size_t* err_off) {
+  const uint64_t len = out_->raw.size();
   const uint64_t n = n_ = idx_.offset.size();
   if (n == 0) return rc_;
   if (hipSetDevice(ctx_->device) != hipSuccess) return CDB_DEVICE_ERROR;
   hipStream_t s = s_ = ctx_->stream;
-  noff_.resize(n);
-  moff_.resize(n);
-  std::vector<uint32_t> ncnt(n), mcnt(n);
   // the raw stream sits after `pad` zero bytes, so the checksummed prefix ends on a CRC tile
   const uint64_t tile = crc_tile_bytes();
   const uint64_t pad = dcrc_.pending ? (tile - dcrc_.len % tile) % tile : 0;
   if ((st_ = alloc(&d_raw_.p, pad + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK) return st_;
-  if ((st_ = alloc(&d_crc_.p, 8, "decode: device checksum word")) != CDB_OK) return st_;
-  // one device block: off | noff | moff | ncount | mcount | kind
-  const size_t head = n * (8 + 1 + 4 + 4 + 8 + 8) + 64;
+  // small device words: crc | node-row total | member-row total | host-tier flag
+  if ((st_ = alloc(&d_crc_.p, 32, "decode: device checksum word")) != CDB_OK) return st_;
+  uint64_t* d_small = (uint64_t*)d_crc_.p;
+  // one device block: off | noff | moff | ncount | mcount | kind | scan partials
+  const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+  const size_t head = n * (8 + 1 + 4 + 4 + 8 + 8) + 16 * tiles + 64;
   if ((st_ = alloc(&d_meta_.p, head, "decode: device entry index")) != CDB_OK) return st_;
   uint8_t* hm = (uint8_t*)d_meta_.p;
   uint64_t* d_off = (uint64_t*)hm;
   uint64_t* d_noff = d_off + n;
   uint64_t* d_moff = d_noff + n;
-  uint32_t* d_ncnt = (uint32_t*)(d_moff + n);
+  uint64_t* d_sums = d_moff + n;  // 2 x tiles
+  uint32_t* d_ncnt = (uint32_t*)(d_sums + 2 * tiles);
   uint32_t* d_mcnt = d_ncnt + n;
   uint8_t* d_kind = (uint8_t*)(d_mcnt + n);
   ck(hipEventRecord(ev_.a, s), "event");
   if (pad) ck(hipMemsetAsync(d_raw_.p, 0, pad, s), "memset(decode)");
+  ck(hipMemsetAsync(d_small, 0, 32, s), "memset(decode)");
   const uint8_t* raw_dev = (const uint8_t*)d_raw_.p + pad;
   if (st_ == CDB_OK) st_ = staged_h2d(ctx_, (void*)raw_dev, out_->raw.data(), len, s);
   if (st_ == CDB_OK) st_ = staged_h2d(ctx_, d_off, idx_.offset.data(), n * 8, s);
@@ -402,22 +423,43 @@ int GpuDecode::prepare(const uint8_t* buf, size_t len, size_t* err_off, DecodeTi
   grid_ = (uint32_t)((n + kDecThreads - 1) / kDecThreads);
   count_kernel<<<grid_, kDecThreads, 0, s>>>(A_);
   ck(hipGetLastError(), "count_kernel");
+  // the child offsets: exclusive scans of the counts on the device (they are only meaningful
+  // when no entry is left to the host tier, which the flag reports)
+  host_tier_flag_kernel<<<(uint32_t)std::min<uint64_t>(grid_, 1024), kDecThreads, 0, s>>>(d_ncnt, d_mcnt, n,
+                                                                                         (unsigned long long*)d_small + 3);
+  ck(hipGetLastError(), "host_tier_flag_kernel");
+  scan_reduce_kernel<uint32_t><<<(uint32_t)tiles, kScanThreads, 0, s>>>(d_ncnt, n, d_sums);
+  scan_sums_kernel<<<1, kScanThreads, 0, s>>>(d_sums, tiles, d_small + 1);
+  scan_apply_kernel<uint32_t, uint64_t><<<(uint32_t)tiles, kScanThreads, 0, s>>>(d_ncnt, n, d_sums, d_noff,
+                                                                               (uint64_t*)nullptr);
+  scan_reduce_kernel<uint32_t><<<(uint32_t)tiles, kScanThreads, 0, s>>>(d_mcnt, n, d_sums + tiles);
+  scan_sums_kernel<<<1, kScanThreads, 0, s>>>(d_sums + tiles, tiles, d_small + 2);
+  scan_apply_kernel<uint32_t, uint64_t><<<(uint32_t)tiles, kScanThreads, 0, s>>>(d_mcnt, n, d_sums + tiles, d_moff,
+                                                                               (uint64_t*)nullptr);
+  ck(hipGetLastError(), "decode scans");
+  if (dcrc_.pending && st_ == CDB_OK)  // the index pass left the stream checksum to the GPU
+    st_ = crc64_device(ctx_, (const uint8_t*)d_raw_.p, pad + dcrc_.len, d_small, s);
+  uint64_t small[4] = {0, 0, 0, 0};
+  ck(hipMemcpyAsync(small, d_small, 32, hipMemcpyDeviceToHost, s), "d2h(decode)");
+  ck(hipStreamSynchronize(s), "sync(decode)");
+  if (st_ != CDB_OK) return st_;
+  if (dcrc_.pending && small[0] != dcrc_.got) {
+    rc_ = CDB_INVALID_SNAPSHOT_CHECKSUM;
+    *err_off = dcrc_.err_off;
+  }
+  if (!small[3]) {  // every entry's children were counted on the device
+    nn_ = small[1];
+    nm_ = small[2];
+    return rc_;
+  }
+  // entries past the per-thread dedup limits: decoded here, into slots reserved by a host scan
+  noff_.resize(n);
+  moff_.resize(n);
+  std::vector<uint32_t> ncnt(n), mcnt(n);
   ck(hipMemcpyAsync(ncnt.data(), d_ncnt, n * 4, hipMemcpyDeviceToHost, s), "d2h(decode)");
   ck(hipMemcpyAsync(mcnt.data(), d_mcnt, n * 4, hipMemcpyDeviceToHost, s), "d2h(decode)");
   ck(hipStreamSynchronize(s), "sync(decode)");
   if (st_ != CDB_OK) return st_;
-  if (dcrc_.pending) {  // the index pass left the stream checksum to the GPU
-    uint64_t crc = 0;
-    if ((st_ = crc64_device(ctx_, (const uint8_t*)d_raw_.p, pad + dcrc_.len, (uint64_t*)d_crc_.p, s)) != CDB_OK)
-      return st_;
-    ck(hipMemcpy(&crc, d_crc_.p, 8, hipMemcpyDeviceToHost), "d2h(crc)");
-    if (st_ != CDB_OK) return st_;
-    if (crc != dcrc_.got) {
-      rc_ = CDB_INVALID_SNAPSHOT_CHECKSUM;
-      *err_off = dcrc_.err_off;
-    }
-  }
-  // entries past the per-thread dedup limits: decoded here, into slots reserved by the scan
   for (uint64_t i = 0; i < n; ++i) {
     if (ncnt[i] != kHostTier && mcnt[i] != kHostTier) continue;
     HostEntry he;
@@ -454,21 +496,23 @@ int GpuDecode::prepare(const uint8_t* buf, size_t len, size_t* err_off, DecodeTi
   return st_ != CDB_OK ? (int)st_ : rc_;
 }
 
-cdb_status GpuDecode::refs_to_batch(const ColVec& ko, const ColVec& kl, const ColVec& vo, const ColVec& vl,
-                                    const ColVec& mo, const ColVec& ml, const ColVec& mvo, const ColVec& mvl) {
+
+cdb_status GpuDecode::refs_to_batch(const DecArgs& A) {
+  static_assert(sizeof(ByteRef) == sizeof(ulonglong2), "byte references download as (offset, length) pairs");
   Batch& b = *out_;
   b.key_ref.resize(n_);
   b.val_ref.resize(n_);
-  for (uint64_t i = 0; i < n_; ++i) {
-    b.key_ref[i] = ByteRef{ko[i], kl[i]};
-    b.val_ref[i] = ByteRef{vo[i], vl[i]};
-  }
   b.m_ref.resize(nm_);
   b.m_vref.resize(nm_);
-  for (uint64_t i = 0; i < nm_; ++i) {
-    b.m_ref[i] = ByteRef{mo[i], ml[i]};
-    b.m_vref[i] = ByteRef{mvo[i], mvl[i]};
-  }
+  std::vector<HostSeg> segs;
+  auto down = [&](void* host, const ulonglong2* dev, uint64_t rows) {
+    if (rows) segs.push_back({host, const_cast<ulonglong2*>(dev), rows * 16});
+  };
+  down(b.key_ref.data(), A.kref, n_);
+  down(b.val_ref.data(), A.vref, n_);
+  down(b.m_ref.data(), A.mref, nm_);
+  down(b.m_vref.data(), A.mvref, nm_);
+  if (!segs.empty() && (st_ = staged_copy(ctx_, segs.data(), segs.size(), false, s_)) != CDB_OK) return st_;
   for (const HostEntry& he : hosted_) {
     const Batch& r = he.rows;
     for (size_t j = 0; j < r.m_pkh.size(); ++j) {
@@ -487,17 +531,17 @@ cdb_status GpuDecode::emit_host(DecodeTiming* tm) {
   if ((st_ = alloc(&d_rows_.p, rows_words * 8, "decode: device row columns")) != CDB_OK) return st_;
   uint64_t* w = (uint64_t*)d_rows_.p;
   DecArgs& A = A_;
+  uint64_t* const w0 = w;
+  auto align16 = [&]() { w += (w - w0) & 1; };  // reference pairs are 16-B stores
   for (int c = 0; c < 7; ++c, w += n) A.k[c] = w;
-  A.kref_off = w; w += n;
-  A.kref_len = w; w += n;
-  A.vref_off = w; w += n;
-  A.vref_len = w; w += n;
+  align16();
+  A.kref = (ulonglong2*)w; w += 2 * n;
+  A.vref = (ulonglong2*)w; w += 2 * n;
   for (int c = 0; c < 6; ++c, w += nn) A.nd[c] = w;
   for (int c = 0; c < 6; ++c, w += nm) A.mb[c] = w;
-  A.mref_off = w; w += nm;
-  A.mref_len = w; w += nm;
-  A.mvref_off = w; w += nm;
-  A.mvref_len = w; w += nm;
+  align16();
+  A.mref = (ulonglong2*)w; w += 2 * nm;
+  A.mvref = (ulonglong2*)w; w += 2 * nm;
   A.pos = 0;
   emit_kernel<<<grid_, kDecThreads, 0, s>>>(A);
   ck(hipGetLastError(), "emit_kernel");
@@ -512,23 +556,14 @@ cdb_status GpuDecode::emit_host(DecodeTiming* tm) {
   };
   ColVec* kc[7] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
   for (int c = 0; c < 7; ++c) down(kc[c], A.k[c], n);
-  ColVec ko, kl, vo, vl;
-  down(&ko, A.kref_off, n);
-  down(&kl, A.kref_len, n);
-  down(&vo, A.vref_off, n);
-  down(&vl, A.vref_len, n);
   ColVec* nc[6] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
   ColVec* mc[6] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
   for (int c = 0; c < 6; ++c) {
     down(nc[c], A.nd[c], nn);
     down(mc[c], A.mb[c], nm);
   }
-  ColVec mo, ml, mvo, mvl;
-  down(&mo, A.mref_off, nm);
-  down(&ml, A.mref_len, nm);
-  down(&mvo, A.mvref_off, nm);
-  down(&mvl, A.mvref_len, nm);
   if ((st_ = staged_copy(ctx_, segs.data(), segs.size(), false, s)) != CDB_OK) return st_;
+  if ((st_ = refs_to_batch(A)) != CDB_OK) return st_;
   ck(hipEventRecord(ev_.b, s), "event");
   ck(hipStreamSynchronize(s), "sync(decode)");
   if (st_ != CDB_OK) return st_;
@@ -537,7 +572,6 @@ cdb_status GpuDecode::emit_host(DecodeTiming* tm) {
     hipEventElapsedTime(&ms, ev_.a, ev_.b);
     tm->device_ms = ms;
   }
-  refs_to_batch(ko, kl, vo, vl, mo, ml, mvo, mvl);
   // the host tier's children, src fields made absolute
   for (const HostEntry& he : hosted_) {
     const Batch& r = he.rows;
@@ -582,14 +616,10 @@ cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint6
     A.nd[c] = nd[c];
     A.mb[c] = mb[c];
   }
-  A.kref_off = w; w += n;
-  A.kref_len = w; w += n;
-  A.vref_off = w; w += n;
-  A.vref_len = w; w += n;
-  A.mref_off = w; w += nm;
-  A.mref_len = w; w += nm;
-  A.mvref_off = w; w += nm;
-  A.mvref_len = w; w += nm;
+  A.kref = (ulonglong2*)w; w += 2 * n;
+  A.vref = (ulonglong2*)w; w += 2 * n;
+  A.mref = (ulonglong2*)w; w += 2 * nm;
+  A.mvref = (ulonglong2*)w; w += 2 * nm;
   A.pos = pos;
   emit_kernel<<<grid_, kDecThreads, 0, s>>>(A);
   ck(hipGetLastError(), "emit_kernel");
@@ -623,21 +653,7 @@ cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint6
   }
   if (!segs.empty() && (st_ = staged_copy(ctx_, segs.data(), segs.size(), true, s)) != CDB_OK) return st_;
   // the byte references down into the batch
-  ColVec ko, kl, vo, vl, mo, ml, mvo, mvl;
-  std::vector<HostSeg> dsegs;
-  auto down = [&](ColVec* v, const uint64_t* dev, uint64_t rows) {
-    v->resize(rows);
-    if (rows) dsegs.push_back({v->data(), const_cast<uint64_t*>(dev), rows * 8});
-  };
-  down(&ko, A.kref_off, n);
-  down(&kl, A.kref_len, n);
-  down(&vo, A.vref_off, n);
-  down(&vl, A.vref_len, n);
-  down(&mo, A.mref_off, nm);
-  down(&ml, A.mref_len, nm);
-  down(&mvo, A.mvref_off, nm);
-  down(&mvl, A.mvref_len, nm);
-  if ((st_ = staged_copy(ctx_, dsegs.data(), dsegs.size(), false, s)) != CDB_OK) return st_;
+  if ((st_ = refs_to_batch(A)) != CDB_OK) return st_;
   ck(hipEventRecord(ev_.b, s), "event");
   ck(hipStreamSynchronize(s), "sync(decode)");
   if (st_ != CDB_OK) return st_;
@@ -647,7 +663,8 @@ cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint6
     tm->device_ms = ms;
   }
   (void)nn;
-  return refs_to_batch(ko, kl, vo, vl, mo, ml, mvo, mvl);
+  return CDB_OK;
+
 }
 
 int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off,
@@ -666,12 +683,27 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
   std::vector<std::unique_ptr<GpuDecode>> dec;
   int rc_all = CDB_OK;
   uint64_t tot[3] = {0, 0, 0};
+  // the sequential host index passes of the snapshots run side by side (one thread each, at most
+  // 16 at once); their statuses are then taken in snapshot order, as one pass after another would
+  std::vector<int> irc(n, CDB_OK);
+  std::vector<size_t> ieo(n, 0);
+  for (uint32_t i = 0; i < n; ++i) dec.emplace_back(new GpuDecode(ctx, outs[i], flags));
+  {
+    const uint32_t nt = std::min<uint32_t>(n, 16);
+    std::atomic<uint32_t> next{0};
+    auto work = [&]() {
+      for (uint32_t i; (i = next.fetch_add(1)) < n;) irc[i] = dec[i]->index(bufs[i], lens[i], &ieo[i], nullptr);
+    };
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+  }
+  if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
   for (uint32_t i = 0; i < n; ++i) {
-    dec.emplace_back(new GpuDecode(ctx, outs[i], flags));
-    size_t eo = 0;
-    DecodeTiming t1;
-    const int rc = dec.back()->prepare(bufs[i], lens[i], &eo, &t1);
-    if (tm) tm->index_ms += t1.index_ms;
+    size_t eo = ieo[i];
+    int rc = irc[i];
+    if (rc == CDB_OK || rc == CDB_INVALID_SNAPSHOT_CHECKSUM) rc = dec[i]->prepare_device(&eo);
     if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) {
       *failed = i;
       *err_off = eo;
@@ -682,9 +714,9 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
       *failed = i;
       *err_off = eo;
     }
-    tot[0] += dec.back()->keys();
-    tot[1] += dec.back()->nodes();
-    tot[2] += dec.back()->members();
+    tot[0] += dec[i]->keys();
+    tot[1] += dec[i]->nodes();
+    tot[2] += dec[i]->members();
   }
   if (tot[0] >= (1ull << 32) || tot[1] >= (1ull << 32) || tot[2] >= (1ull << 32))
     return fail(ctx, CDB_BAD_ARGUMENT, "decoded rows exceed 2^32 per family");

@@ -105,6 +105,8 @@ struct CompactArgs {
   const unsigned long long* base_tot;  // dense rows already placed by the wave tier, per family
   uint64_t cap[3];                     // rows of each family's sparse slots and dense output
   uint32_t* err;                       // set when an index falls outside them
+  const uint32_t* skip_if;             // pipelined ranges: nothing to do once a bucket went to a
+                                       // workgroup tier (everything is compacted again at the end)
 };
 
 // Sparse-by-bucket outputs -> dense arrays; child ranges become absolute row indices.
@@ -236,7 +238,7 @@ __device__ __forceinline__ void compact_chunk(const CompactArgs& A, CompactLds& 
 __global__ void __launch_bounds__(kCompactWaves * 64) compact_kernel(CompactArgs A, uint32_t nbuckets) {
   __shared__ CompactLds lds_all[kCompactWaves];
   CompactLds& L = lds_all[threadIdx.x >> 6];
-  if (nbuckets == 0) return;
+  if (nbuckets == 0 || (A.skip_if && *A.skip_if)) return;
   const uint32_t n1 = nbuckets - 1;
   const uint64_t ck = (A.kdoff[n1] + A.kout[n1] + kCompactChunk - 1) / kCompactChunk;
   const uint64_t cn = (A.ndoff[n1] + A.nout[n1] + kCompactChunk - 1) / kCompactChunk;
@@ -972,6 +974,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   uint32_t* d_cerr = (uint32_t*)(misc + 104);   // zeroed with the misc header
   uint32_t* d_cerr_p = (uint32_t*)(misc + 108);  // the pipelined compaction's
   C.err = d_cerr;
+  C.skip_if = nullptr;
   uint64_t* d_pipe = nullptr;  // [P + 1][3] dense bases | [P][3] range totals
   static const bool wide_serial = std::getenv("CDB_WIDE_SERIAL") != nullptr;
   hipStream_t ws = wide_serial ? s : ctx->side;
@@ -1046,6 +1049,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
       Cp.kdoff += lo; Cp.ndoff += lo; Cp.mdoff += lo;
       Cp.base_tot = (const unsigned long long*)base;
       Cp.err = d_cerr_p;
+      Cp.skip_if = d_big_count;  // (pushed during this or an earlier range's merge)
       compact_kernel<<<1024, 64 * kCompactWaves, 0, cs>>>(Cp, nr_b);
       CDB_TRY(launch_check(ctx, cs, "compact_kernel"));
     }

@@ -7,7 +7,7 @@ cd $GRAFT_REPO_ROOT
 O=gpurun_out
 T=${TAG:-sweep}
 if [ -z "$NO_TESTS" ]; then
-timeout -k 10 700 python -u -m pytest ${FILES:-tests} -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_$T.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error|error" $O/pytest_$T.log | head -20; tail -5 $O/pytest_$T.log; exit 1; }
+timeout -k 10 700 python -u -m pytest ${FILES:-tests} -m gpu -x -v --timeout 150 --timeout-method thread > $O/pytest_$T.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error|error" $O/pytest_$T.log | head -20; tail -5 $O/pytest_$T.log; exit 1; }
 tail -1 $O/pytest_$T.log
 fi
 for v in ${VALS:-default}; do
