@@ -116,7 +116,7 @@ class BatchInfo(ctypes.Structure):
 
 class MergeOpts(ctypes.Structure):
     _fields_ = [("flags", ctypes.c_uint32), ("force_tier", ctypes.c_uint32), ("gc_watermark", ctypes.c_uint64),
-                ("key_shift", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("key_shift", ctypes.c_uint32), ("pipe_ranges", ctypes.c_uint32)]
 
 
 class MergeStats(ctypes.Structure):
@@ -577,12 +577,13 @@ class DB:
 
     def merge_batches(self, batches: Sequence[Batch], strict_dict_panic: bool = False,
                       gc_watermark: Optional[int] = None, gc_members: bool = False,
-                      force_tier: int = 0) -> Merged:
+                      force_tier: int = 0, pipe_ranges: int = 0) -> Merged:
         n = len(batches)
         arr = (ctypes.c_void_p * max(n, 1))(*[b.handle for b in batches])
         opts = MergeOpts()
         opts.flags = (MERGE_STRICT_DICT_PANIC if strict_dict_panic else 0)
         opts.force_tier = force_tier
+        opts.pipe_ranges = pipe_ranges
         if gc_watermark is not None:
             opts.flags |= MERGE_GC_DELETES | (MERGE_GC_MEMBERS if gc_members else 0)
             opts.gc_watermark = gc_watermark

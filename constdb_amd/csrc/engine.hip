@@ -954,7 +954,10 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     return e ? (uint32_t)std::max(1, std::atoi(e)) : 8u;
   }();
   // (small merges: the ranges' extra launches cost more than the overlap wins; C1 0.8 -> 1.6 ms)
-  const uint32_t P = (dense || wave_pf() != 0 || K + N + M < (64ull << 20) || nb < 64ull * pipe_env) ? 1 : pipe_env;
+  const uint32_t pipe_opt = opts ? opts->pipe_ranges : 0;
+  const uint32_t P = (dense || wave_pf() != 0) ? 1
+                     : pipe_opt ? (uint32_t)std::min<uint64_t>(pipe_opt, std::max<uint64_t>(nb, 1))
+                     : (K + N + M < (64ull << 20) || nb < 64ull * pipe_env) ? 1 : pipe_env;
   const bool pipelined = P > 1;
   CompactArgs C;
   C.ks = ksp[0];

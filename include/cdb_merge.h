@@ -144,7 +144,9 @@ typedef struct cdb_merge_opts {
   uint64_t gc_watermark; /* ReplicaManager::min_uuid (replica/replica.rs:87-89) */
   uint32_t key_shift;    /* multi-GPU: the top `key_shift` bits of every key hash are the owner
                             rank (all equal on one device), so local buckets use the bits below */
-  uint32_t reserved;
+  uint32_t pipe_ranges;  /* testing only: 0 = automatic (the bucket phase runs in 8 ranges, each
+                            compacted while the next merges, for merges of >= 64M rows); n >= 1 =
+                            exactly n ranges whatever the size */
 } cdb_merge_opts;
 
 typedef struct cdb_merge_stats {

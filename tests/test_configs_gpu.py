@@ -135,6 +135,18 @@ def test_c5_scaled_bit_exact(ctx, universe, events):
     assert m.stats.hot_buckets + m.stats.mid_buckets > 0
 
 
+def test_c5_pipelined_ranges_bit_exact(ctx):
+    """C5 with the bucket phase in 8 ranges (cdb_merge_opts.pipe_ranges; automatic only from 64M
+    rows): bit-exact against the oracle although the workgroup tiers add outputs after the ranges."""
+    cfg = configs.c5(cdb, universe=100_000, events=800_000)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(8)]
+    rc, want, ost = cdb_oracle.fold(snaps)
+    assert rc == 0
+    m = cdb.DB(ctx).merge_snapshots(snaps, pipe_ranges=8)
+    assert m.canonical_dump() == want
+    assert m.stats.hot_buckets + m.stats.mid_buckets > 0
+
+
 def test_c3_chip_wide_child_path_repeatable(ctx):
     """Every bucket of a C3 merge through the over-capacity tier (force_tier=2: key table, tag
     sort, per-run fold): bit-exact three times over. The tag sort keeps rows of one (key,
