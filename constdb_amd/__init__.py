@@ -201,7 +201,8 @@ ABI_FUNCTIONS = (
     "cdb_merged_free", "cdb_free",
     "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_partition_owner", "cdb_gen_default",
     "cdb_gen_snapshot", "cdb_gen_device", "cdb_decode_ops", "cdb_ops_info_get", "cdb_ops_free", "cdb_apply_ops", "cdb_gen_ops",
-    "cdb_encode_snapshot", "cdb_crc64_gpu", "cdb_upload_batches", "cdb_decode_snapshots_device")
+    "cdb_encode_snapshot", "cdb_crc64_gpu", "cdb_upload_batches", "cdb_decode_snapshots_device",
+    "cdb_decode_ops_gpu", "cdb_ops_column")
 
 _lib = None
 
@@ -249,6 +250,10 @@ def lib():
         "cdb_gen_device": (c_st, [vp, P(GenConfig), P(DevInput)]),
         "cdb_decode_ops": (c_st, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, P(vp), P(ctypes.c_size_t)]),
         "cdb_ops_info_get": (c_st, [vp, P(OpsInfo)]),
+        "cdb_decode_ops_gpu": (c_st, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, P(vp),
+                                      P(ctypes.c_size_t), P(ctypes.c_double), P(ctypes.c_double),
+                                      P(ctypes.c_uint32)]),
+        "cdb_ops_column": (c_st, [vp, ctypes.c_int, ctypes.c_int, P(P(ctypes.c_uint64)), P(ctypes.c_uint64)]),
         "cdb_ops_free": (None, [vp]),
         "cdb_gen_ops": (c_st, [P(GenConfig), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P(vp),
                                P(ctypes.c_size_t)]),
@@ -438,6 +443,19 @@ class Ops:
         lib().cdb_ops_info_get(self._h, ctypes.byref(i))
         return i
 
+    def column(self, family: int, col: int):
+        """A copy of one column as a numpy uint64 array (cdb_ops_column: byte references come as
+        (offset, length) pairs)."""
+        import numpy as np
+        data = ctypes.POINTER(ctypes.c_uint64)()
+        n = ctypes.c_uint64()
+        st = lib().cdb_ops_column(self._h, family, col, ctypes.byref(data), ctypes.byref(n))
+        if st != OK:
+            _raise(st)
+        if n.value == 0:
+            return np.zeros(0, dtype=np.uint64)
+        return np.ctypeslib.as_array(data, shape=(n.value,)).copy()
+
     def __del__(self):
         try:
             if self._h:
@@ -455,6 +473,26 @@ def decode_ops(data: bytes, uuid_he_sent: int, allow_partial: bool = False) -> O
     h = ctypes.c_void_p()
     off = ctypes.c_size_t()
     st = lib().cdb_decode_ops(None, bytes(data), len(data), uuid_he_sent, ctypes.byref(h), ctypes.byref(off))
+    if st == NEED_MORE_MSG and allow_partial and h:
+        return Ops(h, complete=False, consumed=off.value)
+    if st != OK:
+        if h:
+            lib().cdb_ops_free(h)
+        _raise(st, offset=off.value)
+    return Ops(h, consumed=len(data))
+
+
+def decode_ops_gpu(ctx: "Context", data: bytes, uuid_he_sent: int, allow_partial: bool = False,
+                   timing: Optional[dict] = None) -> Ops:
+    """cdb_decode_ops_gpu: the same decode with the per-message work on the GPU. timing (a dict)
+    receives host_ms, device_ms and used_gpu."""
+    h = ctypes.c_void_p()
+    off = ctypes.c_size_t()
+    hm, dm, ug = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint32()
+    st = lib().cdb_decode_ops_gpu(ctx.handle, bytes(data), len(data), uuid_he_sent, ctypes.byref(h), ctypes.byref(off),
+                                  ctypes.byref(hm), ctypes.byref(dm), ctypes.byref(ug))
+    if timing is not None:
+        timing.update(host_ms=hm.value, device_ms=dm.value, used_gpu=bool(ug.value))
     if st == NEED_MORE_MSG and allow_partial and h:
         return Ops(h, complete=False, consumed=off.value)
     if st != OK:

@@ -659,6 +659,60 @@ cdb_status cdb_decode_ops(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t
   return (cdb_status)rc;
 }
 
+cdb_status cdb_decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_he_sent, cdb_ops** out,
+                              size_t* err_offset, double* host_ms, double* device_ms, uint32_t* used_gpu) {
+  if (!ctx || !out || (!buf && len)) return CDB_BAD_ARGUMENT;
+  *out = nullptr;
+  if (host_ms) *host_ms = 0;
+  if (device_ms) *device_ms = 0;
+  if (used_gpu) *used_gpu = 1;
+  auto o = std::make_unique<cdb_ops>();
+  o->b = std::make_shared<Batch>();
+  size_t eo = 0;
+  int rc = CDB_OK;
+  if (decode_ops_gpu(ctx, buf, len, uuid_he_sent, o->b.get(), &o->info, &eo, &rc, host_ms, device_ms) != 0) {
+    // a shape the device path leaves to the host decoder: the whole stream goes there
+    (void)hipGetLastError();
+    if (used_gpu) *used_gpu = 0;
+    o->b = std::make_shared<Batch>();
+    const auto t0 = std::chrono::steady_clock::now();
+    rc = decode_ops(buf, len, uuid_he_sent, o->b.get(), &o->info, &eo);
+    if (host_ms) *host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  if (err_offset) *err_offset = eo;
+  if (rc == CDB_OK || rc == CDB_NEED_MORE_MSG) *out = o.release();
+  return (cdb_status)rc;
+}
+
+cdb_status cdb_ops_column(const cdb_ops* ops, int family, int col, const uint64_t** data, uint64_t* n) {
+  if (!ops || !data || !n) return CDB_BAD_ARGUMENT;
+  const Batch& b = *ops->b;
+  const ColVec* k[] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
+  const ColVec* nd[] = {&b.n_pkh, &b.n_pkf, &b.n_node, &b.n_v, &b.n_t, &b.n_meta};
+  const ColVec* mb[] = {&b.m_pkh, &b.m_pkf, &b.m_h, &b.m_f, &b.m_t, &b.m_meta};
+  const RefVec* r = nullptr;
+  const ColVec* v = nullptr;
+  if (family == 0 && col >= 0 && col < kKeyCols) v = k[col];
+  else if (family == 0 && col == kKeyCols) r = &b.key_ref;
+  else if (family == 0 && col == kKeyCols + 1) r = &b.val_ref;
+  else if (family == 1 && col >= 0 && col < kNodeCols) v = nd[col];
+  else if (family == 2 && col >= 0 && col < kMemberCols) v = mb[col];
+  else if (family == 2 && col == kMemberCols) r = &b.m_ref;
+  else if (family == 2 && col == kMemberCols + 1) r = &b.m_vref;
+  if (v) {
+    *data = v->data();
+    *n = v->size();
+    return CDB_OK;
+  }
+  if (r) {
+    static_assert(sizeof(ByteRef) == 16, "(offset, length) pairs");
+    *data = reinterpret_cast<const uint64_t*>(r->data());
+    *n = 2 * r->size();
+    return CDB_OK;
+  }
+  return CDB_BAD_ARGUMENT;
+}
+
 cdb_status cdb_ops_info_get(const cdb_ops* ops, cdb_ops_info* info) {
   if (!ops || !info) return CDB_BAD_ARGUMENT;
   *info = ops->info;

@@ -35,6 +35,12 @@ enum OpCode : uint32_t {
 int decode_ops(const uint8_t* buf, size_t len, uint64_t uuid_he_sent, Batch* out, cdb_ops_info* info,
                size_t* err_off);
 
+// The same decode with the per-message work on the GPU (ops_gpu.hip). Returns 1 when the
+// stream needs decode_ops instead (rare shapes, or a device failure); otherwise 0 with the
+// decode's status in *rc (CDB_OK, CDB_NEED_MORE_MSG or CDB_INVALID_REQUEST_MSG).
+int decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_he_sent, Batch* out,
+                   cdb_ops_info* info, size_t* err_off, int* rc, double* host_ms, double* device_ms);
+
 // Device apply (ops_apply.hip): state = merge-result columns (host), ops = the op batch at fold
 // position pos_ops; out = merge-result columns (host).
 cdb_status apply_ops_impl(cdb_ctx* ctx, const ColVec* sk, const ColVec* sn, const ColVec* sm, const Batch& ops, uint32_t pos_ops,

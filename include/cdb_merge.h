@@ -274,6 +274,23 @@ typedef struct cdb_ops_info {
 } cdb_ops_info;
 cdb_status cdb_decode_ops(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_he_sent, cdb_ops** out,
                           size_t* err_offset);
+/* The same decode with the per-message work on the GPU (the framing being replaced
+ * is conn/buf_read.rs:102-111): every '*' at a line start is a candidate message start, one
+ * thread per candidate parses the RESP value there, the host follows the chain of sizes from
+ * byte 0 (candidates inside bulk payloads are never reached), one thread per message decodes
+ * pull.rs:184-235 up to the uuid gate and the handler's arguments, the host runs the gate
+ * (sequential: it carries uuid_he_sent), and one thread per applied op writes its rows and
+ * hashes. The result equals cdb_decode_ops's field for field, statuses and offsets included.
+ * Streams the device path leaves to the host (an integer argument whose decimal form differs
+ * from its digits, top-level values that are not arrays, nesting deeper than 16) are decoded by
+ * cdb_decode_ops; *used_gpu (may be NULL) tells which ran. *host_ms / *device_ms (may be NULL):
+ * the host part (chain walk, gate, arena copy) and the rest of the call. */
+cdb_status cdb_decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_he_sent, cdb_ops** out,
+                              size_t* err_offset, double* host_ms, double* device_ms, uint32_t* used_gpu);
+/* Read-only view of one column of a decoded op stream (family 0: kh kf ct ut dt aux meta, then
+ * key_ref and val_ref as (offset, length) pairs; 1: pkh pkf node v t meta; 2: pkh pkf mh mf t meta,
+ * then m_ref and m_vref as pairs). *n counts u64 words. */
+cdb_status cdb_ops_column(const cdb_ops* ops, int family, int col, const uint64_t** data, uint64_t* n);
 cdb_status cdb_ops_info_get(const cdb_ops* ops, cdb_ops_info* info);
 void cdb_ops_free(cdb_ops* ops);
 
