@@ -202,7 +202,7 @@ ABI_FUNCTIONS = (
     "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_partition_owner", "cdb_gen_default",
     "cdb_gen_snapshot", "cdb_gen_device", "cdb_decode_ops", "cdb_ops_info_get", "cdb_ops_free", "cdb_apply_ops", "cdb_gen_ops",
     "cdb_encode_snapshot", "cdb_crc64_gpu", "cdb_upload_batches", "cdb_decode_snapshots_device",
-    "cdb_decode_ops_gpu", "cdb_ops_column")
+    "cdb_decode_ops_gpu", "cdb_ops_column", "cdb_snapshot_index_selftest")
 
 _lib = None
 
@@ -254,6 +254,8 @@ def lib():
                                       P(ctypes.c_size_t), P(ctypes.c_double), P(ctypes.c_double),
                                       P(ctypes.c_uint32)]),
         "cdb_ops_column": (c_st, [vp, ctypes.c_int, ctypes.c_int, P(P(ctypes.c_uint64)), P(ctypes.c_uint64)]),
+        "cdb_snapshot_index_selftest": (c_st, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+                                               P(ctypes.c_uint64)]),
         "cdb_ops_free": (None, [vp]),
         "cdb_gen_ops": (c_st, [P(GenConfig), ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, P(vp),
                                P(ctypes.c_size_t)]),

@@ -94,8 +94,10 @@ struct DeferredCrc {
 };
 // With `crc` non-null and at least one entry indexed, the checksum is not computed here but
 // described in *crc for the caller to check.
+// threads > 1: a large DATAS section is indexed by that many threads (speculative sync points,
+// stitched in order; the result is the sequential pass's, entry for entry).
 int index_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, EntryIndex* idx, size_t* err_off,
-                   DeferredCrc* crc = nullptr);
+                   DeferredCrc* crc = nullptr, uint32_t threads = 1);
 struct DecodeTiming {
   double index_ms = 0;   // host pass
   double device_ms = 0;  // uploads, both kernels, downloads (HIP events)

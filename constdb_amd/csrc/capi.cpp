@@ -684,6 +684,30 @@ cdb_status cdb_decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint
   return (cdb_status)rc;
 }
 
+cdb_status cdb_snapshot_index_selftest(const uint8_t* buf, size_t len, uint32_t flags, uint32_t threads,
+                                       uint64_t* entries) {
+  Batch b1, b2;
+  EntryIndex i1, i2;
+  DeferredCrc c1, c2;
+  size_t e1 = 0, e2 = 0;
+  const int r1 = index_snapshot(buf, len, flags, &b1, &i1, &e1, &c1, 1);
+  const int r2 = index_snapshot(buf, len, flags, &b2, &i2, &e2, &c2, threads);
+  if (entries) *entries = i1.offset.size();
+  const bool same = r1 == r2 && e1 == e2 && i1.offset == i2.offset && i1.kind == i2.kind && c1.pending == c2.pending &&
+                    c1.len == c2.len && c1.got == c2.got && c1.err_off == c2.err_off && b1.n_data == b2.n_data &&
+                    b1.n_expires == b2.n_expires && b1.n_deletes == b2.n_deletes;
+  if (!same && std::getenv("CDB_SELFTEST_VERBOSE")) {
+    size_t k = 0;
+    while (k < i1.offset.size() && k < i2.offset.size() && i1.offset[k] == i2.offset[k] && i1.kind[k] == i2.kind[k]) ++k;
+    fprintf(stderr, "selftest: rc %d/%d err %zu/%zu entries %zu/%zu first diff %zu (%llu/%llu) data %llu/%llu crc %d/%d %llu/%llu\n",
+            r1, r2, e1, e2, i1.offset.size(), i2.offset.size(), k,
+            (unsigned long long)(k < i1.offset.size() ? i1.offset[k] : 0), (unsigned long long)(k < i2.offset.size() ? i2.offset[k] : 0),
+            (unsigned long long)b1.n_data, (unsigned long long)b2.n_data, (int)c1.pending, (int)c2.pending,
+            (unsigned long long)c1.len, (unsigned long long)c2.len);
+  }
+  return same ? CDB_OK : CDB_DEVICE_ERROR;
+}
+
 cdb_status cdb_ops_column(const cdb_ops* ops, int family, int col, const uint64_t** data, uint64_t* n) {
   if (!ops || !data || !n) return CDB_BAD_ARGUMENT;
   const Batch& b = *ops->b;

@@ -5,7 +5,12 @@
 // from one in-memory buffer in a single pass (the reference issues one awaited
 // read_exact per varint flag byte and CRCs byte-slices as it goes) and emits SoA rows.
 #include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
+#include <vector>
 
 #include "../../include/cdb_merge.h"
 #include "batch.h"
@@ -139,6 +144,11 @@ struct Decoder {
   const uint8_t* base;
   EntryIndex* idx = nullptr;  // index mode (GPU decode): validate and record, no rows
   DeferredCrc* dcrc = nullptr;  // index mode: leave the checksum to the GPU
+  uint32_t threads = 1;         // index mode: threads for a large DATAS section (parallel_datas)
+  bool speculative = false;     // parallel_datas' walks: counts the rest of the stream cannot hold
+                                // fail at once (the sequential pass reports those streams)
+
+  bool parallel_datas(uint64_t cnt);
 
   bool str(std::string* s) {
     ByteRef r;
@@ -156,6 +166,7 @@ struct Decoder {
   bool counter(uint64_t kh, uint64_t kf, uint64_t* total) {
     uint64_t cnt;
     if (!c.length(&cnt)) return false;
+    if (speculative && cnt > (c.n - c.off) / 3) return false;  // 3 varints of >= 1 byte each
     if (idx) {  // index mode: skip the triples, the GPU parses them
       for (uint64_t i = 0; i < cnt; ++i) {
         uint64_t x;
@@ -209,12 +220,14 @@ struct Decoder {
     std::vector<Op> ops;
     uint64_t na;
     if (!c.length(&na)) return false;
+    if (speculative && na > (c.n - c.off) / 2) return false;  // a span and a varint each
     if (idx) {  // index mode: skip the tags, the GPU parses them
       ByteRef r;
       uint64_t t, nd;
       for (uint64_t i = 0; i < na; ++i)
         if (!c.span(&r) || !c.u64(&t) || (is_dict && !c.span(&r))) return false;
       if (!c.length(&nd)) return false;
+      if (speculative && nd > (c.n - c.off) / 2) return false;
       for (uint64_t i = 0; i < nd; ++i)
         if (!c.span(&r) || !c.u64(&t)) return false;
       return true;
@@ -371,6 +384,10 @@ struct Decoder {
       } else if (flag == 5 || flag == 6 || flag == 7) {  // DATAS / EXPIRES / DELETES
         uint64_t cnt;
         if (!c.length(&cnt)) return fail();
+        if (flag == 5 && idx && parallel_datas(cnt)) {  // indexed side by side (c.off at its end)
+          b->n_data += cnt;
+          continue;
+        }
         for (uint64_t i = 0; i < cnt; ++i) {
           bool ok = flag == 5 ? data_entry() : side_entry(flag == 6 ? TAG_EXPIRE : TAG_DELETE);
           if (!ok) return fail();
@@ -419,6 +436,141 @@ struct Decoder {
   }
 };
 
+// The DATAS section of a large snapshot, indexed by several threads. The format has no sync
+// marks (an entry starts where its predecessor ends), so each thread speculates:
+//   * thread t's range starts at a byte offset B_t; it looks for the first offset o >= B_t from
+//     which kSyncEntries consecutive entries parse (data entries have a tag byte that must be
+//     0, 3, 4 or 5, and every span must fit: a wrong offset almost never survives 16 of them),
+//     then records the entries from o until one starts at or past B_{t+1};
+//   * stitching, in order: the true chain enters range t at `cur` (range 0: the section start).
+//     Parsing is deterministic from an offset, so if cur is one of thread t's recorded offsets,
+//     thread t's entries from there on ARE the true chain; otherwise range t is parsed again from
+//     cur on this thread. The section ends after `cnt` entries (later ranges parsed the next
+//     sections' bytes as data entries: discarded).
+// Any error on the true chain, or a thread that gave up, hands the whole section back to the
+// sequential loop (false), so statuses and offsets stay the loader's.
+constexpr uint32_t kSyncEntries = 16;
+constexpr uint64_t kParallelMinEntries = 1u << 17;
+constexpr uint64_t kSyncSearch = 1u << 20;  // bytes a thread searches for its first entry
+constexpr uint64_t kSyncEntryMax = 1u << 16; // largest entry a sync chain may hold
+
+bool Decoder::parallel_datas(uint64_t cnt) {
+  const uint64_t S = c.off, end = c.n;
+  if (threads < 2 || cnt < kParallelMinEntries || end - S < (uint64_t)threads * 4096) return false;
+  const uint32_t T = threads;
+  std::vector<uint64_t> B(T + 1);
+  for (uint32_t t = 0; t <= T; ++t) B[t] = S + (end - S) * t / T;
+  struct Part {
+    std::vector<uint64_t> off;
+    uint64_t stop = 0;     // offset of the first entry at or past the range end (or of the failure)
+    bool ok = false;       // reached the range end without a parse error
+  };
+  std::vector<Part> parts(T);
+  auto walk = [&](uint64_t from, uint64_t lim, Part& P) {  // entries from `from` up to lim
+    Decoder d{Cursor{base, end}, b, base};
+    EntryIndex scratch;
+    d.idx = &scratch;
+    d.speculative = true;
+    d.c.off = from;
+    P.off.clear();
+    P.off.reserve((lim - from) / 40 + 16);
+    while (d.c.off < lim) {
+      const uint64_t at = d.c.off;
+      scratch.offset.clear();
+      scratch.kind.clear();
+      if (!d.data_entry()) {
+        P.stop = at;
+        P.ok = false;
+        return;
+      }
+      P.off.push_back(at);
+    }
+    P.stop = d.c.off;
+    P.ok = true;
+  };
+  auto work = [&](uint32_t t) {
+    Part& P = parts[t];
+    uint64_t o = B[t];
+    if (t > 0) {  // speculative sync point
+      Decoder d{Cursor{base, end}, b, base};
+      EntryIndex scratch;
+      d.idx = &scratch;
+      d.speculative = true;
+      const uint64_t last = std::min(end, B[t] + kSyncSearch);
+      for (; o < last; ++o) {
+        d.c.off = o;
+        d.c.err = CDB_OK;
+        uint32_t k = 0;
+        for (; k < kSyncEntries && d.c.off < end; ++k) {
+          scratch.offset.clear();
+          scratch.kind.clear();
+          const uint64_t at = d.c.off;
+          // (a wrong offset can read a huge "length" that still fits the stream and land on true
+          // entries after it: sync points only come from chains of small entries)
+          if (!d.data_entry() || d.c.off - at > kSyncEntryMax) break;
+        }
+        if (k == kSyncEntries) break;
+      }
+      if (o >= last) {
+        P.ok = false;
+        P.stop = B[t];
+        return;
+      }
+    }
+    walk(o, B[t + 1], P);
+  };
+  {
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < T; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+  }
+  if (std::getenv("CDB_SELFTEST_VERBOSE"))
+    for (uint32_t t = 0; t < T; ++t)
+      fprintf(stderr, "part %u: B %llu ok %d n %zu first %llu stop %llu\n", t, (unsigned long long)B[t], (int)parts[t].ok,
+              parts[t].off.size(), (unsigned long long)(parts[t].off.empty() ? 0 : parts[t].off[0]),
+              (unsigned long long)parts[t].stop);
+  // stitch
+  const size_t base_n = idx->offset.size();
+  idx->offset.reserve(base_n + cnt);
+  idx->kind.reserve(base_n + cnt);
+  auto rollback = [&]() {
+    idx->offset.resize(base_n);
+    idx->kind.resize(base_n);
+    return false;
+  };
+  uint64_t cur = S, got = 0;
+  for (uint32_t t = 0; t < T && got < cnt; ++t) {
+    Part& P = parts[t];
+    auto it = std::lower_bound(P.off.begin(), P.off.end(), cur);
+    if (it == P.off.end() || *it != cur) {  // the true chain is not thread t's: parse again from cur
+      Part R;
+      walk(cur, std::max(cur, B[t + 1]), R);
+      P = std::move(R);
+      it = P.off.begin();
+    }
+    // entries parsed before a failure are the chain's (parsing is deterministic from an offset);
+    // the failure itself matters only if the section needs entries past it
+    for (; it != P.off.end() && got < cnt; ++it, ++got) {
+      idx->offset.push_back(*it);
+      idx->kind.push_back(0);
+    }
+    if (got < cnt) {
+      if (!P.ok) return rollback();  // an error on the true chain: the sequential loop reports it
+      cur = P.stop;
+    }
+  }
+  if (got < cnt) return rollback();  // (the stream ended first: the sequential loop reports where)
+  // the section ends after its last entry: parse that entry again for its end offset
+  Decoder d{Cursor{base, end}, b, base};
+  EntryIndex scratch;
+  d.idx = &scratch;
+  d.c.off = idx->offset.back();
+  if (!d.data_entry()) return rollback();
+  c.off = d.c.off;
+  return true;
+}
+
 }  // namespace
 
 int decode_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off) {
@@ -429,11 +581,12 @@ int decode_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, 
 }
 
 int index_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, EntryIndex* idx, size_t* err_off,
-                   DeferredCrc* crc) {
+                   DeferredCrc* crc, uint32_t threads) {
   adopt_raw(out, buf, len);
   Decoder d{Cursor{out->raw.data(), out->raw.size()}, out, out->raw.data()};
   d.idx = idx;
   d.dcrc = crc;
+  d.threads = threads;
   idx->offset.reserve(len / 48 + 16);  // generator-shaped streams run ~58 bytes per entry
   idx->kind.reserve(len / 48 + 16);
   *err_off = 0;

@@ -22,6 +22,7 @@
 #include <atomic>
 #include <chrono>
 #include <thread>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -334,6 +335,7 @@ class GpuDecode {
   uint64_t keys() const { return n_; }
   uint64_t nodes() const { return nn_; }
   uint64_t members() const { return nm_; }
+  uint32_t index_threads_ = 1;  // threads of the host index pass's DATAS section
 
  private:
   struct HostEntry {
@@ -373,7 +375,7 @@ class GpuDecode {
 
 int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTiming* tm) {
   const auto t0 = std::chrono::steady_clock::now();
-  rc_ = index_snapshot(buf, len, flags_, out_, &idx_, err_off, &dcrc_);
+  rc_ = index_snapshot(buf, len, flags_, out_, &idx_, err_off, &dcrc_, index_threads_);
   if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return rc_;
 }
@@ -667,9 +669,19 @@ cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint6
 
 }
 
+uint32_t host_index_threads() {
+  static const uint32_t t = [] {
+    const char* e = std::getenv("CDB_INDEX_THREADS");
+    const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+    return e ? (uint32_t)std::max(1, std::atoi(e)) : std::min(16u, hw);
+  }();
+  return t;
+}
+
 int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off,
                         DecodeTiming* tm) {
   GpuDecode d(ctx, out, flags);
+  d.index_threads_ = host_index_threads();
   const int rc = d.prepare(buf, len, err_off, tm);
   if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) return rc;
   const cdb_status st = d.emit_host(tm);
@@ -687,7 +699,10 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
   // 16 at once); their statuses are then taken in snapshot order, as one pass after another would
   std::vector<int> irc(n, CDB_OK);
   std::vector<size_t> ieo(n, 0);
-  for (uint32_t i = 0; i < n; ++i) dec.emplace_back(new GpuDecode(ctx, outs[i], flags));
+  for (uint32_t i = 0; i < n; ++i) {
+    dec.emplace_back(new GpuDecode(ctx, outs[i], flags));
+    dec.back()->index_threads_ = std::max(1u, host_index_threads() / std::max(1u, n));  // (threads left over)
+  }
   {
     const uint32_t nt = std::min<uint32_t>(n, 16);
     std::atomic<uint32_t> next{0};

@@ -292,6 +292,12 @@ cdb_status cdb_decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint
  * then m_ref and m_vref as pairs). *n counts u64 words. */
 cdb_status cdb_ops_column(const cdb_ops* ops, int family, int col, const uint64_t** data, uint64_t* n);
 cdb_status cdb_ops_info_get(const cdb_ops* ops, cdb_ops_info* info);
+/* Testing only (no device needed): the GPU decode's host index pass with a large DATAS section
+ * split over `threads` threads (speculative sync points, stitched in order) against the
+ * sequential pass: CDB_OK when status, error offset, entry offsets and kinds, section counts
+ * and the deferred checksum are identical. *entries = the entries indexed. */
+cdb_status cdb_snapshot_index_selftest(const uint8_t* buf, size_t len, uint32_t flags, uint32_t threads,
+                                       uint64_t* entries);
 void cdb_ops_free(cdb_ops* ops);
 
 typedef struct cdb_apply_stats {
