@@ -6,6 +6,7 @@
 // read_exact per varint flag byte and CRCs byte-slices as it goes) and emits SoA rows.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -147,6 +148,7 @@ struct Decoder {
   uint32_t threads = 1;         // index mode: threads for a large DATAS section (parallel_datas)
   bool speculative = false;     // parallel_datas' walks: counts the rest of the stream cannot hold
                                 // fail at once (the sequential pass reports those streams)
+  uint64_t spec_max = ~0ull;    // ... and, in the sync search, counts past this many bytes
 
   bool parallel_datas(uint64_t cnt);
 
@@ -166,7 +168,7 @@ struct Decoder {
   bool counter(uint64_t kh, uint64_t kf, uint64_t* total) {
     uint64_t cnt;
     if (!c.length(&cnt)) return false;
-    if (speculative && cnt > (c.n - c.off) / 3) return false;  // 3 varints of >= 1 byte each
+    if (speculative && cnt > std::min<uint64_t>(c.n - c.off, spec_max) / 3) return false;  // 3 varints of >= 1 byte
     if (idx) {  // index mode: skip the triples, the GPU parses them
       for (uint64_t i = 0; i < cnt; ++i) {
         uint64_t x;
@@ -220,14 +222,14 @@ struct Decoder {
     std::vector<Op> ops;
     uint64_t na;
     if (!c.length(&na)) return false;
-    if (speculative && na > (c.n - c.off) / 2) return false;  // a span and a varint each
+    if (speculative && na > std::min<uint64_t>(c.n - c.off, spec_max) / 2) return false;  // a span and a varint
     if (idx) {  // index mode: skip the tags, the GPU parses them
       ByteRef r;
       uint64_t t, nd;
       for (uint64_t i = 0; i < na; ++i)
         if (!c.span(&r) || !c.u64(&t) || (is_dict && !c.span(&r))) return false;
       if (!c.length(&nd)) return false;
-      if (speculative && nd > (c.n - c.off) / 2) return false;
+      if (speculative && nd > std::min<uint64_t>(c.n - c.off, spec_max) / 2) return false;
       for (uint64_t i = 0; i < nd; ++i)
         if (!c.span(&r) || !c.u64(&t)) return false;
       return true;
@@ -300,6 +302,7 @@ struct Decoder {
     }
     ByteRef k;
     if (!c.span(&k)) return false;
+    if (speculative && k.len > spec_max) return false;
     uint64_t ct, ut, dt;
     if (!c.u64(&ct) || !c.u64(&ut) || !c.u64(&dt)) return false;
     uint8_t tag;
@@ -496,6 +499,7 @@ bool Decoder::parallel_datas(uint64_t cnt) {
       EntryIndex scratch;
       d.idx = &scratch;
       d.speculative = true;
+      d.spec_max = kSyncEntryMax;
       const uint64_t last = std::min(end, B[t] + kSyncSearch);
       for (; o < last; ++o) {
         d.c.off = o;
@@ -519,12 +523,14 @@ bool Decoder::parallel_datas(uint64_t cnt) {
     }
     walk(o, B[t + 1], P);
   };
+  const auto tp0 = std::chrono::steady_clock::now();
   {
     std::vector<std::thread> th;
     for (uint32_t t = 1; t < T; ++t) th.emplace_back(work, t);
     work(0);
     for (auto& x : th) x.join();
   }
+  const auto tp1 = std::chrono::steady_clock::now();
   if (std::getenv("CDB_SELFTEST_VERBOSE"))
     for (uint32_t t = 0; t < T; ++t)
       fprintf(stderr, "part %u: B %llu ok %d n %zu first %llu stop %llu\n", t, (unsigned long long)B[t], (int)parts[t].ok,
@@ -540,34 +546,54 @@ bool Decoder::parallel_datas(uint64_t cnt) {
     return false;
   };
   uint64_t cur = S, got = 0;
+  uint32_t rewalks = 0;
+  Decoder d{Cursor{base, end}, b, base};  // entries the threads' chains do not hold
+  EntryIndex scratch;
+  d.idx = &scratch;
+  d.speculative = true;
   for (uint32_t t = 0; t < T && got < cnt; ++t) {
     Part& P = parts[t];
-    auto it = std::lower_bound(P.off.begin(), P.off.end(), cur);
-    if (it == P.off.end() || *it != cur) {  // the true chain is not thread t's: parse again from cur
-      Part R;
-      walk(cur, std::max(cur, B[t + 1]), R);
-      P = std::move(R);
-      it = P.off.begin();
-    }
-    // entries parsed before a failure are the chain's (parsing is deterministic from an offset);
-    // the failure itself matters only if the section needs entries past it
-    for (; it != P.off.end() && got < cnt; ++it, ++got) {
-      idx->offset.push_back(*it);
+    // a speculative chain either is the true one or joins it within a few entries (parsing
+    // from a shared offset is deterministic): entries from cur are parsed here until they reach
+    // an offset thread t recorded, then thread t's entries are taken from there
+    auto join = std::lower_bound(P.off.begin(), P.off.end(), cur);
+    bool walked = false;
+    while (got < cnt && cur < B[t + 1] && !(join != P.off.end() && *join == cur)) {
+      scratch.offset.clear();
+      scratch.kind.clear();
+      d.c.off = cur;
+      if (!d.data_entry()) return rollback();  // an error on the true chain: the sequential loop reports it
+      idx->offset.push_back(cur);
       idx->kind.push_back(0);
+      ++got;
+      cur = d.c.off;
+      walked = true;
+      while (join != P.off.end() && *join < cur) ++join;
     }
+    rewalks += walked;
+    if (got >= cnt || join == P.off.end() || *join != cur) continue;  // (cur left range t)
+    const uint64_t take = std::min<uint64_t>((uint64_t)(P.off.end() - join), cnt - got);
+    idx->offset.insert(idx->offset.end(), join, join + take);
+    idx->kind.resize(idx->kind.size() + take, 0);
+    got += take;
     if (got < cnt) {
-      if (!P.ok) return rollback();  // an error on the true chain: the sequential loop reports it
+      if (!P.ok) return rollback();  // thread t's chain (the true one) failed there
       cur = P.stop;
     }
   }
   if (got < cnt) return rollback();  // (the stream ended first: the sequential loop reports where)
+  if (std::getenv("CDB_SELFTEST_TIMING"))
+    fprintf(stderr, "parallel_datas: %u threads %.1f ms, stitch %.1f ms (%u ranges parsed again), %llu entries\n", T,
+            std::chrono::duration<double, std::milli>(tp1 - tp0).count(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp1).count(), rewalks,
+            (unsigned long long)cnt);
   // the section ends after its last entry: parse that entry again for its end offset
-  Decoder d{Cursor{base, end}, b, base};
-  EntryIndex scratch;
-  d.idx = &scratch;
-  d.c.off = idx->offset.back();
-  if (!d.data_entry()) return rollback();
-  c.off = d.c.off;
+  Decoder e{Cursor{base, end}, b, base};
+  EntryIndex last;
+  e.idx = &last;
+  e.c.off = idx->offset.back();
+  if (!e.data_entry()) return rollback();
+  c.off = e.c.off;
   return true;
 }
 
