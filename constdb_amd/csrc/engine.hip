@@ -292,12 +292,22 @@ int aos_tile() {
 }
 
 Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
-  // Wave-sized buckets: ~40 key rows and ~40 child rows (nodes + members) on average.
+  // Wave-sized buckets: ~40 key rows and at most ~80 child rows (nodes + members) on average.
   // A wave holds 64 key rows (128 in the wide kernel) and 128 child rows, so only the
-  // far tail of the bucket-size distribution reaches the workgroup tier.
-  uint64_t target = 40;
+  // far tail of the bucket-size distribution reaches the workgroup tier. A key's children never
+  // split across buckets, so when keys own many children each (more than 8 on average, as in C3:
+  // ~300 member rows per key) wave-sized buckets cannot hold them and the wave kernels mostly
+  // pass them on: such inputs get a few thousand large buckets instead, all merged by the
+  // chip-wide child path (key table, tag sort, per-run fold). Measured C3 ms/step by child
+  // target (key target 40): 40 22.0, 120 18.3, 240 16.1, 520 13.4, 1024 11.2, 4096 8.7; with key
+  // target 120 as well, 4096 8.3. C5 (2 children per key) by child target: 40 26.0, 80 24.0,
+  // 160-240 24.0 (key-bound); C1 and C4 have fewer children than keys and are key-bound.
+  const bool child_heavy = N + M > 8 * K;
+  uint64_t target = child_heavy ? 120 : 40;
   if (const char* e = std::getenv("CDB_PLAN_TARGET")) target = (uint64_t)std::max(8, std::min(120, std::atoi(e)));
-  const uint64_t want = std::max<uint64_t>({(K + target - 1) / target, (N + M + target - 1) / target, 1});
+  uint64_t ctarget = child_heavy ? 4096 : std::max<uint64_t>(target, 80);
+  if (const char* e = std::getenv("CDB_PLAN_CTARGET")) ctarget = (uint64_t)std::max(8, std::min(65536, std::atoi(e)));
+  const uint64_t want = std::max<uint64_t>({(K + target - 1) / target, (N + M + ctarget - 1) / ctarget, 1});
   Plan p;
   // The last level moves only a row index, so it takes a large fan-out (segments of
   // ~d_last buckets, a few hundred KB, stay cache-resident for the bucket kernels' gathers)

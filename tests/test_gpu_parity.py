@@ -182,15 +182,28 @@ def test_wave_tiers_natural(db):
     assert m3.stats.wide_buckets > m.stats.wide_buckets
 
 
-@pytest.mark.parametrize("tier", [0, 3])
-def test_wide_children(db, tier):
-    """Set/dict keys with up to 8 x 24 member rows: buckets of 129..256 child rows take the
-    wide kernel's four-rows-per-lane path."""
+def _wide_children_snaps():
     cfg = cdb.gen_config(seed=33, universe=30000, n_replicas=8, replica_hi=8, mix_bytes=10, mix_counter=10,
                          mix_set=40, mix_dict=40, mean_members=12, member_universe=24, del_permille=300)
-    snaps = [cdb.gen_snapshot(cfg, r) for r in range(8)]
-    m = _check(db, snaps, tier=tier)
+    return [cdb.gen_snapshot(cfg, r) for r in range(8)]
+
+
+@pytest.mark.parametrize("tier", [0, 3])
+def test_wide_children(db, tier, monkeypatch):
+    """Set/dict keys with up to 8 x 24 member rows: buckets of 129..256 child rows take the
+    wide kernel's four-rows-per-lane path. (More than 8 children per key: the default plan
+    makes large buckets for the chip-wide child path, so wave-sized ones are asked for here.)"""
+    monkeypatch.setenv("CDB_PLAN_TARGET", "40")
+    monkeypatch.setenv("CDB_PLAN_CTARGET", "80")
+    m = _check(db, _wide_children_snaps(), tier=tier)
     assert m.stats.wide_buckets > 0
+
+
+def test_child_heavy_default_plan(db):
+    """The same input under the default plan for child-heavy inputs (make_plan, engine.hip):
+    a few large buckets, merged by the over-capacity tiers."""
+    m = _check(db, _wide_children_snaps())
+    assert m.stats.mid_buckets + m.stats.hot_buckets > 0
 
 
 def test_generator_set_heavy_gc(db):
