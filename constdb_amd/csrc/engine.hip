@@ -610,13 +610,14 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   std::vector<uint32_t> wide_ids, legacy;  // wide: the chip-wide child path
   std::vector<uint32_t> hk_off(1, 0), c_off(1, 0);
   std::vector<uint32_t> lk, ln, lm;
-  uint64_t tk = 0, tc = 0;
+  uint64_t tk = 0, tc = 0, cmax = 0;
   for (uint32_t i : order) {
     const uint32_t K = cnt3[3 * i], N = cnt3[3 * i + 1], M = cnt3[3 * i + 2];
     if (!legacy_all && K <= (uint32_t)kCapK && tk + K < (1ull << 23) && tc + N + M < (1ull << 32)) {
       wide_ids.push_back(ids[i]);
       tk += K;
       tc += N + M;
+      cmax = std::max<uint64_t>(cmax, N + M);
       hk_off.push_back((uint32_t)tk);
       c_off.push_back((uint32_t)tc);
     } else {
@@ -665,11 +666,25 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   HA.h_first = HA.hk_kout + H;
   HA.H = H;
   HA.n_children = tc;
-  HA.id_shift = 30;
+  // Tag layout W = G << g_shift | id hash bits << 6 | pos, sorted on g_shift + gbits bits in 8-bit
+  // passes. The id bits only separate a key's children: ids sharing them take the successor-
+  // selection fold (exact, but slow for long runs), so a bucket of c children gets at least
+  // log2(c) + 9 of them (about c / 1024 rows sharing), and where fewer than 34 bits reach the
+  // next pass boundary they save whole passes: C3 (buckets of a few thousand children, a
+  // 400K-key table) sorts in 6 passes instead of 8; C5's hottest keys keep all 34.
+  int gbits = 0, cbits = 0;
+  while (gbits < 32 && (tk >> gbits)) ++gbits;
+  while (cbits < 40 && (cmax >> cbits)) ++cbits;
+  int min_id = std::max(kHotMinIdBits, cbits + 9);
+  if (const char* e = std::getenv("CDB_HOT_MIN_ID_BITS")) min_id = std::max(1, std::atoi(e));
+  const int passes = (gbits + 6 + std::min(min_id, kHotIdBits - 6) + 7) / 8;
+  int id_bits = std::min(kHotIdBits - 6, 8 * passes - 6 - gbits);
   if (const char* e = std::getenv("CDB_HOT_ID_BITS")) {  // tests: fewer id bits force the collision path
     const int bits = std::atoi(e);
-    if (bits >= 1 && bits <= 34) HA.id_shift = 64 - bits;
+    if (bits >= 1 && bits <= kHotIdBits - 6) id_bits = bits;
   }
+  HA.g_shift = 6 + id_bits;
+  HA.id_shift = 64 - id_bits;
   CDB_HIP(hipMemcpyAsync(d_ids, wide_ids.data(), H * 4, hipMemcpyHostToDevice, s), "h2d");
   CDB_HIP(hipMemcpyAsync(d_hk_off, hk_off.data(), (H + 1) * 4, hipMemcpyHostToDevice, s), "h2d");
   CDB_HIP(hipMemcpyAsync(d_c_off, c_off.data(), (H + 1) * 4, hipMemcpyHostToDevice, s), "h2d");
@@ -705,9 +720,7 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   if (tc) {
     hot_tag_kernel<<<grid, 256, 0, s>>>(A, HA);
     CDB_TRY(launch_check(ctx, s, "hot_tag_kernel"));
-    int gbits = 0;
-    while (gbits < 32 && (tk >> gbits)) ++gbits;
-    CDB_TRY(radix_sort_pairs(ctx, &HA.w, &HA.v, w2, v2, tc, kHotIdBits + gbits, s));
+    CDB_TRY(radix_sort_pairs(ctx, &HA.w, &HA.v, w2, v2, tc, HA.g_shift + gbits, s));
   }
   hot_first_kernel<<<(H + 255) / 256, 256, 0, s>>>(HA);
   CDB_TRY(launch_check(ctx, s, "hot_first_kernel"));

@@ -8,8 +8,9 @@
 //   hot_tag_kernel  : one thread per child: finds its key (binary search of the bucket's table),
 //                     decides whether it takes part (head type, element type, remote dels
 //                     ignored, exactly as the wave tier) and tags it with
-//                     W = G << 40 | id-hash[63:30] << 6 | pos, so that a run's rows arrive in
-//                     fold order unless two ids share 34 hash bits;
+//                     W = G << g_shift | id-hash top (g_shift - 6) bits << 6 | pos, so that a
+//                     run's rows arrive in fold order unless two ids share those hash bits
+//                     (g_shift: 40, or less where that saves a sort pass -- see over_capacity);
 //   radix sort of (W, child) pairs (radix.hip.h), stable, so equal W keep (bucket, row) order;
 //   hot_fold_kernel : one thread per W-run (a (key, child id) group, ~ one row per replica):
 //                     folds every exact child id of the run in (pos, src) order -- Counter::merge's
@@ -25,7 +26,8 @@
 
 namespace cdb {
 
-constexpr int kHotIdBits = 40;  // W = G << 40 | (child-id hash >> id_shift) << 6 | pos
+constexpr int kHotIdBits = 40;     // largest g_shift: W = G << 40 | (child-id hash >> 30) << 6 | pos
+constexpr int kHotMinIdBits = 20;  // fewest id-hash bits chosen to save a sort pass
 
 struct HotArgs {
   const uint32_t* ids;       // hot bucket of h
@@ -46,7 +48,8 @@ struct HotArgs {
   const uint32_t *rank_n, *rank_m;  // exclusive scans of emit_n / emit_m
   uint32_t* h_first;         // per h: first sorted position of its children
   uint64_t n_children;
-  int id_shift;              // W's id bits = id hash >> id_shift (30; larger in tests: collisions)
+  int id_shift;              // W's id bits = id hash >> id_shift (64 + 6 - g_shift; larger in tests)
+  int g_shift;               // W's key-id bits start here (kHotIdBits or less)
   uint32_t* run_list;        // sorted position of every run's first row, ascending
   const uint64_t* run_count; // runs in run_list (device)
   uint32_t* fold_q;          // per run start: the sorted position whose row is the output
@@ -122,7 +125,7 @@ __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
       const bool cand = isn || meta_tag(m) == KIND_ADD || p == hp;  // remote dels ignored
       if (type_ok && elem_ok && cand) {
         const uint64_t ih = isn ? mix64(id1) : id1;
-        w = ((uint64_t)(g0 + lo) << kHotIdBits) | ((ih >> H.id_shift) << 6) | p;
+        w = ((uint64_t)(g0 + lo) << H.g_shift) | ((ih >> H.id_shift) << 6) | p;
       }
     } else {
       ++orph;
@@ -211,7 +214,7 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
       h = hc & 0x7FFFFFFFu;
       isn = (hc >> 31) == 0;
       b = H.ids[h];
-      G = (uint32_t)(W >> kHotIdBits);
+      G = (uint32_t)(W >> H.g_shift);
       if (pass == 1) obase = (isn ? H.rank_n[p] - H.rank_n[H.h_first[h]] : H.rank_m[p] - H.rank_m[H.h_first[h]]);
     }
     uint32_t nout = 0;
@@ -383,7 +386,7 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
 __global__ void hot_first_kernel(HotArgs H) {
   const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= H.H) return;
-  const uint64_t key = (uint64_t)H.hk_off[h] << kHotIdBits;
+  const uint64_t key = (uint64_t)H.hk_off[h] << H.g_shift;
   uint64_t lo = 0, hi = H.n_children;
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
