@@ -190,7 +190,7 @@ class GenConfig(ctypes.Structure):
         "n_replicas", "key_permille", "mix_bytes", "mix_counter", "mix_set", "mix_dict", "conflict_ppm",
         "tie_permille", "max_nodes", "mean_members", "member_universe", "del_permille", "side_permille",
         "value_min", "value_max", "shard", "n_shards", "replica_lo", "replica_hi", "flags", "hot_zipf_milli",
-        "reserved")] + [("hot_events", ctypes.c_uint64)]
+        "stream")] + [("hot_events", ctypes.c_uint64)]
 
 
 # exported C-ABI function names (tests check the .so exports every one of them)
@@ -202,7 +202,8 @@ ABI_FUNCTIONS = (
     "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_partition_owner", "cdb_gen_default",
     "cdb_gen_snapshot", "cdb_gen_device", "cdb_decode_ops", "cdb_ops_info_get", "cdb_ops_free", "cdb_apply_ops", "cdb_gen_ops",
     "cdb_encode_snapshot", "cdb_crc64_gpu", "cdb_upload_batches", "cdb_decode_snapshots_device",
-    "cdb_decode_ops_gpu", "cdb_ops_column", "cdb_snapshot_index_selftest")
+    "cdb_decode_ops_gpu", "cdb_ops_column", "cdb_snapshot_index_selftest", "cdb_merge_into",
+    "cdb_merged_from_device", "cdb_dev_state_rows")
 
 _lib = None
 
@@ -238,6 +239,9 @@ def lib():
         "cdb_batch_free": (None, [vp]),
         "cdb_merge": (c_st, [vp, P(vp), ctypes.c_uint32, P(MergeOpts), P(vp), P(MergeStats)]),
         "cdb_merged_canonical_dump": (c_st, [vp, vp, P(vp), P(ctypes.c_size_t)]),
+        "cdb_merge_into": (c_st, [vp, vp, P(vp), ctypes.c_uint32, P(MergeOpts), P(vp), P(MergeStats)]),
+        "cdb_merged_from_device": (c_st, [vp, vp, P(vp), ctypes.c_uint32, P(DevOutput), P(vp)]),
+        "cdb_dev_state_rows": (c_st, [vp, P(DevOutput), P(DevRows), P(DevRows), P(DevRows), vp]),
         "cdb_merged_replicas": (c_st, [vp, P(P(ReplicaEntry)), P(ctypes.c_size_t)]),
         "cdb_merged_free": (None, [vp]),
         "cdb_free": (None, [vp]),
@@ -514,6 +518,10 @@ class Merged:
         self.stats = stats
         self._inputs = list(inputs)   # keep the byte arenas alive
 
+    @property
+    def handle(self):
+        return self._h
+
     def canonical_dump(self) -> bytes:
         out = ctypes.c_void_p()
         n = ctypes.c_size_t()
@@ -620,13 +628,7 @@ class DB:
                       force_tier: int = 0, pipe_ranges: int = 0) -> Merged:
         n = len(batches)
         arr = (ctypes.c_void_p * max(n, 1))(*[b.handle for b in batches])
-        opts = MergeOpts()
-        opts.flags = (MERGE_STRICT_DICT_PANIC if strict_dict_panic else 0)
-        opts.force_tier = force_tier
-        opts.pipe_ranges = pipe_ranges
-        if gc_watermark is not None:
-            opts.flags |= MERGE_GC_DELETES | (MERGE_GC_MEMBERS if gc_members else 0)
-            opts.gc_watermark = gc_watermark
+        opts = merge_opts(strict_dict_panic, gc_watermark, gc_members, force_tier, pipe_ranges)
         st = MergeStats()
         h = ctypes.c_void_p()
         rc = lib().cdb_merge(self.ctx.handle, arr, n, ctypes.byref(opts), ctypes.byref(h), ctypes.byref(st))
@@ -639,6 +641,49 @@ class DB:
 
     def merge_snapshots(self, snapshots: Sequence[bytes], **kw) -> Merged:
         return self.merge_batches([decode_snapshot(s) for s in snapshots], **kw)
+
+    def merge_into(self, state: Merged, batches: Sequence[Batch], strict_dict_panic: bool = False,
+                   gc_watermark: Optional[int] = None, gc_members: bool = False, force_tier: int = 0,
+                   pipe_ranges: int = 0) -> Merged:
+        """cdb_merge_into: `batches` merged into the existing result `state` (fold position 0),
+        as the reference merges peer snapshots into its live DB (replica/pull.rs:120-128)."""
+        n = len(batches)
+        arr = (ctypes.c_void_p * max(n, 1))(*[b.handle for b in batches])
+        opts = merge_opts(strict_dict_panic, gc_watermark, gc_members, force_tier, pipe_ranges)
+        st = MergeStats()
+        h = ctypes.c_void_p()
+        rc = lib().cdb_merge_into(self.ctx.handle, state.handle, arr, n, ctypes.byref(opts), ctypes.byref(h),
+                                  ctypes.byref(st))
+        if rc not in (OK, DICT_MERGE_UNIMPLEMENTED):
+            _raise(rc, self.ctx.last_error())
+        m = Merged(self.ctx, h, st, state._inputs + list(batches))
+        if rc == DICT_MERGE_UNIMPLEMENTED:
+            raise DictMergeUnimplemented(self.ctx.last_error())
+        return m
+
+
+def merge_opts(strict_dict_panic: bool = False, gc_watermark: Optional[int] = None, gc_members: bool = False,
+               force_tier: int = 0, pipe_ranges: int = 0) -> MergeOpts:
+    opts = MergeOpts()
+    opts.flags = (MERGE_STRICT_DICT_PANIC if strict_dict_panic else 0)
+    opts.force_tier = force_tier
+    opts.pipe_ranges = pipe_ranges
+    if gc_watermark is not None:
+        opts.flags |= MERGE_GC_DELETES | (MERGE_GC_MEMBERS if gc_members else 0)
+        opts.gc_watermark = gc_watermark
+    return opts
+
+
+def merged_from_device(ctx: Context, dout: "DevOutput", inputs: Sequence[Batch], state: Optional[Merged] = None,
+                       stats: Optional[MergeStats] = None) -> Merged:
+    """cdb_merged_from_device: the host view of a cdb_merge_device result (rows downloaded, bytes
+    resolved through `inputs`, and through `state` for fold position 0 when given)."""
+    n = len(inputs)
+    arr = (ctypes.c_void_p * max(n, 1))(*[b.handle for b in inputs])
+    h = ctypes.c_void_p()
+    ctx.check(lib().cdb_merged_from_device(ctx.handle, state.handle if state else None, arr, n, ctypes.byref(dout),
+                                           ctypes.byref(h)))
+    return Merged(ctx, h, stats if stats is not None else MergeStats(), (state._inputs if state else []) + list(inputs))
 
 
 # ----------------------------------------------------------------- synthetic inputs

@@ -7,9 +7,10 @@ generator (cdb_gen_device, rows written straight into HBM) draw identical replic
   C1/C2  2-node MEET: 1M Bytes keys + 1M counters per node (counters carry the writing node's
          own id, one node each), 50 % key overlap per type; B merged into A (R = 2).
   C3     set/dict add-win merge: 4 replicas, each the state left by replaying 10M
-         sadd/srem/hset/hdel commands (Zipf members) over 100K keys through the device op
-         apply (R8, type_set.rs:13-67, type_hash.rs:11-71); merged with DB::gc at the median
-         member time (db.rs:82-119).
+         sadd/srem/hset/hdel commands (Zipf members) over 100K keys (one type per key on every
+         replica) through the device op apply (R8, type_set.rs:13-67, type_hash.rs:11-71) on top
+         of a synced state holding Expires and Deletes; merged with DB::gc at the median member
+         time (db.rs:82-119).
   C4     8-replica anti-entropy: 60/30/5/5 Bytes/Counter/Set/Dict, 0.1 % type conflicts,
          p(key in replica) = 0.5; per GPU a 62.5M-key shard (N = 8 -> 500M keys).
   C5     Zipf hot keys: children per key ~ rank^-1.1 over 10M keys, 80M node/member rows over
@@ -50,24 +51,40 @@ def c5(cdb, universe=10_000_000, events=80_000_000, replicas=8, seed=5):
 
 def c3_ops_config(cdb, replica, keys=100_000, members=1000, seed=3):
     """Generator config of replica `replica`'s op stream: set/dict keys only, members drawn
-    Zipf-skewed from `members` per key, only sadd/srem/hset/hdel."""
-    return cdb.gen_config(seed=seed * 1000 + replica, universe=keys, n_replicas=1, mix_bytes=0,
-                          mix_counter=0, mix_set=50, mix_dict=50, member_universe=members,
+    Zipf-skewed from `members` per key, only sadd/srem/hset/hdel. The seed is shared by every
+    replica, so a key has ONE type everywhere (gen_type); `stream` salts the per-op draws, so each
+    replica replays its own commands."""
+    return cdb.gen_config(seed=seed, universe=keys, n_replicas=1, mix_bytes=0, mix_counter=0, mix_set=50,
+                          mix_dict=50, member_universe=members, stream=replica + 1,
                           flags=cdb.GEN_OPS_ZIPF_MEMBERS | cdb.GEN_OPS_TAGS_ONLY)
+
+
+def c3_base_config(cdb, replicas=4, keys=100_000, seed=3, side_permille=50):
+    """The state every C3 replica syncs from first: no data entries, only Expires and Deletes for
+    ~5 % of the keys each (pull.rs:129-130 -> DB::expire_at / DB::delete, db.rs:68-76). The
+    reference creates a Deletes entry only through DB::delete (a snapshot's Deletes) or DB::query
+    on an expired key (db.rs:53-66); delset / deldict only tag members (type_set.rs:117-135,
+    type_hash.rs:102-120). So this is where the C3 states' Deletes -- the garbage DB::gc
+    collects -- come from, besides the expiries the replayed commands trigger."""
+    return cdb.gen_config(seed=seed * 1000 + 17, universe=keys, n_replicas=replicas, key_permille=0,
+                          mix_bytes=0, mix_counter=0, mix_set=50, mix_dict=50, side_permille=side_permille,
+                          replica_lo=0, replica_hi=replicas)
 
 
 def c3_snapshots(cdb, ctx, ops_per_replica=10_000_000, replicas=4, keys=100_000, members=1000,
                  seed=3, zipf_milli=900, log=None):
-    """The C3 replica states: replica r = cdb_apply_ops of its own op stream on an empty state
-    (the device op apply of SURVEY §8f.2), written back as a snapshot by cdb_encode_snapshot.
-    Returns the snapshot bytes of every replica."""
+    """The C3 replica states: replica r = its base state (c3_base_config: Expires + Deletes) with
+    its own op stream applied by cdb_apply_ops (the device op apply of SURVEY §8f.2: DB::query's
+    expiry included), written back as a snapshot by cdb_encode_snapshot. Returns the snapshot
+    bytes of every replica."""
     db = cdb.DB(ctx)
+    base = c3_base_config(cdb, replicas, keys, seed)
     snaps = []
     for r in range(replicas):
         ops_bytes = cdb.gen_ops(c3_ops_config(cdb, r, keys, members, seed), ops_per_replica, 0, zipf_milli)
         ops = cdb.decode_ops(ops_bytes, 0)
         del ops_bytes
-        state = db.merge_snapshots([]).apply_ops(ops)
+        state = db.merge_snapshots([cdb.gen_snapshot(base, r)]).apply_ops(ops)
         data, _ = state.encode_snapshot(node_id=r + 1, alias=f"n{r + 1}", addr=f"127.0.0.1:{9001 + r}",
                                         replicas=None)
         snaps.append(data)

@@ -220,17 +220,19 @@ std::string hex(const uint8_t* p, uint64_t n) {
 
 }  // namespace
 
-// Copies batches [0, n) into the device columns of `din` (sized for their sum, batch i's rows
-// after batch i-1's) through the pinned staging ring and stamps fold position i into batch i's
-// meta words on the device.
-static cdb_status upload_batches(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, cdb_dev_input* din) {
+// Copies batches [0, n) into the device columns of `din` (batch i's rows after batch i-1's,
+// from row `at[f]` of family f on) through the pinned staging ring and stamps fold position
+// pos0 + i into batch i's meta words on the device.
+static cdb_status upload_batches(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, cdb_dev_input* din,
+                                 const uint64_t* at = nullptr, uint32_t pos0 = 0) {
   for (uint32_t i = 0; i < n; ++i)
     if (inputs[i]->b->rows_on_device) return fail(ctx, CDB_BAD_ARGUMENT, "a batch's rows are already in HBM");
   std::vector<HostSeg> segs;
   auto put = [&](const cdb_dev_rows& r, int c, uint64_t off, const ColVec& v) {
     if (!v.empty()) segs.push_back({const_cast<uint64_t*>(v.data()), r.col[c] + off, v.size() * 8});
   };
-  uint64_t ok = 0, on = 0, om = 0;
+  const uint64_t k0 = at ? at[0] : 0, n0 = at ? at[1] : 0, m0 = at ? at[2] : 0;
+  uint64_t ok = k0, on = n0, om = m0;
   for (uint32_t i = 0; i < n; ++i) {
     const Batch& b = *inputs[i]->b;
     const ColVec* kc[kKeyCols] = {&b.kh, &b.kf, &b.ct, &b.ut, &b.dt, &b.aux, &b.meta};
@@ -244,18 +246,85 @@ static cdb_status upload_batches(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_
     om += b.n_members();
   }
   cdb_status st = staged_copy(ctx, segs.data(), segs.size(), true, ctx->stream);
-  ok = on = om = 0;
+  ok = k0, on = n0, om = m0;
   for (uint32_t i = 0; i < n && st == CDB_OK; ++i) {
     const Batch& b = *inputs[i]->b;
-    if ((st = stamp_pos(ctx, din->keys.col[K_META] + ok, b.n_keys(), i, ctx->stream)) != CDB_OK ||
-        (st = stamp_pos(ctx, din->nodes.col[C_META] + on, b.n_nodes(), i, ctx->stream)) != CDB_OK ||
-        (st = stamp_pos(ctx, din->members.col[C_META] + om, b.n_members(), i, ctx->stream)) != CDB_OK)
+    if ((st = stamp_pos(ctx, din->keys.col[K_META] + ok, b.n_keys(), pos0 + i, ctx->stream)) != CDB_OK ||
+        (st = stamp_pos(ctx, din->nodes.col[C_META] + on, b.n_nodes(), pos0 + i, ctx->stream)) != CDB_OK ||
+        (st = stamp_pos(ctx, din->members.col[C_META] + om, b.n_members(), pos0 + i, ctx->stream)) != CDB_OK)
       break;
     ok += b.n_keys();
     on += b.n_nodes();
     om += b.n_members();
   }
   return st;
+}
+
+// A host result's rows as fold position 0 of the next merge, at rows [0, n) of each family of
+// `din` (cdb_merge_into): the key columns kh kf ct ut dt, win staged into aux and meta, then
+// state_rows on the device (pos 0, src = the row, aux = a counter's sum).
+static cdb_status upload_state(cdb_ctx* ctx, const cdb_merged& m, cdb_dev_input* din) {
+  std::vector<HostSeg> segs;
+  auto put = [&](const cdb_dev_rows& r, int c, const ColVec& v) {
+    if (!v.empty()) segs.push_back({const_cast<uint64_t*>(v.data()), r.col[c], v.size() * 8});
+  };
+  const int kmap[kKeyCols] = {O_KH, O_KF, O_CT, O_UT, O_DT, O_WIN, O_META};
+  for (int c = 0; c < kKeyCols; ++c) put(din->keys, c, m.k[kmap[c]]);
+  for (int c = 0; c < kNodeCols; ++c) put(din->nodes, c, m.nd[c]);
+  for (int c = 0; c < kMemberCols; ++c) put(din->members, c, m.mb[c]);
+  cdb_status st = staged_copy(ctx, segs.data(), segs.size(), true, ctx->stream);
+  if (st == CDB_OK) st = state_rows(ctx, din->keys.col[K_META], din->keys.col[K_AUX], m.k[O_KH].size(), ctx->stream);
+  if (st == CDB_OK) st = state_rows(ctx, din->nodes.col[C_META], nullptr, m.nd[0].size(), ctx->stream);
+  if (st == CDB_OK) st = state_rows(ctx, din->members.col[C_META], nullptr, m.mb[0].size(), ctx->stream);
+  return st;
+}
+
+// Downloads a compacted device result into m's host columns through the staging ring.
+static cdb_status download_result(cdb_ctx* ctx, const cdb_dev_output& dout, cdb_merged* m) {
+  std::vector<HostSeg> dsegs;
+  auto down = [&](ColVec* dst, int nc, const cdb_dev_rows& r) {
+    for (int c = 0; c < nc; ++c) {
+      dst[c].resize(r.n);  // default-initialised: no zero fill
+      advise_huge(dst[c].data(), r.n * 8);
+      if (r.n) dsegs.push_back({dst[c].data(), r.col[c], r.n * 8});
+    }
+  };
+  down(m->k, kKeyOutCols, dout.keys);
+  down(m->nd, kNodeCols, dout.nodes);
+  down(m->mb, kMemberCols, dout.members);
+  return staged_copy(ctx, dsegs.data(), dsegs.size(), false, ctx->stream);
+}
+
+// A result whose fold position 0 was `state` (cdb_merge_into, cdb_merged_from_device with a
+// state): its byte references become references into state's inputs, so the result stands on
+// one flat input list, state's inputs then the new batches (position p >= 1 -> P0 + p - 1, P0 =
+// state's input count). A reference (0, src) names row src of the state, whose own reference of
+// the same kind is taken: the key row's meta for key bytes, its win for a Bytes value, a
+// member's meta for member and field bytes, a node's meta (the head of its segment).
+static void flatten_onto(cdb_merged* m, const cdb_merged& state, uint32_t n_new) {
+  const uint64_t P0 = state.inputs.size();
+  auto remap = [&](uint64_t ref, const ColVec& state_col, bool keep_tag) -> uint64_t {
+    const uint32_t p = meta_pos(ref);
+    if (p == 0) {
+      const uint64_t w = state_col[meta_src(ref)];
+      return keep_tag ? meta_pack(meta_tag(ref), meta_pos(w), meta_src(w)) : meta_order(w);
+    }
+    return meta_pack(keep_tag ? meta_tag(ref) : 0, (uint32_t)(P0 + p - 1), meta_src(ref));
+  };
+  const uint64_t nk = m->k[O_KH].size();
+  for (uint64_t r = 0; r < nk; ++r) {
+    const uint64_t mt = m->k[O_META][r];
+    const uint32_t T = meta_tag(mt);
+    // a side row's win is its last (pos, src); a Bytes key's win the value's (pos, src); a
+    // counter's win is its sum, a set's / dict's 0
+    if (T == TAG_BYTES) m->k[O_WIN][r] = remap(m->k[O_WIN][r], state.k[O_WIN], false);
+    else if (T == TAG_EXPIRE || T == TAG_DELETE) m->k[O_WIN][r] = remap(m->k[O_WIN][r], state.k[O_META], false);
+    m->k[O_META][r] = remap(mt, state.k[O_META], true);
+  }
+  for (uint64_t r = 0; r < m->nd[0].size(); ++r) m->nd[C_META][r] = remap(m->nd[C_META][r], state.nd[C_META], true);
+  for (uint64_t r = 0; r < m->mb[0].size(); ++r) m->mb[C_META][r] = remap(m->mb[C_META][r], state.mb[C_META], true);
+  m->inputs = state.inputs;
+  (void)n_new;
 }
 
 extern "C" {
@@ -410,18 +479,7 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, const c
   const auto t2 = std::chrono::steady_clock::now();
   auto* m = new cdb_merged();
   for (uint32_t i = 0; i < n; ++i) m->inputs.push_back(inputs[i]->b);
-  std::vector<HostSeg> dsegs;
-  auto down = [&](ColVec* dst, int nc, const cdb_dev_rows& r) {
-    for (int c = 0; c < nc; ++c) {
-      dst[c].resize(r.n);  // default-initialised: no zero fill
-      advise_huge(dst[c].data(), r.n * 8);
-      if (r.n) dsegs.push_back({dst[c].data(), r.col[c], r.n * 8});
-    }
-  };
-  down(m->k, kKeyOutCols, dout.keys);
-  down(m->nd, kNodeCols, dout.nodes);
-  down(m->mb, kMemberCols, dout.members);
-  if ((st = staged_copy(ctx, dsegs.data(), dsegs.size(), false, ctx->stream)) != CDB_OK) {
+  if ((st = download_result(ctx, dout, m)) != CDB_OK) {
     delete m;
     return st;
   }
@@ -461,6 +519,78 @@ cdb_status cdb_upload_batches(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n
     return st;
   }
   out->n_pos = n;
+  return CDB_OK;
+}
+
+cdb_status cdb_merge_into(cdb_ctx* ctx, cdb_merged* state, cdb_batch* const* inputs, uint32_t n,
+                          const cdb_merge_opts* opts, cdb_merged** out, cdb_merge_stats* stats) {
+  if (!ctx || !state || !out || (n && !inputs)) return CDB_BAD_ARGUMENT;
+  *out = nullptr;
+  if (n + 1 > (uint32_t)kMaxPos) return fail(ctx, CDB_BAD_ARGUMENT, "at most 62 batches merged into a state");
+  if (state->inputs.size() + n > 255) return fail(ctx, CDB_BAD_ARGUMENT, "at most 255 inputs behind one result");
+  for (uint32_t i = 0; i < n; ++i)
+    if (!inputs[i] || inputs[i]->b->rows_on_device)
+      return fail(ctx, CDB_BAD_ARGUMENT, "cdb_merge_into: a batch's rows are in HBM; merge them with cdb_merge_device");
+  hipSetDevice(ctx->device);
+  const uint64_t sk = state->k[O_KH].size(), sn = state->nd[0].size(), sm = state->mb[0].size();
+  uint64_t K = sk, N = sn, M = sm;
+  for (uint32_t i = 0; i < n; ++i) {
+    K += inputs[i]->b->n_keys();
+    N += inputs[i]->b->n_nodes();
+    M += inputs[i]->b->n_members();
+  }
+  cdb_dev_input din;
+  std::memset(&din, 0, sizeof din);
+  cdb_dev_output dout;
+  std::memset(&dout, 0, sizeof dout);
+  din.n_pos = n + 1;
+  cdb_status st = CDB_OK;
+  auto block = [&](int slot, int ncol, uint64_t rows, cdb_dev_rows* r) -> cdb_status {
+    const uint64_t cap = std::max<uint64_t>(rows, 1);
+    auto* p = static_cast<uint64_t*>(ws_get(ctx, slot, ncol * cap * 8, &st));
+    if (!p) return st;
+    std::memset(r, 0, sizeof *r);
+    for (int c = 0; c < ncol; ++c) r->col[c] = p + c * cap;
+    r->n = rows;
+    return CDB_OK;
+  };
+  if ((st = block(WS_HOST_IN_K, kKeyCols, K, &din.keys)) != CDB_OK ||
+      (st = block(WS_HOST_IN_N, kNodeCols, N, &din.nodes)) != CDB_OK ||
+      (st = block(WS_HOST_IN_M, kMemberCols, M, &din.members)) != CDB_OK ||
+      (st = block(WS_HOST_OUT_K, kKeyOutCols, K, &dout.keys)) != CDB_OK ||
+      (st = block(WS_HOST_OUT_N, kNodeCols, N, &dout.nodes)) != CDB_OK ||
+      (st = block(WS_HOST_OUT_M, kMemberCols, M, &dout.members)) != CDB_OK)
+    return st;
+  const uint64_t at[3] = {sk, sn, sm};
+  if ((st = upload_state(ctx, *state, &din)) != CDB_OK) return st;
+  if ((st = upload_batches(ctx, inputs, n, &din, at, 1)) != CDB_OK) return st;
+  dout.compact = 1;
+  cdb_merge_stats local;
+  st = merge_device_impl(ctx, &din, opts, &dout, stats ? stats : &local, ctx->stream);
+  if (st != CDB_OK && st != CDB_DICT_MERGE_UNIMPLEMENTED) return st;
+  const cdb_status merge_st = st;
+  auto m = std::make_unique<cdb_merged>();
+  if ((st = download_result(ctx, dout, m.get())) != CDB_OK) return st;
+  flatten_onto(m.get(), *state, n);
+  for (uint32_t i = 0; i < n; ++i) m->inputs.push_back(inputs[i]->b);
+  *out = m.release();
+  return merge_st;
+}
+
+cdb_status cdb_merged_from_device(cdb_ctx* ctx, cdb_merged* state, cdb_batch* const* inputs, uint32_t n,
+                                  const cdb_dev_output* dout, cdb_merged** out) {
+  if (!ctx || !dout || !out || (n && !inputs)) return CDB_BAD_ARGUMENT;
+  *out = nullptr;
+  if ((state ? state->inputs.size() : 0) + n > 255) return fail(ctx, CDB_BAD_ARGUMENT, "at most 255 inputs behind one result");
+  for (uint32_t i = 0; i < n; ++i)
+    if (!inputs[i]) return CDB_BAD_ARGUMENT;
+  hipSetDevice(ctx->device);
+  auto m = std::make_unique<cdb_merged>();
+  cdb_status st = download_result(ctx, *dout, m.get());
+  if (st != CDB_OK) return st;
+  if (state) flatten_onto(m.get(), *state, n);
+  for (uint32_t i = 0; i < n; ++i) m->inputs.push_back(inputs[i]->b);
+  *out = m.release();
   return CDB_OK;
 }
 

@@ -81,5 +81,9 @@ void advise_huge(void* p, size_t bytes);
 uint64_t crc_tile_bytes();
 cdb_status crc64_device(cdb_ctx* ctx, const uint8_t* dev, uint64_t padded, uint64_t* d_crc, hipStream_t s);
 cdb_status stamp_pos(cdb_ctx* ctx, uint64_t* meta, uint64_t n, uint32_t pos, hipStream_t s);
+// A merge result's family as fold position 0 of the next merge, in place in the input rows:
+// meta <- tag | pos 0 | src = row; for keys (aux != null) also aux <- the counter sum (the
+// result's win, staged in aux) for counters, 0 otherwise.
+cdb_status state_rows(cdb_ctx* ctx, uint64_t* meta, uint64_t* aux, uint64_t n, hipStream_t s);
 
 }  // namespace cdb

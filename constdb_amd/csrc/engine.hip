@@ -80,6 +80,18 @@ __global__ void stamp_pos_kernel(uint64_t* __restrict__ meta, uint64_t n, uint32
   }
 }
 
+// A result row as an input row of fold position 0 (cdb_dev_state_rows, cdb_merge_into): the
+// reference merges peer snapshots into the live server.db (replica/pull.rs:120-128, db.rs:31-43),
+// whose rows are what the previous merge produced. A counter's load-time total (aux) is its sum
+// (type_counter.rs:89-91, the result's win); src is the row in the result, which resolves bytes.
+__global__ void state_rows_kernel(uint64_t* __restrict__ meta, uint64_t* __restrict__ aux, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t T = meta_tag(meta[i]);
+    if (aux) aux[i] = T == TAG_COUNTER ? aux[i] : 0;
+    meta[i] = meta_pack(T, 0, i);
+  }
+}
+
 __global__ void iota_kernel(uint32_t* p, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     p[i] = (uint32_t)i;
@@ -480,6 +492,13 @@ cdb_status stamp_pos(cdb_ctx* ctx, uint64_t* meta, uint64_t n, uint32_t pos, hip
   const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 4096);
   stamp_pos_kernel<<<(uint32_t)blocks, 256, 0, s>>>(meta, n, pos);
   return launch_check(ctx, s, "stamp_pos");
+}
+
+cdb_status state_rows(cdb_ctx* ctx, uint64_t* meta, uint64_t* aux, uint64_t n, hipStream_t s) {
+  if (n == 0) return CDB_OK;
+  const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 4096);
+  state_rows_kernel<<<(uint32_t)blocks, 256, 0, s>>>(meta, aux, n);
+  return launch_check(ctx, s, "state_rows");
 }
 
 namespace {
@@ -1327,6 +1346,30 @@ cdb_status cdb_partition_owner(cdb_ctx* ctx, const cdb_dev_rows* in, int ncols, 
   for (uint64_t i = 0; i < nb; ++i) counts[i] = n ? h[i] : 0;
   out->n = n;
   return CDB_OK;
+}
+
+cdb_status cdb_dev_state_rows(cdb_ctx* ctx, const cdb_dev_output* state, cdb_dev_rows* keys, cdb_dev_rows* nodes,
+                              cdb_dev_rows* members, void* stream) {
+  if (!ctx || !state || !keys || !nodes || !members) return CDB_BAD_ARGUMENT;
+  hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  const cdb_dev_rows* src[3] = {&state->keys, &state->nodes, &state->members};
+  cdb_dev_rows* dst[3] = {keys, nodes, members};
+  for (int f = 0; f < 3; ++f) {
+    const uint64_t n = src[f]->n;
+    // key out kh kf ct ut dt meta win cref -> in kh kf ct ut dt aux(<- win) meta(<- meta);
+    // children keep their six columns
+    const int map_k[7] = {O_KH, O_KF, O_CT, O_UT, O_DT, O_WIN, O_META};
+    for (int c = 0; c < (f == 0 ? kKeyCols : kNodeCols); ++c) {
+      const uint64_t* from = src[f]->col[f == 0 ? map_k[c] : c];
+      if (n && (!from || !dst[f]->col[c])) return fail(ctx, CDB_BAD_ARGUMENT, "cdb_dev_state_rows: missing column");
+      if (n && from != dst[f]->col[c])
+        CDB_HIP(hipMemcpyAsync(dst[f]->col[c], from, n * 8, hipMemcpyDeviceToDevice, s), "d2d");
+    }
+    dst[f]->n = n;
+    CDB_TRY(state_rows(ctx, dst[f]->col[f == 0 ? K_META : C_META], f == 0 ? dst[f]->col[K_AUX] : nullptr, n, s));
+  }
+  return hip_check(ctx, hipStreamSynchronize(s), "cdb_dev_state_rows");
 }
 
 cdb_status cdb_merge_device(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts, cdb_dev_output* out,

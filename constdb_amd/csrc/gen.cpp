@@ -278,8 +278,11 @@ extern "C" cdb_status cdb_gen_ops(const cdb_gen_config* cfg, uint64_t n_ops, uin
   const double s = zipf_milli / 1000.0;
   uint8_t kb[24], mb[24];
   const uint32_t mu = g.member_universe ? g.member_universe : 1;
+  // the per-op draws use a replica slot of their own: 0xFFFE, or one salted by cfg->stream (the
+  // key types stay gen_type's, a function of the seed alone)
+  const uint32_t os = cfg->stream ? 0x10000u + cfg->stream : 0xFFFEu;
   for (uint64_t q = 0; q < n_ops; ++q) {
-    const uint64_t u0 = grnd(g, q, 0xFFFE, 1), u1 = grnd(g, q, 0xFFFE, 2), u2 = grnd(g, q, 0xFFFE, 3);
+    const uint64_t u0 = grnd(g, q, os, 1), u1 = grnd(g, q, os, 2), u2 = grnd(g, q, os, 3);
     // key index: uniform, or a power-law skew (rank ~ x^(1/(1-s)) for x uniform in (0,1])
     const bool zmem = (g.flags & kGenOpsZipfMembers) != 0, tags_only = (g.flags & kGenOpsTagsOnly) != 0;
     const uint64_t i = zmem ? u0 % g.universe : skewed(u0, zmem ? 0 : s, g.universe, true);
@@ -319,14 +322,14 @@ extern "C" cdb_status cdb_gen_ops(const cdb_gen_config* cfg, uint64_t n_ops, uin
     if (!std::strcmp(name, "set")) {
       const uint32_t vl = g.value_min + (uint32_t)(u0 % (g.value_max >= g.value_min ? g.value_max - g.value_min + 1 : 1));
       uint8_t v[64];
-      for (uint32_t b = 0; b < vl && b < 64; ++b) v[b] = (uint8_t)('a' + (grnd(g, q, 0xFFFE, 10 + b / 8) >> (8 * (b % 8))) % 26);
+      for (uint32_t b = 0; b < vl && b < 64; ++b) v[b] = (uint8_t)('a' + (grnd(g, q, os, 10 + b / 8) >> (8 * (b % 8))) % 26);
       w.bulk(v, std::min<uint32_t>(vl, 64));
     } else if (!std::strcmp(name, "delcnt")) {
       w.integer((int64_t)node);
       w.integer(-(int64_t)(u1 % 100));
     } else if (nargs > 1) {
       for (uint32_t j = 0; j < nm; ++j) {
-        const uint64_t mj = zmem ? skewed(grnd(g, q, 0xFFFE, 20 + j), s, mu, false) : (u0 >> 16) % mu + j;
+        const uint64_t mj = zmem ? skewed(grnd(g, q, os, 20 + j), s, mu, false) : (u0 >> 16) % mu + j;
         const int ml = member_bytes(mj, mb);
         w.bulk(mb, ml);
         if (!std::strcmp(name, "hset")) w.bulk("v", 1);

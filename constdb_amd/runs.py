@@ -1,11 +1,19 @@
 """Sorted runs on the host side of the C-ABI (setup helpers, torch on device columns).
 
 A replica state this engine produced -- a merge result, or a snapshot encoded from one --
-holds its rows in key-hash order. Grouping a batch's rows into one such run per fold position
-(replica) lets cdb_merge_device take the sorted-run path (runs.hip.h: run directories, no
-partition pass), and lets the multi-GPU exchange (dist.py) send each owner its rows as
-contiguous slices of every run. These helpers establish that layout for generated inputs;
-they are setup, never part of a timed merge step.
+holds its rows in key-hash order. Grouping a batch's rows into runs ordered by key hash lets
+cdb_merge_device take the sorted-run path (runs.hip.h: run directories, no partition pass), and
+lets the multi-GPU exchange (dist.py) send each owner its rows as contiguous slices of every run.
+
+Two layouts:
+  * one run per fold position (every key row of a replica in one hash-ordered run): what a merge
+    result kept in HBM as the next merge's position 0 is (cdb_dev_state_rows);
+  * three key runs per fold position -- DATAS, EXPIRES, DELETES, each hash-ordered -- and one
+    child run (padded with two empty runs): what decoding a snapshot this engine encoded yields
+    (the encoder writes each section in the result's hash order, cdb_encode_snapshot), i.e. the
+    run layout cdb_decode_snapshots_device reports.
+These helpers establish a layout for generated inputs; they are setup, never part of a timed
+merge step.
 """
 from __future__ import annotations
 
@@ -22,21 +30,33 @@ def wrap(ptr: int, n: int):
     return torch.as_tensor(_Cai(), device="cuda")
 
 
-def run_order(kh, meta):
-    """Permutation ordering rows by (fold position, unsigned key hash), stable; and the row
-    count of every position. kh / meta: int64 tensors of one family."""
+def run_order(kh, meta, sections: bool = False, key_family: bool = False):
+    """Permutation ordering rows by (fold position, [section,] unsigned key hash), stable, and the
+    run index of every row (pos, or 3 pos + section with `sections`). kh / meta: int64 tensors of
+    one family; key_family: meta's tag gives the section (data / expires / deletes)."""
     import torch
     o = torch.sort(kh ^ SIGN, stable=True).indices
     pos = (meta >> 48) & 0xFF
-    o = o[torch.sort(pos[o], stable=True).indices]
-    return o, pos
+    if sections:
+        sec = torch.zeros_like(pos)
+        if key_family:
+            tag = (meta >> 56) & 0xFF
+            sec = torch.where(tag == 6, 1, torch.where(tag == 7, 2, 0))
+        run = 3 * pos + sec
+    else:
+        run = pos
+    o = o[torch.sort(run[o], stable=True).indices]
+    return o, run
 
 
-def sort_into_runs(din, n_runs: int | None = None) -> None:
-    """Reorders every family's device rows of a cdb_dev_input by (fold position, key hash) in
-    place -- one run per position -- and records the runs in din.n_runs / din.run_start."""
+def sort_into_runs(din, n_runs: int | None = None, sections: bool = False) -> None:
+    """Reorders every family's device rows of a cdb_dev_input in place into runs -- one per fold
+    position, or with `sections` three per position (see the module doc) -- and records them in
+    din.n_runs / din.run_start."""
     import torch
     R = din.n_pos if n_runs is None else n_runs
+    if sections:
+        R = 3 * din.n_pos
     din.n_runs = R
     for f, (rows, ncol) in enumerate(zip((din.keys, din.nodes, din.members), FAMILY_COLS)):
         n = rows.n
@@ -46,9 +66,9 @@ def sort_into_runs(din, n_runs: int | None = None) -> None:
             continue
         kh = wrap(rows.col[0], n)
         meta = wrap(rows.col[ncol - 1], n)
-        o, pos = run_order(kh, meta)
-        counts = torch.bincount(pos, minlength=R).tolist()
-        del pos
+        o, run = run_order(kh, meta, sections, key_family=(f == 0))
+        counts = torch.bincount(run, minlength=R).tolist()
+        del run
         for c in range(ncol):
             col = wrap(rows.col[c], n)
             col.copy_(col[o])

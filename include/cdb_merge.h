@@ -33,17 +33,17 @@ extern "C" {
 /* Status codes map 1:1 onto the decode-path CstError variants (src/lib.rs:146-175). */
 typedef enum cdb_status {
   CDB_OK = 0,
-  CDB_INVALID_SNAPSHOT = 1,          /* CstError::InvalidSnapshot(offset)      lib.rs:157 */
-  CDB_INVALID_SNAPSHOT_CHECKSUM = 2, /* CstError::InvalidSnapshotChecksum      lib.rs:173 */
-  CDB_INVALID_TYPE = 3,              /* CstError::InvalidType (unknown tag)    lib.rs:151, object.rs:121 */
-  CDB_IO_ERROR = 4,                  /* CstError::IoError (truncated stream)   lib.rs:161 */
+  CDB_INVALID_SNAPSHOT = 1,          /* CstError::InvalidSnapshot(offset)      lib.rs:158 */
+  CDB_INVALID_SNAPSHOT_CHECKSUM = 2, /* CstError::InvalidSnapshotChecksum      lib.rs:174 */
+  CDB_INVALID_TYPE = 3,              /* CstError::InvalidType (unknown tag)    lib.rs:152, object.rs:121 */
+  CDB_IO_ERROR = 4,                  /* CstError::IoError (truncated stream)   lib.rs:162 */
   CDB_DICT_MERGE_UNIMPLEMENTED = 5,  /* Dict::merge's unimplemented!() panic,  lwwhash.rs:180 (strict mode) */
   CDB_BAD_ARGUMENT = 6,
   CDB_DEVICE_ERROR = 7,              /* a HIP call failed */
   CDB_OUT_OF_MEMORY = 8,
   CDB_NO_DEVICE = 9,                 /* no gfx950 device visible: the engine never falls back to the CPU */
-  CDB_INVALID_REQUEST_MSG = 10,      /* CstError::InvalidRequestMsg: malformed RESP  lib.rs:155, conn/buf_read.rs:114-200 */
-  CDB_NEED_MORE_MSG = 11             /* CstError::NeedMoreMsg: the stream ends inside a message  lib.rs:153 */
+  CDB_INVALID_REQUEST_MSG = 10,      /* CstError::InvalidRequestMsg: malformed RESP  lib.rs:156, conn/buf_read.rs:114-200 */
+  CDB_NEED_MORE_MSG = 11             /* CstError::NeedMoreMsg: the stream ends inside a message  lib.rs:154 */
 } cdb_status;
 
 typedef struct cdb_ctx cdb_ctx;       /* device, streams, workspace */
@@ -170,6 +170,16 @@ typedef struct cdb_merge_stats {
 
 cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n,
                      const cdb_merge_opts* opts, cdb_merged** out, cdb_merge_stats* stats);
+
+/* Merges n decoded snapshots into an existing result, the way the reference merges every peer
+ * snapshot into its live DB (replica/pull.rs:120-128 -> DB::merge_entry, db.rs:31-43, which
+ * mutates server.db): `state` is fold position 0, inputs[i] position i + 1. The same as cdb_merge
+ * over [decode(encode(state)), inputs...] without the round trip: state's rows go to the device
+ * as input rows (a counter's load-time total is its sum, every other field as stored). *out is
+ * a new result (state is unchanged) whose bytes resolve through state's inputs, then `inputs`
+ * (at most 255 in all behind one result; encode + decode starts a fresh chain). */
+cdb_status cdb_merge_into(cdb_ctx* ctx, cdb_merged* state, cdb_batch* const* inputs, uint32_t n,
+                          const cdb_merge_opts* opts, cdb_merged** out, cdb_merge_stats* stats);
 
 /* Canonical dump of a merge result: keys sorted by bytes, members by bytes, counter nodes
  * by id, then expires and deletes (the text format of oracle/constdb_oracle.py's
@@ -357,6 +367,24 @@ cdb_status cdb_partition_owner(cdb_ctx* ctx, const cdb_dev_rows* in, int ncols, 
  * replica set resident in HBM and merge it with cdb_merge_device (what cdb_merge does per call). */
 cdb_status cdb_upload_batches(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, cdb_dev_input* out);
 
+/* The host view of a cdb_merge_device result (compacted): its rows are downloaded, and bytes
+ * resolve through inputs[i] for fold position i -- or, with `state` non-NULL (the result the
+ * device merge's position 0 came from, via cdb_dev_state_rows), position 0 through state and
+ * position i >= 1 through inputs[i - 1], as cdb_merge_into. inputs may be batches whose rows are
+ * in HBM (cdb_decode_snapshots_device). The result supports everything a cdb_merge result does
+ * (canonical dump, replicas, encode, op apply, cdb_merge_into). */
+cdb_status cdb_merged_from_device(cdb_ctx* ctx, cdb_merged* state, cdb_batch* const* inputs, uint32_t n,
+                                  const cdb_dev_output* out, cdb_merged** m);
+
+/* A merge result kept in HBM as fold position 0 of the next cdb_merge_device (the reference's
+ * persistent server.db, replica/pull.rs:120-128): the compacted `state` rows are copied into
+ * caller-allocated input rows (7 / 6 / 6 columns, at least state's row counts; ->n is set) as
+ * key rows kh kf ct ut dt aux meta (aux = a counter's sum) and children unchanged, every meta
+ * word with pos 0 and src = the row in `state`. A merge result is in key-hash order, so these
+ * rows are ONE run of every family for the next merge (run_start[f] = {0, n, ...}). */
+cdb_status cdb_dev_state_rows(cdb_ctx* ctx, const cdb_dev_output* state, cdb_dev_rows* keys, cdb_dev_rows* nodes,
+                              cdb_dev_rows* members, void* stream);
+
 /* Allocates device columns for `rows` rows of a family (8 u64 columns) in *r. */
 cdb_status cdb_dev_rows_alloc(cdb_ctx* ctx, cdb_dev_rows* r, uint64_t rows, int ncols);
 void cdb_dev_rows_release(cdb_ctx* ctx, cdb_dev_rows* r);
@@ -387,7 +415,9 @@ typedef struct cdb_gen_config {
   uint32_t flags;                /* CDB_GEN_* below */
   uint32_t hot_zipf_milli;       /* config C5: children per key follow rank^-(s/1000) over key index
                                     rank i + 1 (0 = off; then max_nodes / mean_members apply) */
-  uint32_t reserved;
+  uint32_t stream;               /* cdb_gen_ops: salt of the per-op draws (command, key, members,
+                                    uuids) so replicas sharing a seed -- and so every key's type --
+                                    replay different streams (0: the unsalted stream) */
   uint64_t hot_events;           /* config C5: expected node/member rows over all replicas */
 } cdb_gen_config;
 enum {

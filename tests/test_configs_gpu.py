@@ -110,16 +110,20 @@ def test_c1_full_size_bit_exact(ctx):
 
 
 # ------------------------------------------------------------------ C3
-def test_c3_full_size_bit_exact(ctx):
-    """C3: 4 replica states from 10M sadd/srem/hset/hdel each (device op apply), merged with
-    DB::gc at the median member time; bit-exact against the oracle's fold + gc."""
-    snaps = configs.c3_snapshots(cdb, ctx)
+def test_c3_full_size_bit_exact(ctx, c3_snaps):
+    """C3: 4 replica states from 10M sadd/srem/hset/hdel each (device op apply on a synced state
+    holding Expires and Deletes), merged with DB::gc at the median member time; bit-exact against
+    the oracle's fold + gc. Every replica agrees on a key's type, and GC removes Deletes."""
+    snaps = c3_snaps
     batches = [cdb.decode_snapshot(s) for s in snaps]
     wm = configs.median_member_time(cdb, batches)
     assert wm > 0
+    assert sum(b.info().n_deletes for b in batches) > 0
     m = _check(ctx, snaps)
     assert m.stats.member_rows_in > 1_000_000
-    _check(ctx, snaps, gc=wm)
+    assert m.stats.type_conflicts < 0.01 * m.stats.key_rows_in
+    g = _check(ctx, snaps, gc=wm)
+    assert g.stats.deletes_gced > 0
 
 
 # ------------------------------------------------------------------ C5
