@@ -277,8 +277,26 @@ def run_single(cdb, args):
     return res
 
 
+def spawn_ranks(args):
+    """`--gpus N` (N > 1) without a launcher: start N ranks (one process per GPU) under
+    torch.distributed.run as a child process, before this process touches any GPU, and exit with
+    its status. Rank 0's JSON line goes to our stdout unchanged."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"--gpus {args.gpus} without WORLD_SIZE: launching {args.gpus} ranks")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(spawn_ranks(args))
     # RCCL and the HIP runtime may print banners on the C-level stdout: keep fd 1 for the
     # single JSON line and send everything else to stderr.
     json_fd = os.dup(1)
