@@ -29,7 +29,7 @@ sys.path.insert(0, ROOT)
 # SURVEY.md §8d algorithmic row widths (bytes): compulsory read + write per row
 W_KEY, W_NODE, W_SET, W_DICT = 50, 33, 34, 42
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
 # the merge pipeline's kernels (everything cdb_merge_device launches; not the generator)
 MERGE_KERNEL_PREFIXES = ("part_", "bucket_", "compact", "scan_", "stats_reduce", "gc_lastbad", "set_dir",
                          "stamp_pos", "iota", "hot_", "sorted_", "seg_", "run_", "mat_", "radix_hist",
@@ -45,13 +45,21 @@ def parse():
     ap.add_argument("--universe-per-gpu", type=int, default=62_500_000)
     ap.add_argument("--replicas", type=int, default=8)
     ap.add_argument("--seed", type=int, default=4)
-    ap.add_argument("--cpu-universe", type=int, default=2_000_000,
+    ap.add_argument("--cpu-universe", type=int, default=10_000_000,
                     help="key universe of the bounded C4 CPU-baseline sample (same generator config)")
-    ap.add_argument("--cpu-reps", type=int, default=5)
+    ap.add_argument("--cpu-reps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the multi-GPU (RCCL all-to-all) path even when WORLD_SIZE == 1")
     ap.add_argument("--c3-ops", type=int, default=10_000_000, help="ops per replica of config c3")
+    ap.add_argument("--single-process", action="store_true",
+                    help="one process drives every GPU: a multi-device context (cdb_ctx_create_multi) and "
+                         "cdb_merge_sharded, rows exchanged by RCCL inside the library")
+    ap.add_argument("--devices", default=None,
+                    help="--single-process: device slots, e.g. 0,1,2,3 (default 0..gpus-1); a device listed twice "
+                         "gives two shards on one GPU (rows then move by device copies)")
+    ap.add_argument("--no-general", action="store_true",
+                    help="skip the general_input figures (the same rows merged unsorted, on the partition path)")
     ap.add_argument("--force-tier", type=int, default=0, help="testing: cdb_merge_opts.force_tier")
     ap.add_argument("--input-order", default="sorted", choices=["sorted", "hash-random"],
                     help="sorted: every replica's rows form one run in key-hash order (as this engine's merge "
@@ -190,26 +198,16 @@ def setup(cdb, ctx, args):
 SIGN = -(1 << 63)
 
 
-def run_single(cdb, args):
-    if args.input_order == "sorted":
-        import torch  # noqa: F401 -- before libcdbmerge: one HIP runtime per process
-    ctx = cdb.Context(0)
+def timed_merges(cdb, ctx, din, opts, args, steps):
+    """`warmup` untimed merges, then `steps` timed ones (host wall: cdb_merge_device synchronises
+    its stream before returning). Returns (ms per step, per-phase HIP-event ms, last stats)."""
     L = cdb.lib()
-    din, opts, info = setup(cdb, ctx, args)
-    if args.input_order == "sorted":
-        from constdb_amd.runs import sort_into_runs
-        sort_into_runs(din)
-        info["workload"] += ("; input: one key-hash-ordered run per replica (as this engine's merge output and "
-                             "snapshots encoded from it arrive): the sorted-run path")
-    else:
-        info["workload"] += "; input: rows in generator order, random in key hash: the partition path"
     dout = cdb.DevOutput()
     ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.keys), din.keys.n, 8))
     ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.nodes), din.nodes.n, 6))
     ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.members), din.members.n, 6))
     dout.compact = 1
     st = cdb.MergeStats()
-    opts.force_tier = args.force_tier
 
     def step():
         ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(din), ctypes.byref(opts), ctypes.byref(dout),
@@ -218,19 +216,52 @@ def run_single(cdb, args):
     for _ in range(args.warmup):
         step()
     acc = dict(partition=0.0, bucket=0.0, finish=0.0, device=0.0)
-    t0 = time.perf_counter()  # cdb_merge_device synchronises its stream before returning
-    for _ in range(args.steps):
+    t0 = time.perf_counter()
+    for _ in range(steps):
         step()
         acc["bucket"] += st.bucket_ms
         acc["partition"] += st.partition_ms
         acc["finish"] += st.finish_ms
         acc["device"] += st.device_ms
     t1 = time.perf_counter()
-    ms = (t1 - t0) * 1e3 / args.steps
-    per = {k: v / args.steps for k, v in acc.items()}
+    for fam in (dout.keys, dout.nodes, dout.members):
+        L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
+    return (t1 - t0) * 1e3 / steps, {k: v / steps for k, v in acc.items()}, st
+
+
+def run_single(cdb, args):
+    import torch  # noqa: F401 -- before libcdbmerge: one HIP runtime per process
+    ctx = cdb.Context(0)
+    L = cdb.lib()
+    din, opts, info = setup(cdb, ctx, args)
+    opts.force_tier = args.force_tier
     from constdb_amd import configs
+    general = None
+    if args.input_order == "sorted" and not args.no_general:
+        # the same rows in the order the setup left them (generator / batch order: random in key hash),
+        # merged on the general (partition) path -- what a caller whose rows are not in runs gets
+        log("general-input path (partition) on the unsorted rows")
+        gms, gper, gst = timed_merges(cdb, ctx, din, opts, args, args.steps)
+        gB = alg_bytes(gst, configs.DICT_MEMBER_SHARE[args.config])
+        gtr = pmc_traffic(args.config + "_general")
+        general = {"ms_per_step": gms, "value": gst.key_rows_in / (gms * 1e-3), "merge_path": "partition",
+                   "phases_ms": {"partition": gper["partition"], "bucket_merge": gper["bucket"],
+                                 "finish": gper["finish"], "device_total": gper["device"]},
+                   "roofline_frac": gB / (gper["device"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                   "traffic": gtr["total"] if gtr else None,
+                   "traffic_over_alg": gtr["total"] / gB if gtr else None,
+                   "traffic_source": gtr["source"] if gtr else None}
+    if args.input_order == "sorted":
+        from constdb_amd.runs import sort_into_runs
+        sort_into_runs(din)
+        info["workload"] += ("; input: one key-hash-ordered run per replica (a merge result kept as position 0, "
+                             "or a snapshot this engine encoded, decoded by cdb_decode_snapshots_device): "
+                             "the sorted-run path")
+    else:
+        info["workload"] += "; input: rows in generator order, random in key hash: the partition path"
+    ms, per, st = timed_merges(cdb, ctx, din, opts, args, args.steps)
     B = alg_bytes(st, configs.DICT_MEMBER_SHARE[args.config])
-    tr = pmc_traffic(args.config)
+    tr = pmc_traffic(args.config if args.input_order == "sorted" else args.config + "_general")
     res = {
         "metric": "merged CRDT entries/sec (snapshot merge)",
         "value": st.key_rows_in / (ms * 1e-3),
@@ -271,9 +302,77 @@ def run_single(cdb, args):
     }
     if tr:
         res["roofline"]["traffic_per_kernel"] = tr["per_kernel"]
-    for fam in (dout.keys, dout.nodes, dout.members, din.keys, din.nodes, din.members):
+    if general is not None:
+        res["general_input"] = general
+    for fam in (din.keys, din.nodes, din.members):
         L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
     res["_sample"] = info["sample"]
+    return res
+
+
+def run_single_process(cdb, args):
+    """One process, every device slot of a multi-device context (the reference's one server process,
+    server.rs:95,128-130): replica r on slot r*N/R as one key-hash-ordered run, cdb_merge_sharded per
+    step (owner splits, RCCL point-to-point inside the library, per-device merges)."""
+    import torch  # noqa: F401 -- before libcdbmerge: one HIP runtime per process
+    from constdb_amd import configs
+    from constdb_amd.runs import sort_into_runs
+    devs = [int(x) for x in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    N = len(devs)
+    L = cdb.lib()
+    ctx = cdb.Context(devices=devs)
+    R = args.replicas
+    universe = args.universe_per_gpu * N
+    ins = []
+    for i in range(N):
+        c = ctx.shard(i)
+        cfg = configs.c4(cdb, universe, R, args.seed, i * R // N, (i + 1) * R // N)
+        d = cdb.DevInput()
+        c.check(L.cdb_gen_device(c.handle, ctypes.byref(cfg), ctypes.byref(d)))
+        d.n_pos = R
+        torch.cuda.set_device(devs[i])
+        sort_into_runs(d, R)
+        ins.append(d)
+        log(f"slot {i} (device {devs[i]}): {d.keys.n} key rows")
+    for _ in range(args.warmup):
+        outs, sts, xs = cdb.merge_sharded(ctx, ins)
+    acc = dict(split=0.0, exchange=0.0, merge=0.0)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        outs, sts, xs = cdb.merge_sharded(ctx, ins)
+        acc["split"] += xs.split_ms
+        acc["exchange"] += xs.exchange_ms
+        acc["merge"] += xs.merge_ms
+    t1 = time.perf_counter()
+    ms = (t1 - t0) * 1e3 / args.steps
+    per = {k: v / args.steps for k, v in acc.items()}
+    entries = sum(s.key_rows_in for s in sts)
+    B = sum(alg_bytes(s, configs.DICT_MEMBER_SHARE["c4"]) for s in sts)
+    link = max((xs.link_bytes[i][j] for i in range(N) for j in range(N) if i != j), default=0)
+    res = {
+        "metric": "merged CRDT entries/sec (snapshot merge)", "value": entries / (ms * 1e-3), "unit": "entries/s",
+        "n_gpus": len(set(devs)), "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic: seeded GenModel replica states generated in HBM, each replica one key-hash-ordered run",
+        "config": {"workload": f"C4 anti-entropy: {universe} keys x {R} replicas over device slots {devs}, one "
+                               f"process (cdb_merge_sharded)", "config": "c4", "replicas": R,
+                   "key_rows_in_total": entries, "parallelism": f"key-hash sharding x{N} (single process)",
+                   "transport": {0: "none", 1: "RCCL point-to-point", 2: "device copies"}[xs.transport],
+                   "merge_path": "sorted runs" if all(s.sorted_runs for s in sts) else "partition"},
+        "exchange": {"split_ms": per["split"], "ms": per["exchange"], "bytes_moved_per_step": xs.bytes_moved,
+                     "max_link_bytes": link,
+                     "max_link_GBps": link / (per["exchange"] * 1e-3) / 1e9 if per["exchange"] > 0 and link else None,
+                     "transfers": xs.transfers},
+        "merge_ms": per["merge"],
+        "roofline": {"bound": "hbm", "kernel": "merge pipeline of every device (HIP events); B_alg summed over "
+                                               "devices / slowest device's merge time",
+                     "achieved": B / (per["merge"] * 1e-3) / 1e9, "peak": 8000.0 * len(set(devs)), "unit": "GB/s",
+                     "frac": B / (per["merge"] * 1e-3) / 1e9 / (8000.0 * len(set(devs))), "alg_bytes": B,
+                     "traffic": None},
+    }
+    for i in range(N):
+        for fam in (ins[i].keys, ins[i].nodes, ins[i].members):
+            L.cdb_dev_rows_release(ctx.shard(i).handle, ctypes.byref(fam))
     return res
 
 
@@ -295,7 +394,7 @@ def spawn_ranks(args):
 
 def main():
     args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.single_process:
         raise SystemExit(spawn_ranks(args))
     # RCCL and the HIP runtime may print banners on the C-level stdout: keep fd 1 for the
     # single JSON line and send everything else to stderr.
@@ -308,9 +407,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
+    if args.single_process:
+        res = run_single_process(cdb, args)
+        sample = None
+    elif world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if world > 1 or args.force_dist:
+    elif world > 1 or args.force_dist:
         if args.config != "c4":
             raise SystemExit("the multi-GPU bench runs config c4")
         from constdb_amd import dist

@@ -185,6 +185,20 @@ class DevOutput(ctypes.Structure):
                 ("reserved", ctypes.c_uint32)]
 
 
+class ExchangeStats(ctypes.Structure):
+    """cdb_exchange_stats: the sharded merge's split / exchange / merge figures."""
+    _fields_ = [("n_devices", ctypes.c_uint32), ("transport", ctypes.c_uint32), ("packed", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)] + [(n, ctypes.c_double) for n in (
+                    "split_ms", "exchange_ms", "merge_ms", "total_ms")] + [(n, ctypes.c_uint64) for n in (
+                    "bytes_moved", "bytes_local", "transfers")] + [("link_bytes", (ctypes.c_uint64 * 8) * 8)]
+
+    def as_dict(self):
+        d = {n: getattr(self, n) for n, _ in self._fields_ if n not in ("link_bytes", "reserved")}
+        k = self.n_devices
+        d["link_bytes"] = [[self.link_bytes[i][j] for j in range(k)] for i in range(k)]
+        return d
+
+
 class GenConfig(ctypes.Structure):
     _fields_ = [("seed", ctypes.c_uint64), ("universe", ctypes.c_uint64)] + [(n, ctypes.c_uint32) for n in (
         "n_replicas", "key_permille", "mix_bytes", "mix_counter", "mix_set", "mix_dict", "conflict_ppm",
@@ -203,7 +217,8 @@ ABI_FUNCTIONS = (
     "cdb_gen_snapshot", "cdb_gen_device", "cdb_decode_ops", "cdb_ops_info_get", "cdb_ops_free", "cdb_apply_ops", "cdb_gen_ops",
     "cdb_encode_snapshot", "cdb_crc64_gpu", "cdb_upload_batches", "cdb_decode_snapshots_device",
     "cdb_decode_ops_gpu", "cdb_ops_column", "cdb_snapshot_index_selftest", "cdb_merge_into",
-    "cdb_merged_from_device", "cdb_dev_state_rows")
+    "cdb_merged_from_device", "cdb_dev_state_rows", "cdb_ctx_create_multi", "cdb_ctx_device_count",
+    "cdb_ctx_shard", "cdb_merge_sharded")
 
 _lib = None
 
@@ -228,6 +243,10 @@ def lib():
     P = ctypes.POINTER
     sig = {
         "cdb_ctx_create": (c_st, [P(vp), ctypes.c_int]),
+        "cdb_ctx_create_multi": (c_st, [P(vp), ctypes.c_int, P(ctypes.c_int)]),
+        "cdb_ctx_device_count": (ctypes.c_int, [vp]),
+        "cdb_ctx_shard": (vp, [vp, ctypes.c_int]),
+        "cdb_merge_sharded": (c_st, [vp, P(DevInput), P(MergeOpts), P(DevOutput), P(MergeStats), P(ExchangeStats)]),
         "cdb_ctx_destroy": (None, [vp]),
         "cdb_last_error": (ctypes.c_char_p, [vp]),
         "cdb_decode_snapshot": (c_st, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32, P(vp),
@@ -288,14 +307,36 @@ def crc64_gpu(ctx: "Context", data: bytes) -> int:
 
 # ----------------------------------------------------------------- context
 class Context:
-    """A device context (cdb_ctx). Needs a visible gfx950 GPU; raises NoDevice otherwise."""
+    """A device context (cdb_ctx). Needs a visible gfx950 GPU; raises NoDevice otherwise.
+    Context(devices=[...]) is a multi-device context (cdb_ctx_create_multi): one engine context per
+    device slot, RCCL between distinct devices; shard(i) is slot i's context."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices: Optional[Sequence[int]] = None, _borrowed=None):
         self._ctx = ctypes.c_void_p()
-        st = lib().cdb_ctx_create(ctypes.byref(self._ctx), device)
+        self._owner = None
+        if _borrowed is not None:  # a slot of a multi-device context (owned by it)
+            self._ctx, self._owner = ctypes.c_void_p(_borrowed[0]), _borrowed[1]
+            self.device = device
+            return
+        if devices is None:
+            st = lib().cdb_ctx_create(ctypes.byref(self._ctx), device)
+            self.device = device
+        else:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            st = lib().cdb_ctx_create_multi(ctypes.byref(self._ctx), len(devices), arr)
+            self.device = devices[0]
         if st != OK:
             _raise(st, "no HIP device" if st == NO_DEVICE else "cdb_ctx_create failed")
-        self.device = device
+
+    @property
+    def n_devices(self) -> int:
+        return lib().cdb_ctx_device_count(self._ctx)
+
+    def shard(self, i: int) -> "Context":
+        h = lib().cdb_ctx_shard(self._ctx, i)
+        if not h:
+            raise IndexError(i)
+        return Context(device=-1, _borrowed=(h, self))
 
     @property
     def handle(self):
@@ -309,7 +350,7 @@ class Context:
             _raise(st, self.last_error())
 
     def close(self):
-        if self._ctx:
+        if self._ctx and self._owner is None:
             lib().cdb_ctx_destroy(self._ctx)
             self._ctx = ctypes.c_void_p()
 
@@ -672,6 +713,22 @@ def merge_opts(strict_dict_panic: bool = False, gc_watermark: Optional[int] = No
         opts.flags |= MERGE_GC_DELETES | (MERGE_GC_MEMBERS if gc_members else 0)
         opts.gc_watermark = gc_watermark
     return opts
+
+
+def merge_sharded(ctx: "Context", inputs: Sequence["DevInput"], **kw):
+    """cdb_merge_sharded over every device slot of a multi-device context: inputs[i] are the rows
+    on slot i. Returns (outputs: list of DevOutput (library-owned, valid until the next call),
+    per-slot MergeStats, ExchangeStats)."""
+    n = ctx.n_devices
+    if len(inputs) != n:
+        raise ValueError(f"{n} device slots, {len(inputs)} inputs")
+    ins = (DevInput * n)(*inputs)
+    outs = (DevOutput * n)()
+    sts = (MergeStats * n)()
+    xs = ExchangeStats()
+    opts = merge_opts(**kw)
+    ctx.check(lib().cdb_merge_sharded(ctx.handle, ins, ctypes.byref(opts), outs, sts, ctypes.byref(xs)))
+    return list(outs), list(sts), xs
 
 
 def merged_from_device(ctx: Context, dout: "DevOutput", inputs: Sequence[Batch], state: Optional[Merged] = None,

@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libcdbmerge.so")
 OBJ = os.path.join(HERE, "build", "obj")
-SOURCES = ["engine.hip", "gen_device.hip", "decode_gpu.hip", "ops_apply.hip", "ops_gpu.hip", "encode_gpu.hip",
+SOURCES = ["engine.hip", "gen_device.hip", "decode_gpu.hip", "ops_apply.hip", "ops_gpu.hip", "encode_gpu.hip", "shard.hip",
            "group.cpp", "capi.cpp", "decode.cpp", "gen.cpp", "ops.cpp"]
 HEADERS = ["common.h", "batch.h", "engine.h", "partition.hip.h", "bucket.hip.h", "bucket_wave.hip.h",
            "gen_model.h", "ops.h", "runs.hip.h", "hot.hip.h", "radix.hip.h", "tile.hip.h"]

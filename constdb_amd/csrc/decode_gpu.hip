@@ -86,6 +86,7 @@ struct DecArgs {
   uint64_t* mb[6];                  // pkh pkf mh mf t meta
   ulonglong2 *mref, *mvref;          // Batch::m_ref / m_vref
   uint32_t pos;                     // fold position stamped into meta (device-resident emit)
+  const uint32_t* dest;             // device-resident emit: key row of entry i (null: row i)
 };
 
 struct Head {  // the part of a DATAS entry before the payload
@@ -194,15 +195,16 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
   if (i >= A.n) return;
   const uint8_t* p = A.raw;
   uint64_t o = A.off[i];
+  const uint64_t kr = A.dest ? A.dest[i] : i;  // the key row (its src stays the entry index)
   if (A.kind[i] != 0) {  // EXPIRES / DELETES: key, t (read_key_int, snapshot.rs:289-295)
     const Span key = rd_span(p, o);
     const uint64_t t = (uint64_t)rd_int(p, o);
     const Hash128 h = hash_bytes(p + key.off, key.len, kDomainKey);
-    A.k[0][i] = h.h;
-    A.k[1][i] = h.f;
-    A.k[2][i] = t;
-    A.k[3][i] = A.k[4][i] = A.k[5][i] = 0;
-    A.k[6][i] = meta_pack(A.kind[i] == 1 ? TAG_EXPIRE : TAG_DELETE, A.pos, i);
+    A.k[0][kr] = h.h;
+    A.k[1][kr] = h.f;
+    A.k[2][kr] = t;
+    A.k[3][kr] = A.k[4][kr] = A.k[5][kr] = 0;
+    A.k[6][kr] = meta_pack(A.kind[i] == 1 ? TAG_EXPIRE : TAG_DELETE, A.pos, i);
     A.kref[i] = make_ulonglong2(key.off, key.len);
     A.vref[i] = make_ulonglong2(0, 0);
     return;
@@ -273,15 +275,68 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
       ++row;
     }
   }
-  A.k[0][i] = h.h;
-  A.k[1][i] = h.f;
-  A.k[2][i] = hd.ct;
-  A.k[3][i] = hd.ut;
-  A.k[4][i] = hd.dt;
-  A.k[5][i] = aux;
-  A.k[6][i] = meta_pack(hd.tag, A.pos, i);
+  A.k[0][kr] = h.h;
+  A.k[1][kr] = h.f;
+  A.k[2][kr] = hd.ct;
+  A.k[3][kr] = hd.ut;
+  A.k[4][kr] = hd.dt;
+  A.k[5][kr] = aux;
+  A.k[6][kr] = meta_pack(hd.tag, A.pos, i);
   A.kref[i] = make_ulonglong2(hd.key.off, hd.key.len);
   A.vref[i] = make_ulonglong2(val.off, val.len);
+}
+
+// ---- key-hash order of a snapshot written from a merge result (decode_snapshots_gpu_device)
+// A merge result is in key-hash order, and the writer emits its DATAS, EXPIRES and DELETES rows
+// as three sections (server.rs:183-215 -> db.rs:122-136), each in that order. The device rows of
+// such a snapshot are made ONE run of key rows -- the three sections merged by hash, DATAS first
+// on ties, then EXPIRES -- so that the merge takes the sorted-run path. Its children already are
+// one run each: they follow their DATAS entries.
+//   key_hash_kernel : every entry's key hash (the first 8 bytes of what emit_kernel writes);
+//   order_check     : a section that decreases somewhere sets the flag (no run: the merge then
+//                     partitions these rows, as for a snapshot in the reference's HashMap order);
+//   dest_kernel     : row of entry i = its index in its section + the rows of the other sections
+//                     before it (binary searches: earlier sections count ties, later ones not).
+__global__ void __launch_bounds__(kDecThreads) key_hash_kernel(DecArgs A, uint64_t* __restrict__ kh) {
+  const uint64_t i = (uint64_t)blockIdx.x * kDecThreads + threadIdx.x;
+  if (i >= A.n) return;
+  uint64_t o = A.off[i];
+  const Span key = rd_span(A.raw, o);  // every entry kind starts with its key
+  kh[i] = hash_bytes(A.raw + key.off, key.len, kDomainKey).h;
+}
+
+struct Sections {
+  uint64_t b[4];  // section s = entries [b[s], b[s + 1]): DATAS, EXPIRES, DELETES
+};
+
+__global__ void __launch_bounds__(kDecThreads) order_check_kernel(const uint64_t* __restrict__ kh, Sections S,
+                                                                  unsigned long long* flag) {
+  const uint64_t i = (uint64_t)blockIdx.x * kDecThreads + threadIdx.x;
+  const uint64_t n = S.b[3];
+  const bool bad = i + 1 < n && i + 1 != S.b[1] && i + 1 != S.b[2] && kh[i] > kh[i + 1];
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1ull);
+}
+
+__device__ __forceinline__ uint64_t count_below(const uint64_t* kh, uint64_t lo, uint64_t hi, uint64_t v, bool ties) {
+  uint64_t a = lo, b = hi;  // first row in [lo, hi) whose hash is > v (ties) or >= v (no ties)
+  while (a < b) {
+    const uint64_t m = (a + b) >> 1;
+    if (ties ? kh[m] <= v : kh[m] < v) a = m + 1;
+    else b = m;
+  }
+  return a - lo;
+}
+
+__global__ void __launch_bounds__(kDecThreads) dest_kernel(const uint64_t* __restrict__ kh, Sections S,
+                                                           uint32_t* __restrict__ dest) {
+  const uint64_t i = (uint64_t)blockIdx.x * kDecThreads + threadIdx.x;
+  if (i >= S.b[3]) return;
+  const int s = i < S.b[1] ? 0 : i < S.b[2] ? 1 : 2;
+  const uint64_t v = kh[i];
+  uint64_t r = i - S.b[s];
+  for (int t = 0; t < 3; ++t)
+    if (t != s) r += count_below(kh, S.b[t], S.b[t + 1], v, t < s);
+  dest[i] = (uint32_t)r;
 }
 
 // Any entry left to the host tier (its count is the kHostTier marker)?
@@ -330,8 +385,13 @@ class GpuDecode {
   // everything after it (returns the index pass's status when the device part succeeds)
   int prepare_device(size_t* err_off);
   cdb_status emit_host(DecodeTiming* tm);
-  cdb_status emit_device(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t pos,
+  cdb_status emit_device(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t pos, bool run,
                          DecodeTiming* tm);
+  // key-hash order (after prepare_device): queues the key-hash pass and the sections' order check
+  // on the context's stream; the verdict reads after a synchronisation (read_order).
+  cdb_status order_check();
+  bool read_order() const { return ordered_ && !order_flag_; }
+  unsigned long long order_flag_ = 0;  // written by the D2H copy queued in order_check
   uint64_t keys() const { return n_; }
   uint64_t nodes() const { return nn_; }
   uint64_t members() const { return nm_; }
@@ -367,7 +427,9 @@ class GpuDecode {
   uint64_t n_ = 0, nn_ = 0, nm_ = 0;
   std::vector<uint64_t> noff_, moff_;
   std::vector<HostEntry> hosted_;
-  DevBuf d_raw_, d_meta_, d_crc_, d_rows_;
+  DevBuf d_raw_, d_meta_, d_crc_, d_rows_, d_ord_;
+  bool ordered_ = false;  // the sections are contiguous, in DATAS, EXPIRES, DELETES order
+  Sections sec_{};
   DecArgs A_;
   uint32_t grid_ = 0;
   EvPair ev_;
@@ -599,8 +661,42 @@ cdb_status GpuDecode::emit_host(DecodeTiming* tm) {
   return CDB_OK;
 }
 
+cdb_status GpuDecode::order_check() {
+  ordered_ = false;
+  order_flag_ = 0;
+  const uint64_t n = n_;
+  if (n == 0) {
+    ordered_ = true;
+    return CDB_OK;
+  }
+  if (n >= (1ull << 32)) return CDB_OK;
+  uint64_t cnt[3] = {0, 0, 0};
+  uint8_t prev = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint8_t k = idx_.kind[i];
+    if (k < prev || k > 2) return CDB_OK;  // sections out of the writer's order: no run
+    prev = k;
+    ++cnt[k];
+  }
+  sec_.b[0] = 0;
+  sec_.b[1] = cnt[0];
+  sec_.b[2] = cnt[0] + cnt[1];
+  sec_.b[3] = n;
+  if ((st_ = alloc(&d_ord_.p, n * 12 + 64, "decode: key-hash order scratch")) != CDB_OK) return st_;
+  uint64_t* kh = (uint64_t*)d_ord_.p;
+  unsigned long long* flag = (unsigned long long*)(kh + n);
+  ck(hipMemsetAsync(flag, 0, 8, s_), "memset(decode order)");
+  key_hash_kernel<<<grid_, kDecThreads, 0, s_>>>(A_, kh);
+  ck(hipGetLastError(), "key_hash_kernel");
+  order_check_kernel<<<grid_, kDecThreads, 0, s_>>>(kh, sec_, flag);
+  ck(hipGetLastError(), "order_check_kernel");
+  ck(hipMemcpyAsync(&order_flag_, flag, 8, hipMemcpyDeviceToHost, s_), "d2h(decode order)");
+  ordered_ = st_ == CDB_OK;
+  return st_;
+}
+
 cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t pos,
-                                  DecodeTiming* tm) {
+                                  bool run, DecodeTiming* tm) {
   out_->rows_on_device = true;
   out_->dev_rows[0] = n_;
   out_->dev_rows[1] = nn_;
@@ -623,6 +719,14 @@ cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint6
   A.mref = (ulonglong2*)w; w += 2 * nm;
   A.mvref = (ulonglong2*)w; w += 2 * nm;
   A.pos = pos;
+  A.dest = nullptr;
+  if (run && n > 1 && sec_.b[1] != n) {  // side sections to merge into the DATAS order
+    const uint64_t* kh = (const uint64_t*)d_ord_.p;
+    uint32_t* dest = (uint32_t*)(kh + n + 8);
+    dest_kernel<<<grid_, kDecThreads, 0, s>>>(kh, sec_, dest);
+    ck(hipGetLastError(), "dest_kernel");
+    A.dest = dest;
+  }
   emit_kernel<<<grid_, kDecThreads, 0, s>>>(A);
   ck(hipGetLastError(), "emit_kernel");
   if (st_ != CDB_OK) return st_;
@@ -737,8 +841,16 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
   }
   if (tot[0] >= (1ull << 32) || tot[1] >= (1ull << 32) || tot[2] >= (1ull << 32))
     return fail(ctx, CDB_BAD_ARGUMENT, "decoded rows exceed 2^32 per family");
-  std::memset(din, 0, sizeof *din);
   cdb_status st;
+  // one run per snapshot when every snapshot is in key-hash order (written from a merge result)
+  bool runs = n <= CDB_MAX_RUNS;
+  for (uint32_t i = 0; i < n && runs; ++i)
+    if ((st = dec[i]->order_check()) != CDB_OK) return st;
+  if (runs) {
+    if ((st = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync(decode order)")) != CDB_OK) return st;
+    for (uint32_t i = 0; i < n; ++i) runs = runs && dec[i]->read_order();
+  }
+  std::memset(din, 0, sizeof *din);
   if ((st = cdb_dev_rows_alloc(ctx, &din->keys, tot[0], kKeyCols)) != CDB_OK ||
       (st = cdb_dev_rows_alloc(ctx, &din->nodes, tot[1], kNodeCols)) != CDB_OK ||
       (st = cdb_dev_rows_alloc(ctx, &din->members, tot[2], kMemberCols)) != CDB_OK) {
@@ -756,7 +868,9 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     for (int c = 0; c < kNodeCols; ++c) nd[c] = din->nodes.col[c] + o[1];
     for (int c = 0; c < kMemberCols; ++c) mb[c] = din->members.col[c] + o[2];
     DecodeTiming t1;
-    if ((st = dec[i]->emit_device(k, nd, mb, i, &t1)) != CDB_OK) {
+    if (runs)
+      for (int f = 0; f < 3; ++f) din->run_start[f][i] = o[f];
+    if ((st = dec[i]->emit_device(k, nd, mb, i, runs, &t1)) != CDB_OK) {
       cdb_dev_rows_release(ctx, &din->keys);
       cdb_dev_rows_release(ctx, &din->nodes);
       cdb_dev_rows_release(ctx, &din->members);
@@ -768,6 +882,10 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     o[2] += dec[i]->members();
   }
   din->n_pos = n;
+  if (runs) {
+    din->n_runs = n;
+    for (int f = 0; f < 3; ++f) din->run_start[f][n] = o[f];
+  }
   if (tm)  // everything but the host index passes (the snapshots' device work overlaps)
     tm->device_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count() - tm->index_ms;

@@ -5,8 +5,13 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/cdb_merge.h"
+
+namespace cdb {
+struct Node;  // RCCL communicators of a multi-device context (shard.hip)
+}
 
 struct cdb_ctx {
   int device = 0;
@@ -19,13 +24,17 @@ struct cdb_ctx {
   hipEvent_t ev_cs = nullptr, ev_cw = nullptr, ev_cdone = nullptr;  // pipelined compaction (side2)
   std::string last_error;
   struct Buf { void* p = nullptr; size_t bytes = 0; };
-  Buf ws[32];  // named workspace slots, grown on demand, reused across calls
+  Buf ws[48];  // named workspace slots, grown on demand, reused across calls
   uint32_t wave_slots[2] = {0, 0};
   void* pin = nullptr;                                // pinned staging ring of host<->device copies
   hipEvent_t pin_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   uint64_t pin_next = 0;                              // next slot of the ring (continues across calls)
   uint64_t runs_host[3 * 65] = {};                    // sorted-run path: run starts staged for the device
   uint32_t runs_err = 0;                              // sorted-run path: run_mark_kernel's verdict
+  // multi-device context (cdb_ctx_create_multi): this context is device slot 0; shards[i - 1] is
+  // the context of device slot i; node holds the RCCL communicators (shard.hip)
+  std::vector<cdb_ctx*> shards;
+  cdb::Node* node = nullptr;
 };
 
 namespace cdb {
@@ -48,9 +57,13 @@ enum WsSlot {
   WS_HOTC3, WS_HOTMETA, WS_HOTK, WS_HOTCH, WS_RADIX,    // over-capacity child path (hot.hip.h)
   WS_MAT,                                               // sorted-run path: materialisation counts
   WS_PIPE,                                              // pipelined bucket phase: range bases, totals
+  WS_XK, WS_XN, WS_XM,                                  // sharded merge: received rows per family
+  WS_YK, WS_YN, WS_YM,                                  // sharded merge: this device's output rows
+  WS_PK, WS_PN, WS_PM,                                  // sharded merge: owner-packed rows (inputs not in runs)
+  WS_SPLIT,                                             // sharded merge: owner splits of the runs
   WS_COUNT
 };
-static_assert(WS_COUNT <= 32, "cdb_ctx::ws has 32 slots");
+static_assert(WS_COUNT <= 48, "cdb_ctx::ws has 48 slots");
 
 struct Batch;
 struct DecodeTiming;
@@ -60,6 +73,11 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
                                 uint32_t flags, Batch* const* outs, cdb_dev_input* din, uint32_t* failed,
                                 size_t* err_off, DecodeTiming* tm);
 cdb_status fail(cdb_ctx* ctx, cdb_status st, const std::string& msg);
+// The device merge pipeline (engine.hip) on stream s of ctx's device.
+cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts, cdb_dev_output* out,
+                             cdb_merge_stats* stats, hipStream_t s);
+// Releases a multi-device context's node (RCCL communicators; shard.hip).
+void node_destroy(Node* n);
 cdb_status hip_check(cdb_ctx* ctx, hipError_t e, const char* what);
 cdb_status launch_check(cdb_ctx* ctx, hipStream_t s, const char* what);
 void* ws_get(cdb_ctx* ctx, int slot, size_t bytes, cdb_status* st);

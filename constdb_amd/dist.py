@@ -240,8 +240,13 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
             state[key] = b
         return b
 
-    def step():
+    ev = []  # per timed step: (start, exchanged) events on the step's stream
+
+    def step(timed=False):
         with torch.cuda.stream(cs):
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(cs)
             if world == 1:  # every row is this rank's own: the runs are the merge input as they lie
                 d2 = cdb.DevInput()
                 d2.keys, d2.nodes, d2.members = (_rows_from_tensor(cdb, fams[f], n_in[f]) for f in range(3))
@@ -251,14 +256,19 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
                     for r in range(R + 1):
                         d2.run_start[f][r] = starts[f][r]
                 state["ops"], state["runs"] = 0, R
+                state["sent"] = [0] * world
                 total = n_in
             else:
                 plan = make_plan(fams, starts, world, rank)
                 recv = [buf(("recv", f), FAMILY_COLS[f], max(plan.total[f], 1)) for f in range(3)]
                 state["ops"] = exchange_runs(fams, plan, recv)
                 state["runs"] = len(plan.runs)
+                state["sent"] = sent_bytes(plan, fams)
                 d2 = _merge_input(cdb, recv, plan, R)
                 total = plan.total
+            if timed:
+                e1.record(cs)
+                ev.append((e0, e1))
             dout = cdb.DevOutput()
             outs = [buf(("out", f), OUT_COLS[f], max(total[f], 1)) for f in range(3)]
             dout.keys, dout.nodes, dout.members = (_rows_from_tensor(cdb, t, 0) for t in outs)
@@ -277,19 +287,23 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(timed=True)
         dev_ms += st.device_ms
     torch.cuda.synchronize()
     dist.barrier()
     t1 = time.perf_counter()
-    el = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    tot = torch.tensor(n_in, dtype=torch.int64, device=dev)
-    dist.all_reduce(tot)
-    ms = el.item() * 1e3 / args.steps
-    entries = int(tot[0].item())
+    xch_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
     B = alg_bytes(st)
     dm = dev_ms / args.steps
+    sent = state["sent"]
+    # max over ranks: step time, exchange time, merge time, largest per-link bytes; sums: rows, B_alg, bytes
+    mx = torch.tensor([t1 - t0, xch_ms, dm, float(max(sent) if sent else 0)], dtype=torch.float64, device=dev)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    sm = torch.tensor([float(n_in[0]), B, float(sum(sent))], dtype=torch.float64, device=dev)
+    dist.all_reduce(sm)
+    ms = mx[0].item() * 1e3 / args.steps
+    xms, mms, link_max = mx[1].item(), mx[2].item(), mx[3].item()
+    entries, B_tot, moved = int(sm[0].item()), sm[1].item(), sm[2].item()
     res = {
         "metric": "merged CRDT entries/sec (snapshot merge)",
         "value": entries / (ms * 1e-3),
@@ -310,13 +324,41 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
                    "config": "c4", "replicas": R, "key_rows_in_total": entries,
                    "parallelism": f"key-hash sharding x{world}", "p2p_ops_per_step": state["ops"],
                    "merge_path": "sorted runs" if st.sorted_runs else "partition"},
-        "roofline": {"bound": "hbm", "kernel": "whole merge pipeline on rank 0 (cdb_merge_device, HIP events)",
-                     "achieved": B / (dm * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
-                     "frac": B / (dm * 1e-3) / 1e9 / 8000.0, "alg_bytes": B, "traffic": None},
+        # the all-to-all replaced by point-to-point slices, reported apart from the merge
+        "exchange": {"ms": xms, "bytes_moved_per_step": moved,
+                     "max_link_bytes": link_max,
+                     "max_link_GBps": link_max / (xms * 1e-3) / 1e9 if xms > 0 else None,
+                     "link_peak_GBps": XGMI_LINK_GBPS,
+                     "note": "ms = owner splits + count all_to_all + point-to-point transfers on the step's stream "
+                             "(HIP events), max over ranks; link = one (source, destination) rank pair"},
+        "merge_ms": mms,
+        "roofline": {"bound": "hbm", "kernel": "merge pipeline of every rank (cdb_merge_device, HIP events); "
+                                               "B_alg summed over ranks / slowest rank's merge time",
+                     "achieved": B_tot / (mms * 1e-3) / 1e9, "peak": 8000.0 * world, "unit": "GB/s",
+                     "frac": B_tot / (mms * 1e-3) / 1e9 / (8000.0 * world), "alg_bytes": B_tot,
+                     "traffic": None,
+                     "traffic_note": "PMC counters are collected on the 1-GPU line (profiles/), whose per-rank "
+                                     "work is the same (weak scaling)"},
     }
     dist.barrier()
     dist.destroy_process_group()
     return res
+
+
+XGMI_LINK_GBPS = 153.0  # one xGMI link, per direction (MI355X: 7 links per GPU)
+
+
+def sent_bytes(plan: Plan, fams):
+    """Bytes this rank sends to each peer in one step (its own slices excluded)."""
+    out = [0] * plan.world
+    for peer in range(plan.world):
+        if peer == plan.rank:
+            continue
+        for f in range(3):
+            nc = fams[f].shape[0]
+            for r in range(plan.R):
+                out[peer] += (plan.splits[f][r][peer + 1] - plan.splits[f][r][peer]) * nc * 8
+    return out
 
 
 def sharded_merge(cdb, ctx, din, n_pos: int, stream=None, max_piece_bytes: int = MAX_PIECE_BYTES):

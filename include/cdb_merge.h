@@ -91,7 +91,13 @@ cdb_status cdb_decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len,
  * emitted into it at fold position i -- row for row what cdb_upload_batches leaves from the
  * host-decoded batches. batches[i] receives snapshot i's host side (bytes, byte references,
  * header, replica entries, cdb_batch_info) to resolve merge outputs by src; its row columns
- * stay in HBM, so cdb_merge, cdb_upload_batches and cdb_batch_column reject it. Errors: *failed
+ * stay in HBM, so cdb_merge, cdb_upload_batches and cdb_batch_column reject it.
+ * Sorted runs: when every snapshot's DATAS, EXPIRES and DELETES sections are each in key-hash
+ * order (a snapshot cdb_encode_snapshot wrote from a merge result), snapshot i's key rows are
+ * placed as ONE run in key-hash order (the three sections merged, DATAS first on equal hashes;
+ * meta src still names the entry), its node and member rows are one run each, and out->n_runs = n
+ * with run_start set: cdb_merge_device then takes the sorted-run path. Otherwise (the
+ * reference's HashMap order) rows keep stream order and n_runs = 0. Errors: *failed
  * is the snapshot, *err_offset the byte offset in it, and nothing is allocated; a checksum
  * mismatch (CDB_INVALID_SNAPSHOT_CHECKSUM) still returns every batch and the rows, as the
  * reference merges a snapshot's entries before it reaches the checksum. */
@@ -337,8 +343,10 @@ typedef struct cdb_dev_input {
   uint32_t n_runs;  /* 0: rows in any order (the partition path). 1..64: the rows of every family
                        are n_runs consecutive runs, run r = rows [run_start[f][r], run_start[f][r+1])
                        of family f (0 keys, 1 nodes, 2 members), each non-decreasing in column 0
-                       (the key hash; children: the parent key hash) -- one run per replica, as
-                       this engine's merge output and snapshots encoded from it are. Then the
+                       (the key hash; children: the parent key hash) -- one run per replica.
+                       Producers: cdb_dev_state_rows (a merge result as position 0), and
+                       cdb_decode_snapshots_device over snapshots cdb_encode_snapshot wrote
+                       (their three key sections merged back into one run on decode). Then the
                        merge reads the runs in place (no partition pass). A run found out of
                        order, or more than 32 runs, send the merge to the partition path; the
                        result is the same. */
@@ -392,6 +400,49 @@ void cdb_dev_rows_release(cdb_ctx* ctx, cdb_dev_rows* r);
  * out->*.n receive the output row counts. Synchronises before returning. */
 cdb_status cdb_merge_device(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts,
                             cdb_dev_output* out, cdb_merge_stats* stats, void* stream);
+
+/* ------------------------------------------------------------------ several GPUs in one process
+ * SURVEY §8b/§8e. The reference merges in ONE server process (server.rs:95,128-130); a node's GPUs
+ * are driven the same way: one context over device_count devices (one stream set and workspace
+ * per device), with RCCL communicators between them (ncclCommInitAll; RCCL is loaded on first use).
+ * Keys shard by owner = the top log2(device_count) bits of the key hash (children follow their
+ * parent key), so every §8a rule stays local to one device: no collective beyond the row exchange.
+ * Device slot i may name any visible device; a device listed twice gives two shards on one GPU
+ * (testing), whose rows then move by device copies instead of RCCL. device_count must be a power
+ * of two, at most 8. The single-device functions take a multi-device context as its slot 0. */
+cdb_status cdb_ctx_create_multi(cdb_ctx** out, int device_count, const int* devices);
+int cdb_ctx_device_count(const cdb_ctx* ctx);
+/* The context of device slot i (slot 0: ctx itself), for per-device calls (cdb_gen_device,
+ * cdb_dev_rows_alloc, cdb_decode_snapshots_device, ...). Owned by ctx; NULL if out of range. */
+cdb_ctx* cdb_ctx_shard(cdb_ctx* ctx, int i);
+
+typedef struct cdb_exchange_stats {
+  uint32_t n_devices;
+  uint32_t transport;        /* 0 none (one device), 1 RCCL point-to-point, 2 device/peer copies */
+  uint32_t packed;           /* devices whose input was not in sorted runs: rows grouped by owner first */
+  uint32_t reserved;
+  double split_ms;           /* owner splits of every input (+ run order check / owner pack), host wall */
+  double exchange_ms;        /* the row transfers until every device holds its rows, host wall */
+  double merge_ms;           /* the slowest device's merge pipeline (HIP events) */
+  double total_ms;           /* the whole call, host wall */
+  uint64_t bytes_moved;      /* bytes that crossed between devices */
+  uint64_t bytes_local;      /* bytes a device kept (its own owner slices, device copies) */
+  uint64_t transfers;        /* point-to-point operations (or peer copies) posted */
+  uint64_t link_bytes[8][8]; /* [source slot][destination slot] */
+} cdb_exchange_stats;
+
+/* One sharded merge step over every device of ctx (replica/pull.rs:120-128 for a whole node):
+ * in[i] are the rows resident on device slot i (any fold positions; n_runs >= 1 for key-hash-
+ * ordered runs, each run's owner slices then move as they are; n_runs = 0, or runs found out of
+ * order, are grouped by owner on that device first). Each device receives the rows it owns -- as
+ * runs when every source was in runs, so its merge takes the sorted-run path -- and merges them
+ * (cdb_merge_device with key_shift = log2(device_count); opts->key_shift is ignored). out[i]
+ * receives device slot i's compacted result (keys in key-hash order): library-owned columns in
+ * that device's workspace, valid until the next cdb_merge_sharded on ctx or cdb_ctx_destroy; cref
+ * child ranges index out[i]'s own child rows. stats (may be NULL) is an array of device_count;
+ * xs (may be NULL) the exchange figures. */
+cdb_status cdb_merge_sharded(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts, cdb_dev_output* out,
+                             cdb_merge_stats* stats, cdb_exchange_stats* xs);
 
 /* ------------------------------------------------------------------ synthetic inputs
  * Seeded generator of replica states. Writes snapshot bytes

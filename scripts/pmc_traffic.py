@@ -10,14 +10,35 @@ import json
 import sys
 
 
+def _name(r):
+    return r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("cdb::", "").replace("void ", "")
+
+
 def load(d, counter):
-    per = collections.defaultdict(list)
+    """Per kernel, the counter's bytes of every dispatch between a merge_begin_marker and the next
+    merge_end_marker (the engine brackets each merge with them), so that a bench's setup kernels
+    (generator, op apply, the input sort) are not counted. Without markers: every dispatch."""
+    rows = []
     for f in glob.glob(f"{d}/**/run_counter_collection.csv", recursive=True):
-        for r in csv.DictReader(open(f)):
-            if r["Counter_Name"].startswith(counter):
-                name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("cdb::", "")
-                name = name.replace("void ", "")
-                per[name].append(float(r["Counter_Value"]) * 1024.0)
+        rows += [r for r in csv.DictReader(open(f)) if r["Counter_Name"].startswith(counter) or "marker" in r["Kernel_Name"]]
+    rows.sort(key=lambda r: (r["Process_Id"], int(r["Dispatch_Id"])))
+    marked = any("merge_begin_marker" in r["Kernel_Name"] for r in rows)
+    per = collections.defaultdict(list)
+    inside = not marked
+    seen = set()
+    for r in rows:
+        n = _name(r)
+        if n == "merge_begin_marker":
+            inside = True
+            continue
+        if n == "merge_end_marker":
+            inside = False
+            continue
+        key = (r["Process_Id"], r["Dispatch_Id"], r["Counter_Name"])
+        if not inside or not r["Counter_Name"].startswith(counter) or key in seen:
+            continue
+        seen.add(key)
+        per[n].append(float(r["Counter_Value"]) * 1024.0)
     return per
 
 

@@ -51,6 +51,10 @@ PIN_SIZE(cdb_gen_config, 112);
 PIN_OFF(cdb_gen_config, replica_hi, 88);
 PIN_OFF(cdb_gen_config, flags, 92);
 PIN_OFF(cdb_gen_config, hot_events, 104);
+PIN_SIZE(cdb_exchange_stats, 584);
+PIN_OFF(cdb_exchange_stats, split_ms, 16);
+PIN_OFF(cdb_exchange_stats, bytes_moved, 48);
+PIN_OFF(cdb_exchange_stats, link_bytes, 72);
 _Static_assert(CDB_NEED_MORE_MSG == 11 && CDB_INVALID_REQUEST_MSG == 10 && CDB_DEVICE_ERROR == 7,
                "status codes are part of the ABI");
 

@@ -87,6 +87,13 @@ def _worker(rank, world, port, q, piece=None):
                     want_ops += nc * (-(-(e - a) // p_rows))
                     want_ops += nc * (-(-plan.recv[peer][f][r] // p_rows))
         ok = ok and ops == want_ops
+        # the bench line's exchange bytes: what all ranks send to others == what all receive from others
+        sent = cdist.sent_bytes(plan, fams)
+        got_b = sum(plan.recv[s][f][r] * fams[f].shape[0] * 8 for s in range(world) if s != rank
+                    for f in range(3) for r in range(R))
+        tot = torch.tensor([float(sum(sent)), float(got_b)], dtype=torch.float64)
+        dist.all_reduce(tot)
+        ok = ok and sent[rank] == 0 and tot[0].item() == tot[1].item() and (world == 1 or tot[0].item() > 0)
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()

@@ -274,6 +274,47 @@ def test_device_state_chain_vs_oracle(ctx):
         del keep
 
 
+# ------------------------------------------------------------------ a producer of sorted runs
+def _hash_ordered_snapshots(ctx, snaps):
+    """Each replica state as the engine would write it back (replica/pull.rs:120-128 then
+    server.rs:183-215): merged once, encoded -- DATAS, EXPIRES and DELETES each in key-hash order."""
+    db = cdb.DB(ctx)
+    return [db.merge_snapshots([s]).encode_snapshot(replicas=None)[0] for s in snaps]
+
+
+@pytest.mark.parametrize("seed,gc", [(0, False), (1, True), (2, False)])
+def test_encode_decode_device_runs_vs_oracle(ctx, seed, gc):
+    """encode -> GPU decode into HBM -> cdb_merge_device: the decoder places each snapshot's key rows
+    as one key-hash-ordered run (its three sections merged), so the merge takes the sorted-run path
+    with no setup sort; the result equals the oracle's fold of the same snapshots. Snapshots in
+    generator order (not hash-ordered) get no runs."""
+    cfg = _small(300 + seed, 20000 + 10000 * seed, 3 + 2 * seed, conflict_ppm=20000, tie_permille=100,
+                 side_permille=300, mix_set=20, mix_dict=20, del_permille=300)
+    raw = [cdb.gen_snapshot(cfg, r) for r in range(cfg.n_replicas)]
+    batches, din = cdb.decode_snapshots_device(ctx, raw)
+    assert din.n_runs == 0
+    _release(ctx, din)
+    encs = _hash_ordered_snapshots(ctx, raw)
+    wm = (configs.T0_MS + (1 << 19)) << 22 if gc else None
+    rc, want, ost = cdb_oracle.fold(encs, flags=cdb_oracle.FLAG_GC if gc else 0, gc_watermark=wm or 0)
+    assert rc == 0
+    batches, din = cdb.decode_snapshots_device(ctx, encs)
+    dout = _out_for(ctx, din)
+    try:
+        assert din.n_runs == len(encs)
+        assert [din.run_start[0][r] for r in (0, len(encs))] == [0, din.keys.n]
+        st = _merge_device(ctx, din, dout, gc_watermark=wm)
+        assert st.sorted_runs == 1
+        m = cdb.merged_from_device(ctx, dout, batches, stats=st)
+        got = m.canonical_dump()
+        assert got == want, _diff(got, want)
+        assert st.type_conflicts == ost.type_conflicts
+        if gc:
+            assert st.deletes_gced > 0
+    finally:
+        _release(ctx, din, dout)
+
+
 # ------------------------------------------------------------------ full size, sorted runs
 def test_full_c4_shard_sorted_runs_invariants(ctx):
     """bench.py's workload on the path it measures (62.5M-key universe x 8 replicas, ~270M key
