@@ -72,17 +72,6 @@ struct BucketArgs {
   unsigned long long* stats;
   uint32_t* hot_list;
   uint32_t* hot_count;
-  // Single-pass output placement (wave tier). When lb_k is set, the wave kernel writes its
-  // buckets' outputs straight into the dense outputs dko / dno / dmo at offsets found by a
-  // decoupled look-back over per-bucket status words (flag:2 | count or inclusive prefix:62,
-  // one array per family); lb_tot receives the wave tier's totals. Every other tier writes
-  // sparse-by-bucket as before and is compacted after them.
-  unsigned long long *lb_k, *lb_n, *lb_m;
-  unsigned long long* lb_tot;
-  uint32_t* lb_err;
-  uint64_t* dko[kKeyOutCols];
-  uint64_t* dno[kNodeCols];
-  uint64_t* dmo[kMemberCols];
   const uint32_t* hot_in;     // hot kernel: bucket ids to process
   uint64_t* hot_scratch;      // hot kernel: global scratch slab
   const uint64_t* hot_scratch_off;  // per hot bucket, u64 offset into the slab

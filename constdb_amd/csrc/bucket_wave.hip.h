@@ -42,13 +42,6 @@ constexpr int kWavesPerWG = 4;
 #ifndef CDB_WAVE_STOP
 #define CDB_WAVE_STOP 99
 #endif
-// Cooperative row loads (load_cols_coop) cut the vector-memory accesses per row 3-4x but were
-// measured slower on MI355X (wave kernel 16.2 -> 17.2 ms, wide 5.0 -> 8.8 ms on the C4 shard:
-// the LDS transpose and its syncs cost more than the saved accesses). Off by default.
-#ifndef CDB_COOP_LOADS
-#define CDB_COOP_LOADS 0
-#endif
-constexpr bool kCoopLoads = CDB_COOP_LOADS;
 constexpr uint64_t kM44 = (1ull << 44) - 1, kM42 = (1ull << 42) - 1;
 
 // Per-wave LDS. KE = key rows per lane (1 or 2); child rows per lane CE = 2 KE.
@@ -240,156 +233,6 @@ __device__ __forceinline__ void load_cols(const BucketArgs& A, const WaveDir& d,
   }
 }
 
-// One 64-row half of a bucket's child rows through the staging area (compile-time H: the
-// piece registers and the WaveIn slot are never indexed dynamically, which put them in scratch).
-template <int H, int KE>
-__device__ __forceinline__ void coop_child_half(ulonglong2* st, int lane, uint32_t C, WaveIn<KE>& in, ulonglong2 a0,
-                                                ulonglong2 a1, ulonglong2 a2) {
-  wave_sync();  // the previous reads of the staging area are done
-  st[lane] = a0;  // pieces x = 64 k + lane of this half
-  st[64 + lane] = a1;
-  st[128 + lane] = a2;
-  wave_sync();
-  const uint32_t c = 64 * H + lane;
-  const ulonglong2 q0 = st[lane * 3], q1 = st[lane * 3 + 1], q2 = st[lane * 3 + 2];
-  const bool v = c < C;
-  in.cpkh[H] = v ? q0.x : 0;
-  in.cpkf[H] = v ? q0.y : 0;
-  in.cid1[H] = v ? q1.x : 0;
-  in.cid2[H] = v ? q1.y : 0;
-  in.ct[H] = v ? q2.x : 0;
-  in.cm[H] = v ? q2.y : 0;
-}
-
-// The same columns, loaded cooperatively: a row's 16-B pieces are fetched by adjacent lanes
-// of ONE load instruction (4 lanes per 64-B key row, 3 per 48-B child row), so an instruction
-// touches 16 key rows (21 child rows) instead of 64 and the vector-memory path handles a
-// row's line once instead of once per piece (it was busy ~93 % of the kernel). Every global
-// load is issued up front; the pieces are then transposed through the wave's LDS row area
-// (L.col, free until the keys are scattered) into the lane-per-row registers of WaveIn.
-template <int KE>
-__device__ __forceinline__ void load_cols_coop(const BucketArgs& A, const WaveDir& d, const WavePerm<KE>& p, int lane,
-                                               WaveIn<KE>& in, WaveLds<KE>& L) {
-  static_assert(sizeof(L.ccol) >= 64 * KE * 64, "key rows are staged in the row area");
-  in.d = d;
-  const uint32_t C = d.N + d.M;
-  ulonglong2 kq[4 * KE], cq[6 * KE];
-#pragma unroll
-  for (int i = 0; i < 4 * KE; ++i) {  // key row r = 16 i + lane / 4, piece lane % 4
-    const uint32_t r = 16 * i + (lane >> 2);
-    const uint32_t ridx = (uint32_t)__shfl((int)p.krow[i >> 2], (int)(r & 63), 64);
-    // unconditional: slots past the bucket read row 0 (always allocated; one shared line) and
-    // are masked after the transpose (a select on the load became a scratch-backed flat load)
-    kq[i] = reinterpret_cast<const ulonglong2*>(A.kr + (uint64_t)ridx * kKeyStride)[lane & 3];
-  }
-#pragma unroll
-  for (int i = 0; i < 6 * KE; ++i) {  // child piece x = 64 i + lane: row x / 3 (of 64 h ..), piece x % 3
-    const int h = i / 3;                 // 64-row half: 3 instructions each
-    const uint32_t x = 64 * (i % 3) + lane, rl = x / 3, q = x - 3 * rl;
-    const uint32_t c = 64 * h + rl;
-    const uint32_t ridx = (uint32_t)__shfl((int)p.crow[h], (int)rl, 64);
-    const uint64_t* base = c < d.N ? A.nr : A.mr;
-    cq[i] = reinterpret_cast<const ulonglong2*>(base + (uint64_t)ridx * kChildStride)[q];
-  }
-  ulonglong2* st = reinterpret_cast<ulonglong2*>(&L.ccol[0][0]);
-#pragma unroll
-  for (int i = 0; i < 4 * KE; ++i) st[(16 * i + (lane >> 2)) * 4 + (lane & 3)] = kq[i];
-  wave_sync();
-#pragma unroll
-  for (int e = 0; e < KE; ++e) {
-    const uint32_t c = lane + 64 * e;
-    const ulonglong2 q0 = st[c * 4], q1 = st[c * 4 + 1], q2 = st[c * 4 + 2], q3 = st[c * 4 + 3];
-    const bool v = c < d.K;
-    in.kh[e] = v ? q0.x : 0;
-    in.kf[e] = v ? q0.y : 0;
-    in.kct[e] = v ? q1.x : 0;
-    in.kut[e] = v ? q1.y : 0;
-    in.kdt[e] = v ? q2.x : 0;
-    in.kaux[e] = v ? q2.y : 0;
-    in.kmeta[e] = v ? q3.x : 0;
-  }
-  coop_child_half<0>(st, lane, C, in, cq[0], cq[1], cq[2]);
-  coop_child_half<1>(st, lane, C, in, cq[3], cq[4], cq[5]);
-  if constexpr (KE == 2) {
-    coop_child_half<2>(st, lane, C, in, cq[6], cq[7], cq[8]);
-    coop_child_half<3>(st, lane, C, in, cq[9], cq[10], cq[11]);
-  }
-  wave_sync();  // the row area is the wave's again
-}
-
-// Decoupled look-back (single-pass prefix over buckets in dispatch order). Publishes bucket
-// b's output counts (flag A), walks back over its predecessors 64 at a time until every family
-// meets an inclusive prefix (flag P), then publishes its own inclusive prefixes. Returns the
-// exclusive prefixes. Buckets are dispatched in increasing order (one per wave, no XCD remap),
-// so the lowest unfinished bucket is always resident and never waits: the walk terminates.
-// A bounded spin turns a broken invariant into an error flag instead of a hang.
-constexpr unsigned long long kLbA = 1ull << 62, kLbP = 2ull << 62, kLbV = kLbA - 1;
-constexpr uint32_t kLbSpinLimit = 1u << 16;  // ~0.1 s of polling
-
-__device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long lb_load(unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void lookback(const BucketArgs& A, uint32_t b, int lane, uint32_t ak, uint32_t an,
-                                         uint32_t am, uint64_t& xk, uint64_t& xn, uint64_t& xm) {
-  if (lane == 0) {
-    lb_store(&A.lb_k[b], kLbA | ak);
-    lb_store(&A.lb_n[b], kLbA | an);
-    lb_store(&A.lb_m[b], kLbA | am);
-  }
-  uint64_t acc[3] = {0, 0, 0};
-  bool done[3] = {false, false, false};
-  unsigned long long* st[3] = {A.lb_k, A.lb_n, A.lb_m};
-  int64_t j = (int64_t)b - 1;
-  uint32_t spins = 0;
-  while (j >= 0 && !(done[0] && done[1] && done[2])) {
-    const int64_t q = j - lane;
-    unsigned long long v[3];
-#pragma unroll
-    for (int f = 0; f < 3; ++f) v[f] = q >= 0 ? lb_load(&st[f][q]) : kLbP;  // before bucket 0: prefix 0
-    bool retry = false;
-    int first_p[3];
-#pragma unroll
-    for (int f = 0; f < 3; ++f) {
-      const uint64_t pm = __ballot((v[f] >> 62) == 2), xm_ = __ballot((v[f] >> 62) == 0);
-      first_p[f] = pm ? __builtin_ctzll(pm) : 64;
-      const uint64_t upto_p = first_p[f] >= 63 ? ~0ull : ((2ull << first_p[f]) - 1);
-      retry |= !done[f] && (xm_ & upto_p) != 0;
-    }
-    if (retry) {
-      if (++spins > kLbSpinLimit) {  // cannot happen with in-order dispatch; never hang
-        if (lane == 0) atomicOr(A.lb_err, 1u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-#pragma unroll
-    for (int f = 0; f < 3; ++f) {
-      if (done[f]) continue;
-      acc[f] += wave_sum_u64(lane <= first_p[f] ? (v[f] & kLbV) : 0);
-      done[f] = first_p[f] < 64;
-    }
-    j -= 64;
-  }
-  xk = acc[0];
-  xn = acc[1];
-  xm = acc[2];
-  if (lane == 0) {
-    lb_store(&A.lb_k[b], kLbP | (xk + ak));
-    lb_store(&A.lb_n[b], kLbP | (xn + an));
-    lb_store(&A.lb_m[b], kLbP | (xm + am));
-    if (b + 1 == A.nbuckets) {
-      A.lb_tot[0] = xk + ak;
-      A.lb_tot[1] = xn + an;
-      A.lb_tot[2] = xm + am;
-    }
-  }
-}
-
 // One bucket on one wave, up to 64*KE key rows and 128*KE child rows, from the columns in
 // `in`. KE = 1 leaves buckets over that capacity to bucket_wide_kernel and lists those over
 // ITS capacity (and forced tiers) for the workgroup tier. `next()` runs exactly once, as
@@ -402,17 +245,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   constexpr uint32_t KC = WaveLds<KE>::KC, CC = WaveLds<KE>::CC;
   const BucketArgs& A = W.A;
   const uint32_t K = in.d.K, N = in.d.N, M = in.d.M;
-  // single-pass placement: every bucket of this kernel takes part in the look-back, those
-  // left to another tier with zero counts (their outputs are compacted after that tier)
-  const bool dense = KE == 1 && A.lb_k != nullptr;
-  auto pass_on = [&]() {
-    if (dense) {
-      uint64_t x0, x1, x2;
-      lookback(A, b, lane, 0, 0, 0, x0, x1, x2);
-    }
-  };
   auto push = [&](uint32_t* list, uint32_t* count) {
-    pass_on();
     if (lane == 0) {  // no outputs until the workgroup tier's (a pipelined compaction may read them first)
       A.kout[b] = A.nout[b] = A.mout[b] = 0;
       list[atomicAdd(count, 1u)] = b;
@@ -426,7 +259,6 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     }
     if (K > KC || N + M > CC || A.force_tier == 3) {
       next();
-      pass_on();
       return;
     }
   }
@@ -799,18 +631,8 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     En[e] = __ballot(cemit[e] && knode[e]);
     Em[e] = __ballot(cemit[e] && !knode[e]);
   }
-  // output positions: the bucket's sparse slots (input offsets), or dense offsets from the
-  // look-back over every earlier bucket's output counts
-  uint64_t xk = kb, xn = nb0, xm = mb0;
-  if (dense) {
-    uint32_t an = 0, am = 0;
-#pragma unroll
-    for (int e = 0; e < CE; ++e) {
-      an += __popcll(En[e]);
-      am += __popcll(Em[e]);
-    }
-    lookback(A, b, lane, kout, an, am, xk, xn, xm);
-  }
+  // output positions: the bucket's sparse slots (its input offsets); compact_kernel packs them
+  const uint64_t xk = kb, xn = nb0, xm = mb0;
   uint32_t nbase = 0, mbase = 0;
 #pragma unroll
   for (int e = 0; e < CE; ++e) {
@@ -819,15 +641,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
       const uint64_t o = (knode[e] ? xn : xm) + crank;
       const uint32_t k = (uint32_t)(sw_[e] >> 56) & (KC - 1);
       const uint64_t id2 = knode[e] ? c_v[e] : sid2[e];
-      if (dense) {
-        uint64_t* const* O = knode[e] ? A.dno : A.dmo;
-        O[C_PKH][o] = L.okh[k];
-        O[C_PKF][o] = L.okf[k];
-        O[C_ID1][o] = sid1[e];
-        O[C_ID2][o] = id2;
-        O[C_T][o] = c_t[e];
-        O[C_META][o] = c_m[e];
-      } else {  // one whole 48-B AoS row: three 16-B stores
+      {  // one whole 48-B AoS row: three 16-B stores
         ulonglong2* row = (ulonglong2*)((knode[e] ? A.nos : A.mos) + o * kChildStride);
         row[0] = make_ulonglong2(L.okh[k], L.okf[k]);
         row[1] = make_ulonglong2(sid1[e], id2);
@@ -850,19 +664,9 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
       const uint32_t r = orank[e];
       const uint64_t o = xk + r;
       const uint64_t win = (fam[e] == 0 && o_T[e] == TAG_COUNTER) ? L.osum[r] : o_win[e];
-      // child ranges: bucket-relative (compaction makes them absolute), or absolute already
-      const uint64_t cb = dense ? (o_T[e] == TAG_COUNTER ? xn : xm) : 0;
-      const uint64_t cref = cref_pack(L.ocnt[r] ? cb + L.ocb[r] : 0, L.ocnt[r]);
-      if (dense) {
-        A.dko[O_KH][o] = kh[e];
-        A.dko[O_KF][o] = kf[e];
-        A.dko[O_CT][o] = o_ct[e];
-        A.dko[O_UT][o] = o_ut[e];
-        A.dko[O_DT][o] = o_dt[e];
-        A.dko[O_META][o] = o_meta[e];
-        A.dko[O_WIN][o] = win;
-        A.dko[O_CREF][o] = cref;
-      } else {  // one whole 64-B AoS row: four 16-B stores
+      // child ranges: bucket-relative (compaction makes them absolute)
+      const uint64_t cref = cref_pack(L.ocnt[r] ? L.ocb[r] : 0, L.ocnt[r]);
+      {  // one whole 64-B AoS row: four 16-B stores
         ulonglong2* row = (ulonglong2*)(A.kos + o * kKeyOutCols);
         row[0] = make_ulonglong2(kh[e], kf[e]);
         row[1] = make_ulonglong2(o_ct[e], o_ut[e]);
@@ -871,10 +675,10 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
       }
     }
   }
-  if (lane == 0) {  // a dense bucket leaves nothing for compaction
-    A.kout[b] = dense ? 0 : kout;
-    A.nout[b] = dense ? 0 : nbase;
-    A.mout[b] = dense ? 0 : mbase;
+  if (lane == 0) {
+    A.kout[b] = kout;
+    A.nout[b] = nbase;
+    A.mout[b] = mbase;
   }
   unsigned long long* st = stat_shard(A.stats);
   // per-lane counts are small (<= 64 KE segment rows, <= CE children): summed by bit slices
@@ -900,82 +704,8 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   }
 }
 
-constexpr uint32_t kXcds = 8;
 
-// Every bucket, one wave each (<= 64 key rows, <= 128 child rows per wave). Persistent and
-// software-pipelined (the launch is a multiple of 8 workgroups that fills the chip once):
-//   * workgroups are dispatched round-robin over the 8 XCDs (each with its own L2), so
-//     blockIdx % 8 is the XCD; XCD x owns the contiguous bucket range [x nb/8, (x+1) nb/8),
-//     whose buckets share final partition segments that then stay in that XCD's L2, and its
-//     waves take the range's buckets round-robin (the XCD's waves sweep it together);
-//   * a bucket costs three dependent memory round trips (directory -> row indices ->
-//     columns). While a wave folds bucket i's children, the loads of bucket i+1 are already
-//     in flight: PF = 2 issues its column gathers there (and bucket i+2's row indices), PF = 1
-//     only its row indices (fewer live registers, more resident waves: the gathers are then
-//     issued at the top of the iteration). The directory entries are fetched a bucket ahead.
-template <int PF>
-__device__ __forceinline__ void wave_stream(const WaveArgs& W, WaveLds<1>* lds_all, uint32_t b, uint32_t hi,
-                                            uint32_t stride) {
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const BucketArgs& A = W.A;
-  if (b >= hi) return;
-  // A directory entry is one vector load: lane f < 6 reads field f, then readlane.
-  const uint32_t* dir_f = lane == 0 ? A.kcnt : lane == 1 ? A.ncnt : lane == 2 ? A.mcnt
-                        : lane == 3 ? A.kbase : lane == 4 ? A.nbase : A.mbase;
-  auto dir_issue = [&](uint32_t bb) -> uint32_t { return (lane < 6 && bb < hi) ? dir_f[bb] : 0u; };
-  auto dir_take = [&](uint32_t v) {
-    WaveDir d;
-    d.K = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
-    d.N = (uint32_t)__builtin_amdgcn_readlane((int)v, 1);
-    d.M = (uint32_t)__builtin_amdgcn_readlane((int)v, 2);
-    d.kb = (uint32_t)__builtin_amdgcn_readlane((int)v, 3);
-    d.nb0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 4);
-    d.mb0 = (uint32_t)__builtin_amdgcn_readlane((int)v, 5);
-    return d;
-  };
-  WaveIn<1> cur;
-  WavePerm<1> p;
-  if (PF == 2) {
-    WaveDir dn;  // directory of the next bucket (its row indices are in p)
-    {
-      const WaveDir d0 = dir_take(dir_issue(b));
-      load_perm<1>(A, d0, lane, p);
-      load_cols<1>(A, d0, p, lane, cur);
-      dn = dir_take(dir_issue(b + stride));
-      load_perm<1>(A, dn, lane, p);
-    }
-    uint32_t dv = dir_issue(b + 2 * stride);
-    for (;;) {
-      const uint32_t bn = b + stride;
-      wave_bucket<1>(W, lds_all[wv], b, lane, cur, [&]() {
-        // dv is the oldest load in flight: take it before issuing the column gathers, so
-        // that waiting for it never waits for them
-        const WaveDir dnn = dir_take(dv);
-        load_cols<1>(A, dn, p, lane, cur);  // bucket bn (no loads past the range: empty dir)
-        load_perm<1>(A, dnn, lane, p);      // bucket bn + stride
-        dn = dnn;
-        dv = dir_issue(bn + 2 * stride);
-      });
-      if (bn >= hi) break;
-      b = bn;
-    }
-  } else {
-    WaveDir dc = dir_take(dir_issue(b));  // this bucket (its row indices are in p)
-    load_perm<1>(A, dc, lane, p);
-    uint32_t dv = dir_issue(b + stride);
-    for (;;) {
-      const uint32_t bn = b + stride;
-      load_cols<1>(A, dc, p, lane, cur);
-      wave_bucket<1>(W, lds_all[wv], b, lane, cur, [&]() {
-        dc = dir_take(dv);             // bucket bn
-        load_perm<1>(A, dc, lane, p);
-        dv = dir_issue(bn + stride);
-      });
-      if (bn >= hi) break;
-      b = bn;
-    }
-  }
-}
+constexpr uint32_t kXcds = 8;
 
 // Workgroups are dispatched round-robin over the 8 XCDs (each with its own L2). Remap so
 // that XCD x runs one contiguous range of blocks: neighbouring buckets share a final
@@ -985,50 +715,22 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t i, uint32_t G) {
   return x * q + min(x, r) + j;
 }
 
-// G > 0: each wave runs G consecutive buckets (the grid covers every bucket once, in
-// dispatch order, so the chip's active buckets stay a narrow window of the bucket range);
-// G == 0: persistent grid, XCD x sweeps [x nb/8, (x+1) nb/8) with its waves round-robin.
-template <int PF>
-__device__ __forceinline__ void wave_dispatch(const WaveArgs& W, WaveLds<1>* lds_all, uint32_t G) {
-  const int wv = threadIdx.x >> 6;
-  if (G) {
-    const uint32_t b0 = (xcd_block(blockIdx.x, gridDim.x) * kWavesPerWG + wv) * G;
-    wave_stream<PF>(W, lds_all, b0, min(W.nbuckets, b0 + G), 1);
-  } else {
-    const uint32_t x = blockIdx.x % kXcds;
-    const uint32_t lo = (uint32_t)((uint64_t)W.nbuckets * x / kXcds);
-    const uint32_t hi = (uint32_t)((uint64_t)W.nbuckets * (x + 1) / kXcds);
-    wave_stream<PF>(W, lds_all, lo + (blockIdx.x / kXcds) * kWavesPerWG + wv, hi,
-                    (gridDim.x / kXcds) * kWavesPerWG);
-  }
-}
-
 // One bucket per wave, no loop: the fewest live registers and so the most resident waves
-// (5 per SIMD), which is what hides the bucket's memory round trips best (measured: the
-// pipelined variants below lose more to their lower occupancy than they gain).
+// (5 per SIMD), which is what hides the bucket's memory round trips best (software-pipelined
+// variants that prefetched the next bucket lost more to their lower occupancy than they gained;
+// DESIGN.md §4a').
 __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_kernel(WaveArgs W) {
   __shared__ WaveLds<1> lds_all[kWavesPerWG];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  // buckets in dispatch order (the look-back relies on it; an XCD remap measured no faster
-  // with whole-row reads)
+  // buckets in dispatch order (an XCD remap measured no faster with whole-row reads)
   const uint32_t b = W.blo + blockIdx.x * kWavesPerWG + wv;
   if (b >= W.bhi) return;
   const WaveDir d = load_dir(W.A, b);
   WavePerm<1> p;
   WaveIn<1> in;
   load_perm<1>(W.A, d, lane, p);
-  if (kCoopLoads) load_cols_coop<1>(W.A, d, p, lane, in, lds_all[wv]);
-  else load_cols<1>(W.A, d, p, lane, in);
+  load_cols<1>(W.A, d, p, lane, in);
   wave_bucket<1>(W, lds_all[wv], b, lane, in, []() {});
-}
-
-__global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_pf2_kernel(WaveArgs W, uint32_t G) {
-  __shared__ WaveLds<1> lds_all[kWavesPerWG];
-  wave_dispatch<2>(W, lds_all, G);
-}
-__global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wave_pf1_kernel(WaveArgs W, uint32_t G) {
-  __shared__ WaveLds<1> lds_all[kWavesPerWG];
-  wave_dispatch<1>(W, lds_all, G);
 }
 
 // Buckets over bucket_wave_kernel's capacity but within this kernel's.
@@ -1057,8 +759,7 @@ __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_kernel(WaveArgs 
       WavePerm<2> p;
       WaveIn<2> in;
       load_perm<2>(W.A, d, lane, p);
-      if (kCoopLoads) load_cols_coop<2>(W.A, d, p, lane, in, lds_all[wv]);
-      else load_cols<2>(W.A, d, p, lane, in);
+      load_cols<2>(W.A, d, p, lane, in);
       wave_bucket<2>(W, lds_all[wv], bb, lane, in, []() {});
     }
   }

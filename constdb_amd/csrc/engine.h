@@ -25,7 +25,6 @@ struct cdb_ctx {
   std::string last_error;
   struct Buf { void* p = nullptr; size_t bytes = 0; };
   Buf ws[48];  // named workspace slots, grown on demand, reused across calls
-  uint32_t wave_slots[2] = {0, 0};
   void* pin = nullptr;                                // pinned staging ring of host<->device copies
   hipEvent_t pin_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   uint64_t pin_next = 0;                              // next slot of the ring (continues across calls)
@@ -50,7 +49,6 @@ enum WsSlot {
   WS_PERM,                                              // final-level row permutations (u32)
   WS_STATS,                                             // statistic shards
   WS_KHCOL,                                             // key-hash column of the row level
-  WS_LOOKBACK,                                          // output look-back status words
   WS_HOST_IN_K, WS_HOST_IN_N, WS_HOST_IN_M,             // cdb_merge: uploaded batches
   WS_HOST_OUT_K, WS_HOST_OUT_N, WS_HOST_OUT_M,          // cdb_merge: device-side result
   WS_RUNDIR, WS_RUNMISC,                                // sorted-run path: run directories, gap lists

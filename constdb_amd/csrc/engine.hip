@@ -119,7 +119,7 @@ struct CompactArgs {
   uint64_t* nd[kNodeCols];
   uint64_t* md[kMemberCols];
   const uint32_t *kbase, *nbase, *mbase, *kout, *nout, *mout, *kdoff, *ndoff, *mdoff;
-  const unsigned long long* base_tot;  // dense rows already placed by the wave tier, per family
+  const unsigned long long* base_tot;  // dense row base per family (a pipelined range's; else zero)
   uint64_t cap[3];                     // rows of each family's sparse slots and dense output
   uint32_t* err;                       // set when an index falls outside them
   const uint32_t* skip_if;             // pipelined ranges: nothing to do once a bucket went to a
@@ -298,17 +298,9 @@ struct Plan {
   bool seg_final = false;  // the last level runs per row-level segment (part_final_kernel)
 };
 
-// Tile of the row-level scatter (CDB_AOS_TILE = 1024 or 2048).
-int aos_tile() {
-  static const int t = [] {
-    const char* e = std::getenv("CDB_AOS_TILE");
-    const int v = e ? std::atoi(e) : 1024;
-    return v == 2048 || v == 512 ? v : 1024;
-  }();
-  return t;
-}
-
 Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
+  // Test hooks (the only environment knobs of the merge): CDB_PLAN_TARGET / CDB_PLAN_CTARGET
+  // override the key / child rows per bucket, so that tests can push buckets into given tiers.
   // Wave-sized buckets: ~40 key rows and at most ~80 child rows (nodes + members) on average.
   // A wave holds 64 key rows (128 in the wide kernel) and 128 child rows, so only the
   // far tail of the bucket-size distribution reaches the workgroup tier. A key's children never
@@ -329,18 +321,16 @@ Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
   // The last level moves only a row index, so it takes a large fan-out (segments of
   // ~d_last buckets, a few hundred KB, stay cache-resident for the bucket kernels' gathers)
   // and the column-moving levels get small fan-outs (long contiguous write runs).
-  uint32_t dlast = 256;
-  if (const char* e = std::getenv("CDB_PLAN_DLAST")) dlast = (uint32_t)std::max(2, std::min(512, std::atoi(e)));
+  const uint32_t dlast = 256;
   // Mode 2 (default): ONE moving level of fan-out d0 <= 2048 that writes rows, then the
   // per-segment final level (fan-out d1 <= 8192). Segments are then ~13 MB (all families): the
   // bucket kernels' row reads come from the Infinity Cache, one line per row, instead of
   // needing a second full column-moving pass to make segments L2-sized (mode 1).
-  int mode = 2;
-  if (const char* e = std::getenv("CDB_PLAN_MODE")) mode = std::atoi(e);
-  uint64_t d0pref = 768;  // measured on the C4 shard: 768 < 1024 < 512 < 2048 ms/step
-  if (const char* e = std::getenv("CDB_PLAN_D0")) d0pref = (uint64_t)std::max(64, std::min(2048, std::atoi(e)));
-  const uint64_t dcap = aos_tile() == 2048 ? 2048 : 1024;  // local digit slots of the row-level kernel
-  if (mode == 2 && want > 4096 && want <= dcap * kFinalMaxD) {
+  // (Mode 1, SoA levels before the row level so that segments are L2-sized, is what remains for
+  // inputs too small or too large for mode 2.)
+  const uint64_t d0pref = 768;  // measured on the C4 shard: 768 < 1024 < 512 < 2048 ms/step
+  const uint64_t dcap = 1024;   // local digit slots of the row-level kernel
+  if (want > 4096 && want <= dcap * kFinalMaxD) {
     p.levels = 2;
     p.seg_final = true;
     const uint64_t d0min = (want + kFinalMaxD - 1) / kFinalMaxD;
@@ -427,15 +417,8 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const
         // before a per-segment final level, leave each row's u16 digit in place of the key hash
         uint16_t* dig = plan.seg_final ? reinterpret_cast<uint16_t*>(khcol) : nullptr;
         const uint32_t d1 = plan.seg_final ? plan.d[l + 1] : 0;
-        if (aos_tile() == 2048)
-          part_scatter_aos_kernel<NC, W, 2048, 2048><<<(n + 2047) / 2048, kPartThreads, 0, s>>>(
-              ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor, dig, d1);
-        else if (aos_tile() == 512)
-          part_scatter_aos_kernel<NC, W, 512, 1024><<<(n + 511) / 512, kPartThreads, 0, s>>>(
-              ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor, dig, d1);
-        else
-          part_scatter_aos_kernel<NC, W, 1024, 1024><<<(n + 1023) / 1024, kPartThreads, 0, s>>>(
-              ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor, dig, d1);
+        part_scatter_aos_kernel<NC, W, 1024, 1024><<<(n + 1023) / 1024, kPartThreads, 0, s>>>(
+            ci, dst[0], khcol, n, nprev, plan.d[l], shift, d.cursor, dig, d1);
         CDB_TRY(launch_check(ctx, s, "partition (row level)"));
         *rows = dst[0];
         for (int c = 0; c < NC; ++c) spare[c] = (dst == A ? Bf : A)[c];
@@ -448,46 +431,6 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const
     nprev = ncur;
   }
   return CDB_OK;
-}
-
-// Wave-kernel variant (CDB_WAVE_PF, default 0): 0 = one bucket per wave (bucket_wave_kernel);
-// 1 / 2 = the software-pipelined kernels, which prefetch the next bucket's row indices (1)
-// or also its columns (2) and run CDB_WAVE_G buckets per wave (0 = a persistent grid).
-int wave_pf() {
-  static const int pf = [] {
-    const char* e = std::getenv("CDB_WAVE_PF");
-    return e ? std::max(0, std::min(2, std::atoi(e))) : 0;
-  }();
-  return pf;
-}
-
-uint32_t wave_g() {
-  static const uint32_t g = [] {
-    const char* e = std::getenv("CDB_WAVE_G");
-    return e ? (uint32_t)std::max(0, std::min(64, std::atoi(e))) : 8u;
-  }();
-  return g;
-}
-
-uint32_t wave_grid(cdb_ctx* ctx, uint64_t nb) {
-  const int pf = wave_pf();
-  if (pf == 0) return (uint32_t)((nb + kWavesPerWG - 1) / kWavesPerWG);
-  if (const uint32_t G = wave_g()) return (uint32_t)((nb + (uint64_t)G * kWavesPerWG - 1) / ((uint64_t)G * kWavesPerWG));
-  const int v = pf - 1;
-  if (!ctx->wave_slots[v]) {  // persistent: every resident workgroup slot once, a multiple of 8
-    int cus = 0, per_cu = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus < 1)
-      cus = 256;
-    const hipError_t e = v ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bucket_wave_pf2_kernel,
-                                                                         kWavesPerWG * 64, 0)
-                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bucket_wave_pf1_kernel,
-                                                                         kWavesPerWG * 64, 0);
-    if (e != hipSuccess || per_cu < 1) per_cu = 1;
-    ctx->wave_slots[v] = (uint32_t)(cus * per_cu);
-  }
-  const uint64_t want = (nb + kWavesPerWG - 1) / kWavesPerWG;
-  const uint64_t g = std::min<uint64_t>(ctx->wave_slots[v], want);
-  return (uint32_t)std::max<uint64_t>(kXcds, (g + kXcds - 1) / kXcds * kXcds);
 }
 
 }  // namespace
@@ -612,68 +555,13 @@ cdb_status radix_sort_pairs(cdb_ctx* ctx, uint64_t** k, uint32_t** v, uint64_t* 
   return CDB_OK;
 }
 
-// Buckets beyond the workgroup tier's LDS pool (the mid kernel lists them). Buckets whose keys fit
-// the pool take the chip-wide child path (hot.hip.h); any other (more than kCapK key rows in one
-// bucket, or CDB_HOT_LEGACY set) runs the whole bucket algorithm on one workgroup over a global
-// scratch slab (bucket_hot_kernel).
-cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list, uint32_t hot, hipStream_t s) {
+// The chip-wide child path (hot.hip.h) over one batch of buckets: ids in ascending order, their
+// key rows (prefix hk_off) and child rows (prefix c_off); tk < 2^23 key rows and tc < 2^32 child
+// rows in the batch (the key table's index width in the sort tag and the child row indices).
+cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& wide_ids,
+                     const std::vector<uint32_t>& hk_off, const std::vector<uint32_t>& c_off, uint64_t tk,
+                     uint64_t tc, uint64_t cmax, hipStream_t s) {
   cdb_status st = CDB_OK;
-  uint32_t* d_cnt3 = (uint32_t*)ws_get(ctx, WS_HOTC3, 4ull * hot * sizeof(uint32_t), &st);
-  if (!d_cnt3) return st;
-  hot_counts_kernel<<<(hot + 255) / 256, 256, 0, s>>>(A, d_hot_list, hot, d_cnt3);
-  CDB_TRY(launch_check(ctx, s, "hot_counts_kernel"));
-  std::vector<uint32_t> ids(hot), cnt3(3ull * hot);
-  CDB_HIP(hipMemcpyAsync(ids.data(), d_hot_list, hot * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");
-  CDB_HIP(hipMemcpyAsync(cnt3.data(), d_cnt3, 3ull * hot * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");
-  CDB_HIP(hipStreamSynchronize(s), "sync");
-  std::vector<uint32_t> order(hot);
-  for (uint32_t i = 0; i < hot; ++i) order[i] = i;
-  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return ids[a] < ids[b]; });
-  static const bool legacy_env = std::getenv("CDB_HOT_LEGACY") != nullptr;
-  const bool legacy_all = legacy_env || A.force_tier == 4;
-  std::vector<uint32_t> wide_ids, legacy;  // wide: the chip-wide child path
-  std::vector<uint32_t> hk_off(1, 0), c_off(1, 0);
-  std::vector<uint32_t> lk, ln, lm;
-  uint64_t tk = 0, tc = 0, cmax = 0;
-  for (uint32_t i : order) {
-    const uint32_t K = cnt3[3 * i], N = cnt3[3 * i + 1], M = cnt3[3 * i + 2];
-    if (!legacy_all && K <= (uint32_t)kCapK && tk + K < (1ull << 23) && tc + N + M < (1ull << 32)) {
-      wide_ids.push_back(ids[i]);
-      tk += K;
-      tc += N + M;
-      cmax = std::max<uint64_t>(cmax, N + M);
-      hk_off.push_back((uint32_t)tk);
-      c_off.push_back((uint32_t)tc);
-    } else {
-      legacy.push_back(ids[i]);
-      lk.push_back(K);
-      ln.push_back(N);
-      lm.push_back(M);
-    }
-  }
-  if (!legacy.empty()) {
-    const uint32_t nl = (uint32_t)legacy.size();
-    std::vector<uint64_t> off(nl);
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < nl; ++i) {
-      off[i] = total;
-      total += hot_scratch_words(lk[i], std::max(ln[i], lm[i]));
-      total = (total + 15) & ~uint64_t(15);
-    }
-    uint8_t* slab = (uint8_t*)ws_get(ctx, WS_HOT, total * 8 + nl * 12 + 64, &st);
-    if (!slab) return st;
-    uint64_t* d_off = (uint64_t*)(slab + total * 8);
-    uint32_t* d_ids = (uint32_t*)(d_off + nl);
-    CDB_HIP(hipMemcpyAsync(d_off, off.data(), nl * 8, hipMemcpyHostToDevice, s), "h2d");
-    CDB_HIP(hipMemcpyAsync(d_ids, legacy.data(), nl * 4, hipMemcpyHostToDevice, s), "h2d");
-    A.hot_in = d_ids;
-    A.hot_scratch = (uint64_t*)slab;
-    A.hot_scratch_off = d_off;
-    bucket_hot_kernel<<<nl, kBktThreads, 0, s>>>(A);
-    CDB_TRY(launch_check(ctx, s, "bucket_hot_kernel"));
-    CDB_HIP(hipStreamSynchronize(s), "sync");  // the host vectors above are copy sources
-  }
-  if (wide_ids.empty()) return CDB_OK;
   const uint32_t H = (uint32_t)wide_ids.size();
   // device: ids[H] | hk_off[H + 1] | c_off[H + 1] | hk_kout[H] | h_first[H] | run count
   uint32_t* meta = (uint32_t*)ws_get(ctx, WS_HOTMETA, (5ull * H + 6) * sizeof(uint32_t), &st);
@@ -699,11 +587,11 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   int gbits = 0, cbits = 0;
   while (gbits < 32 && (tk >> gbits)) ++gbits;
   while (cbits < 40 && (cmax >> cbits)) ++cbits;
-  int min_id = std::max(kHotMinIdBits, cbits + 9);
-  if (const char* e = std::getenv("CDB_HOT_MIN_ID_BITS")) min_id = std::max(1, std::atoi(e));
+  const int min_id = std::max(kHotMinIdBits, cbits + 9);
   const int passes = (gbits + 6 + std::min(min_id, kHotIdBits - 6) + 7) / 8;
   int id_bits = std::min(kHotIdBits - 6, 8 * passes - 6 - gbits);
-  if (const char* e = std::getenv("CDB_HOT_ID_BITS")) {  // tests: fewer id bits force the collision path
+  // test hook: fewer id bits force the collision (successor-selection) fold
+  if (const char* e = std::getenv("CDB_HOT_ID_BITS")) {
     const int bits = std::atoi(e);
     if (bits >= 1 && bits <= kHotIdBits - 6) id_bits = bits;
   }
@@ -771,7 +659,90 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   }
   hot_finish_kernel<<<H, 256, 0, s>>>(A, HA);
   CDB_TRY(launch_check(ctx, s, "hot_finish_kernel"));
-  CDB_HIP(hipStreamSynchronize(s), "sync");  // the host vectors above are copy sources
+  CDB_HIP(hipStreamSynchronize(s), "sync");  // the host vectors are copy sources
+  return CDB_OK;
+}
+
+// Buckets beyond the workgroup tier's LDS pool (the mid kernel lists them), and the mid tier's
+// buckets when there are many. Buckets whose keys fit the pool take the chip-wide child path, in
+// batches of fewer than kHotKeyCap key rows (the key table's index width): a child-heavy input of
+// any size stays on it. A bucket of more than kCapK key rows (or force_tier 4) runs the whole
+// bucket algorithm on one workgroup over a global scratch slab (bucket_hot_kernel).
+constexpr uint64_t kHotKeyCap = 1ull << 23;
+
+cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list, uint32_t hot, hipStream_t s) {
+  cdb_status st = CDB_OK;
+  uint32_t* d_cnt3 = (uint32_t*)ws_get(ctx, WS_HOTC3, 4ull * hot * sizeof(uint32_t), &st);
+  if (!d_cnt3) return st;
+  hot_counts_kernel<<<(hot + 255) / 256, 256, 0, s>>>(A, d_hot_list, hot, d_cnt3);
+  CDB_TRY(launch_check(ctx, s, "hot_counts_kernel"));
+  std::vector<uint32_t> ids(hot), cnt3(3ull * hot);
+  CDB_HIP(hipMemcpyAsync(ids.data(), d_hot_list, hot * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");
+  CDB_HIP(hipMemcpyAsync(cnt3.data(), d_cnt3, 3ull * hot * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");
+  CDB_HIP(hipStreamSynchronize(s), "sync");
+  std::vector<uint32_t> order(hot);
+  for (uint32_t i = 0; i < hot; ++i) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return ids[a] < ids[b]; });
+  // test hook: a smaller batch cap runs the chip-wide path in many batches on small inputs
+  static const uint64_t key_cap = [] {
+    const char* e = std::getenv("CDB_HOT_KEY_CAP");
+    return e ? std::max<uint64_t>(kCapK + 1, std::min<uint64_t>(kHotKeyCap, std::strtoull(e, nullptr, 10)))
+             : kHotKeyCap;
+  }();
+  const bool legacy_all = A.force_tier == 4;
+  std::vector<uint32_t> wide_ids, legacy;  // wide: the chip-wide child path
+  std::vector<uint32_t> hk_off(1, 0), c_off(1, 0);
+  std::vector<uint32_t> lk, ln, lm;
+  uint64_t tk = 0, tc = 0, cmax = 0;
+  auto flush = [&]() -> cdb_status {
+    if (wide_ids.empty()) return CDB_OK;
+    const cdb_status r = chip_wide(ctx, A, wide_ids, hk_off, c_off, tk, tc, cmax, s);
+    wide_ids.clear();
+    hk_off.assign(1, 0);
+    c_off.assign(1, 0);
+    tk = tc = cmax = 0;
+    return r;
+  };
+  for (uint32_t i : order) {
+    const uint32_t K = cnt3[3 * i], N = cnt3[3 * i + 1], M = cnt3[3 * i + 2];
+    if (legacy_all || K > (uint32_t)kCapK) {
+      legacy.push_back(ids[i]);
+      lk.push_back(K);
+      ln.push_back(N);
+      lm.push_back(M);
+      continue;
+    }
+    if (tk + K >= key_cap || tc + N + M >= (1ull << 32)) CDB_TRY(flush());
+    wide_ids.push_back(ids[i]);
+    tk += K;
+    tc += N + M;
+    cmax = std::max<uint64_t>(cmax, N + M);
+    hk_off.push_back((uint32_t)tk);
+    c_off.push_back((uint32_t)tc);
+  }
+  CDB_TRY(flush());
+  if (!legacy.empty()) {
+    const uint32_t nl = (uint32_t)legacy.size();
+    std::vector<uint64_t> off(nl);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < nl; ++i) {
+      off[i] = total;
+      total += hot_scratch_words(lk[i], std::max(ln[i], lm[i]));
+      total = (total + 15) & ~uint64_t(15);
+    }
+    uint8_t* slab = (uint8_t*)ws_get(ctx, WS_HOT, total * 8 + nl * 12 + 64, &st);
+    if (!slab) return st;
+    uint64_t* d_off = (uint64_t*)(slab + total * 8);
+    uint32_t* d_ids = (uint32_t*)(d_off + nl);
+    CDB_HIP(hipMemcpyAsync(d_off, off.data(), nl * 8, hipMemcpyHostToDevice, s), "h2d");
+    CDB_HIP(hipMemcpyAsync(d_ids, legacy.data(), nl * 4, hipMemcpyHostToDevice, s), "h2d");
+    A.hot_in = d_ids;
+    A.hot_scratch = (uint64_t*)slab;
+    A.hot_scratch_off = d_off;
+    bucket_hot_kernel<<<nl, kBktThreads, 0, s>>>(A);
+    CDB_TRY(launch_check(ctx, s, "bucket_hot_kernel"));
+    CDB_HIP(hipStreamSynchronize(s), "sync");  // the host vectors above are copy sources
+  }
   return CDB_OK;
 }
 }  // namespace
@@ -812,17 +783,17 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   Dir dnd{dir + 5 * dn, dir + 6 * dn, dir + 7 * dn, dir + 8 * dn, dir + 9 * dn};
   Dir dm{dir + 10 * dn, dir + 11 * dn, dir + 12 * dn, dir + 13 * dn, dir + 14 * dn};
   // misc: stats[8] u64 | last_bad u64 | totals[3] u64 | hot_count u32 | big_count u32 | compaction error u32 |
-  //       hot_list[nb] u32 | big_list[nb] u32
-  uint8_t* misc = (uint8_t*)ws_get(ctx, WS_MISC, 128 + 2 * nb * sizeof(uint32_t), &st);
+  //       pipelined compaction error u32 | (112) | zero[3] u64 at 128 | hot_list[nb] u32 at 160 | big_list[nb] u32
+  uint8_t* misc = (uint8_t*)ws_get(ctx, WS_MISC, 160 + 2 * nb * sizeof(uint32_t), &st);
   if (!misc) return st;
   unsigned long long* d_stats = (unsigned long long*)misc;
   unsigned long long* d_last_bad = (unsigned long long*)(misc + 64);
   uint64_t* d_totals = (uint64_t*)(misc + 72);
   uint32_t* d_hot_count = (uint32_t*)(misc + 96);
   uint32_t* d_big_count = (uint32_t*)(misc + 100);
-  uint32_t* d_hot_list = (uint32_t*)(misc + 128);
+  uint32_t* d_hot_list = (uint32_t*)(misc + 160);
   uint32_t* d_big_list = d_hot_list + nb;
-  CDB_HIP(hipMemsetAsync(misc, 0, 128, s), "memset misc");
+  CDB_HIP(hipMemsetAsync(misc, 0, 160, s), "memset misc");
   unsigned long long* d_shards =
       (unsigned long long*)ws_get(ctx, WS_STATS, kStatShards * kStatStride * sizeof(unsigned long long), &st);
   if (!d_shards) return st;
@@ -848,8 +819,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   RunView RV;
   std::memset(&RV, 0, sizeof RV);
   bool use_runs = false;
-  static const bool no_runs = std::getenv("CDB_NO_RUNS") != nullptr;
-  if (in->n_runs && !no_runs) {
+  if (in->n_runs) {
     const Dir dirs[3] = {dk, dnd, dm};
     CDB_TRY(runs_directory(ctx, in, nb, shift, dirs, &RV, &use_runs, s));
   }
@@ -867,56 +837,26 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   if (!khcol) return st;
   // the three families partition independently (own buffers, directories, scan scratch):
   // nodes and members run on side streams beside the keys
-  static const bool part_serial = std::getenv("CDB_PART_SERIAL") != nullptr;
-  hipStream_t sn = part_serial ? s : ctx->side, sm = part_serial ? s : ctx->side2;
-  if (!part_serial) {
-    CDB_HIP(hipEventRecord(ctx->ev_pfork, s), "event");
-    CDB_HIP(hipStreamWaitEvent(sn, ctx->ev_pfork, 0), "wait");
-    CDB_HIP(hipStreamWaitEvent(sm, ctx->ev_pfork, 0), "wait");
-  }
+  hipStream_t sn = ctx->side, sm = ctx->side2;
+  CDB_HIP(hipEventRecord(ctx->ev_pfork, s), "event");
+  CDB_HIP(hipStreamWaitEvent(sn, ctx->ev_pfork, 0), "wait");
+  CDB_HIP(hipStreamWaitEvent(sm, ctx->ev_pfork, 0), "wait");
   CDB_TRY(partition_family<kKeyCols, kKeyStride>(ctx, kin, K, plan, shift, KA, KB, dk, &krows, ksp, khcol, kperm, s,
                                                  WS_SCAN));
   CDB_TRY(partition_family<kNodeCols, kChildStride>(ctx, nin, N, plan, shift, NA, NB, dnd, &nrows, nsp, khcol + K,
                                                     nperm, sn, WS_SCAN2));
   CDB_TRY(partition_family<kMemberCols, kChildStride>(ctx, min_, M, plan, shift, MA, MBf, dm, &mrows, msp,
                                                       khcol + K + N, mperm, sm, WS_SCAN3));
-  if (!part_serial) {
-    CDB_HIP(hipEventRecord(ctx->ev_pn, sn), "event");
-    CDB_HIP(hipEventRecord(ctx->ev_pm, sm), "event");
-    CDB_HIP(hipStreamWaitEvent(s, ctx->ev_pn, 0), "wait");
-    CDB_HIP(hipStreamWaitEvent(s, ctx->ev_pm, 0), "wait");
-  }
+  CDB_HIP(hipEventRecord(ctx->ev_pn, sn), "event");
+  CDB_HIP(hipEventRecord(ctx->ev_pm, sm), "event");
+  CDB_HIP(hipStreamWaitEvent(s, ctx->ev_pn, 0), "wait");
+  CDB_HIP(hipStreamWaitEvent(s, ctx->ev_pm, 0), "wait");
   {  // sparse key outputs (8 columns) go to the ping-pong buffer that does not hold the rows
     uint64_t* const* free_k = (krows == KA[0]) ? KB : KA;
     for (int c = 0; c < 8; ++c) ksp[c] = free_k[c];
   }
   }  // partition path
 
-  if (!use_runs && std::getenv("CDB_VERIFY_PARTITION")) {  // debugging aid: perm must be a permutation
-    CDB_HIP(hipStreamSynchronize(s), "sync");
-    const uint64_t fam_n[3] = {K, N, M};
-    const uint32_t* fam_p[3] = {kperm, nperm, mperm};
-    const Dir* fam_d[3] = {&dk, &dnd, &dm};
-    for (int f = 0; f < 3; ++f) {
-      const uint64_t n = fam_n[f];
-      if (!n) continue;
-      std::vector<uint32_t> hp(n), hb(nb), hc(nb);
-      CDB_HIP(hipMemcpy(hp.data(), fam_p[f], n * 4, hipMemcpyDeviceToHost), "d2h");
-      CDB_HIP(hipMemcpy(hb.data(), fam_d[f]->base, nb * 4, hipMemcpyDeviceToHost), "d2h");
-      CDB_HIP(hipMemcpy(hc.data(), fam_d[f]->hist, nb * 4, hipMemcpyDeviceToHost), "d2h");
-      std::vector<uint8_t> seen(n, 0);
-      uint64_t bad = 0, tot = 0;
-      for (uint64_t i = 0; i < n; ++i) {
-        if (hp[i] >= n || seen[hp[i]]) ++bad;
-        else seen[hp[i]] = 1;
-      }
-      for (uint64_t b = 0; b < nb; ++b) tot += hc[b];
-      if (bad || tot != n)
-        return fail(ctx, CDB_DEVICE_ERROR, "partition verify: family " + std::to_string(f) + " n=" + std::to_string(n) +
-                                               " bad=" + std::to_string(bad) + " total=" + std::to_string(tot) +
-                                               " levels=" + std::to_string(plan.levels) + " nb=" + std::to_string(nb));
-    }
-  }
   CDB_HIP(hipEventRecord(ctx->ev_part, s), "event");
   // ---- 2. GC watermark scan (DB::gc's LIFO stop point)
   if ((flags & CDB_MERGE_GC_DELETES) && K) {
@@ -958,32 +898,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   A.stats = d_shards;
   A.hot_list = d_hot_list;
   A.hot_count = d_hot_count;
-  // look-back status words (3 x nb) | wave-tier totals (3) | error flag. Off by default
-  // (CDB_LOOKBACK=1 turns it on): it removes the compaction of the wave tier's rows (finish
-  // 6.6 -> 0.8 ms on the C4 shard) but a bucket's counts are known only at its very end, so
-  // waves queue behind their slowest predecessor and the bucket phase goes 19 -> 48 ms.
-  static const bool lookback_on = [] {
-    const char* e = std::getenv("CDB_LOOKBACK");
-    return e && std::atoi(e) == 1;
-  }();
-  const bool dense = lookback_on && wave_pf() == 0;
-  unsigned long long* lbw =
-      (unsigned long long*)ws_get(ctx, WS_LOOKBACK, (3 * nb + 4) * sizeof(unsigned long long) + 64, &st);
-  if (!lbw) return st;
-  unsigned long long* d_lb_tot = lbw + 3 * nb;  // zero unless the wave tier places rows
-  CDB_HIP(hipMemsetAsync(lbw, 0, (3 * nb + 4) * sizeof(unsigned long long), s), "memset lookback");
-  if (dense) {
-    A.lb_k = lbw;
-    A.lb_n = lbw + nb;
-    A.lb_m = lbw + 2 * nb;
-    A.lb_tot = d_lb_tot;
-    A.lb_err = (uint32_t*)(d_lb_tot + 3);
-    for (int c = 0; c < kKeyOutCols; ++c) A.dko[c] = out->keys.col[c];
-    for (int c = 0; c < kNodeCols; ++c) {
-      A.dno[c] = out->nodes.col[c];
-      A.dmo[c] = out->members.col[c];
-    }
-  }
+  // zero dense bases of the compaction (a pipelined range adds its range base instead)
+  const unsigned long long* d_zero3 = (const unsigned long long*)(misc + 128);
   WaveArgs WA;
   WA.A = A;
   WA.nbuckets = (uint32_t)nb;
@@ -997,15 +913,11 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   // into the dense outputs on stream cs while range p + 1 merges: the tiers are VALU-bound and
   // the compaction HBM-bound, so the two overlap. Only valid when no bucket goes to a workgroup
   // tier (those add outputs after every range): then everything is compacted again at the end.
-  static const uint32_t pipe_env = [] {
-    const char* e = std::getenv("CDB_PIPE");
-    return e ? (uint32_t)std::max(1, std::atoi(e)) : 8u;
-  }();
   // (small merges: the ranges' extra launches cost more than the overlap wins; C1 0.8 -> 1.6 ms)
+  constexpr uint32_t kPipeRanges = 8;
   const uint32_t pipe_opt = opts ? opts->pipe_ranges : 0;
-  const uint32_t P = (dense || wave_pf() != 0) ? 1
-                     : pipe_opt ? (uint32_t)std::min<uint64_t>(pipe_opt, std::max<uint64_t>(nb, 1))
-                     : (K + N + M < (64ull << 20) || nb < 64ull * pipe_env) ? 1 : pipe_env;
+  const uint32_t P = pipe_opt ? (uint32_t)std::min<uint64_t>(pipe_opt, std::max<uint64_t>(nb, 1))
+                     : (K + N + M < (64ull << 20) || nb < 64ull * kPipeRanges) ? 1 : kPipeRanges;
   const bool pipelined = P > 1;
   CompactArgs C;
   C.ks = ksp[0];
@@ -1019,7 +931,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   C.kbase = dk.base; C.nbase = dnd.base; C.mbase = dm.base;
   C.kout = dk.out; C.nout = dnd.out; C.mout = dm.out;
   C.kdoff = dk.doff; C.ndoff = dnd.doff; C.mdoff = dm.doff;
-  C.base_tot = d_lb_tot;
+  C.base_tot = d_zero3;
   C.cap[0] = K;
   C.cap[1] = N;
   C.cap[2] = M;
@@ -1028,26 +940,15 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   C.err = d_cerr;
   C.skip_if = nullptr;
   uint64_t* d_pipe = nullptr;  // [P + 1][3] dense bases | [P][3] range totals
-  static const bool wide_serial = std::getenv("CDB_WIDE_SERIAL") != nullptr;
-  hipStream_t ws = wide_serial ? s : ctx->side;
+  hipStream_t ws = ctx->side;
   hipStream_t cs = ctx->side2;
-  if (!wide_serial) CDB_HIP(hipStreamWaitEvent(ws, ctx->ev_fork, 0), "wait");
+  CDB_HIP(hipStreamWaitEvent(ws, ctx->ev_fork, 0), "wait");
   if (pipelined) {
     d_pipe = (uint64_t*)ws_get(ctx, WS_PIPE, (6 * P + 3) * sizeof(uint64_t), &st);
     if (!d_pipe) return st;
     CDB_HIP(hipStreamWaitEvent(cs, ctx->ev_fork, 0), "wait");
     CDB_HIP(hipMemsetAsync(d_pipe, 0, 3 * sizeof(uint64_t), cs), "memset pipe");
   }
-  static const int tile_nw = [] {  // staged tiles of NW buckets on the sorted-run path (0: off)
-    const char* e = std::getenv("CDB_TILE_NW");
-    return e ? std::atoi(e) : 0;
-  }();
-  // extra (unused) LDS per wave-tier workgroup: caps how many share a CU, leaving room for the
-  // pipelined compaction's waves beside them
-  static const uint32_t wave_dyn_lds = [] {
-    const char* e = std::getenv("CDB_WAVE_DYN_LDS");
-    return e ? (uint32_t)std::atoi(e) : 0u;
-  }();
   for (uint32_t p = 0; p < P; ++p) {
     const uint32_t lo = (uint32_t)(nb * p / P), hi = (uint32_t)(nb * (p + 1) / P), nr_b = hi - lo;
     WA.blo = lo;
@@ -1055,25 +956,13 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     if (nr_b == 0) continue;
     const uint32_t gw = (uint32_t)std::min<uint64_t>((nr_b + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024);
     if (use_runs) {
-      if (tile_nw == 4)
-        bucket_tile_runs_kernel<4><<<(nr_b + 3) / 4, 4 * 64, 0, s>>>(WA);
-      else if (tile_nw == 8)
-        bucket_tile_runs_kernel<8><<<(nr_b + 7) / 8, 8 * 64, 0, s>>>(WA);
-      else if (tile_nw == 16)
-        bucket_tile_runs_kernel<16><<<(nr_b + 15) / 16, 16 * 64, 0, s>>>(WA);
-      else
-        bucket_wave_runs_kernel<<<(nr_b + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, wave_dyn_lds, s>>>(WA);
+      bucket_wave_runs_kernel<<<(nr_b + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, 0, s>>>(WA);
       CDB_TRY(launch_check(ctx, s, "bucket_wave_runs_kernel"));
       // the wide tier's buckets are disjoint from the wave tier's: beside it on a side stream
       bucket_wide_runs_kernel<<<gw, kWavesPerWG * 64, 0, ws>>>(WA);
       CDB_TRY(launch_check(ctx, ws, "bucket_wide_runs_kernel"));
     } else {
-      if (wave_pf() == 0)
-        bucket_wave_kernel<<<(nr_b + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, 0, s>>>(WA);
-      else if (wave_pf() == 1)
-        bucket_wave_pf1_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
-      else
-        bucket_wave_pf2_kernel<<<wave_grid(ctx, nb), kWavesPerWG * 64, 0, s>>>(WA, wave_g());
+      bucket_wave_kernel<<<(nr_b + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, 0, s>>>(WA);
       CDB_TRY(launch_check(ctx, s, "bucket_wave_kernel"));
       bucket_wide_kernel<<<gw, kWavesPerWG * 64, 0, ws>>>(WA);
       CDB_TRY(launch_check(ctx, ws, "bucket_wide_kernel"));
@@ -1081,10 +970,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     if (pipelined) {  // range p: scans and compaction on cs once both tiers are through it
       CDB_HIP(hipEventRecord(ctx->ev_cs, s), "event");
       CDB_HIP(hipStreamWaitEvent(cs, ctx->ev_cs, 0), "wait");
-      if (!wide_serial) {
-        CDB_HIP(hipEventRecord(ctx->ev_cw, ws), "event");
-        CDB_HIP(hipStreamWaitEvent(cs, ctx->ev_cw, 0), "wait");
-      }
+      CDB_HIP(hipEventRecord(ctx->ev_cw, ws), "event");
+      CDB_HIP(hipStreamWaitEvent(cs, ctx->ev_cw, 0), "wait");
       uint64_t* base = d_pipe + 3 * p;
       uint64_t* tot = d_pipe + 3 * (P + 1) + 3 * p;
       CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dk.out + lo, nr_b, dk.doff + lo, (uint32_t*)nullptr, tot + 0, cs,
@@ -1106,10 +993,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
       CDB_TRY(launch_check(ctx, cs, "compact_kernel"));
     }
   }
-  if (!wide_serial) {
-    CDB_HIP(hipEventRecord(ctx->ev_join, ws), "event");
-    CDB_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0), "wait");
-  }
+  CDB_HIP(hipEventRecord(ctx->ev_join, ws), "event");
+  CDB_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0), "wait");
   WA.blo = 0;
   WA.bhi = (uint32_t)nb;
   if (use_runs) {
@@ -1148,11 +1033,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   uint32_t counts[2] = {0, 0};  // hot, big (mid tier)
   CDB_HIP(hipMemcpyAsync(counts, d_hot_count, sizeof counts, hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipStreamSynchronize(s), "sync");
-  static const uint32_t mid_chip = [] {
-    const char* e = std::getenv("CDB_MID_CHIPWIDE");  // buckets from which the mid tier goes chip-wide
-    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 4096u;
-  }();
-  const bool mid_wide = A.force_tier == 0 && mid_chip && counts[1] >= mid_chip;
+  constexpr uint32_t kMidChipWide = 4096;  // mid-tier buckets from which they go chip-wide
+  const bool mid_wide = A.force_tier == 0 && counts[1] >= kMidChipWide;
   if (mid_wide) {
     CDB_TRY(over_capacity(ctx, A, d_big_list, counts[1], s));
   } else {
@@ -1193,17 +1075,13 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   merge_end_marker<<<1, 1, 0, s>>>();
 
   uint64_t totals[3];
-  unsigned long long hs[ST_COUNT], wave_tot[4];
+  unsigned long long hs[ST_COUNT];
   CDB_HIP(hipMemcpyAsync(totals, d_totals, sizeof totals, hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipMemcpyAsync(hs, d_stats, sizeof hs, hipMemcpyDeviceToHost, s), "d2h");
-  CDB_HIP(hipMemcpyAsync(wave_tot, d_lb_tot, sizeof wave_tot, hipMemcpyDeviceToHost, s), "d2h");
   uint32_t cerr = 0;
   CDB_HIP(hipMemcpyAsync(&cerr, d_cerr, sizeof cerr, hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipStreamSynchronize(s), "sync");
   if (cerr) return fail(ctx, CDB_DEVICE_ERROR, "compaction: a source or destination row fell outside the family's rows");
-  if ((uint32_t)wave_tot[3])
-    return fail(ctx, CDB_DEVICE_ERROR, "output look-back did not converge (bucket dispatch order violated)");
-  for (int f = 0; f < 3; ++f) totals[f] += wave_tot[f];
   out->keys.n = totals[0];
   out->nodes.n = totals[1];
   out->members.n = totals[2];

@@ -227,174 +227,6 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, 5) bucket_wave_runs_kernel(W
   }
 }
 
-// ---------------------------------------------------------------- staged tiles
-// NW consecutive buckets per workgroup, one per wave. The rows of a tile are, per (family, run),
-// ONE contiguous slice of the run (the run is sorted), so the workgroup first copies every
-// slice into LDS with consecutive threads on consecutive rows of a column: each cache line is
-// fetched once and used whole by this workgroup. (A wave reading its own bucket straight from
-// the runs -- bucket_wave_runs_kernel -- touches 8-16 partly used lines per column load, and a
-// line is fetched again by every neighbouring bucket's wave: L2->L1 traffic ~3x the bytes.)
-// Each wave then copies its bucket's rows from LDS into registers; after a barrier the staging
-// area is dead and becomes the waves' WaveLds (a union), so the LDS footprint is the waves'.
-// A tile whose rows exceed the staging capacity (64 NW rows per group) loads from the runs.
-constexpr uint32_t kTileMaxRuns = 32;  // the wave tiers take at most 32 runs (2 nr child lanes)
-
-template <int NW>
-struct TileStage {
-  uint64_t k[kKeyCols][64 * NW];   // key rows: the slices of runs 0 .. nr-1
-  uint64_t c[kNodeCols][64 * NW];  // child rows: node slices of every run, then member slices
-  uint32_t trd[3][kTileMaxRuns][NW + 1];   // run-relative first row of bucket b0 + j
-  uint32_t tpre[2][2 * kTileMaxRuns + 1];  // staging offset of each slice (keys, children)
-};
-template <int NW>
-union TileLds {
-  TileStage<NW> st;
-  WaveLds<1> w[NW];
-};
-
-// Last slice s < L with pre[s] <= i (pre non-decreasing, pre[0] = 0).
-__device__ __forceinline__ uint32_t tile_slice(const uint32_t* pre, uint32_t L, uint32_t i) {
-  uint32_t lo = 0, hi = L;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (pre[mid] <= i) lo = mid;
-    else hi = mid;
-  }
-  return lo;
-}
-
-// The lane map of bucket b0 + w inside the staged tile (RunMap with staging indices).
-template <int NW>
-__device__ __forceinline__ RunMap tile_map(const uint32_t (*trd)[kTileMaxRuns][NW + 1], const uint32_t* pre,
-                                           uint32_t nr, int w, int lane, bool children) {
-  RunMap q;
-  q.L = children ? 2 * nr : nr;
-  uint32_t n = 0, base = 0;
-  if ((uint32_t)lane < q.L) {
-    const int f = children ? 1 + (lane >= (int)nr) : 0;
-    const uint32_t r = (uint32_t)lane - (f == 2 ? nr : 0);
-    const uint32_t s = trd[f][r][w];
-    n = trd[f][r][w + 1] - s;
-    base = pre[lane] + (s - trd[f][r][0]);
-  }
-  uint32_t incl = n;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += t;
-  }
-  q.incl = incl;
-  q.off = (uint64_t)(base - (incl - n));  // (wraps: only off + c, c >= incl - n, is used)
-  return q;
-}
-
-template <int NW>
-__global__ void __launch_bounds__(NW * 64, NW == 4 ? 5 : 4) bucket_tile_runs_kernel(WaveArgs W) {
-  static_assert(sizeof(TileStage<NW>) <= sizeof(WaveLds<1>) * NW, "the tile metadata fits the waves' LDS");
-  __shared__ TileLds<NW> U;
-  auto& trd = U.st.trd;
-  auto& tpre = U.st.tpre;
-  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  const RunView& V = W.V;
-  const uint32_t nr = V.nr;
-  const uint32_t tile = xcd_block(blockIdx.x, gridDim.x);
-  const uint32_t b0 = W.blo + tile * NW, b = b0 + wv;
-  const bool has = b < W.bhi;
-  WaveDir d;
-  if (has) d = load_dir(W.A, b);
-  // 0. the tile's run directory and the slices' staging offsets
-  const uint32_t per_f = nr * (NW + 1);
-  for (uint32_t i = tid; i < 3 * per_f; i += NW * 64) {
-    const uint32_t f = i / per_f, rem = i - f * per_f, r = rem / (NW + 1), j = rem - r * (NW + 1);
-    trd[f][r][j] = V.rdir[f][(uint64_t)r * V.nbp1 + min(b0 + j, W.bhi)];
-  }
-  __syncthreads();
-  if (wv < 2) {
-    const uint32_t L = wv ? 2 * nr : nr;
-    uint32_t n = 0;
-    if ((uint32_t)lane < L) {
-      const int f = wv ? 1 + (lane >= (int)nr) : 0;
-      const uint32_t r = (uint32_t)lane - (f == 2 ? nr : 0);
-      n = trd[f][r][NW] - trd[f][r][0];
-    }
-    uint32_t incl = n;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += t;
-    }
-    if ((uint32_t)lane < L) tpre[wv][lane] = incl - n;
-    if ((uint32_t)lane == L - 1) tpre[wv][L] = incl;  // the total
-  }
-  __syncthreads();
-  const uint32_t nk = tpre[0][nr], nc = tpre[1][2 * nr];
-  WaveIn<1> in;
-  if (nk <= 64 * NW && nc <= 64 * NW) {  // uniform over the workgroup
-    // 1. stage every slice, column by column (consecutive threads: consecutive rows)
-    for (uint32_t i = tid; i < nk; i += NW * 64) {
-      const uint32_t r = tile_slice(tpre[0], nr, i);
-      const uint64_t src = V.rbase[r] + trd[0][r][0] + (i - tpre[0][r]);
-      uint64_t v[kKeyCols];
-#pragma unroll
-      for (int c = 0; c < kKeyCols; ++c) v[c] = V.kin[c][src];
-#pragma unroll
-      for (int c = 0; c < kKeyCols; ++c) U.st.k[c][i] = v[c];
-    }
-    for (uint32_t i = tid; i < nc; i += NW * 64) {
-      const uint32_t s = tile_slice(tpre[1], 2 * nr, i);
-      const int f = 1 + (s >= nr);
-      const uint32_t r = s - (f == 2 ? nr : 0);
-      const uint64_t src = V.rbase[f * (kMaxRuns + 1) + r] + trd[f][r][0] + (i - tpre[1][s]);
-      const uint64_t* const* col = f == 1 ? V.nin : V.min;
-      uint64_t v[kNodeCols];
-#pragma unroll
-      for (int c = 0; c < kNodeCols; ++c) v[c] = col[c][src];
-#pragma unroll
-      for (int c = 0; c < kNodeCols; ++c) U.st.c[c][i] = v[c];
-    }
-    __syncthreads();
-    // 2. each wave: its bucket's rows, slot by slot, into registers
-    if (has) {
-      const RunMap qk = tile_map<NW>(trd, tpre[0], nr, wv, lane, false);
-      const RunMap qc = tile_map<NW>(trd, tpre[1], nr, wv, lane, true);
-      in.d = d;
-      const uint32_t C = d.N + d.M;
-      in.kh[0] = in.kf[0] = in.kct[0] = in.kut[0] = in.kdt[0] = in.kaux[0] = in.kmeta[0] = 0;
-      const uint32_t kr = (uint32_t)run_row(qk, lane);
-      if ((uint32_t)lane < d.K) {
-        in.kh[0] = U.st.k[K_KH][kr];
-        in.kf[0] = U.st.k[K_KF][kr];
-        in.kct[0] = U.st.k[K_CT][kr];
-        in.kut[0] = U.st.k[K_UT][kr];
-        in.kdt[0] = U.st.k[K_DT][kr];
-        in.kaux[0] = U.st.k[K_AUX][kr];
-        in.kmeta[0] = U.st.k[K_META][kr];
-      }
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const uint32_t c = lane + 64 * e;
-        in.cpkh[e] = in.cpkf[e] = in.cid1[e] = in.cid2[e] = in.ct[e] = in.cm[e] = 0;
-        if (__ballot(c < C) == 0) continue;
-        const uint32_t cr = (uint32_t)run_row(qc, c);
-        if (c < C) {
-          in.cpkh[e] = U.st.c[C_PKH][cr];
-          in.cpkf[e] = U.st.c[C_PKF][cr];
-          in.cid1[e] = U.st.c[C_ID1][cr];
-          in.cid2[e] = U.st.c[C_ID2][cr];
-          in.ct[e] = U.st.c[C_T][cr];
-          in.cm[e] = U.st.c[C_META][cr];
-        }
-      }
-    }
-    __syncthreads();  // the staging area is the waves' LDS from here on
-  } else {
-    __syncthreads();  // every wave has read the totals before any wave's LDS overwrites them
-    if (has) load_runs<1>(W, d, b, lane, in);
-  }
-  if (!has) return;
-  wave_bucket<1>(W, U.w[wv], b, lane, in, []() {});
-}
-
 // The wide tier (65..128 key rows or 129..256 child rows) on the runs: as bucket_wide_kernel.
 __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_runs_kernel(WaveArgs W) {
   __shared__ WaveLds<2> lds_all[kWavesPerWG];

@@ -9,9 +9,9 @@ Two layouts:
   * one run per fold position (every key row of a replica in one hash-ordered run): what a merge
     result kept in HBM as the next merge's position 0 is (cdb_dev_state_rows);
   * three key runs per fold position -- DATAS, EXPIRES, DELETES, each hash-ordered -- and one
-    child run (padded with two empty runs): what decoding a snapshot this engine encoded yields
-    (the encoder writes each section in the result's hash order, cdb_encode_snapshot), i.e. the
-    run layout cdb_decode_snapshots_device reports.
+    child run (padded with two empty runs): the sections of a snapshot this engine encoded as
+    they lie in the stream (cdb_decode_snapshots_device merges them back into one run per
+    snapshot on decode; this layout exercises runs of very different lengths).
 These helpers establish a layout for generated inputs; they are setup, never part of a timed
 merge step.
 """

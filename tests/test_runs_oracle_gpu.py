@@ -1,7 +1,9 @@
 """The sorted-run merge path -- the path every bench line measures -- against the oracle directly.
 
 Rows are decoded on the host, uploaded (cdb_upload_batches), laid out as hash-ordered runs on the
-device (constdb_amd/runs.py: one run per replica, or the decoder's three key runs per replica),
+device (constdb_amd/runs.py: one run per replica, or three key runs per replica -- DATAS, EXPIRES,
+DELETES as an encoded snapshot lists them), or decoded on the GPU from snapshots this engine encoded
+(cdb_decode_snapshots_device places each as one run),
 merged by cdb_merge_device (asserted to take the sorted-run path), and the result's canonical
 dump (cdb_merged_from_device) is compared byte for byte with the C++ oracle's sequential fold
 (oracle/cdb_oracle.cpp: db.rs:31-119, object.rs:63-83, type_counter.rs:59-91,
@@ -112,7 +114,7 @@ def _small(seed, universe, replicas, **kw):
 @pytest.mark.parametrize("seed", range(8))
 def test_runs_random_vs_oracle(ctx, seed):
     """Random replica states with type conflicts, forced time ties, side maps, long member lists;
-    one run per replica (even seeds) or the decoder's three key runs per replica (odd)."""
+    one run per replica (even seeds) or three key runs per replica (odd)."""
     cfg = _small(100 + seed, 1500 + 2500 * seed, 1 + seed % 8, conflict_ppm=30000, tie_permille=150,
                  side_permille=250, mean_members=3 + seed, del_permille=300)
     snaps = [cdb.gen_snapshot(cfg, r) for r in range(cfg.n_replicas)]
@@ -295,7 +297,7 @@ def test_encode_decode_device_runs_vs_oracle(ctx, seed, gc):
     assert din.n_runs == 0
     _release(ctx, din)
     encs = _hash_ordered_snapshots(ctx, raw)
-    wm = (configs.T0_MS + (1 << 19)) << 22 if gc else None
+    wm = (configs.T0_MS + (1 << 30)) << 22 if gc else None  # after every time: DB::gc takes every Delete
     rc, want, ost = cdb_oracle.fold(encs, flags=cdb_oracle.FLAG_GC if gc else 0, gc_watermark=wm or 0)
     assert rc == 0
     batches, din = cdb.decode_snapshots_device(ctx, encs)
