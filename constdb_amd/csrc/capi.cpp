@@ -800,7 +800,9 @@ cdb_status cdb_decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint
   o->b = std::make_shared<Batch>();
   size_t eo = 0;
   int rc = CDB_OK;
-  if (decode_ops_gpu(ctx, buf, len, uuid_he_sent, o->b.get(), &o->info, &eo, &rc, host_ms, device_ms) != 0) {
+  const int g = decode_ops_gpu(ctx, buf, len, uuid_he_sent, o->b.get(), &o->info, &eo, &rc, host_ms, device_ms);
+  if (g < 0) return (cdb_status)(-g);  // a device fault or out of memory: reported, not masked
+  if (g != 0) {
     // a shape the device path leaves to the host decoder: the whole stream goes there
     (void)hipGetLastError();
     if (used_gpu) *used_gpu = 0;

@@ -10,8 +10,14 @@
 //                     ignored, exactly as the wave tier) and tags it with
 //                     W = G << g_shift | id-hash top (g_shift - 6) bits << 6 | pos, so that a
 //                     run's rows arrive in fold order unless two ids share those hash bits
-//                     (g_shift: 40, or less where that saves a sort pass -- see over_capacity);
-//   radix sort of (W, child) pairs (radix.hip.h), stable, so equal W keep (bucket, row) order;
+//                     (g_shift: 40, or less where that saves a sort pass -- see chip_wide); a
+//                     child that takes no part gets its bucket's marker (every W bit of the
+//                     bucket's last key set: pos 63, which no row has), so it sorts to the end of
+//                     its bucket's children and every bucket's children keep their flat range;
+//   sort of each bucket's (W, child) pairs inside that range: one workgroup in LDS for a bucket of
+//                     at most kLocalSortMax children (bitonic on (W, child)), the LSD radix sort
+//                     of radix.hip.h over the larger buckets' pairs gathered together (W orders
+//                     them by bucket, then in place again);
 //   hot_fold_kernel : one thread per W-run (a (key, child id) group, ~ one row per replica):
 //                     folds every exact child id of the run in (pos, src) order -- Counter::merge's
 //                     head-t rule or LWWHash::set's later-wins rule -- counting outputs (pass 0)
@@ -46,7 +52,6 @@ struct HotArgs {
   uint32_t* c_h;             // bucket h of flat child j, bit 31 = member
   uint32_t *emit_n, *emit_m; // per sorted position: outputs of the run starting there
   const uint32_t *rank_n, *rank_m;  // exclusive scans of emit_n / emit_m
-  uint32_t* h_first;         // per h: first sorted position of its children
   uint64_t n_children;
   int id_shift;              // W's id bits = id hash >> id_shift (64 + 6 - g_shift; larger in tests)
   int g_shift;               // W's key-id bits start here (kHotIdBits or less)
@@ -66,6 +71,13 @@ __device__ __forceinline__ uint32_t hot_bucket_of(const HotArgs& H, uint64_t j) 
   }
   return lo;
 }
+
+// The W of bucket h's children that take no part: above every W of the bucket (its last key id,
+// every id bit, pos 63) and below every W of the next bucket.
+__device__ __forceinline__ uint64_t hot_marker(const HotArgs& H, uint32_t h) {
+  return ((uint64_t)H.hk_off[h + 1] << H.g_shift) - 1;
+}
+__device__ __forceinline__ bool hot_takes_part(uint64_t W) { return (W & 63) != 63; }
 
 __global__ void __launch_bounds__(kBktThreads) hot_keys_kernel(BucketArgs A, HotArgs H) {
   __shared__ LdsPool L;
@@ -117,7 +129,7 @@ __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
       lo = less ? mid + 1 : lo;
       hi = less ? hi : mid;
     }
-    uint64_t w = ~0ull;
+    uint64_t w = hot_marker(H, h);
     if (lo < kout && H.hk_h[g0 + lo] == pkh && H.hk_f[g0 + lo] == pkf && (H.hk_tp[g0 + lo] & 0xFF) <= TAG_SET) {
       const uint32_t T = H.hk_tp[g0 + lo] & 0xFF, hp = H.hk_tp[g0 + lo] >> 8, p = meta_pos(m);
       const bool type_ok = isn ? T == TAG_COUNTER : (T == TAG_SET || T == TAG_DICT);
@@ -169,7 +181,9 @@ __global__ void __launch_bounds__(256) hot_runflag_kernel(HotArgs H, uint32_t* _
   for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < H.n_children;
        p += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t W = H.w[p];
-    flag[p] = W != ~0ull && !(p > 0 && (H.w[p - 1] >> 6) == (W >> 6));  // a run: equal W but the pos bits
+    // a run: equal W but the pos bits (a marker never starts one; one before W belongs to an
+    // earlier bucket, so it never hides a start either)
+    flag[p] = hot_takes_part(W) && !(p > 0 && (H.w[p - 1] >> 6) == (W >> 6));
   }
 }
 __global__ void __launch_bounds__(256) hot_runlist_kernel(HotArgs H, const uint32_t* __restrict__ flag,
@@ -184,8 +198,8 @@ constexpr uint32_t kFoldFast = 8;  // runs up to this many rows: rows in registe
 // One thread per run. Pass 0: the run's output count (emit_n / emit_m at its first position)
 // and, for a run of one exact id whose rows arrive in strictly increasing (pos, src) order (the
 // tag's low bits are the position) and no longer than kFoldFast, the output row's position and
-// value (fold_q / fold_v); pass 1 writes outputs at their rank. Other runs (ids sharing 34 hash
-// bits, long runs) fold by successor selection in both passes: each step selects the successor
+// value (fold_q / fold_v); pass 1 writes outputs at their rank. Other runs (ids sharing the
+// tag's id-hash bits -- g_shift - 6 of them, 20 to 34 -- and long runs) fold by successor selection in both passes: each step selects the successor
 // of the last visited row (O(run^2) over rows in L2, no per-thread arrays), so rows are folded
 // in order whatever order the sort left them in. Loops have wave-uniform trip counts with
 // per-lane predicates: a loop-carried row must not be a live-out of a loop with divergent exits
@@ -203,7 +217,7 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
     uint32_t nrows = 0;
     if (act) {
       uint64_t e = p + 1;
-      while (e < H.n_children && (H.w[e] >> 6) == (W >> 6)) ++e;
+      while (e < H.n_children && (H.w[e] >> 6) == (W >> 6) && hot_takes_part(H.w[e])) ++e;
       nrows = (uint32_t)(e - p);
     }
     uint32_t hc = 0, h = 0, b = 0, G = 0;
@@ -215,7 +229,7 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
       isn = (hc >> 31) == 0;
       b = H.ids[h];
       G = (uint32_t)(W >> H.g_shift);
-      if (pass == 1) obase = (isn ? H.rank_n[p] - H.rank_n[H.h_first[h]] : H.rank_m[p] - H.rank_m[H.h_first[h]]);
+      if (pass == 1) obase = (isn ? H.rank_n[p] - H.rank_n[H.c_off[h]] : H.rank_m[p] - H.rank_m[H.c_off[h]]);
     }
     uint32_t nout = 0;
     // this run's contribution to its key's row: outputs, first output slot, counter sum (one
@@ -382,18 +396,75 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
   if (pass == 0 && gcm) atomicAdd(&stat_shard(A.stats)[ST_MEMBERS_GCED], gcm);
 }
 
-// First sorted position of each hot bucket's children (sorted by W, whose top bits are G).
-__global__ void hot_first_kernel(HotArgs H) {
-  const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
-  if (h >= H.H) return;
-  const uint64_t key = (uint64_t)H.hk_off[h] << H.g_shift;
-  uint64_t lo = 0, hi = H.n_children;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (H.w[mid] < key) lo = mid + 1;
-    else hi = mid;
+// ---- per-bucket sort of the (W, child) pairs (every bucket's children keep their flat range)
+constexpr uint32_t kLocalSortMax = 8192;
+
+// One workgroup per listed bucket of at most N children: bitonic sort on (W, child) in LDS, in
+// place. (W, child) pairs are distinct, so the order is total and the result deterministic.
+template <uint32_t N>
+__global__ void __launch_bounds__(512) hot_local_sort_kernel(uint64_t* __restrict__ w, uint32_t* __restrict__ v,
+                                                             const uint32_t* __restrict__ c_off,
+                                                             const uint32_t* __restrict__ list) {
+  __shared__ uint64_t sk[N];
+  __shared__ uint32_t sv[N];
+  const uint32_t h = list[blockIdx.x];
+  const uint32_t b0 = c_off[h], cnt = c_off[h + 1] - b0;
+  uint32_t n = 2;
+  while (n < cnt) n <<= 1;
+  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    sk[i] = i < cnt ? w[b0 + i] : ~0ull;
+    sv[i] = i < cnt ? v[b0 + i] : ~0u;
   }
-  H.h_first[h] = (uint32_t)lo;
+  __syncthreads();
+  for (uint32_t k = 2; k <= n; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t a = sk[i], c = sk[ixj];
+          const uint32_t av = sv[i], cv = sv[ixj];
+          const bool gt = a > c || (a == c && av > cv);
+          if (gt == ((i & k) == 0)) {
+            sk[i] = c;
+            sk[ixj] = a;
+            sv[i] = cv;
+            sv[ixj] = av;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+    w[b0 + i] = sk[i];
+    v[b0 + i] = sv[i];
+  }
+}
+
+// The larger buckets' pairs, gathered into one array in bucket order (to) or back (!to): list[i]
+// is a larger bucket, loff the prefix of their child counts.
+__global__ void __launch_bounds__(256) hot_gather_kernel(uint64_t* __restrict__ w, uint32_t* __restrict__ v,
+                                                         uint64_t* __restrict__ gw, uint32_t* __restrict__ gv,
+                                                         const uint32_t* __restrict__ c_off,
+                                                         const uint32_t* __restrict__ list,
+                                                         const uint64_t* __restrict__ loff, uint32_t nl, uint64_t n,
+                                                         int to) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t lo = 0, hi = nl;  // last l with loff[l] <= i
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (loff[mid] <= i) lo = mid;
+      else hi = mid;
+    }
+    const uint64_t f = c_off[list[lo]] + (i - loff[lo]);
+    if (to) {
+      gw[i] = w[f];
+      gv[i] = v[f];
+    } else {
+      w[f] = gw[i];
+      v[f] = gv[i];
+    }
+  }
 }
 
 // Key rows: counter sums and child ranges (bucket-relative, as every tier leaves them for the

@@ -516,7 +516,8 @@ struct DevArr {
 
 }  // namespace
 
-// 0: done (*out filled, status in *rc); 1: the stream needs the host decoder.
+// 0: done (*out filled, status in *rc); 1: the stream needs the host decoder; < 0: a HIP call
+// failed (-status, ctx->last_error says which): reported to the caller, never a silent fallback.
 int decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_he_sent, Batch* out,
                    cdb_ops_info* info, size_t* err_off, int* rc_out, double* host_ms, double* device_ms) {
   using clk = std::chrono::steady_clock;
@@ -528,7 +529,7 @@ int decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_h
   st.uuid_he_sent = uuid_he_sent;
   *err_off = 0;
   *rc_out = CDB_OK;
-  if (hipSetDevice(ctx->device) != hipSuccess) return 1;
+  if (hipSetDevice(ctx->device) != hipSuccess) return -(int)fail(ctx, CDB_DEVICE_ERROR, "hipSetDevice");
   hipStream_t s = ctx->stream;
   cdb_status cs = CDB_OK;
   auto ck = [&](hipError_t e, const char* what) {
@@ -545,7 +546,7 @@ int decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_h
   ck(hipMalloc(&d_raw.p, len + 16), "hipMalloc(resp)");
   ck(hipMalloc(&d_tiles.p, (2 * tiles + 2) * sizeof(uint32_t) + (2 * ((tiles + kScanTile - 1) / kScanTile) + 8) * 8),
      "hipMalloc(resp)");
-  if (cs != CDB_OK) return 1;
+  if (cs != CDB_OK) return -(int)cs;
   RespArgs A;
   std::memset(&A, 0, sizeof A);
   A.b = d_raw.p;
@@ -559,7 +560,7 @@ int decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_h
   const auto t0 = clk::now();
   adopt_raw(&b, buf, len);  // (the batch's arena; overlaps the upload's tail)
   th += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-  if (cs != CDB_OK) return 1;
+  if (cs != CDB_OK) return -(int)cs;
   resp_cand_count<<<(uint32_t)tiles, kRespThreads, 0, s>>>(A);
   const uint64_t stiles = (tiles + kScanTile - 1) / kScanTile;
   scan_reduce_kernel<uint32_t><<<(uint32_t)stiles, kScanThreads, 0, s>>>(A.tile_cnt, tiles, d_sums);
@@ -569,12 +570,12 @@ int decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_h
   uint64_t nc = 0;
   ck(hipMemcpyAsync(&nc, d_tot, 8, hipMemcpyDeviceToHost, s), "d2h(resp)");
   ck(hipStreamSynchronize(s), "sync(resp)");
-  if (cs != CDB_OK) return 1;
+  if (cs != CDB_OK) return -(int)cs;
   if (nc >= (1ull << 32) - 1) return 1;
   A.n_cand = nc;
   DevArr<uint8_t> d_cand;  // cand u64 | size u32 | status u8
   ck(hipMalloc(&d_cand.p, nc * 13 + 64), "hipMalloc(resp)");
-  if (cs != CDB_OK) return 1;
+  if (cs != CDB_OK) return -(int)cs;
   A.cand = (uint64_t*)d_cand.p;
   A.size = (uint32_t*)(A.cand + nc);
   A.status = (uint8_t*)(A.size + nc);
@@ -589,7 +590,7 @@ int decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_h
   if (cs == CDB_OK && nc) cs = staged_d2h(ctx, h_cand.data(), A.cand, nc * 8, s);
   if (cs == CDB_OK && nc) cs = staged_d2h(ctx, h_size.data(), A.size, nc * 4, s);
   if (cs == CDB_OK && nc) cs = staged_d2h(ctx, h_status.data(), A.status, nc, s);
-  if (cs != CDB_OK) return 1;
+  if (cs != CDB_OK) return -(int)cs;
   // ---- the chain of messages from byte 0 (host): where the host decoder would stop, we stop
   const auto t1 = clk::now();
   std::vector<uint32_t> chain;
@@ -627,7 +628,7 @@ int decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_h
   DevArr<uint8_t> d_msg;  // chain u32 | cls u8 | flags u8 | last u64 | cur u64 | nn u32 | nm u32 | emit u32 | orow nrow mrow u32
   const size_t msg_bytes = nmsg * (4 + 1 + 1 + 8 + 8 + 4 + 4 + 4 + 12) + 256;
   ck(hipMalloc(&d_msg.p, msg_bytes), "hipMalloc(resp)");
-  if (cs != CDB_OK) return 1;
+  if (cs != CDB_OK) return -(int)cs;
   {
     uint8_t* w = d_msg.p;
     auto take = [&](size_t bytes) {
@@ -648,7 +649,7 @@ int decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_h
     A.flags = take(nmsg);
   }
   if (nmsg && cs == CDB_OK) cs = staged_h2d(ctx, (void*)A.chain, chain.data(), nmsg * 4, s);
-  if (cs != CDB_OK) return 1;
+  if (cs != CDB_OK) return -(int)cs;
   const uint32_t mgrid = (uint32_t)std::min<uint64_t>((nmsg + kRespThreads - 1) / kRespThreads, 16384);
   if (nmsg) {
     resp_classify<<<mgrid, kRespThreads, 0, s>>>(A);
@@ -662,7 +663,7 @@ int decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_h
     if (cs == CDB_OK) cs = staged_d2h(ctx, h_last.data(), A.last, nmsg * 8, s);
     if (cs == CDB_OK) cs = staged_d2h(ctx, h_cur.data(), A.curu, nmsg * 8, s);
   }
-  if (cs != CDB_OK) return 1;
+  if (cs != CDB_OK) return -(int)cs;
   // ---- the uuid gate (pull.rs:199-209), message by message
   const auto t2 = clk::now();
   std::vector<uint32_t> emit(nmsg, 0);
@@ -698,13 +699,13 @@ int decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_h
   th += std::chrono::duration<double, std::milli>(clk::now() - t2).count();
   // ---- op rows: scans of the emitted messages' row counts, then the emit pass
   if (nmsg && cs == CDB_OK) cs = staged_h2d(ctx, (void*)A.emit, emit.data(), nmsg * 4, s);
-  if (cs != CDB_OK) return 1;
+  if (cs != CDB_OK) return -(int)cs;
   uint64_t tot[3] = {0, 0, 0};
   {
     DevArr<uint64_t> d_s;
     const uint64_t mt = (nmsg + kScanTile - 1) / kScanTile;
     ck(hipMalloc(&d_s.p, (3 * (mt + 1) + 8) * 8), "hipMalloc(resp)");
-    if (cs != CDB_OK) return 1;
+    if (cs != CDB_OK) return -(int)cs;
     ck(hipMemsetAsync(d_s.p + 3 * (mt + 1), 0, 64, s), "memset(resp)");
     uint64_t* dt = d_s.p + 3 * (mt + 1);
     if (nmsg) {  // nn / nm count only for emitted messages: masked in place
@@ -722,14 +723,14 @@ int decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_h
     ck(hipGetLastError(), "resp scans");
     if (nmsg) ck(hipMemcpyAsync(tot, dt, 24, hipMemcpyDeviceToHost, s), "d2h(resp)");
     ck(hipStreamSynchronize(s), "sync(resp)");
-    if (cs != CDB_OK) return 1;
+    if (cs != CDB_OK) return -(int)cs;
   }
   const uint64_t no = tot[0], nn = tot[1], nm = tot[2];
   if (no != n_emit) return 1;
   DevArr<uint64_t> d_rows;
   const size_t words = no * 11 + nn * 6 + nm * 10 + 16;
   ck(hipMalloc(&d_rows.p, words * 8), "hipMalloc(resp rows)");
-  if (cs != CDB_OK) return 1;
+  if (cs != CDB_OK) return -(int)cs;
   {
     uint64_t* w = d_rows.p;
     uint64_t* const w0 = w;
@@ -776,7 +777,7 @@ int decode_ops_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t uuid_h
   down(b.m_vref.data(), A.mvref, nm * 16);
   if (!segs.empty()) cs = staged_copy(ctx, segs.data(), segs.size(), false, s);
   ck(hipStreamSynchronize(s), "sync(resp)");
-  if (cs != CDB_OK) return 1;
+  if (cs != CDB_OK) return -(int)cs;
   b.n_data = no;
   st.n_ops = no;
   st.n_node_args = nn;

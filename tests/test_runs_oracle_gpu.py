@@ -127,6 +127,16 @@ def test_runs_forced_tiers_vs_oracle(ctx, tier):
     check_runs(ctx, [cdb.gen_snapshot(cfg, r) for r in range(5)], force_tier=tier)
 
 
+def test_chip_wide_in_batches_vs_oracle(ctx, monkeypatch):
+    """The chip-wide child path run in many batches (the key-table cap lowered from 2^23 to 2000 key
+    rows by the CDB_HOT_KEY_CAP test hook), every bucket sent through it (force_tier 2): equal to
+    the oracle. At full scale a child-heavy input of more than 2^23 key rows takes this path."""
+    monkeypatch.setenv("CDB_HOT_KEY_CAP", "2000")
+    cfg = _small(77, 30000, 4, mix_set=30, mix_dict=30, mean_members=12, side_permille=100, conflict_ppm=10000,
+                 del_permille=300)
+    check_runs(ctx, [cdb.gen_snapshot(cfg, r) for r in range(4)], force_tier=2)
+
+
 def test_runs_gc_vs_oracle(ctx):
     cfg = _small(7, 20000, 4, mix_set=40, mix_dict=40, side_permille=300, del_permille=400)
     wm = (configs.T0_MS + (1 << 19)) << 22
