@@ -92,12 +92,31 @@ struct DeferredCrc {
   uint64_t len = 0, got = 0;
   size_t err_off = 0;
 };
+// A large DATAS section met before any other entry, left to the device index (decode_gpu.hip):
+// the host pass stops at its first entry (index_snapshot returns kIndexDeferred and a cursor),
+// the device finds the entries' offsets, and index_resume continues after the section's last
+// entry (the sections after it, the checksum) with the same checks and error offsets.
+constexpr int kIndexDeferred = -100;
+constexpr uint64_t kDeviceIndexMinEntries = 1u << 17;
+struct DeferredDatas {
+  bool pending = false;
+  uint64_t start = 0;  // byte offset of the section's first entry
+  uint64_t count = 0;  // the section's entry count
+};
+struct IndexCursor;
 // With `crc` non-null and at least one entry indexed, the checksum is not computed here but
 // described in *crc for the caller to check.
 // threads > 1: a large DATAS section is indexed by that many threads (speculative sync points,
 // stitched in order; the result is the sequential pass's, entry for entry).
+// defer and cursor non-null: a large first DATAS section is deferred as described above. buf may
+// be null when `out` already holds the bytes (a second, host-only pass after a device fallback).
 int index_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, EntryIndex* idx, size_t* err_off,
-                   DeferredCrc* crc = nullptr, uint32_t threads = 1);
+                   DeferredCrc* crc = nullptr, uint32_t threads = 1, DeferredDatas* defer = nullptr,
+                   IndexCursor** cursor = nullptr);
+int index_resume(IndexCursor* ic, uint64_t datas_end, size_t* err_off);
+void index_cursor_free(IndexCursor* ic);
+// The end offset of the DATAS entry at `off` (false: it does not parse).
+bool index_data_entry_end(const Batch& b, uint64_t off, uint64_t* end);
 struct DecodeTiming {
   double index_ms = 0;   // host pass
   double device_ms = 0;  // uploads, both kernels, downloads (HIP events)

@@ -149,6 +149,7 @@ struct Decoder {
   bool speculative = false;     // parallel_datas' walks: counts the rest of the stream cannot hold
                                 // fail at once (the sequential pass reports those streams)
   uint64_t spec_max = ~0ull;    // ... and, in the sync search, counts past this many bytes
+  DeferredDatas* defer = nullptr;  // index mode: a large first DATAS section is left to the device
 
   bool parallel_datas(uint64_t cnt);
 
@@ -370,6 +371,15 @@ struct Decoder {
     c.off = 11;
     // Node (snapshot.rs:140-153)
     if (!c.u64(&b->node_id) || !str(&b->alias) || !str(&b->addr) || !c.u64(&b->uuid_he_sent)) return fail();
+    return loop(flags, err_off);
+  }
+
+  // The sections, from c.off on (run; and after a deferred DATAS section, from its end).
+  int loop(uint32_t flags, size_t* err_off) {
+    auto fail = [&]() {
+      *err_off = c.off;
+      return c.err == CDB_OK ? CDB_INVALID_SNAPSHOT : c.err;
+    };
     for (;;) {
       uint8_t flag;
       if (!c.u8(&flag)) return fail();  // convert_stat (snapshot.rs:222-241)
@@ -387,6 +397,11 @@ struct Decoder {
       } else if (flag == 5 || flag == 6 || flag == 7) {  // DATAS / EXPIRES / DELETES
         uint64_t cnt;
         if (!c.length(&cnt)) return fail();
+        if (flag == 5 && idx && defer && idx->offset.empty() && cnt >= kDeviceIndexMinEntries) {
+          *defer = DeferredDatas{true, (uint64_t)c.off, cnt};  // the device finds the entries
+          b->n_data += cnt;
+          return kIndexDeferred;
+        }
         if (flag == 5 && idx && parallel_datas(cnt)) {  // indexed side by side (c.off at its end)
           b->n_data += cnt;
           continue;
@@ -399,7 +414,7 @@ struct Decoder {
         else if (flag == 6) b->n_expires += cnt;
         else b->n_deletes += cnt;
       } else if (flag == 8) {  // SNAPSHOT_FLAG_CHECKSUM
-        const bool defer = dcrc && idx && !idx->offset.empty();
+        const bool defer = dcrc && idx && (!idx->offset.empty() || (this->defer && this->defer->pending));
         if (defer) {  // same prefix, value and error offset as below, checked by the caller
           int64_t got;
           if (flags & CDB_DECODE_REFERENCE_CHECKSUM) {
@@ -599,6 +614,29 @@ bool Decoder::parallel_datas(uint64_t cnt) {
 
 }  // namespace
 
+struct IndexCursor {
+  Decoder d;
+  uint32_t flags;
+};
+
+int index_resume(IndexCursor* ic, uint64_t datas_end, size_t* err_off) {
+  ic->d.c.off = datas_end;
+  ic->d.c.err = CDB_OK;
+  *err_off = 0;
+  return ic->d.loop(ic->flags, err_off);
+}
+void index_cursor_free(IndexCursor* ic) { delete ic; }
+
+bool index_data_entry_end(const Batch& b, uint64_t off, uint64_t* end) {
+  Decoder d{Cursor{b.raw.data(), b.raw.size()}, const_cast<Batch*>(&b), b.raw.data()};
+  EntryIndex scratch;
+  d.idx = &scratch;
+  d.c.off = off;
+  if (!d.data_entry()) return false;
+  *end = d.c.off;
+  return true;
+}
+
 int decode_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, size_t* err_off) {
   adopt_raw(out, buf, len);
   Decoder d{Cursor{out->raw.data(), out->raw.size()}, out, out->raw.data()};
@@ -607,16 +645,21 @@ int decode_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, 
 }
 
 int index_snapshot(const uint8_t* buf, size_t len, uint32_t flags, Batch* out, EntryIndex* idx, size_t* err_off,
-                   DeferredCrc* crc, uint32_t threads) {
-  adopt_raw(out, buf, len);
+                   DeferredCrc* crc, uint32_t threads, DeferredDatas* defer, IndexCursor** cursor) {
+  if (buf) adopt_raw(out, buf, len);
   Decoder d{Cursor{out->raw.data(), out->raw.size()}, out, out->raw.data()};
   d.idx = idx;
   d.dcrc = crc;
   d.threads = threads;
-  idx->offset.reserve(len / 48 + 16);  // generator-shaped streams run ~58 bytes per entry
-  idx->kind.reserve(len / 48 + 16);
+  d.defer = defer && cursor ? defer : nullptr;
+  if (!d.defer) {
+    idx->offset.reserve(len / 48 + 16);  // generator-shaped streams run ~58 bytes per entry
+    idx->kind.reserve(len / 48 + 16);
+  }
   *err_off = 0;
-  return d.run(flags, err_off);
+  const int rc = d.run(flags, err_off);
+  if (rc == kIndexDeferred) *cursor = new IndexCursor{d, flags};
+  return rc;
 }
 
 // The entries the GPU found too large for its per-entry dedup: decoded here, exactly as

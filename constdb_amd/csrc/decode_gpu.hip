@@ -339,6 +339,150 @@ __global__ void __launch_bounds__(kDecThreads) dest_kernel(const uint64_t* __res
   dest[i] = (uint32_t)r;
 }
 
+// ---- the entry index of a large DATAS section on the device
+// The format has no sync marks: an entry starts where its predecessor ends. Each thread takes a
+// chunk of kIdxChunk bytes of the section and speculates, as the host threads of
+// decode.cpp::parallel_datas do: the first offset of its chunk from which kIdxSync consecutive
+// entries of at most 64 KB parse is taken as an entry start (a wrong offset almost never survives
+// that many), then the thread walks entries until one starts past its chunk. The host stitches the
+// chains in order from the section start (a chunk whose sync point is not where the true chain
+// enters it is walked again on the host, a few KB), and a second pass writes every offset of the
+// true chain. The checks are the loader's (read_integer bounds, negative lengths, the tag byte),
+// plus bounds no valid entry can exceed, so a chain the device accepts the host accepts too; any
+// failure on the true chain hands the section back to the host index pass.
+constexpr uint64_t kIdxChunk = 8192;
+constexpr uint32_t kIdxSync = 16;
+constexpr uint64_t kIdxEntryMax = 1u << 16;
+
+struct DCur {
+  const uint8_t* p;
+  uint64_t n, off;
+};
+__device__ __forceinline__ bool dc_int(DCur& c, int64_t* v) {
+  if (c.off >= c.n) return false;
+  const uint32_t f = c.p[c.off++];
+  const uint32_t sz = (f >> 6) == 0 ? 0 : (f >> 6) == 1 ? 1 : (f >> 6) == 2 ? 3 : 8;
+  if (sz > c.n - c.off) return false;
+  uint64_t x = sz == 8 ? 0 : (f & 0x3F);
+  for (uint32_t i = 0; i < sz; ++i) x = (x << 8) | c.p[c.off + i];
+  c.off += sz;
+  *v = (int64_t)x;
+  return true;
+}
+__device__ __forceinline__ bool dc_len(DCur& c, uint64_t* l) {
+  int64_t v;
+  if (!dc_int(c, &v) || v < 0) return false;
+  *l = (uint64_t)v;
+  return true;
+}
+__device__ __forceinline__ bool dc_span(DCur& c, uint64_t lim) {
+  uint64_t l;
+  if (!dc_len(c, &l) || l > c.n - c.off || l > lim) return false;
+  c.off += l;
+  return true;
+}
+// One DATAS entry (read_entry + the load_snapshot payloads), skipped; lim bounds every length.
+__device__ bool dc_data_entry(DCur& c, uint64_t lim) {
+  int64_t v;
+  if (!dc_span(c, lim) || !dc_int(c, &v) || !dc_int(c, &v) || !dc_int(c, &v)) return false;
+  if (c.off >= c.n) return false;
+  const uint32_t tag = c.p[c.off++];
+  uint64_t cnt;
+  switch (tag) {
+    case TAG_COUNTER:
+      if (!dc_len(c, &cnt) || cnt > min(c.n - c.off, lim) / 3) return false;
+      for (uint64_t i = 0; i < cnt; ++i)
+        if (!dc_int(c, &v) || !dc_int(c, &v) || !dc_int(c, &v)) return false;
+      return true;
+    case TAG_BYTES:
+      return dc_span(c, lim);
+    case TAG_SET:
+    case TAG_DICT: {
+      const bool dict = tag == TAG_DICT;
+      if (!dc_len(c, &cnt) || cnt > min(c.n - c.off, lim) / 2) return false;
+      for (uint64_t i = 0; i < cnt; ++i)
+        if (!dc_span(c, lim) || !dc_int(c, &v) || (dict && !dc_span(c, lim))) return false;
+      if (!dc_len(c, &cnt) || cnt > min(c.n - c.off, lim) / 2) return false;
+      for (uint64_t i = 0; i < cnt; ++i)
+        if (!dc_span(c, lim) || !dc_int(c, &v)) return false;
+      return true;
+    }
+    default:
+      return false;
+  }
+}
+
+struct IdxArgs {
+  const uint8_t* raw;
+  uint64_t n;          // stream length
+  uint64_t S;          // the section's first entry
+  uint32_t T;          // chunks: chunk t = [S + t kIdxChunk, S + (t + 1) kIdxChunk)
+  uint64_t* sync;      // per chunk: the chain's first entry (~0: none found)
+  uint32_t* count;     // per chunk: entries from sync until one starts past the chunk
+  uint64_t* stop;      // per chunk: where the walk stopped (the first entry past it, or a failure)
+  uint8_t* ok;         // per chunk: the walk reached the chunk end
+  const uint64_t* tstart;  // record pass: the true chain's first entry in chunk t (~0: not on it)
+  const uint64_t* tbase;   // record pass: index of that entry in the section
+  const uint32_t* tcount;  // record pass: entries of the true chain in chunk t
+  uint64_t* out;           // record pass: entry offsets
+};
+
+__global__ void __launch_bounds__(256) idx_walk_kernel(IdxArgs a) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.T) return;
+  const uint64_t lo = a.S + (uint64_t)t * kIdxChunk, hi = min(a.n, lo + kIdxChunk);
+  DCur c{a.raw, a.n, lo};
+  uint64_t o = lo;
+  if (t > 0) {
+    bool found = false;
+    for (; o < hi && !found; ++o) {  // (the search stays inside the chunk)
+      DCur s{a.raw, a.n, o};
+      uint32_t k = 0;
+      for (; k < kIdxSync && s.off < a.n; ++k) {
+        const uint64_t at = s.off;
+        if (!dc_data_entry(s, kIdxEntryMax) || s.off - at > kIdxEntryMax) break;
+      }
+      found = k == kIdxSync;
+    }
+    if (!found) {
+      a.sync[t] = ~0ull;
+      a.count[t] = 0;
+      a.stop[t] = lo;
+      a.ok[t] = 0;
+      return;
+    }
+    --o;
+  }
+  c.off = o;
+  uint32_t k = 0;
+  bool good = true;
+  while (c.off < hi) {
+    const uint64_t at = c.off;
+    if (!dc_data_entry(c, ~0ull)) {
+      c.off = at;
+      good = false;
+      break;
+    }
+    ++k;
+  }
+  a.sync[t] = o;
+  a.count[t] = k;
+  a.stop[t] = c.off;
+  a.ok[t] = good ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(256) idx_record_kernel(IdxArgs a) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.T || a.tstart[t] == ~0ull) return;
+  DCur c{a.raw, a.n, a.tstart[t]};
+  const uint64_t b = a.tbase[t];
+  const uint32_t m = a.tcount[t];
+  for (uint32_t k = 0; k < m; ++k) {
+    a.out[b + k] = c.off;
+    if (!dc_data_entry(c, ~0ull)) return;  // (cannot fail: the same chain parsed in the walk)
+  }
+}
+
 // Any entry left to the host tier (its count is the kHostTier marker)?
 __global__ void host_tier_flag_kernel(const uint32_t* __restrict__ nc, const uint32_t* __restrict__ mc, uint64_t n,
                                       unsigned long long* flag) {
@@ -396,6 +540,7 @@ class GpuDecode {
   uint64_t nodes() const { return nn_; }
   uint64_t members() const { return nm_; }
   uint32_t index_threads_ = 1;  // threads of the host index pass's DATAS section
+  double device_index_ms_ = 0;  // the DATAS section's device index + the resumed host pass
 
  private:
   struct HostEntry {
@@ -415,6 +560,10 @@ class GpuDecode {
   // byte references straight into the batch (pairs as written by the emit pass), then the host
   // tier's member references
   cdb_status refs_to_batch(const DecArgs& A);
+  // a deferred DATAS section: its entries indexed on the device, then the host pass resumed after
+  // it (1: the device gave up, the host pass was run instead)
+  int finish_index(size_t* err_off);
+  int device_datas(uint64_t* datas_end);
 
   cdb_ctx* ctx_;
   Batch* out_;
@@ -427,7 +576,15 @@ class GpuDecode {
   uint64_t n_ = 0, nn_ = 0, nm_ = 0;
   std::vector<uint64_t> noff_, moff_;
   std::vector<HostEntry> hosted_;
-  DevBuf d_raw_, d_meta_, d_crc_, d_rows_, d_ord_;
+  DevBuf d_raw_, d_meta_, d_crc_, d_rows_, d_ord_, d_idx_raw_;
+  DeferredDatas defer_;
+  IndexCursor* cursor_ = nullptr;
+  struct CursorFree {
+    IndexCursor** p;
+    ~CursorFree() {
+      if (*p) index_cursor_free(*p);
+    }
+  } cursor_free_{&cursor_};
   bool ordered_ = false;  // the sections are contiguous, in DATAS, EXPIRES, DELETES order
   Sections sec_{};
   DecArgs A_;
@@ -437,12 +594,135 @@ class GpuDecode {
 
 int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTiming* tm) {
   const auto t0 = std::chrono::steady_clock::now();
-  rc_ = index_snapshot(buf, len, flags_, out_, &idx_, err_off, &dcrc_, index_threads_);
+  rc_ = index_snapshot(buf, len, flags_, out_, &idx_, err_off, &dcrc_, index_threads_, &defer_, &cursor_);
+  if (rc_ == kIndexDeferred) rc_ = CDB_OK;  // the DATAS section is indexed in prepare_device
   if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return rc_;
 }
 
+int GpuDecode::device_datas(uint64_t* datas_end) {
+  const uint64_t len = out_->raw.size(), S = defer_.start, cnt = defer_.count;
+  hipStream_t s = ctx_->stream;
+  if ((st_ = alloc(&d_idx_raw_.p, len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK) return -1;
+  if ((st_ = staged_h2d(ctx_, d_idx_raw_.p, out_->raw.data(), len, s)) != CDB_OK) return -1;
+  const uint32_t T = (uint32_t)((len - S + kIdxChunk - 1) / kIdxChunk);
+  DevBuf work;
+  const size_t wbytes = (size_t)T * (8 + 4 + 8 + 1 + 8 + 8 + 4) + 64;
+  if ((st_ = alloc(&work.p, wbytes, "decode: device entry index scratch")) != CDB_OK) return -1;
+  IdxArgs a;
+  a.raw = (const uint8_t*)d_idx_raw_.p;
+  a.n = len;
+  a.S = S;
+  a.T = T;
+  uint8_t* w = (uint8_t*)work.p;
+  a.sync = (uint64_t*)w;
+  a.stop = a.sync + T;
+  uint64_t* d_tstart = a.stop + T;
+  uint64_t* d_tbase = d_tstart + T;
+  a.count = (uint32_t*)(d_tbase + T);
+  uint32_t* d_tcount = a.count + T;
+  a.ok = (uint8_t*)(d_tcount + T);
+  a.tstart = d_tstart;
+  a.tbase = d_tbase;
+  a.tcount = d_tcount;
+  idx_walk_kernel<<<(T + 255) / 256, 256, 0, s>>>(a);
+  ck(hipGetLastError(), "idx_walk_kernel");
+  std::vector<uint64_t> sync(T), stop(T), tstart(T, ~0ull), tbase(T, 0);
+  std::vector<uint32_t> count(T), tcount(T, 0);
+  std::vector<uint8_t> ok(T);
+  ck(hipMemcpyAsync(sync.data(), a.sync, T * 8ull, hipMemcpyDeviceToHost, s), "d2h(index)");
+  ck(hipMemcpyAsync(stop.data(), a.stop, T * 8ull, hipMemcpyDeviceToHost, s), "d2h(index)");
+  ck(hipMemcpyAsync(count.data(), a.count, T * 4ull, hipMemcpyDeviceToHost, s), "d2h(index)");
+  ck(hipMemcpyAsync(ok.data(), a.ok, T, hipMemcpyDeviceToHost, s), "d2h(index)");
+  ck(hipStreamSynchronize(s), "sync(index)");
+  if (st_ != CDB_OK) return -1;
+  // stitch: the true chain from the section start, chunk by chunk
+  uint64_t cur = S, got = 0;
+  for (uint32_t t = 0; t < T && got < cnt; ++t) {
+    const uint64_t hi = std::min<uint64_t>(len, S + (uint64_t)(t + 1) * kIdxChunk);
+    if (cur >= hi) continue;  // an entry spans the whole chunk
+    const uint64_t need = cnt - got;
+    if (sync[t] == cur && (ok[t] || count[t] >= need)) {  // thread t's chain is the true one
+      const uint32_t m = (uint32_t)std::min<uint64_t>(count[t], need);
+      tstart[t] = cur;
+      tbase[t] = got;
+      tcount[t] = m;
+      got += m;
+      cur = stop[t];
+      continue;
+    }
+    if (sync[t] == cur) return 1;  // the true chain fails inside the section: the host reports it
+    // the true chain enters the chunk elsewhere: walk it here (at most a chunk of entries)
+    uint32_t m = 0;
+    const uint64_t c0 = cur;
+    while (cur < hi && m < need) {
+      uint64_t e;
+      if (!index_data_entry_end(*out_, cur, &e)) return 1;
+      cur = e;
+      ++m;
+    }
+    tstart[t] = c0;
+    tbase[t] = got;
+    tcount[t] = m;
+    got += m;
+  }
+  if (got < cnt) return 1;  // the stream ends inside the section
+  // every offset of the true chain, written on the device, then into the host index
+  ck(hipMemcpyAsync(d_tstart, tstart.data(), T * 8ull, hipMemcpyHostToDevice, s), "h2d(index)");
+  ck(hipMemcpyAsync(d_tbase, tbase.data(), T * 8ull, hipMemcpyHostToDevice, s), "h2d(index)");
+  ck(hipMemcpyAsync(d_tcount, tcount.data(), T * 4ull, hipMemcpyHostToDevice, s), "h2d(index)");
+  DevBuf offs;
+  if ((st_ = alloc(&offs.p, cnt * 8, "decode: device entry offsets")) != CDB_OK) return -1;
+  a.out = (uint64_t*)offs.p;
+  idx_record_kernel<<<(T + 255) / 256, 256, 0, s>>>(a);
+  ck(hipGetLastError(), "idx_record_kernel");
+  idx_.offset.resize(cnt);
+  if (st_ == CDB_OK) st_ = staged_d2h(ctx_, idx_.offset.data(), offs.p, cnt * 8, s);
+  ck(hipStreamSynchronize(s), "sync(index)");
+  if (st_ != CDB_OK) return -1;
+  if (!index_data_entry_end(*out_, idx_.offset.back(), datas_end)) return 1;
+  return 0;
+}
+
+int GpuDecode::finish_index(size_t* err_off) {
+  if (!cursor_) return rc_;
+  if (hipSetDevice(ctx_->device) != hipSuccess) return fail(ctx_, CDB_DEVICE_ERROR, "hipSetDevice");
+  uint64_t end = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int dv = device_datas(&end);
+  if (dv < 0) return st_;
+  if (dv == 0) {
+    std::vector<uint64_t> datas(std::move(idx_.offset));
+    idx_.offset.clear();
+    idx_.kind.clear();
+    rc_ = index_resume(cursor_, end, err_off);  // EXPIRES, DELETES, the checksum
+    std::vector<uint64_t> all;
+    all.reserve(datas.size() + idx_.offset.size());
+    all.insert(all.end(), datas.begin(), datas.end());
+    all.insert(all.end(), idx_.offset.begin(), idx_.offset.end());
+    std::vector<uint8_t> kinds(datas.size(), 0);
+    kinds.insert(kinds.end(), idx_.kind.begin(), idx_.kind.end());
+    idx_.offset.swap(all);
+    idx_.kind.swap(kinds);
+  } else {  // the host index pass over the whole stream: its statuses and offsets
+    if (d_idx_raw_.p) (void)hipFree(d_idx_raw_.p);
+    d_idx_raw_.p = nullptr;
+    idx_ = EntryIndex{};
+    dcrc_ = DeferredCrc{};
+    *out_ = Batch{std::move(out_->raw)};
+    rc_ = index_snapshot(nullptr, out_->raw.size(), flags_, out_, &idx_, err_off, &dcrc_, index_threads_);
+  }
+  index_cursor_free(cursor_);
+  cursor_ = nullptr;
+  device_index_ms_ = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return rc_;
+}
+
 int GpuDecode::prepare_device(size_t* err_off) {
+  if (cursor_) {
+    const int rc = finish_index(err_off);
+    if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) return rc;
+  }
   const uint64_t len = out_->raw.size();
   const uint64_t n = n_ = idx_.offset.size();
   if (n == 0) return rc_;
@@ -471,7 +751,13 @@ int GpuDecode::prepare_device(size_t* err_off) {
   if (pad) ck(hipMemsetAsync(d_raw_.p, 0, pad, s), "memset(decode)");
   ck(hipMemsetAsync(d_small, 0, 32, s), "memset(decode)");
   const uint8_t* raw_dev = (const uint8_t*)d_raw_.p + pad;
-  if (st_ == CDB_OK) st_ = staged_h2d(ctx_, (void*)raw_dev, out_->raw.data(), len, s);
+  if (st_ == CDB_OK && d_idx_raw_.p) {  // already on the device (the DATAS index): moved to its CRC place
+    ck(hipMemcpyAsync((void*)raw_dev, d_idx_raw_.p, len, hipMemcpyDeviceToDevice, s), "d2d(decode)");
+    ck(hipStreamSynchronize(s), "sync(decode)");
+    (void)hipFree(d_idx_raw_.p);
+    d_idx_raw_.p = nullptr;
+  } else if (st_ == CDB_OK)
+    st_ = staged_h2d(ctx_, (void*)raw_dev, out_->raw.data(), len, s);
   if (st_ == CDB_OK) st_ = staged_h2d(ctx_, d_off, idx_.offset.data(), n * 8, s);
   ck(hipMemcpyAsync(d_kind, idx_.kind.data(), n, hipMemcpyHostToDevice, s), "h2d(decode)");
   if (st_ != CDB_OK) return st_;

@@ -53,7 +53,6 @@ enum WsSlot {
   WS_HOST_OUT_K, WS_HOST_OUT_N, WS_HOST_OUT_M,          // cdb_merge: device-side result
   WS_RUNDIR, WS_RUNMISC,                                // sorted-run path: run directories, gap lists
   WS_HOTC3, WS_HOTMETA, WS_HOTK, WS_HOTCH, WS_RADIX,    // over-capacity child path (hot.hip.h)
-  WS_HOTSORT,                                           // its larger buckets' pairs, gathered
   WS_MAT,                                               // sorted-run path: materialisation counts
   WS_PIPE,                                              // pipelined bucket phase: range bases, totals
   WS_XK, WS_XN, WS_XM,                                  // sharded merge: received rows per family

@@ -545,7 +545,7 @@ cdb_status radix_sort_pairs(cdb_ctx* ctx, uint64_t** k, uint32_t** v, uint64_t* 
     radix_hist_kernel<<<tiles, kRadixThreads, 0, s>>>(ka, n, sh, hist, tiles);
     CDB_TRY(launch_check(ctx, s, "radix_hist_kernel"));
     CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, hist, 256ull * tiles, base, (uint32_t*)nullptr, nullptr, s));
-    radix_scatter_kernel<<<tiles, kRadixThreads, 0, s>>>(ka, va, n, sh, hist, base, tiles, kb, vb);
+    radix_scatter_kernel<<<tiles, kRadixThreads, 0, s>>>(ka, va, n, sh, base, tiles, kb, vb);
     CDB_TRY(launch_check(ctx, s, "radix_scatter_kernel"));
     std::swap(ka, kb);
     std::swap(va, vb);
@@ -563,8 +563,8 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
                      uint64_t tc, uint64_t cmax, hipStream_t s) {
   cdb_status st = CDB_OK;
   const uint32_t H = (uint32_t)wide_ids.size();
-  // device: ids[H] | hk_off[H + 1] | c_off[H + 1] | hk_kout[H] | run count | sort lists
-  uint32_t* meta = (uint32_t*)ws_get(ctx, WS_HOTMETA, (9ull * H + 32) * sizeof(uint32_t), &st);
+  // device: ids[H] | hk_off[H + 1] | c_off[H + 1] | hk_kout[H] | run count
+  uint32_t* meta = (uint32_t*)ws_get(ctx, WS_HOTMETA, (5ull * H + 8) * sizeof(uint32_t), &st);
   if (!meta) return st;
   HotArgs HA;
   std::memset(&HA, 0, sizeof HA);
@@ -576,9 +576,6 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   HA.c_off = d_c_off;
   HA.hk_kout = d_c_off + H + 1;
   uint64_t* d_runs = (uint64_t*)(((uintptr_t)(HA.hk_kout + H) + 7) & ~(uintptr_t)7);
-  uint32_t* d_small = (uint32_t*)(d_runs + 1);  // bucket lists of the per-bucket sort
-  uint64_t* d_loff = (uint64_t*)(((uintptr_t)(d_small + H) + 7) & ~(uintptr_t)7);  // H + 1 (larger buckets)
-  uint32_t* d_large = (uint32_t*)(d_loff + H + 1);
   HA.H = H;
   HA.n_children = tc;
   // Tag layout W = G << g_shift | id hash bits << 6 | pos, sorted on g_shift + gbits bits in 8-bit
@@ -632,54 +629,12 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   hot_keys_kernel<<<H, kBktThreads, 0, s>>>(A, HA);
   CDB_TRY(launch_check(ctx, s, "hot_keys_kernel"));
   const uint32_t grid = (uint32_t)std::min<uint64_t>((tc + 255) / 256, 16384);
-  // host-side plan of the per-bucket sort: buckets of at most 2048 / kLocalSortMax children sort
-  // in one workgroup's LDS; the larger ones share the LSD radix sort
-  std::vector<uint32_t> small2k, small8k, large;
-  std::vector<uint64_t> loff(1, 0);
-  for (uint32_t h = 0; h < H; ++h) {
-    const uint32_t c = c_off[h + 1] - c_off[h];
-    if (c <= 1) continue;
-    if (c <= 2048) small2k.push_back(h);
-    else if (c <= kLocalSortMax) small8k.push_back(h);
-    else {
-      large.push_back(h);
-      loff.push_back(loff.back() + c);
-    }
-  }
   if (tc) {
     hot_tag_kernel<<<grid, 256, 0, s>>>(A, HA);
     CDB_TRY(launch_check(ctx, s, "hot_tag_kernel"));
-    const uint32_t n2 = (uint32_t)small2k.size(), n8 = (uint32_t)small8k.size();
-    if (n2 + n8) {
-      std::vector<uint32_t> lists(small2k);
-      lists.insert(lists.end(), small8k.begin(), small8k.end());
-      CDB_HIP(hipMemcpyAsync(d_small, lists.data(), lists.size() * 4, hipMemcpyHostToDevice, s), "h2d");
-      CDB_HIP(hipStreamSynchronize(s), "sync");  // (lists is a local copy source)
-      if (n2) hot_local_sort_kernel<2048><<<n2, 512, 0, s>>>(HA.w, HA.v, d_c_off, d_small);
-      if (n8) hot_local_sort_kernel<kLocalSortMax><<<n8, 512, 0, s>>>(HA.w, HA.v, d_c_off, d_small + n2);
-      CDB_TRY(launch_check(ctx, s, "hot_local_sort_kernel"));
-    }
-    const uint64_t nl = loff.back();
-    if (nl == tc) {  // every child in a larger bucket: the radix sort in place (ping-pong)
-      CDB_TRY(radix_sort_pairs(ctx, &HA.w, &HA.v, w2, v2, tc, HA.g_shift + gbits, s));
-    } else if (nl) {  // gathered, sorted (in the spare pair), put back
-      const uint32_t L = (uint32_t)large.size();
-      CDB_HIP(hipMemcpyAsync(d_large, large.data(), L * 4, hipMemcpyHostToDevice, s), "h2d");
-      CDB_HIP(hipMemcpyAsync(d_loff, loff.data(), (L + 1) * 8, hipMemcpyHostToDevice, s), "h2d");
-      uint8_t* gs = (uint8_t*)ws_get(ctx, WS_HOTSORT, nl * 12 + 64, &st);
-      if (!gs) return st;
-      uint64_t* gw = (uint64_t*)gs;
-      uint32_t* gv = (uint32_t*)(gw + nl);
-      const uint32_t gg = (uint32_t)std::min<uint64_t>((nl + 255) / 256, 16384);
-      hot_gather_kernel<<<gg, 256, 0, s>>>(HA.w, HA.v, w2, v2, d_c_off, d_large, d_loff, L, nl, 1);
-      CDB_TRY(launch_check(ctx, s, "hot_gather_kernel"));
-      uint64_t* sk = w2;
-      uint32_t* sv = v2;
-      CDB_TRY(radix_sort_pairs(ctx, &sk, &sv, gw, gv, nl, HA.g_shift + gbits, s));
-      hot_gather_kernel<<<gg, 256, 0, s>>>(HA.w, HA.v, sk, sv, d_c_off, d_large, d_loff, L, nl, 0);
-      CDB_TRY(launch_check(ctx, s, "hot_gather_kernel"));
-      CDB_HIP(hipStreamSynchronize(s), "sync");  // (large / loff are copy sources)
-    }
+    // (per-bucket bitonic sorts in LDS measured slower than this global radix sort: C3 9.98 vs
+    // 8.90 ms, C5 25.9 vs 24.3 ms; profiles/r03/experiments_r3.txt)
+    CDB_TRY(radix_sort_pairs(ctx, &HA.w, &HA.v, w2, v2, tc, HA.g_shift + gbits, s));
   }
   if (tc) {
     // the sort's other buffers are free now: fold results per run start

@@ -14,10 +14,9 @@
 //                     child that takes no part gets its bucket's marker (every W bit of the
 //                     bucket's last key set: pos 63, which no row has), so it sorts to the end of
 //                     its bucket's children and every bucket's children keep their flat range;
-//   sort of each bucket's (W, child) pairs inside that range: one workgroup in LDS for a bucket of
-//                     at most kLocalSortMax children (bitonic on (W, child)), the LSD radix sort
-//                     of radix.hip.h over the larger buckets' pairs gathered together (W orders
-//                     them by bucket, then in place again);
+//   radix sort of (W, child) pairs (radix.hip.h), stable, so equal W keep (bucket, row) order;
+//                     W orders the buckets, so bucket h's children (markers last) keep its flat
+//                     range [c_off[h], c_off[h + 1]);
 //   hot_fold_kernel : one thread per W-run (a (key, child id) group, ~ one row per replica):
 //                     folds every exact child id of the run in (pos, src) order -- Counter::merge's
 //                     head-t rule or LWWHash::set's later-wins rule -- counting outputs (pass 0)
@@ -394,77 +393,6 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
     }
   }
   if (pass == 0 && gcm) atomicAdd(&stat_shard(A.stats)[ST_MEMBERS_GCED], gcm);
-}
-
-// ---- per-bucket sort of the (W, child) pairs (every bucket's children keep their flat range)
-constexpr uint32_t kLocalSortMax = 8192;
-
-// One workgroup per listed bucket of at most N children: bitonic sort on (W, child) in LDS, in
-// place. (W, child) pairs are distinct, so the order is total and the result deterministic.
-template <uint32_t N>
-__global__ void __launch_bounds__(512) hot_local_sort_kernel(uint64_t* __restrict__ w, uint32_t* __restrict__ v,
-                                                             const uint32_t* __restrict__ c_off,
-                                                             const uint32_t* __restrict__ list) {
-  __shared__ uint64_t sk[N];
-  __shared__ uint32_t sv[N];
-  const uint32_t h = list[blockIdx.x];
-  const uint32_t b0 = c_off[h], cnt = c_off[h + 1] - b0;
-  uint32_t n = 2;
-  while (n < cnt) n <<= 1;
-  for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    sk[i] = i < cnt ? w[b0 + i] : ~0ull;
-    sv[i] = i < cnt ? v[b0 + i] : ~0u;
-  }
-  __syncthreads();
-  for (uint32_t k = 2; k <= n; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint32_t ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t a = sk[i], c = sk[ixj];
-          const uint32_t av = sv[i], cv = sv[ixj];
-          const bool gt = a > c || (a == c && av > cv);
-          if (gt == ((i & k) == 0)) {
-            sk[i] = c;
-            sk[ixj] = a;
-            sv[i] = cv;
-            sv[ixj] = av;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-    w[b0 + i] = sk[i];
-    v[b0 + i] = sv[i];
-  }
-}
-
-// The larger buckets' pairs, gathered into one array in bucket order (to) or back (!to): list[i]
-// is a larger bucket, loff the prefix of their child counts.
-__global__ void __launch_bounds__(256) hot_gather_kernel(uint64_t* __restrict__ w, uint32_t* __restrict__ v,
-                                                         uint64_t* __restrict__ gw, uint32_t* __restrict__ gv,
-                                                         const uint32_t* __restrict__ c_off,
-                                                         const uint32_t* __restrict__ list,
-                                                         const uint64_t* __restrict__ loff, uint32_t nl, uint64_t n,
-                                                         int to) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t lo = 0, hi = nl;  // last l with loff[l] <= i
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (loff[mid] <= i) lo = mid;
-      else hi = mid;
-    }
-    const uint64_t f = c_off[list[lo]] + (i - loff[lo]);
-    if (to) {
-      gw[i] = w[f];
-      gv[i] = v[f];
-    } else {
-      w[f] = gw[i];
-      v[f] = gv[i];
-    }
-  }
 }
 
 // Key rows: counter sums and child ranges (bucket-relative, as every tier leaves them for the

@@ -4,9 +4,7 @@
 //                         whole array gives every (digit, tile) its first output slot;
 //   radix_scatter_kernel: each tile ranks its pairs stably (wave ballots find the lanes holding
 //                         the same digit; a per-digit running count in LDS carries the order from
-//                         one 256-pair round to the next), stages them in LDS in digit order and
-//                         writes them out in that order: consecutive threads, consecutive slots of
-//                         one digit (a pair written straight from its round touched its own line).
+//                         one 256-pair round to the next) and writes them to their slots.
 // Used by the over-capacity bucket path (hot.hip.h), where a few keys own millions of children.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -46,45 +44,23 @@ __device__ __forceinline__ uint64_t radix_match(uint32_t d, bool valid) {
 
 __global__ void __launch_bounds__(kRadixThreads) radix_scatter_kernel(const uint64_t* __restrict__ kin,
                                                                       const uint32_t* __restrict__ vin, uint64_t n,
-                                                                      int shift, const uint32_t* __restrict__ hist,
-                                                                      const uint32_t* __restrict__ base,
+                                                                      int shift, const uint32_t* __restrict__ base,
                                                                       uint32_t tiles, uint64_t* __restrict__ kout,
                                                                       uint32_t* __restrict__ vout) {
   constexpr int W = kRadixThreads / 64;
-  __shared__ uint64_t sk[kRadixTile];  // the tile's pairs in digit order (stable), then written out
-  __shared__ uint32_t sv[kRadixTile];
-  __shared__ uint32_t start[256];      // tile-local first slot of each digit
-  __shared__ uint32_t run[256];        // next tile-local slot of each digit
-  __shared__ uint32_t wcnt[W][256];    // this round: pairs of each digit per wave
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, tid = threadIdx.x;
+  __shared__ uint32_t run[256];      // pairs of each digit placed by earlier rounds of this tile
+  __shared__ uint32_t wcnt[W][256];  // this round: pairs of each digit per wave
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  run[threadIdx.x] = base[(uint64_t)threadIdx.x * tiles + blockIdx.x];
   const uint64_t t0 = (uint64_t)blockIdx.x * kRadixTile;
-  const uint32_t nt = (uint32_t)min<uint64_t>(kRadixTile, n - t0);
-  // tile-local digit starts: exclusive scan of this tile's histogram (from radix_hist_kernel)
-  {
-    uint32_t c = hist[(uint64_t)tid * tiles + blockIdx.x];
-    uint32_t incl = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += t;
-    }
-    wcnt[0][tid] = incl;  // (scratch) inclusive scan inside each wave
-    __syncthreads();
-    uint32_t add = 0;
-    for (int w = 0; w < wv; ++w) add += wcnt[0][64 * w + 63];
-    start[tid] = add + incl - c;
-    run[tid] = add + incl - c;
-    __syncthreads();
-  }
   const uint64_t lt = lane ? ((~0ull) >> (64 - lane)) : 0ull;
-  // 1. stable ranks inside the tile, pairs staged in LDS in digit order
   for (int r = 0; r < kRadixRounds; ++r) {
-    for (int w = 0; w < W; ++w) wcnt[w][tid] = 0;
+    for (int w = 0; w < W; ++w) wcnt[w][threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t li = (uint32_t)r * kRadixThreads + tid;
-    const bool valid = li < nt;
-    const uint64_t k = valid ? kin[t0 + li] : 0;
-    const uint32_t v = valid ? vin[t0 + li] : 0;
+    const uint64_t i = t0 + (uint64_t)r * kRadixThreads + threadIdx.x;
+    const bool valid = i < n;
+    const uint64_t k = valid ? kin[i] : 0;
+    const uint32_t v = valid ? vin[i] : 0;
     const uint32_t d = (uint32_t)(k >> shift) & 0xFF;
     const uint64_t m = radix_match(d, valid);
     const uint32_t below = (uint32_t)__popcll(m & lt);
@@ -93,22 +69,14 @@ __global__ void __launch_bounds__(kRadixThreads) radix_scatter_kernel(const uint
     if (valid) {
       uint32_t off = run[d] + below;
       for (int w = 0; w < wv; ++w) off += wcnt[w][d];
-      sk[off] = k;
-      sv[off] = v;
+      kout[off] = k;
+      vout[off] = v;
     }
     __syncthreads();
     uint32_t tot = 0;
-    for (int w = 0; w < W; ++w) tot += wcnt[w][tid];
-    run[tid] += tot;
+    for (int w = 0; w < W; ++w) tot += wcnt[w][threadIdx.x];
+    run[threadIdx.x] += tot;
     __syncthreads();
-  }
-  // 2. out in slot order: consecutive threads write consecutive rows of one digit's output range
-  for (uint32_t li = tid; li < nt; li += kRadixThreads) {
-    const uint64_t k = sk[li];
-    const uint32_t d = (uint32_t)(k >> shift) & 0xFF;
-    const uint32_t o = base[(uint64_t)d * tiles + blockIdx.x] + (li - start[d]);
-    kout[o] = k;
-    vout[o] = sv[li];
   }
 }
 

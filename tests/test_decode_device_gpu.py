@@ -101,6 +101,14 @@ def test_device_decode_generator_and_merge(ctx):
         _release(din)
 
 
+def test_device_decode_large_sections(ctx):
+    """Snapshots whose DATAS sections exceed 2^17 entries (indexed on the device) decoded straight
+    into HBM: rows equal the uploaded host batches."""
+    cfg = cdb.gen_config(seed=9, universe=300_000, n_replicas=3, replica_hi=3, side_permille=100)
+    _, din = _check(ctx, [cdb.gen_snapshot(cfg, r) for r in range(3)])
+    _release(din)
+
+
 def test_device_decode_host_tier(ctx):
     """Objects past the per-thread dedup limits (3000 members, 1500 nodes) are decoded on the
     host and uploaded into their reserved rows at the snapshot's fold position."""

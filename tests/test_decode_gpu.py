@@ -179,3 +179,40 @@ def test_decode_gpu_staging_ring_wraps(ctx):
     host = cdb.decode_snapshot(snap)
     for _ in range(2):
         _same_batch(host, cdb.decode_snapshot_gpu(ctx, snap))
+
+
+def test_decode_gpu_device_index_mirrors_host(ctx):
+    """A DATAS section of more than 2^17 entries is indexed on the device (speculative chains per
+    8 KB chunk, stitched from the section start; the host pass resumes after it for EXPIRES,
+    DELETES and the checksum). The batch equals the host decoder's, and on damaged streams --
+    truncated inside the section or after it, bytes flipped inside it, a bad checksum -- the
+    status and the error offset are the host decoder's (the device hands failures back to it)."""
+    import random
+    cfg = cdb.gen_config(seed=21, universe=400_000, n_replicas=2, replica_hi=2, side_permille=150, mix_set=10,
+                         mix_dict=10)
+    snap = cdb.gen_snapshot(cfg, 1)
+    host = cdb.decode_snapshot(snap)
+    assert host.info().n_data > (1 << 17) and host.info().n_expires > 0 and host.info().n_deletes > 0
+    _same_batch(host, cdb.decode_snapshot_gpu(ctx, snap))
+    rng = random.Random(5)
+    cases = [snap[: len(snap) // 2], snap[: len(snap) * 9 // 10], snap[:-9], snap[:-3]]
+    for _ in range(6):
+        bad = bytearray(snap)
+        at = rng.randrange(len(snap) // 10, len(snap) * 8 // 10)
+        bad[at] ^= 1 << rng.randrange(8)
+        cases.append(bytes(bad))
+    bad = bytearray(snap)
+    bad[-2] ^= 0x40
+    cases.append(bytes(bad))
+    for i, case in enumerate(cases):
+        for ref in (False, True):
+            want = got = None
+            try:
+                cdb.decode_snapshot(case, reference_checksum=ref)
+            except cdb.CstError as e:
+                want = (type(e), getattr(e, "offset", None))
+            try:
+                cdb.decode_snapshot_gpu(ctx, case, reference_checksum=ref)
+            except cdb.CstError as e:
+                got = (type(e), getattr(e, "offset", None))
+            assert got == want, (i, ref)
