@@ -1,4 +1,5 @@
 #!/bin/bash
+# (round-2 recipe behind DESIGN.md 4a'; CDB_WIDE_SERIAL, which serialised the wide tier, was removed in round 3)
 # Instruction counts of the sorted-run wave kernel stopped after each phase (variants/libcdb_stopN.so).
 set -o pipefail
 export TMPDIR=/tmp

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (CDB_EXP_NO_LOCAL was a temporary switch of this experiment; the per-bucket sorts it compared were removed)
 # Round 3 experiment: per-bucket LDS sorts (1024 threads, sized) vs the global radix sort for the
 # chip-wide child path (C3, C5), the chip-wide tests, and the selection-loop hazard program.
 set -o pipefail
