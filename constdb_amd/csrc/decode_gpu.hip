@@ -427,13 +427,18 @@ struct IdxArgs {
   uint64_t* out;           // record pass: entry offsets
 };
 
-__global__ void __launch_bounds__(256) idx_walk_kernel(IdxArgs a) {
+// req == null: the speculative pass (sync search, then the walk); req[t] != ~0: walk chunk t again
+// from req[t] (the offset at which the true chain enters it), other chunks keep their results.
+__global__ void __launch_bounds__(256) idx_walk_kernel(IdxArgs a, const uint64_t* __restrict__ req) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= a.T) return;
   const uint64_t lo = a.S + (uint64_t)t * kIdxChunk, hi = min(a.n, lo + kIdxChunk);
   DCur c{a.raw, a.n, lo};
   uint64_t o = lo;
-  if (t > 0) {
+  if (req) {
+    if (req[t] == ~0ull) return;
+    o = req[t];
+  } else if (t > 0) {
     bool found = false;
     for (; o < hi && !found; ++o) {  // (the search stays inside the chunk)
       DCur s{a.raw, a.n, o};
@@ -625,46 +630,69 @@ int GpuDecode::device_datas(uint64_t* datas_end) {
   a.tstart = d_tstart;
   a.tbase = d_tbase;
   a.tcount = d_tcount;
-  idx_walk_kernel<<<(T + 255) / 256, 256, 0, s>>>(a);
+  idx_walk_kernel<<<(T + 255) / 256, 256, 0, s>>>(a, nullptr);
   ck(hipGetLastError(), "idx_walk_kernel");
-  std::vector<uint64_t> sync(T), stop(T), tstart(T, ~0ull), tbase(T, 0);
+  std::vector<uint64_t> sync(T), stop(T), tstart(T, ~0ull), tbase(T, 0), req(T);
   std::vector<uint32_t> count(T), tcount(T, 0);
   std::vector<uint8_t> ok(T);
-  ck(hipMemcpyAsync(sync.data(), a.sync, T * 8ull, hipMemcpyDeviceToHost, s), "d2h(index)");
-  ck(hipMemcpyAsync(stop.data(), a.stop, T * 8ull, hipMemcpyDeviceToHost, s), "d2h(index)");
-  ck(hipMemcpyAsync(count.data(), a.count, T * 4ull, hipMemcpyDeviceToHost, s), "d2h(index)");
-  ck(hipMemcpyAsync(ok.data(), a.ok, T, hipMemcpyDeviceToHost, s), "d2h(index)");
-  ck(hipStreamSynchronize(s), "sync(index)");
+  auto download = [&]() {
+    ck(hipMemcpyAsync(sync.data(), a.sync, T * 8ull, hipMemcpyDeviceToHost, s), "d2h(index)");
+    ck(hipMemcpyAsync(stop.data(), a.stop, T * 8ull, hipMemcpyDeviceToHost, s), "d2h(index)");
+    ck(hipMemcpyAsync(count.data(), a.count, T * 4ull, hipMemcpyDeviceToHost, s), "d2h(index)");
+    ck(hipMemcpyAsync(ok.data(), a.ok, T, hipMemcpyDeviceToHost, s), "d2h(index)");
+    ck(hipStreamSynchronize(s), "sync(index)");
+  };
+  download();
   if (st_ != CDB_OK) return -1;
-  // stitch: the true chain from the section start, chunk by chunk
-  uint64_t cur = S, got = 0;
-  for (uint32_t t = 0; t < T && got < cnt; ++t) {
-    const uint64_t hi = std::min<uint64_t>(len, S + (uint64_t)(t + 1) * kIdxChunk);
-    if (cur >= hi) continue;  // an entry spans the whole chunk
-    const uint64_t need = cnt - got;
-    if (sync[t] == cur && (ok[t] || count[t] >= need)) {  // thread t's chain is the true one
-      const uint32_t m = (uint32_t)std::min<uint64_t>(count[t], need);
+  // stitch: the true chain from the section start, chunk by chunk. A chunk whose sync point is not
+  // where the true chain enters it (a spurious sync inside an entry's bytes) is walked again on the
+  // device from there; its chain usually joins the speculative one, so later chunks keep theirs,
+  // and rounds repeat until every chunk on the chain starts where the chain enters it.
+  bool consistent = false;
+  for (int round = 0; round < 16 && !consistent; ++round) {  // (3-4 rounds on the generator's streams)
+    consistent = true;
+    std::fill(req.begin(), req.end(), ~0ull);
+    uint64_t cur = S, got = 0;
+    for (uint32_t t = 0; t < T && got < cnt; ++t) {
+      const uint64_t hi = std::min<uint64_t>(len, S + (uint64_t)(t + 1) * kIdxChunk);
+      if (cur >= hi) continue;  // an entry spans the whole chunk
+      const uint64_t need = cnt - got;
+      if (sync[t] != cur) {
+        req[t] = cur;
+        consistent = false;
+      } else if (!ok[t] && count[t] < need) {
+        // the chain fails inside the section: on the true chain (every chunk so far consistent)
+        // the host pass reports it; after a re-walk request it is a speculative chain, so the
+        // round ends here and the next one resumes from the re-walked chunks
+        if (consistent) return 1;
+        break;
+      }
+      got += std::min<uint64_t>(count[t], need);
+      cur = stop[t];
+    }
+    if (consistent) break;
+    DevBuf d_req;
+    if ((st_ = alloc(&d_req.p, T * 8ull, "decode: device entry index scratch")) != CDB_OK) return -1;
+    ck(hipMemcpyAsync(d_req.p, req.data(), T * 8ull, hipMemcpyHostToDevice, s), "h2d(index)");
+    idx_walk_kernel<<<(T + 255) / 256, 256, 0, s>>>(a, (const uint64_t*)d_req.p);
+    ck(hipGetLastError(), "idx_walk_kernel");
+    download();
+    if (st_ != CDB_OK) return -1;
+  }
+  if (!consistent) return 1;
+  uint64_t got = 0;
+  {
+    uint64_t cur = S;
+    for (uint32_t t = 0; t < T && got < cnt; ++t) {
+      const uint64_t hi = std::min<uint64_t>(len, S + (uint64_t)(t + 1) * kIdxChunk);
+      if (cur >= hi) continue;
+      const uint32_t m = (uint32_t)std::min<uint64_t>(count[t], cnt - got);
       tstart[t] = cur;
       tbase[t] = got;
       tcount[t] = m;
       got += m;
       cur = stop[t];
-      continue;
     }
-    if (sync[t] == cur) return 1;  // the true chain fails inside the section: the host reports it
-    // the true chain enters the chunk elsewhere: walk it here (at most a chunk of entries)
-    uint32_t m = 0;
-    const uint64_t c0 = cur;
-    while (cur < hi && m < need) {
-      uint64_t e;
-      if (!index_data_entry_end(*out_, cur, &e)) return 1;
-      cur = e;
-      ++m;
-    }
-    tstart[t] = c0;
-    tbase[t] = got;
-    tcount[t] = m;
-    got += m;
   }
   if (got < cnt) return 1;  // the stream ends inside the section
   // every offset of the true chain, written on the device, then into the host index

@@ -481,11 +481,16 @@ cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, uint64_t nb, in
       ctx->runs_host[f * (kMaxRuns + 1) + r] = r <= nr ? in->run_start[f][r] : in->run_start[f][nr];
   CDB_HIP(hipMemcpyAsync(d_rbase, ctx->runs_host, sizeof ctx->runs_host, hipMemcpyHostToDevice, s), "h2d runs");
   CDB_HIP(hipMemsetAsync(d_err, 0, 16, s), "memset");
+  // the three families' directories are independent: nodes and members on the side streams
+  CDB_HIP(hipEventRecord(ctx->ev_pfork, s), "event");
+  CDB_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_pfork, 0), "wait");
+  CDB_HIP(hipStreamWaitEvent(ctx->side2, ctx->ev_pfork, 0), "wait");
   for (int f = 0; f < 3; ++f) {
+    hipStream_t fs = f == 0 ? s : f == 1 ? ctx->side : ctx->side2;
     uint32_t* rd = rdir + f * per_fam;
     for (uint32_t r = 0; r < nr; ++r)  // empty runs: every bucket starts at row 0
       if (in->run_start[f][r + 1] == in->run_start[f][r])
-        CDB_HIP(hipMemsetAsync(rd + r * row, 0, row * sizeof(uint32_t), s), "memset run");
+        CDB_HIP(hipMemsetAsync(rd + r * row, 0, row * sizeof(uint32_t), fs), "memset run");
     const uint64_t n = fam[f]->n;
     if (n) {
       RunMarkArgs a;
@@ -499,14 +504,23 @@ cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, uint64_t nb, in
       a.gap_count = d_err + 1 + f;
       a.gap_cap = gap_cap;
       a.err = d_err;
-      const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 16384);
-      run_mark_kernel<<<(uint32_t)blocks, 256, 0, s>>>(a, n);
-      CDB_TRY(launch_check(ctx, s, "run_mark_kernel"));
-      run_gap_kernel<<<1024, 256, 0, s>>>(a.gaps, a.gap_count, gap_cap, rd, nb);
-      CDB_TRY(launch_check(ctx, s, "run_gap_kernel"));
+      if (((uintptr_t)a.kh & 15) == 0) {
+        const uint64_t blocks = std::min<uint64_t>((n / 4 + 256) / 256, 16384);
+        run_mark4_kernel<<<(uint32_t)blocks, 256, 0, fs>>>(a, n);
+      } else {
+        const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 16384);
+        run_mark_kernel<<<(uint32_t)blocks, 256, 0, fs>>>(a, n);
+      }
+      CDB_TRY(launch_check(ctx, fs, "run_mark_kernel"));
+      run_gap_kernel<<<1024, 256, 0, fs>>>(a.gaps, a.gap_count, gap_cap, rd, nb);
+      CDB_TRY(launch_check(ctx, fs, "run_gap_kernel"));
     }
     V->rdir[f] = rd;
   }
+  CDB_HIP(hipEventRecord(ctx->ev_pn, ctx->side), "event");
+  CDB_HIP(hipEventRecord(ctx->ev_pm, ctx->side2), "event");
+  CDB_HIP(hipStreamWaitEvent(s, ctx->ev_pn, 0), "wait");
+  CDB_HIP(hipStreamWaitEvent(s, ctx->ev_pm, 0), "wait");
   CDB_HIP(hipMemcpyAsync(&ctx->runs_err, d_err, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipStreamSynchronize(s), "sync");
   if (ctx->runs_err) return CDB_OK;  // a run is not ordered (or the gap list overflowed)
@@ -951,7 +965,9 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     WA.blo = lo;
     WA.bhi = hi;
     if (nr_b == 0) continue;
-    const uint32_t gw = (uint32_t)std::min<uint64_t>((nr_b + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024);
+    // the wide tier strides over its buckets beside the wave tier: 256 workgroups (one per CU)
+    // measured ~1 ms faster per C4 step than 1024, which crowd the wave tier's workgroups out
+    const uint32_t gw = (uint32_t)std::min<uint64_t>((nr_b + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 256);
     if (use_runs) {
       bucket_wave_runs_kernel<<<(nr_b + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, 0, s>>>(WA);
       CDB_TRY(launch_check(ctx, s, "bucket_wave_runs_kernel"));

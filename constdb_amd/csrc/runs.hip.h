@@ -87,6 +87,56 @@ __global__ void __launch_bounds__(256) run_mark_kernel(RunMarkArgs a, uint64_t n
   }
 }
 
+// The same, four consecutive rows per thread read as two 16-B loads (the hash column must be
+// 16-B aligned): fewer load instructions and one run lookup per four rows.
+__global__ void __launch_bounds__(256) run_mark4_kernel(RunMarkArgs a, uint64_t n) {
+  __shared__ uint64_t rs[kMaxRuns + 1];
+  for (uint32_t i = threadIdx.x; i <= a.nr; i += blockDim.x) rs[i] = a.rs[i];
+  __syncthreads();
+  const uint64_t groups = (n + 3) / 4;
+  for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < groups; g += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i0 = 4 * g;
+    uint64_t h[4];
+    if (i0 + 3 < n) {
+      const ulonglong2 q0 = reinterpret_cast<const ulonglong2*>(a.kh)[2 * g];
+      const ulonglong2 q1 = reinterpret_cast<const ulonglong2*>(a.kh)[2 * g + 1];
+      h[0] = q0.x;
+      h[1] = q0.y;
+      h[2] = q1.x;
+      h[3] = q1.y;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) h[k] = i0 + k < n ? a.kh[i0 + k] : 0;
+    }
+    uint64_t prev = i0 ? a.kh[i0 - 1] : 0;
+    uint32_t lo = 0, hi = a.nr;  // run of row i0: rs[r] <= i0 < rs[r + 1]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (rs[mid] <= i0) lo = mid;
+      else hi = mid;
+    }
+    uint32_t r = lo;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t i = i0 + k;
+      if (i >= n) break;
+      while (i >= rs[r + 1]) ++r;  // (empty runs in between are skipped too)
+      const uint64_t rel = i - rs[r], len = rs[r + 1] - rs[r];
+      const uint64_t hk = h[k] << a.shift;
+      const uint64_t b = __umul64hi(hk, a.nb);
+      uint64_t c0 = 0;
+      if (rel) {
+        const uint64_t hp = prev << a.shift;
+        if (hp > hk) atomicOr(a.err, 1u);
+        c0 = __umul64hi(hp, a.nb) + 1;
+      }
+      run_fill(a, r, c0, b, (uint32_t)rel);
+      if (rel + 1 == len) run_fill(a, r, b + 1, a.nb, (uint32_t)len);
+      prev = h[k];
+    }
+  }
+}
+
 // The long gaps, one workgroup per entry.
 __global__ void __launch_bounds__(256) run_gap_kernel(const uint32_t* __restrict__ gaps, const uint32_t* gap_count,
                                                       uint32_t gap_cap, uint32_t* __restrict__ rdir, uint64_t nb) {
