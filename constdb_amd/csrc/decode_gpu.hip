@@ -340,18 +340,21 @@ __global__ void __launch_bounds__(kDecThreads) dest_kernel(const uint64_t* __res
 }
 
 // ---- the entry index of a large DATAS section on the device
-// The format has no sync marks: an entry starts where its predecessor ends. Each thread takes a
+// The format has no sync marks: an entry starts where its predecessor ends. One wave takes a
 // chunk of kIdxChunk bytes of the section and speculates, as the host threads of
 // decode.cpp::parallel_datas do: the first offset of its chunk from which kIdxSync consecutive
-// entries of at most 64 KB parse is taken as an entry start (a wrong offset almost never survives
-// that many), then the thread walks entries until one starts past its chunk. The host stitches the
-// chains in order from the section start (a chunk whose sync point is not where the true chain
-// enters it is walked again on the host, a few KB), and a second pass writes every offset of the
-// true chain. The checks are the loader's (read_integer bounds, negative lengths, the tag byte),
-// plus bounds no valid entry can exceed, so a chain the device accepts the host accepts too; any
-// failure on the true chain hands the section back to the host index pass.
+// entries of at most 64 KB parse is taken as an entry start (a wrong offset rarely survives that
+// many; the lanes try 64 offsets at a time, at most kIdxSyncTries of them, so a chunk inside one
+// large entry gives up quickly), then lane 0 walks entries until one starts past the chunk. The
+// host stitches the chains in order from the section start; a chunk whose sync point is not where
+// the true chain enters it (or that has none) is walked again on the device from there, in rounds,
+// and a last pass writes every offset of the true chain. The checks are the loader's
+// (read_integer bounds, negative lengths, the tag byte), plus bounds no valid entry can exceed, so
+// a chain the device accepts the host accepts too; any failure on the true chain hands the
+// section back to the host index pass.
 constexpr uint64_t kIdxChunk = 8192;
 constexpr uint32_t kIdxSync = 16;
+constexpr uint32_t kIdxSyncTries = 256;  // offsets tried per chunk (4 rounds of 64 lanes)
 constexpr uint64_t kIdxEntryMax = 1u << 16;
 
 struct DCur {
@@ -427,38 +430,47 @@ struct IdxArgs {
   uint64_t* out;           // record pass: entry offsets
 };
 
-// req == null: the speculative pass (sync search, then the walk); req[t] != ~0: walk chunk t again
-// from req[t] (the offset at which the true chain enters it), other chunks keep their results.
+// One wave per chunk. req == null: the speculative pass (sync search by the 64 lanes, then the
+// walk by lane 0); req[t] != ~0: lane 0 walks chunk t again from req[t] (the offset at which the
+// true chain enters it), other chunks keep their results.
 __global__ void __launch_bounds__(256) idx_walk_kernel(IdxArgs a, const uint64_t* __restrict__ req) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (t >= a.T) return;
   const uint64_t lo = a.S + (uint64_t)t * kIdxChunk, hi = min(a.n, lo + kIdxChunk);
-  DCur c{a.raw, a.n, lo};
   uint64_t o = lo;
   if (req) {
     if (req[t] == ~0ull) return;
     o = req[t];
   } else if (t > 0) {
-    bool found = false;
-    for (; o < hi && !found; ++o) {  // (the search stays inside the chunk)
-      DCur s{a.raw, a.n, o};
-      uint32_t k = 0;
-      for (; k < kIdxSync && s.off < a.n; ++k) {
-        const uint64_t at = s.off;
-        if (!dc_data_entry(s, kIdxEntryMax) || s.off - at > kIdxEntryMax) break;
+    uint64_t found = ~0ull;
+    for (uint32_t k = 0; k < kIdxSyncTries && found == ~0ull; k += 64) {  // (wave-uniform)
+      const uint64_t at0 = lo + k + lane;
+      bool ok = false;
+      if (at0 < hi) {
+        DCur s{a.raw, a.n, at0};
+        uint32_t q = 0;
+        for (; q < kIdxSync && s.off < a.n; ++q) {
+          const uint64_t at = s.off;
+          if (!dc_data_entry(s, kIdxEntryMax) || s.off - at > kIdxEntryMax) break;
+        }
+        ok = q == kIdxSync;
       }
-      found = k == kIdxSync;
+      const uint64_t m = __ballot(ok);
+      if (m) found = lo + k + __builtin_ctzll(m);
     }
-    if (!found) {
-      a.sync[t] = ~0ull;
-      a.count[t] = 0;
-      a.stop[t] = lo;
-      a.ok[t] = 0;
+    if (found == ~0ull) {
+      if (lane == 0) {
+        a.sync[t] = ~0ull;
+        a.count[t] = 0;
+        a.stop[t] = lo;
+        a.ok[t] = 0;
+      }
       return;
     }
-    --o;
+    o = found;
   }
-  c.off = o;
+  if (lane != 0) return;
+  DCur c{a.raw, a.n, o};
   uint32_t k = 0;
   bool good = true;
   while (c.off < hi) {
@@ -630,7 +642,7 @@ int GpuDecode::device_datas(uint64_t* datas_end) {
   a.tstart = d_tstart;
   a.tbase = d_tbase;
   a.tcount = d_tcount;
-  idx_walk_kernel<<<(T + 255) / 256, 256, 0, s>>>(a, nullptr);
+  idx_walk_kernel<<<(T + 3) / 4, 256, 0, s>>>(a, nullptr);
   ck(hipGetLastError(), "idx_walk_kernel");
   std::vector<uint64_t> sync(T), stop(T), tstart(T, ~0ull), tbase(T, 0), req(T);
   std::vector<uint32_t> count(T), tcount(T, 0);
@@ -645,21 +657,30 @@ int GpuDecode::device_datas(uint64_t* datas_end) {
   download();
   if (st_ != CDB_OK) return -1;
   // stitch: the true chain from the section start, chunk by chunk. A chunk whose sync point is not
-  // where the true chain enters it (a spurious sync inside an entry's bytes) is walked again on the
-  // device from there; its chain usually joins the speculative one, so later chunks keep theirs,
-  // and rounds repeat until every chunk on the chain starts where the chain enters it.
+  // where the chain enters it (a spurious sync inside an entry's bytes, or none found) is walked
+  // again on the device from there; past the first such chunk the chain is speculative (each
+  // chunk's own chain, which usually joins the true one, so later chunks keep theirs), and rounds
+  // repeat until every chunk on the chain starts where the chain enters it.
   bool consistent = false;
   for (int round = 0; round < 16 && !consistent; ++round) {  // (3-4 rounds on the generator's streams)
     consistent = true;
     std::fill(req.begin(), req.end(), ~0ull);
     uint64_t cur = S, got = 0;
+    bool lost = false;  // the speculative chain has no entry point here: adopt the chunk's own
     for (uint32_t t = 0; t < T && got < cnt; ++t) {
       const uint64_t hi = std::min<uint64_t>(len, S + (uint64_t)(t + 1) * kIdxChunk);
-      if (cur >= hi) continue;  // an entry spans the whole chunk
+      if (!lost && cur >= hi) continue;  // an entry spans the whole chunk
       const uint64_t need = cnt - got;
-      if (sync[t] != cur) {
+      if (lost) {
+        if (sync[t] == ~0ull) continue;
+        lost = false;
+      } else if (sync[t] != cur) {
         req[t] = cur;
         consistent = false;
+        if (sync[t] == ~0ull) {
+          lost = true;
+          continue;
+        }
       } else if (!ok[t] && count[t] < need) {
         // the chain fails inside the section: on the true chain (every chunk so far consistent)
         // the host pass reports it; after a re-walk request it is a speculative chain, so the
@@ -674,7 +695,7 @@ int GpuDecode::device_datas(uint64_t* datas_end) {
     DevBuf d_req;
     if ((st_ = alloc(&d_req.p, T * 8ull, "decode: device entry index scratch")) != CDB_OK) return -1;
     ck(hipMemcpyAsync(d_req.p, req.data(), T * 8ull, hipMemcpyHostToDevice, s), "h2d(index)");
-    idx_walk_kernel<<<(T + 255) / 256, 256, 0, s>>>(a, (const uint64_t*)d_req.p);
+    idx_walk_kernel<<<(T + 3) / 4, 256, 0, s>>>(a, (const uint64_t*)d_req.p);
     ck(hipGetLastError(), "idx_walk_kernel");
     download();
     if (st_ != CDB_OK) return -1;
