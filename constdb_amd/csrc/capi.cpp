@@ -46,7 +46,7 @@ int copy_threads() {
   static const int t = [] {
     const char* e = std::getenv("CDB_COPY_THREADS");
     const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
-    const int v = e ? std::atoi(e) : std::min(8, hw);
+    const int v = e ? std::atoi(e) : std::min(16, hw);
     return std::max(1, std::min(64, v));
   }();
   return t;

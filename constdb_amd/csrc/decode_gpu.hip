@@ -543,6 +543,17 @@ class GpuDecode {
   }
   // the host index pass alone (no HIP call: several snapshots are indexed on parallel threads)
   int index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTiming* tm);
+  // the device index of a deferred DATAS section in steps, so that the sections of several
+  // snapshots are indexed side by side (decode_snapshots_gpu_device):
+  //   dd_launch: the bytes up (context stream), the speculative walk and its results down on ks
+  //              (-1: a HIP error, in st_);
+  //   dd_step  : after ks: the stitch; another round of re-walks queued on ks (1), or finished (0:
+  //              the record pass and the host pass resumed after the section; status in status())
+  bool deferred() const { return cursor_ != nullptr; }
+  int dd_launch(hipStream_t ks);
+  int dd_step(size_t* err_off);
+  int dd_host(size_t* err_off);
+  int status() const { return st_ != CDB_OK ? (int)st_ : rc_; }
   // everything after it (returns the index pass's status when the device part succeeds)
   int prepare_device(size_t* err_off);
   cdb_status emit_host(DecodeTiming* tm);
@@ -578,9 +589,25 @@ class GpuDecode {
   // tier's member references
   cdb_status refs_to_batch(const DecArgs& A);
   // a deferred DATAS section: its entries indexed on the device, then the host pass resumed after
-  // it (1: the device gave up, the host pass was run instead)
+  // it (or, where the device gives up, the host pass over the whole stream)
   int finish_index(size_t* err_off);
-  int device_datas(uint64_t* datas_end);
+  void dd_download();
+  int dd_done(int dv, uint64_t end, size_t* err_off);
+  struct DevIndex {
+    hipStream_t ks = nullptr;
+    bool active = false;
+    uint32_t T = 0;
+    int round = 0;
+    IdxArgs a;
+    uint64_t* d_req = nullptr;
+    uint64_t last = 0;  // the section's last entry
+    DevBuf work, offs;
+    EvPair up;  // (a: the snapshot's bytes are on the device)
+    std::vector<uint64_t> sync, stop, req;
+    std::vector<uint32_t> count;
+    std::vector<uint8_t> ok;
+    std::chrono::steady_clock::time_point t0;
+  } di_;
 
   cdb_ctx* ctx_;
   Batch* out_;
@@ -602,6 +629,7 @@ class GpuDecode {
       if (*p) index_cursor_free(*p);
     }
   } cursor_free_{&cursor_};
+  uint64_t dev_datas_ = 0;  // leading entries (the DATAS section) whose offsets are only in di_.offs
   bool ordered_ = false;  // the sections are contiguous, in DATAS, EXPIRES, DELETES order
   Sections sec_{};
   DecArgs A_;
@@ -617,54 +645,77 @@ int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTimi
   return rc_;
 }
 
-int GpuDecode::device_datas(uint64_t* datas_end) {
-  const uint64_t len = out_->raw.size(), S = defer_.start, cnt = defer_.count;
+int GpuDecode::dd_launch(hipStream_t ks) {
+  DevIndex& d = di_;
+  d.t0 = std::chrono::steady_clock::now();
+  d.ks = ks;
+  const uint64_t len = out_->raw.size(), S = defer_.start;
   hipStream_t s = ctx_->stream;
   if ((st_ = alloc(&d_idx_raw_.p, len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK) return -1;
   if ((st_ = staged_h2d(ctx_, d_idx_raw_.p, out_->raw.data(), len, s)) != CDB_OK) return -1;
-  const uint32_t T = (uint32_t)((len - S + kIdxChunk - 1) / kIdxChunk);
-  DevBuf work;
-  const size_t wbytes = (size_t)T * (8 + 4 + 8 + 1 + 8 + 8 + 4) + 64;
-  if ((st_ = alloc(&work.p, wbytes, "decode: device entry index scratch")) != CDB_OK) return -1;
-  IdxArgs a;
+  ck(hipEventRecord(d.up.a, s), "event(index)");
+  ck(hipStreamWaitEvent(ks, d.up.a, 0), "wait(index)");
+  const uint32_t T = d.T = (uint32_t)((len - S + kIdxChunk - 1) / kIdxChunk);
+  const size_t wbytes = (size_t)T * (8 + 4 + 8 + 1 + 8 + 8 + 4 + 8) + 64;
+  if ((st_ = alloc(&d.work.p, wbytes, "decode: device entry index scratch")) != CDB_OK) return -1;
+  IdxArgs& a = d.a;
+  std::memset(&a, 0, sizeof a);
   a.raw = (const uint8_t*)d_idx_raw_.p;
   a.n = len;
   a.S = S;
   a.T = T;
-  uint8_t* w = (uint8_t*)work.p;
+  uint8_t* w = (uint8_t*)d.work.p;
   a.sync = (uint64_t*)w;
   a.stop = a.sync + T;
   uint64_t* d_tstart = a.stop + T;
   uint64_t* d_tbase = d_tstart + T;
-  a.count = (uint32_t*)(d_tbase + T);
+  d.d_req = d_tbase + T;
+  a.count = (uint32_t*)(d.d_req + T);
   uint32_t* d_tcount = a.count + T;
   a.ok = (uint8_t*)(d_tcount + T);
   a.tstart = d_tstart;
   a.tbase = d_tbase;
   a.tcount = d_tcount;
-  idx_walk_kernel<<<(T + 3) / 4, 256, 0, s>>>(a, nullptr);
+  d.sync.assign(T, 0);
+  d.stop.assign(T, 0);
+  d.req.assign(T, ~0ull);
+  d.count.assign(T, 0);
+  d.ok.assign(T, 0);
+  d.round = 0;
+  idx_walk_kernel<<<(T + 3) / 4, 256, 0, ks>>>(a, nullptr);
   ck(hipGetLastError(), "idx_walk_kernel");
-  std::vector<uint64_t> sync(T), stop(T), tstart(T, ~0ull), tbase(T, 0), req(T);
-  std::vector<uint32_t> count(T), tcount(T, 0);
-  std::vector<uint8_t> ok(T);
-  auto download = [&]() {
-    ck(hipMemcpyAsync(sync.data(), a.sync, T * 8ull, hipMemcpyDeviceToHost, s), "d2h(index)");
-    ck(hipMemcpyAsync(stop.data(), a.stop, T * 8ull, hipMemcpyDeviceToHost, s), "d2h(index)");
-    ck(hipMemcpyAsync(count.data(), a.count, T * 4ull, hipMemcpyDeviceToHost, s), "d2h(index)");
-    ck(hipMemcpyAsync(ok.data(), a.ok, T, hipMemcpyDeviceToHost, s), "d2h(index)");
-    ck(hipStreamSynchronize(s), "sync(index)");
-  };
-  download();
-  if (st_ != CDB_OK) return -1;
+  dd_download();
+  d.active = true;
+  return st_ == CDB_OK ? 0 : -1;
+}
+
+void GpuDecode::dd_download() {  // the walk's results to the host, queued on ks
+  DevIndex& d = di_;
+  const uint32_t T = d.T;
+  ck(hipMemcpyAsync(d.sync.data(), d.a.sync, T * 8ull, hipMemcpyDeviceToHost, d.ks), "d2h(index)");
+  ck(hipMemcpyAsync(d.stop.data(), d.a.stop, T * 8ull, hipMemcpyDeviceToHost, d.ks), "d2h(index)");
+  ck(hipMemcpyAsync(d.count.data(), d.a.count, T * 4ull, hipMemcpyDeviceToHost, d.ks), "d2h(index)");
+  ck(hipMemcpyAsync(d.ok.data(), d.a.ok, T, hipMemcpyDeviceToHost, d.ks), "d2h(index)");
+}
+
+// 1: another round of device walks is queued on ks; 2: the section's offsets are in idx_, the host
+// part (dd_host: the host pass resumed after the section) remains; 0: finished (status() holds
+// the outcome: the index pass's status, as finish_index returns it).
+int GpuDecode::dd_step(size_t* err_off) {
+  DevIndex& d = di_;
+  if (!d.active) return 0;
+  ck(hipStreamSynchronize(d.ks), "sync(index)");
+  if (st_ != CDB_OK) return dd_done(-1, 0, err_off);
+  const uint64_t len = out_->raw.size(), S = defer_.start, cnt = defer_.count;
+  const uint32_t T = d.T;
   // stitch: the true chain from the section start, chunk by chunk. A chunk whose sync point is not
   // where the chain enters it (a spurious sync inside an entry's bytes, or none found) is walked
   // again on the device from there; past the first such chunk the chain is speculative (each
   // chunk's own chain, which usually joins the true one, so later chunks keep theirs), and rounds
   // repeat until every chunk on the chain starts where the chain enters it.
-  bool consistent = false;
-  for (int round = 0; round < 16 && !consistent; ++round) {  // (3-4 rounds on the generator's streams)
-    consistent = true;
-    std::fill(req.begin(), req.end(), ~0ull);
+  bool consistent = true;
+  std::fill(d.req.begin(), d.req.end(), ~0ull);
+  {
     uint64_t cur = S, got = 0;
     bool lost = false;  // the speculative chain has no entry point here: adopt the chunk's own
     for (uint32_t t = 0; t < T && got < cnt; ++t) {
@@ -672,88 +723,88 @@ int GpuDecode::device_datas(uint64_t* datas_end) {
       if (!lost && cur >= hi) continue;  // an entry spans the whole chunk
       const uint64_t need = cnt - got;
       if (lost) {
-        if (sync[t] == ~0ull) continue;
+        if (d.sync[t] == ~0ull) continue;
         lost = false;
-      } else if (sync[t] != cur) {
-        req[t] = cur;
+      } else if (d.sync[t] != cur) {
+        d.req[t] = cur;
         consistent = false;
-        if (sync[t] == ~0ull) {
+        if (d.sync[t] == ~0ull) {
           lost = true;
           continue;
         }
-      } else if (!ok[t] && count[t] < need) {
+      } else if (!d.ok[t] && d.count[t] < need) {
         // the chain fails inside the section: on the true chain (every chunk so far consistent)
         // the host pass reports it; after a re-walk request it is a speculative chain, so the
         // round ends here and the next one resumes from the re-walked chunks
-        if (consistent) return 1;
+        if (consistent) return dd_done(1, 0, err_off);
         break;
       }
-      got += std::min<uint64_t>(count[t], need);
-      cur = stop[t];
+      got += std::min<uint64_t>(d.count[t], need);
+      cur = d.stop[t];
     }
-    if (consistent) break;
-    DevBuf d_req;
-    if ((st_ = alloc(&d_req.p, T * 8ull, "decode: device entry index scratch")) != CDB_OK) return -1;
-    ck(hipMemcpyAsync(d_req.p, req.data(), T * 8ull, hipMemcpyHostToDevice, s), "h2d(index)");
-    idx_walk_kernel<<<(T + 3) / 4, 256, 0, s>>>(a, (const uint64_t*)d_req.p);
-    ck(hipGetLastError(), "idx_walk_kernel");
-    download();
-    if (st_ != CDB_OK) return -1;
   }
-  if (!consistent) return 1;
+  if (!consistent) {
+    if (++d.round >= 16) return dd_done(1, 0, err_off);  // (3-4 rounds on the generator's streams)
+    ck(hipMemcpyAsync(d.d_req, d.req.data(), T * 8ull, hipMemcpyHostToDevice, d.ks), "h2d(index)");
+    idx_walk_kernel<<<(T + 3) / 4, 256, 0, d.ks>>>(d.a, d.d_req);
+    ck(hipGetLastError(), "idx_walk_kernel");
+    dd_download();
+    return st_ == CDB_OK ? 1 : dd_done(-1, 0, err_off);
+  }
+  std::vector<uint64_t> tstart(T, ~0ull), tbase(T, 0);
+  std::vector<uint32_t> tcount(T, 0);
   uint64_t got = 0;
   {
     uint64_t cur = S;
     for (uint32_t t = 0; t < T && got < cnt; ++t) {
       const uint64_t hi = std::min<uint64_t>(len, S + (uint64_t)(t + 1) * kIdxChunk);
       if (cur >= hi) continue;
-      const uint32_t m = (uint32_t)std::min<uint64_t>(count[t], cnt - got);
+      const uint32_t m = (uint32_t)std::min<uint64_t>(d.count[t], cnt - got);
       tstart[t] = cur;
       tbase[t] = got;
       tcount[t] = m;
       got += m;
-      cur = stop[t];
+      cur = d.stop[t];
     }
   }
-  if (got < cnt) return 1;  // the stream ends inside the section
+  if (got < cnt) return dd_done(1, 0, err_off);  // the stream ends inside the section
   // every offset of the true chain, written on the device, then into the host index
-  ck(hipMemcpyAsync(d_tstart, tstart.data(), T * 8ull, hipMemcpyHostToDevice, s), "h2d(index)");
-  ck(hipMemcpyAsync(d_tbase, tbase.data(), T * 8ull, hipMemcpyHostToDevice, s), "h2d(index)");
-  ck(hipMemcpyAsync(d_tcount, tcount.data(), T * 4ull, hipMemcpyHostToDevice, s), "h2d(index)");
-  DevBuf offs;
-  if ((st_ = alloc(&offs.p, cnt * 8, "decode: device entry offsets")) != CDB_OK) return -1;
-  a.out = (uint64_t*)offs.p;
-  idx_record_kernel<<<(T + 255) / 256, 256, 0, s>>>(a);
+  ck(hipMemcpyAsync((void*)d.a.tstart, tstart.data(), T * 8ull, hipMemcpyHostToDevice, d.ks), "h2d(index)");
+  ck(hipMemcpyAsync((void*)d.a.tbase, tbase.data(), T * 8ull, hipMemcpyHostToDevice, d.ks), "h2d(index)");
+  ck(hipMemcpyAsync((void*)d.a.tcount, tcount.data(), T * 4ull, hipMemcpyHostToDevice, d.ks), "h2d(index)");
+  // the offsets stay on the device (prepare_device copies them into place); the host needs only
+  // the last one (where the section ends) unless an entry falls to the host tier
+  if ((st_ = alloc(&d.offs.p, cnt * 8, "decode: device entry offsets")) != CDB_OK) return dd_done(-1, 0, err_off);
+  d.a.out = (uint64_t*)d.offs.p;
+  idx_record_kernel<<<(T + 255) / 256, 256, 0, d.ks>>>(d.a);
   ck(hipGetLastError(), "idx_record_kernel");
-  idx_.offset.resize(cnt);
-  if (st_ == CDB_OK) st_ = staged_d2h(ctx_, idx_.offset.data(), offs.p, cnt * 8, s);
-  ck(hipStreamSynchronize(s), "sync(index)");
-  if (st_ != CDB_OK) return -1;
-  if (!index_data_entry_end(*out_, idx_.offset.back(), datas_end)) return 1;
-  return 0;
+  ck(hipMemcpyAsync(&d.last, d.a.out + (cnt - 1), 8, hipMemcpyDeviceToHost, d.ks), "d2h(index)");
+  ck(hipStreamSynchronize(d.ks), "sync(index)");  // (the host vectors above are copy sources)
+  if (st_ != CDB_OK) return dd_done(-1, 0, err_off);
+  return 2;  // the host part (dd_host) is left to the caller: several snapshots run it side by side
 }
 
-int GpuDecode::finish_index(size_t* err_off) {
-  if (!cursor_) return rc_;
-  if (hipSetDevice(ctx_->device) != hipSuccess) return fail(ctx_, CDB_DEVICE_ERROR, "hipSetDevice");
+int GpuDecode::dd_host(size_t* err_off) {
   uint64_t end = 0;
-  const auto t0 = std::chrono::steady_clock::now();
-  const int dv = device_datas(&end);
-  if (dv < 0) return st_;
-  if (dv == 0) {
-    std::vector<uint64_t> datas(std::move(idx_.offset));
+  if (!index_data_entry_end(*out_, di_.last, &end)) return dd_done(1, 0, err_off);
+  return dd_done(0, end, err_off);
+}
+
+// dv 0: the section's offsets are in idx_, the host pass resumes at `end`; 1: the device gave up,
+// the host index pass runs over the whole stream; -1: a HIP error (st_).
+int GpuDecode::dd_done(int dv, uint64_t end, size_t* err_off) {
+  DevIndex& d = di_;
+  d.active = false;
+  if (d.work.p) (void)hipFree(d.work.p);
+  d.work.p = nullptr;
+  if (dv == 0) {  // the section's offsets on the device, the side sections' on the host after them
     idx_.offset.clear();
     idx_.kind.clear();
     rc_ = index_resume(cursor_, end, err_off);  // EXPIRES, DELETES, the checksum
-    std::vector<uint64_t> all;
-    all.reserve(datas.size() + idx_.offset.size());
-    all.insert(all.end(), datas.begin(), datas.end());
-    all.insert(all.end(), idx_.offset.begin(), idx_.offset.end());
-    std::vector<uint8_t> kinds(datas.size(), 0);
-    kinds.insert(kinds.end(), idx_.kind.begin(), idx_.kind.end());
-    idx_.offset.swap(all);
-    idx_.kind.swap(kinds);
-  } else {  // the host index pass over the whole stream: its statuses and offsets
+    dev_datas_ = defer_.count;
+  } else if (dv > 0) {
+    if (d.offs.p) (void)hipFree(d.offs.p);
+    d.offs.p = nullptr;  // the host index pass over the whole stream: its statuses and offsets
     if (d_idx_raw_.p) (void)hipFree(d_idx_raw_.p);
     d_idx_raw_.p = nullptr;
     idx_ = EntryIndex{};
@@ -763,8 +814,22 @@ int GpuDecode::finish_index(size_t* err_off) {
   }
   index_cursor_free(cursor_);
   cursor_ = nullptr;
-  device_index_ms_ = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  return rc_;
+  device_index_ms_ = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d.t0).count();
+  return 0;
+}
+
+int GpuDecode::finish_index(size_t* err_off) {
+  if (!cursor_) return rc_;
+  if (hipSetDevice(ctx_->device) != hipSuccess) return fail(ctx_, CDB_DEVICE_ERROR, "hipSetDevice");
+  if (!di_.active && dd_launch(ctx_->stream) < 0) {
+    dd_done(-1, 0, err_off);
+    return st_;
+  }
+  int r;
+  while ((r = dd_step(err_off)) == 1) {
+  }
+  if (r == 2) dd_host(err_off);
+  return st_ != CDB_OK ? st_ : rc_;
 }
 
 int GpuDecode::prepare_device(size_t* err_off) {
@@ -773,7 +838,7 @@ int GpuDecode::prepare_device(size_t* err_off) {
     if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) return rc;
   }
   const uint64_t len = out_->raw.size();
-  const uint64_t n = n_ = idx_.offset.size();
+  const uint64_t dd = dev_datas_, n = n_ = dd + idx_.offset.size();
   if (n == 0) return rc_;
   if (hipSetDevice(ctx_->device) != hipSuccess) return CDB_DEVICE_ERROR;
   hipStream_t s = s_ = ctx_->stream;
@@ -807,8 +872,12 @@ int GpuDecode::prepare_device(size_t* err_off) {
     d_idx_raw_.p = nullptr;
   } else if (st_ == CDB_OK)
     st_ = staged_h2d(ctx_, (void*)raw_dev, out_->raw.data(), len, s);
-  if (st_ == CDB_OK) st_ = staged_h2d(ctx_, d_off, idx_.offset.data(), n * 8, s);
-  ck(hipMemcpyAsync(d_kind, idx_.kind.data(), n, hipMemcpyHostToDevice, s), "h2d(decode)");
+  if (dd) {  // the DATAS section's offsets from the device index, then the side sections'
+    ck(hipMemcpyAsync(d_off, di_.offs.p, dd * 8, hipMemcpyDeviceToDevice, s), "d2d(decode)");
+    ck(hipMemsetAsync(d_kind, 0, dd, s), "memset(decode)");
+  }
+  if (st_ == CDB_OK) st_ = staged_h2d(ctx_, d_off + dd, idx_.offset.data(), (n - dd) * 8, s);
+  ck(hipMemcpyAsync(d_kind + dd, idx_.kind.data(), n - dd, hipMemcpyHostToDevice, s), "h2d(decode)");
   if (st_ != CDB_OK) return st_;
   std::memset(&A_, 0, sizeof A_);
   A_.raw = raw_dev;
@@ -846,10 +915,23 @@ int GpuDecode::prepare_device(size_t* err_off) {
     rc_ = CDB_INVALID_SNAPSHOT_CHECKSUM;
     *err_off = dcrc_.err_off;
   }
+  if (di_.offs.p) (void)hipFree(di_.offs.p);
+  di_.offs.p = nullptr;
   if (!small[3]) {  // every entry's children were counted on the device
     nn_ = small[1];
     nm_ = small[2];
     return rc_;
+  }
+  if (dd) {  // the host tier re-parses entries by offset: every offset on the host
+    std::vector<uint64_t> all(n);
+    ck(hipMemcpyAsync(all.data(), d_off, n * 8, hipMemcpyDeviceToHost, s), "d2h(decode)");
+    ck(hipStreamSynchronize(s), "sync(decode)");
+    if (st_ != CDB_OK) return st_;
+    std::vector<uint8_t> kinds(dd, 0);
+    kinds.insert(kinds.end(), idx_.kind.begin(), idx_.kind.end());
+    idx_.offset.swap(all);
+    idx_.kind.swap(kinds);
+    dev_datas_ = 0;
   }
   // entries past the per-thread dedup limits: decoded here, into slots reserved by a host scan
   noff_.resize(n);
@@ -903,6 +985,10 @@ cdb_status GpuDecode::refs_to_batch(const DecArgs& A) {
   b.val_ref.resize(n_);
   b.m_ref.resize(nm_);
   b.m_vref.resize(nm_);
+  advise_huge(b.key_ref.data(), n_ * sizeof(ByteRef));  // (fresh pages, first touched by the download)
+  advise_huge(b.val_ref.data(), n_ * sizeof(ByteRef));
+  advise_huge(b.m_ref.data(), nm_ * sizeof(ByteRef));
+  advise_huge(b.m_vref.data(), nm_ * sizeof(ByteRef));
   std::vector<HostSeg> segs;
   auto down = [&](void* host, const ulonglong2* dev, uint64_t rows) {
     if (rows) segs.push_back({host, const_cast<ulonglong2*>(dev), rows * 16});
@@ -1005,10 +1091,11 @@ cdb_status GpuDecode::order_check() {
     return CDB_OK;
   }
   if (n >= (1ull << 32)) return CDB_OK;
-  uint64_t cnt[3] = {0, 0, 0};
+  const uint64_t dd = dev_datas_;  // (leading DATAS entries whose kinds are not on the host)
+  uint64_t cnt[3] = {dd, 0, 0};
   uint8_t prev = 0;
-  for (uint64_t i = 0; i < n; ++i) {
-    const uint8_t k = idx_.kind[i];
+  for (uint64_t i = dd; i < n; ++i) {
+    const uint8_t k = idx_.kind[i - dd];
     if (k < prev || k > 2) return CDB_OK;  // sections out of the writer's order: no run
     prev = k;
     ++cnt[k];
@@ -1156,6 +1243,53 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     for (auto& t : th) t.join();
   }
   if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+  {
+    // the deferred DATAS sections, side by side: every snapshot's bytes go up (one after another
+    // through the staging ring) with its speculative walk queued behind them on its own stream,
+    // then the stitch rounds of all of them interleave, so one snapshot's walks run while the next
+    // one's bytes cross PCIe
+    std::vector<hipStream_t> ks(n, nullptr);
+    std::vector<uint32_t> live;
+    cdb_status st = CDB_OK;
+    for (uint32_t i = 0; i < n && st == CDB_OK; ++i) {
+      if ((irc[i] != CDB_OK && irc[i] != CDB_INVALID_SNAPSHOT_CHECKSUM) || !dec[i]->deferred()) continue;
+      st = hip_check(ctx, hipStreamCreateWithFlags(&ks[i], hipStreamNonBlocking), "stream(index)");
+      if (st == CDB_OK && dec[i]->dd_launch(ks[i]) < 0) {
+        (void)dec[i]->dd_step(&ieo[i]);
+        irc[i] = dec[i]->status();
+        continue;
+      }
+      live.push_back(i);
+    }
+    std::vector<uint32_t> host;  // sections whose host part (the pass resumed after them) remains
+    while (!live.empty()) {
+      std::vector<uint32_t> next;
+      for (uint32_t i : live) {
+        const int r = dec[i]->dd_step(&ieo[i]);
+        if (r == 1) next.push_back(i);
+        else if (r == 2) host.push_back(i);
+        else irc[i] = dec[i]->status();
+      }
+      live.swap(next);
+    }
+    {  // the host parts side by side (one thread each, at most 16 at once)
+      std::atomic<uint32_t> nx{0};
+      auto work = [&]() {
+        for (uint32_t j; (j = nx.fetch_add(1)) < host.size();) {
+          const uint32_t i = host[j];
+          dec[i]->dd_host(&ieo[i]);
+          irc[i] = dec[i]->status();
+        }
+      };
+      std::vector<std::thread> th;
+      for (uint32_t t = 1; t < std::min<uint32_t>((uint32_t)host.size(), 16); ++t) th.emplace_back(work);
+      work();
+      for (auto& t : th) t.join();
+    }
+    for (hipStream_t k : ks)
+      if (k) (void)hipStreamDestroy(k);
+    if (st != CDB_OK) return st;
+  }
   for (uint32_t i = 0; i < n; ++i) {
     size_t eo = ieo[i];
     int rc = irc[i];
