@@ -97,6 +97,14 @@ __global__ void state_rows_kernel(uint64_t* __restrict__ meta, uint64_t* __restr
   }
 }
 
+// Any bucket beyond the wide tier's capacity (or a forced workgroup tier)?
+__global__ void beyond_wide_kernel(BucketArgs A, uint32_t nb, uint32_t* flag) {
+  bool any = false;
+  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += gridDim.x * blockDim.x)
+    any |= A.kcnt[b] > (uint32_t)WaveLds<2>::KC || A.ncnt[b] + A.mcnt[b] > (uint32_t)WaveLds<2>::CC;
+  if (__ballot(any) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
 __global__ void iota_kernel(uint32_t* p, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     p[i] = (uint32_t)i;
@@ -794,7 +802,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   Dir dnd{dir + 5 * dn, dir + 6 * dn, dir + 7 * dn, dir + 8 * dn, dir + 9 * dn};
   Dir dm{dir + 10 * dn, dir + 11 * dn, dir + 12 * dn, dir + 13 * dn, dir + 14 * dn};
   // misc: stats[8] u64 | last_bad u64 | totals[3] u64 | hot_count u32 | big_count u32 | compaction error u32 |
-  //       pipelined compaction error u32 | (112) | zero[3] u64 at 128 | hot_list[nb] u32 at 160 | big_list[nb] u32
+  //       pipelined compaction error u32 | beyond-wide flag u32 at 112 | zero[3] u64 at 128 | hot_list[nb] u32 at 160 | big_list[nb] u32
   uint8_t* misc = (uint8_t*)ws_get(ctx, WS_MISC, 160 + 2 * nb * sizeof(uint32_t), &st);
   if (!misc) return st;
   unsigned long long* d_stats = (unsigned long long*)misc;
@@ -925,10 +933,23 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   // the compaction HBM-bound, so the two overlap. Only valid when no bucket goes to a workgroup
   // tier (those add outputs after every range): then everything is compacted again at the end.
   // (small merges: the ranges' extra launches cost more than the overlap wins; C1 0.8 -> 1.6 ms)
+  // A bucket beyond the wide tier's capacity goes to a workgroup tier, which adds outputs after
+  // every range, so the range compactions would stand down and only their scans would run (C5:
+  // 24 idle scans per step): such merges run as one range (one flag read before the bucket phase).
   constexpr uint32_t kPipeRanges = 8;
   const uint32_t pipe_opt = opts ? opts->pipe_ranges : 0;
+  bool pipe_auto = !(K + N + M < (64ull << 20) || nb < 64ull * kPipeRanges);
+  if (!pipe_opt && pipe_auto) {
+    uint32_t* d_over = (uint32_t*)(misc + 112);  // zeroed with the misc header
+    beyond_wide_kernel<<<(uint32_t)std::min<uint64_t>((nb + 255) / 256, 4096), 256, 0, s>>>(A, (uint32_t)nb, d_over);
+    CDB_TRY(launch_check(ctx, s, "beyond_wide_kernel"));
+    uint32_t over = 0;
+    CDB_HIP(hipMemcpyAsync(&over, d_over, sizeof over, hipMemcpyDeviceToHost, s), "d2h");
+    CDB_HIP(hipStreamSynchronize(s), "sync");
+    pipe_auto = over == 0;
+  }
   const uint32_t P = pipe_opt ? (uint32_t)std::min<uint64_t>(pipe_opt, std::max<uint64_t>(nb, 1))
-                     : (K + N + M < (64ull << 20) || nb < 64ull * kPipeRanges) ? 1 : kPipeRanges;
+                     : pipe_auto ? kPipeRanges : 1;
   const bool pipelined = P > 1;
   CompactArgs C;
   C.ks = ksp[0];
