@@ -801,18 +801,20 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   Dir dk{dir, dir + dn, dir + 2 * dn, dir + 3 * dn, dir + 4 * dn};
   Dir dnd{dir + 5 * dn, dir + 6 * dn, dir + 7 * dn, dir + 8 * dn, dir + 9 * dn};
   Dir dm{dir + 10 * dn, dir + 11 * dn, dir + 12 * dn, dir + 13 * dn, dir + 14 * dn};
-  // misc: stats[8] u64 | last_bad u64 | totals[3] u64 | hot_count u32 | big_count u32 | compaction error u32 |
-  //       pipelined compaction error u32 | beyond-wide flag u32 at 112 | zero[3] u64 at 128 | hot_list[nb] u32 at 160 | big_list[nb] u32
-  uint8_t* misc = (uint8_t*)ws_get(ctx, WS_MISC, 160 + 2 * nb * sizeof(uint32_t), &st);
+  // misc: (64) | last_bad u64 at 64 | totals[3] u64 | hot_count u32 | big_count u32 | compaction error u32 |
+  //       pipelined compaction error u32 | beyond-wide flag u32 at 112 | zero[3] u64 at 128 |
+  //       stats[ST_COUNT] u64 at 160 | hot_list[nb] u32 at 256 | big_list[nb] u32
+  uint8_t* misc = (uint8_t*)ws_get(ctx, WS_MISC, 256 + 2 * nb * sizeof(uint32_t), &st);
   if (!misc) return st;
-  unsigned long long* d_stats = (unsigned long long*)misc;
+  static_assert(ST_COUNT * 8 <= 96, "statistics fit the misc header");
+  unsigned long long* d_stats = (unsigned long long*)(misc + 160);
   unsigned long long* d_last_bad = (unsigned long long*)(misc + 64);
   uint64_t* d_totals = (uint64_t*)(misc + 72);
   uint32_t* d_hot_count = (uint32_t*)(misc + 96);
   uint32_t* d_big_count = (uint32_t*)(misc + 100);
-  uint32_t* d_hot_list = (uint32_t*)(misc + 160);
+  uint32_t* d_hot_list = (uint32_t*)(misc + 256);
   uint32_t* d_big_list = d_hot_list + nb;
-  CDB_HIP(hipMemsetAsync(misc, 0, 160, s), "memset misc");
+  CDB_HIP(hipMemsetAsync(misc, 0, 256, s), "memset misc");
   unsigned long long* d_shards =
       (unsigned long long*)ws_get(ctx, WS_STATS, kStatShards * kStatStride * sizeof(unsigned long long), &st);
   if (!d_shards) return st;
@@ -1146,6 +1148,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     hipEventElapsedTime(&ms, ctx->ev_bucket, ctx->ev1);
     stats->finish_ms = ms;
     stats->sorted_runs = use_runs ? 1 : 0;
+    stats->hot_slow_runs = hs[ST_HOT_SLOW];
   }
   if ((flags & CDB_MERGE_STRICT_DICT_PANIC) && hs[ST_DICT_MERGES])
     return fail(ctx, CDB_DICT_MERGE_UNIMPLEMENTED, "Dict::merge reached (lwwhash.rs:180 unimplemented!())");

@@ -204,7 +204,7 @@ constexpr uint32_t kFoldFast = 8;  // runs up to this many rows: rows in registe
 // per-lane predicates: a loop-carried row must not be a live-out of a loop with divergent exits
 // (gfx950 compilers have produced the first candidate instead of the smallest there).
 __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, int pass) {
-  unsigned long long gcm = 0;
+  unsigned long long gcm = 0, nslow = 0;
   const uint64_t nruns = *H.run_count;
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -322,6 +322,7 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
       }
     }
     // selection path
+    nslow += (pass == 0 && slow) ? 1 : 0;
     uint32_t kslow = slow ? nrows : 0;
     for (int off = 32; off > 0; off >>= 1) kslow = max(kslow, (uint32_t)__shfl_xor((int)kslow, off));
     HotChild last, head;  // last visited row; first row of the id being folded
@@ -393,6 +394,7 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
     }
   }
   if (pass == 0 && gcm) atomicAdd(&stat_shard(A.stats)[ST_MEMBERS_GCED], gcm);
+  if (nslow) atomicAdd(&stat_shard(A.stats)[ST_HOT_SLOW], nslow);
 }
 
 // Key rows: counter sums and child ranges (bucket-relative, as every tier leaves them for the

@@ -170,3 +170,8 @@ def test_c5_child_id_collisions(ctx, monkeypatch):
     snaps = [cdb.gen_snapshot(cfg, r) for r in range(8)]
     m = _check(ctx, snaps, tier=2)
     assert m.stats.hot_buckets > 0
+    slow = m.stats.hot_slow_runs
+    assert slow > 0
+    monkeypatch.delenv("CDB_HOT_ID_BITS")
+    m = _check(ctx, snaps, tier=2)  # sized id bits: about 1 run in 1000 takes the selection path
+    assert m.stats.hot_slow_runs * 20 < slow
