@@ -109,6 +109,55 @@ def test_device_decode_large_sections(ctx):
     _release(din)
 
 
+def test_device_decode_large_sections_with_huge_entries(ctx):
+    """A device-indexed DATAS section holding Zipf-hot keys whose entries run to hundreds of KB
+    (C5's generator at 300K keys): chunks that lie inside one entry find no sync point, or a
+    spurious one in its member list, and the stitch rounds re-walk them from the true chain."""
+    cfg = configs.c5(cdb, universe=300_000, events=3_000_000, replicas=2)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(2)]
+    big = cdb.decode_snapshot(snaps[0]).info()
+    assert big.n_data > (1 << 17)  # the section goes to the device index
+    _, din = _check(ctx, snaps)
+    _release(din)
+    # damage inside the device-indexed section of the second snapshot: the same status and offset
+    # as the host decoder, with the first snapshot indexed beside it
+    for frac in (3, 2):
+        bad = bytearray(snaps[1])
+        at = len(bad) // frac
+        bad[at:at + 8] = b"\xff" * 8
+        want = None
+        try:
+            cdb.decode_snapshot(bytes(bad))
+        except cdb.CstError as e:
+            want = (type(e), getattr(e, "offset", None))
+        if want is None:
+            continue
+        if want[0] is cdb.InvalidSnapshotChecksum:  # the entries still parse: rows returned, batch flagged
+            batches, din = cdb.decode_snapshots_device(ctx, [snaps[0], bytes(bad)])
+            _release(din)
+            assert [b.checksum_ok for b in batches] == [True, False]
+            continue
+        tm = {}
+        with pytest.raises(cdb.CstError) as ei:
+            cdb.decode_snapshots_device(ctx, [snaps[0], bytes(bad)], timing=tm)
+        assert (type(ei.value), getattr(ei.value, "offset", None)) == want and tm["failed"] == 1
+    # a key's length byte broken at 1/8, 1/3 and 2/3 of the stream (entries start with the key
+    # span, "key:<i>" here): the device walk fails on the true chain, the host pass reports it
+    raw = snaps[1]
+    for frac in (8, 3, 1.5):
+        at = raw.index(b"key:", int(len(raw) / frac)) - 1
+        bad = bytearray(raw)
+        bad[at] = 0xFF
+        with pytest.raises(cdb.CstError) as want:
+            cdb.decode_snapshot(bytes(bad))
+        assert type(want.value) is not cdb.InvalidSnapshotChecksum
+        tm = {}
+        with pytest.raises(cdb.CstError) as ei:
+            cdb.decode_snapshots_device(ctx, [snaps[0], bytes(bad)], timing=tm)
+        assert type(ei.value) is type(want.value) and tm["failed"] == 1
+        assert getattr(ei.value, "offset", None) == getattr(want.value, "offset", None)
+
+
 def test_device_decode_host_tier(ctx):
     """Objects past the per-thread dedup limits (3000 members, 1500 nodes) are decoded on the
     host and uploaded into their reserved rows at the snapshot's fold position."""
