@@ -582,7 +582,7 @@ cdb_status radix_sort_pairs(cdb_ctx* ctx, uint64_t** k, uint32_t** v, uint64_t* 
 // rows in the batch (the key table's index width in the sort tag and the child row indices).
 cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& wide_ids,
                      const std::vector<uint32_t>& hk_off, const std::vector<uint32_t>& c_off, uint64_t tk,
-                     uint64_t tc, uint64_t cmax, hipStream_t s) {
+                     uint64_t tc, uint64_t cmax, const RunView* rv, hipStream_t s) {
   cdb_status st = CDB_OK;
   const uint32_t H = (uint32_t)wide_ids.size();
   // device: ids[H] | hk_off[H + 1] | c_off[H + 1] | hk_kout[H] | run count
@@ -590,6 +590,10 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   if (!meta) return st;
   HotArgs HA;
   std::memset(&HA, 0, sizeof HA);
+  if (rv) {  // children read from the runs (their rows were not copied)
+    HA.runs = 1;
+    HA.V = *rv;
+  }
   uint32_t* d_ids = meta;
   uint32_t* d_hk_off = meta + H;
   uint32_t* d_c_off = d_hk_off + H + 1;
@@ -691,7 +695,11 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
 // bucket algorithm on one workgroup over a global scratch slab (bucket_hot_kernel).
 constexpr uint64_t kHotKeyCap = 1ull << 23;
 
-cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list, uint32_t hot, hipStream_t s) {
+// rv / runs_child_max: sorted-run input whose buckets of at most runs_child_max children (and at
+// most kCapK keys) had only their keys copied (MatArgs): those take the chip-wide path in runs
+// mode, in batches of their own.
+cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list, uint32_t hot, hipStream_t s,
+                         const RunView* rv = nullptr, uint32_t runs_child_max = 0) {
   cdb_status st = CDB_OK;
   uint32_t* d_cnt3 = (uint32_t*)ws_get(ctx, WS_HOTC3, 4ull * hot * sizeof(uint32_t), &st);
   if (!d_cnt3) return st;
@@ -713,33 +721,43 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   std::vector<uint32_t> hk_off(1, 0), c_off(1, 0);
   std::vector<uint32_t> lk, ln, lm;
   uint64_t tk = 0, tc = 0, cmax = 0;
+  bool runs_batch = false;  // the batch being built reads its children from the runs
   auto flush = [&]() -> cdb_status {
     if (wide_ids.empty()) return CDB_OK;
-    const cdb_status r = chip_wide(ctx, A, wide_ids, hk_off, c_off, tk, tc, cmax, s);
+    const cdb_status r = chip_wide(ctx, A, wide_ids, hk_off, c_off, tk, tc, cmax, runs_batch ? rv : nullptr, s);
     wide_ids.clear();
     hk_off.assign(1, 0);
     c_off.assign(1, 0);
     tk = tc = cmax = 0;
     return r;
   };
-  for (uint32_t i : order) {
-    const uint32_t K = cnt3[3 * i], N = cnt3[3 * i + 1], M = cnt3[3 * i + 2];
-    if (legacy_all || K > (uint32_t)kCapK) {
-      legacy.push_back(ids[i]);
-      lk.push_back(K);
-      ln.push_back(N);
-      lm.push_back(M);
-      continue;
+  // the same rule as mat_count_kernel's: runs-mode buckets first, then the copied ones
+  auto runs_mode = [&](uint32_t i) {
+    return rv && runs_child_max && !legacy_all && cnt3[3 * i] <= (uint32_t)kCapK &&
+           cnt3[3 * i + 1] + cnt3[3 * i + 2] <= runs_child_max;
+  };
+  for (int pass = 0; pass < 2; ++pass) {
+    runs_batch = pass == 0;
+    for (uint32_t i : order) {
+      if (runs_mode(i) != runs_batch) continue;
+      const uint32_t K = cnt3[3 * i], N = cnt3[3 * i + 1], M = cnt3[3 * i + 2];
+      if (legacy_all || K > (uint32_t)kCapK) {
+        legacy.push_back(ids[i]);
+        lk.push_back(K);
+        ln.push_back(N);
+        lm.push_back(M);
+        continue;
+      }
+      if (tk + K >= key_cap || tc + N + M >= (1ull << 32)) CDB_TRY(flush());
+      wide_ids.push_back(ids[i]);
+      tk += K;
+      tc += N + M;
+      cmax = std::max<uint64_t>(cmax, N + M);
+      hk_off.push_back((uint32_t)tk);
+      c_off.push_back((uint32_t)tc);
     }
-    if (tk + K >= key_cap || tc + N + M >= (1ull << 32)) CDB_TRY(flush());
-    wide_ids.push_back(ids[i]);
-    tk += K;
-    tc += N + M;
-    cmax = std::max<uint64_t>(cmax, N + M);
-    hk_off.push_back((uint32_t)tk);
-    c_off.push_back((uint32_t)tc);
+    CDB_TRY(flush());
   }
-  CDB_TRY(flush());
   if (!legacy.empty()) {
     const uint32_t nl = (uint32_t)legacy.size();
     std::vector<uint64_t> off(nl);
@@ -1033,9 +1051,25 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   CDB_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0), "wait");
   WA.blo = 0;
   WA.bhi = (uint32_t)nb;
+  // ---- 4. buckets beyond the wave tiers: the mid tier (one workgroup per bucket, LDS), or,
+  //         when there are many of them, the chip-wide child path of the over-capacity
+  //         buckets (hot.hip.h): buckets of a few keys with hundreds of children each (C3's
+  //         sets) sort their children serially inside one workgroup, but spread over the chip
+  //         they fold in parallel; then the over-capacity buckets
+  uint32_t counts[2] = {0, 0};  // hot, big (mid tier)
+  CDB_HIP(hipMemcpyAsync(counts, d_hot_count, sizeof counts, hipMemcpyDeviceToHost, s), "d2h");
+  CDB_HIP(hipStreamSynchronize(s), "sync");
+  constexpr uint32_t kMidChipWide = 4096;  // mid-tier buckets from which they go chip-wide
+  const bool mid_wide = A.force_tier == 0 && counts[1] >= kMidChipWide;
+  // Going chip-wide from sorted runs, buckets of at most kRunsChildMax children keep their
+  // children in the runs (only their keys are copied): the tag pass reads each bucket's run slices
+  // in order and the fold's reads stay inside a few hundred KB per bucket (C3: 1.35 ms of copies)
+  constexpr uint32_t kRunsChildMax = 16384;
+  const uint32_t runs_child_max = (use_runs && mid_wide) ? kRunsChildMax : 0;
   if (use_runs) {
     // the workgroup tiers' buckets: copied out of the runs into AoS rows + row indices
     MatArgs MA_;
+    MA_.runs_child_max = runs_child_max;
     MA_.kr = krows;
     MA_.nr = nrows;
     MA_.mr = mrows;
@@ -1061,18 +1095,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     mat_copy_kernel<<<4096, 256, 0, s>>>(WA, MA_, d_big_list);
     CDB_TRY(launch_check(ctx, s, "mat_copy_kernel"));
   }
-  // ---- 4. buckets beyond the wave tiers: the mid tier (one workgroup per bucket, LDS), or,
-  //         when there are many of them, the chip-wide child path of the over-capacity
-  //         buckets (hot.hip.h): buckets of a few keys with hundreds of children each (C3's
-  //         sets) sort their children serially inside one workgroup, but spread over the chip
-  //         they fold in parallel; then the over-capacity buckets
-  uint32_t counts[2] = {0, 0};  // hot, big (mid tier)
-  CDB_HIP(hipMemcpyAsync(counts, d_hot_count, sizeof counts, hipMemcpyDeviceToHost, s), "d2h");
-  CDB_HIP(hipStreamSynchronize(s), "sync");
-  constexpr uint32_t kMidChipWide = 4096;  // mid-tier buckets from which they go chip-wide
-  const bool mid_wide = A.force_tier == 0 && counts[1] >= kMidChipWide;
   if (mid_wide) {
-    CDB_TRY(over_capacity(ctx, A, d_big_list, counts[1], s));
+    CDB_TRY(over_capacity(ctx, A, d_big_list, counts[1], s, use_runs ? &RV : nullptr, runs_child_max));
   } else {
     bucket_mid_kernel<<<std::min<uint64_t>(nb, 2048), kBktThreads, 0, s>>>(A, d_big_list, d_big_count);
     CDB_TRY(launch_check(ctx, s, "bucket_mid_kernel"));

@@ -28,6 +28,7 @@
 
 #include "bucket.hip.h"
 #include "common.h"
+#include "runs.hip.h"
 
 namespace cdb {
 
@@ -59,7 +60,17 @@ struct HotArgs {
   uint32_t* fold_q;          // per run start: the sorted position whose row is the output
                              // (members: the winner; nodes: the head), kNone: selection path
   uint64_t* fold_v;          // per run start: a counter node's folded value
+  // runs mode (sorted-run input, buckets of at most MatArgs::runs_child_max children): the
+  // children are read from the runs' columns (c_row = the absolute run row), not from copies
+  int runs;
+  RunView V;
 };
+
+// A child's columns: its copied AoS row, or (runs mode) the runs' SoA columns.
+__device__ __forceinline__ uint64_t hot_col(const BucketArgs& A, const HotArgs& H, bool isn, uint32_t row, int c) {
+  if (H.runs) return (isn ? H.V.nin : H.V.min)[c][row];
+  return (isn ? A.nr : A.mr)[(uint64_t)row * kChildStride + c];
+}
 
 __device__ __forceinline__ uint32_t hot_bucket_of(const HotArgs& H, uint64_t j) {  // last h: c_off[h] <= j
   uint32_t lo = 0, hi = H.H;
@@ -114,9 +125,24 @@ __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
     const uint32_t h = hot_bucket_of(H, j), b = H.ids[h];
     const uint32_t i = (uint32_t)(j - H.c_off[h]), N = A.ncnt[b];
     const bool isn = i < N;
-    const uint32_t row = isn ? A.np[A.nbase[b] + i] : A.mp[A.mbase[b] + (i - N)];
-    const uint64_t* C = (isn ? A.nr : A.mr) + (uint64_t)row * kChildStride;
-    const uint64_t pkh = C[C_PKH], pkf = C[C_PKF], id1 = C[C_ID1], m = C[C_META];
+    uint32_t row;
+    if (H.runs) {  // the bucket's slices of the family's runs, in run order (as mat_copy lays them)
+      const int f = isn ? 1 : 2;
+      uint32_t k = isn ? i : i - N, r = 0;
+      for (;; ++r) {
+        const uint32_t* d = H.V.rdir[f] + (uint64_t)r * H.V.nbp1 + b;
+        const uint32_t len = d[1] - d[0];
+        if (k < len || r + 1 >= H.V.nr) {
+          row = (uint32_t)(H.V.rbase[f * (kMaxRuns + 1) + r] + d[0] + k);
+          break;
+        }
+        k -= len;
+      }
+    } else {
+      row = isn ? A.np[A.nbase[b] + i] : A.mp[A.mbase[b] + (i - N)];
+    }
+    const uint64_t pkh = hot_col(A, H, isn, row, C_PKH), pkf = hot_col(A, H, isn, row, C_PKF);
+    const uint64_t id1 = hot_col(A, H, isn, row, C_ID1), m = hot_col(A, H, isn, row, C_META);
     // lower bound over the bucket's sorted output keys on (kh << shift, kh, kf)
     const uint32_t g0 = H.hk_off[h], kout = H.hk_kout[h];
     uint32_t lo = 0, hi = kout;
@@ -155,13 +181,12 @@ struct HotChild {
   uint32_t j;
 };
 __device__ __forceinline__ HotChild hot_child(const BucketArgs& A, const HotArgs& H, uint64_t q, bool isn) {
-  const uint32_t j = H.v[q];
-  const uint64_t* C = (isn ? A.nr : A.mr) + (uint64_t)H.c_row[j] * kChildStride;
+  const uint32_t j = H.v[q], row = H.c_row[j];
   HotChild c;
-  c.id1 = C[C_ID1];
-  c.id2 = C[C_ID2];
-  c.t = C[C_T];
-  c.meta = C[C_META];
+  c.id1 = hot_col(A, H, isn, row, C_ID1);
+  c.id2 = hot_col(A, H, isn, row, C_ID2);
+  c.t = hot_col(A, H, isn, row, C_T);
+  c.meta = hot_col(A, H, isn, row, C_META);
   c.j = j;
   return c;
 }
@@ -264,16 +289,14 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
       uint32_t rj[kFoldFast];
 #pragma unroll
       for (uint32_t k = 0; k < kFoldFast; ++k) rj[k] = (fast && k < nrows) ? H.c_row[H.v[p + k]] : 0;
-      const uint64_t* src = isn ? A.nr : A.mr;
       uint64_t xi1[kFoldFast], xi2[kFoldFast], xt[kFoldFast], xm[kFoldFast];
 #pragma unroll
       for (uint32_t k = 0; k < kFoldFast; ++k) {
         if (fast && k < nrows) {
-          const uint64_t* C = src + (uint64_t)rj[k] * kChildStride;
-          xi1[k] = C[C_ID1];
-          xi2[k] = C[C_ID2];
-          xt[k] = C[C_T];
-          xm[k] = C[C_META];
+          xi1[k] = hot_col(A, H, isn, rj[k], C_ID1);
+          xi2[k] = hot_col(A, H, isn, rj[k], C_ID2);
+          xt[k] = hot_col(A, H, isn, rj[k], C_T);
+          xm[k] = hot_col(A, H, isn, rj[k], C_META);
         } else {
           xi1[k] = xi2[k] = xt[k] = xm[k] = 0;
         }

@@ -319,6 +319,9 @@ struct MatArgs {
   uint32_t* chunk0;              // [nb]: exclusive scan of chunks
   const uint64_t* n_chunks;      // total chunks (device)
   uint32_t nb;
+  uint32_t runs_child_max;       // > 0: buckets of at most this many children (and at most kCapK
+                                 // keys) get only their keys copied: the chip-wide path reads
+                                 // their children from the runs (hot.hip.h, HotArgs::runs)
 };
 
 __global__ void __launch_bounds__(256) mat_count_kernel(WaveArgs W, MatArgs M, const uint32_t* __restrict__ list,
@@ -326,18 +329,20 @@ __global__ void __launch_bounds__(256) mat_count_kernel(WaveArgs W, MatArgs M, c
   const RunView& V = W.V;
   const uint32_t total = *count;
   for (uint32_t li = blockIdx.x * blockDim.x + threadIdx.x; li < M.nb; li += gridDim.x * blockDim.x) {
-    uint32_t ch = 0;
+    uint32_t ch = 0, n3[3] = {0, 0, 0};
     for (int f = 0; f < 3; ++f) {
-      uint32_t n = 0;
       if (li < total) {
         const uint32_t b = list[li];
         for (uint32_t r = 0; r < V.nr; ++r) {
           const uint32_t* row = V.rdir[f] + (uint64_t)r * V.nbp1;
-          n += row[b + 1] - row[b];
+          n3[f] += row[b + 1] - row[b];
         }
       }
-      M.cnt[(uint64_t)f * M.nb + li] = n;
-      ch += (n + kMatChunk - 1) / kMatChunk;
+    }
+    if (M.runs_child_max && n3[0] <= (uint32_t)kCapK && n3[1] + n3[2] <= M.runs_child_max) n3[1] = n3[2] = 0;
+    for (int f = 0; f < 3; ++f) {
+      M.cnt[(uint64_t)f * M.nb + li] = n3[f];
+      ch += (n3[f] + kMatChunk - 1) / kMatChunk;
     }
     M.chunks[li] = ch;
   }
