@@ -3,6 +3,7 @@
 #include <stdint.h>
 
 #include <memory>
+#include <mutex>
 #include <utility>
 #include <string>
 #include <vector>
@@ -37,6 +38,8 @@ using RefVec = std::vector<ByteRef, DefaultInitAlloc<ByteRef>>;
 struct ReplicaAdd { uint64_t add_time, node_id; std::string alias, addr; uint64_t uuid; uint32_t seq; };
 struct ReplicaDel { std::string addr; uint64_t t; uint32_t seq; };  // seq: order among the replica entries
 
+struct DeviceRefs;
+
 struct Batch {
   std::vector<uint8_t, DefaultInitAlloc<uint8_t>> raw;  // the snapshot bytes: arena for keys, values, members
 
@@ -64,11 +67,29 @@ struct Batch {
   // (dev_rows = keys, nodes, members there); byte references, header and replicas are here.
   bool rows_on_device = false;
   uint64_t dev_rows[3] = {0, 0, 0};
+  // ... and until a consumer asks (refs_ready), the byte references too.
+  std::shared_ptr<DeviceRefs> dev_refs;
 
   uint64_t n_keys() const { return kh.size(); }
   uint64_t n_nodes() const { return n_pkh.size(); }
   uint64_t n_members() const { return m_pkh.size(); }
 };
+
+// Byte references cdb_decode_snapshots_device left in HBM: key_ref | val_ref (n pairs each),
+// then m_ref | m_vref (nm pairs each) in one allocation on `device`; host-tier member rows are
+// patched in on download. Only the canonical dump and the encoder resolve bytes, so decoding
+// into HBM for a merge does not pay the 32 B/row trip back to the host.
+struct DeviceRefs {
+  struct Patch { uint64_t row; ByteRef m, mv; };
+  int device = 0;
+  void* dev = nullptr;
+  uint64_t n = 0, nm = 0;
+  std::vector<Patch> patch;
+  std::mutex mu;
+  ~DeviceRefs();
+};
+// Downloads b's byte references if they are still in HBM (decode_gpu.hip); thread-safe.
+cdb_status refs_ready(cdb_ctx* ctx, Batch* b);
 
 // Copies a large host buffer with the staging ring's copy threads (capi.cpp).
 void parallel_copy(void* dst, const void* src, size_t bytes);

@@ -595,8 +595,9 @@ cdb_status cdb_merged_from_device(cdb_ctx* ctx, cdb_merged* state, cdb_batch* co
 }
 
 cdb_status cdb_merged_canonical_dump(cdb_ctx* ctx, cdb_merged* m, char** out, size_t* len) {
-  (void)ctx;
   if (!m || !out || !len) return CDB_BAD_ARGUMENT;
+  for (const auto& b : m->inputs)  // (byte references a device decode left in HBM)
+    if (cdb_status st = refs_ready(ctx, b.get()); st != CDB_OK) return st;
   const uint64_t nk = m->k[O_KH].size();
   struct KeyView { const uint8_t* p; uint64_t n; uint64_t row; };
   auto key_of = [&](uint64_t r) {
@@ -917,6 +918,8 @@ cdb_status cdb_encode_snapshot(cdb_ctx* ctx, cdb_merged* m, const cdb_encode_hea
   *out = nullptr;
   *len = 0;
   hipSetDevice(ctx->device);
+  for (const auto& b : m->inputs)
+    if (cdb_status st = refs_ready(ctx, b.get()); st != CDB_OK) return st;
   return encode_snapshot_impl(ctx, *m, *hdr, out, len, stats);
 }
 

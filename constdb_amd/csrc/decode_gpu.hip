@@ -1008,6 +1008,49 @@ cdb_status GpuDecode::refs_to_batch(const DecArgs& A) {
   return CDB_OK;
 }
 
+DeviceRefs::~DeviceRefs() {
+  if (!dev) return;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(device);
+  (void)hipFree(dev);
+  (void)hipSetDevice(cur);
+}
+
+cdb_status refs_ready(cdb_ctx* ctx, Batch* b) {
+  std::shared_ptr<DeviceRefs> r = b->dev_refs;
+  if (!r) return CDB_OK;
+  std::lock_guard<std::mutex> lock(r->mu);
+  if (!r->dev) return CDB_OK;  // (another caller downloaded them)
+  if (!ctx) return CDB_BAD_ARGUMENT;
+  if (ctx->device != r->device) return fail(ctx, CDB_BAD_ARGUMENT, "byte references live on another device");
+  (void)hipSetDevice(ctx->device);
+  const uint64_t n = r->n, nm = r->nm;
+  const ByteRef* d = (const ByteRef*)r->dev;
+  RefVec* dst[4] = {&b->key_ref, &b->val_ref, &b->m_ref, &b->m_vref};
+  const uint64_t rows[4] = {n, n, nm, nm};
+  const ByteRef* src[4] = {d, d + n, d + 2 * n, d + 2 * n + nm};
+  std::vector<HostSeg> segs;
+  for (int c = 0; c < 4; ++c) {
+    dst[c]->resize(rows[c]);
+    advise_huge(dst[c]->data(), rows[c] * sizeof(ByteRef));  // (fresh pages, first touched by the download)
+    if (rows[c]) segs.push_back({dst[c]->data(), const_cast<ByteRef*>(src[c]), rows[c] * sizeof(ByteRef)});
+  }
+  cdb_status st = segs.empty() ? CDB_OK : staged_copy(ctx, segs.data(), segs.size(), false, ctx->stream);
+  if (st != CDB_OK) {
+    for (int c = 0; c < 4; ++c) dst[c]->clear();
+    return st;
+  }
+  for (const DeviceRefs::Patch& p : r->patch) {
+    b->m_ref[p.row] = p.m;
+    b->m_vref[p.row] = p.mv;
+  }
+  (void)hipFree(r->dev);
+  r->dev = nullptr;
+  r->patch.clear();
+  return CDB_OK;
+}
+
 cdb_status GpuDecode::emit_host(DecodeTiming* tm) {
   if (n_ == 0) return CDB_OK;
   const uint64_t n = n_, nn = nn_, nm = nm_;
@@ -1180,8 +1223,6 @@ cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint6
     }
   }
   if (!segs.empty() && (st_ = staged_copy(ctx_, segs.data(), segs.size(), true, s)) != CDB_OK) return st_;
-  // the byte references down into the batch
-  if ((st_ = refs_to_batch(A)) != CDB_OK) return st_;
   ck(hipEventRecord(ev_.b, s), "event");
   ck(hipStreamSynchronize(s), "sync(decode)");
   if (st_ != CDB_OK) return st_;
@@ -1190,6 +1231,18 @@ cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint6
     hipEventElapsedTime(&ms, ev_.a, ev_.b);
     tm->device_ms = ms;
   }
+  // the byte references stay in HBM until the canonical dump or the encoder asks (refs_ready)
+  auto r = std::make_shared<DeviceRefs>();
+  r->device = ctx_->device;
+  r->n = n;
+  r->nm = nm;
+  for (const HostEntry& he : hosted_) {
+    const Batch& hr = he.rows;
+    for (size_t j = 0; j < hr.m_pkh.size(); ++j) r->patch.push_back({moff_[he.i] + j, hr.m_ref[j], hr.m_vref[j]});
+  }
+  r->dev = d_rows_.p;
+  d_rows_.p = nullptr;
+  out_->dev_refs = std::move(r);
   (void)nn;
   return CDB_OK;
 

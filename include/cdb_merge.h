@@ -91,7 +91,9 @@ cdb_status cdb_decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len,
  * emitted into it at fold position i -- row for row what cdb_upload_batches leaves from the
  * host-decoded batches. batches[i] receives snapshot i's host side (bytes, byte references,
  * header, replica entries, cdb_batch_info) to resolve merge outputs by src; its row columns
- * stay in HBM, so cdb_merge, cdb_upload_batches and cdb_batch_column reject it.
+ * stay in HBM, so cdb_merge, cdb_upload_batches and cdb_batch_column reject it. Its byte
+ * references stay in HBM too, until the first cdb_merged_canonical_dump or cdb_encode_snapshot
+ * of a result behind it downloads them (on that call's ctx, which must be this ctx's device).
  * Sorted runs: when every snapshot's DATAS, EXPIRES and DELETES sections are each in key-hash
  * order (a snapshot cdb_encode_snapshot wrote from a merge result), snapshot i's key rows are
  * placed as ONE run in key-hash order (the three sections merged, DATAS first on equal hashes;

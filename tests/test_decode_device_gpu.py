@@ -117,8 +117,11 @@ def test_device_decode_large_sections_with_huge_entries(ctx):
     snaps = [cdb.gen_snapshot(cfg, r) for r in range(2)]
     big = cdb.decode_snapshot(snaps[0]).info()
     assert big.n_data > (1 << 17)  # the section goes to the device index
-    _, din = _check(ctx, snaps)
-    _release(din)
+    batches, din = _check(ctx, snaps)
+    try:
+        _dump_vs_oracle(ctx, snaps, batches, din)
+    finally:
+        _release(din)
     # damage inside the device-indexed section of the second snapshot: the same status and offset
     # as the host decoder, with the first snapshot indexed beside it
     for frac in (3, 2):
@@ -160,10 +163,13 @@ def test_device_decode_large_sections_with_huge_entries(ctx):
 
 def test_device_decode_host_tier(ctx):
     """Objects past the per-thread dedup limits (3000 members, 1500 nodes) are decoded on the
-    host and uploaded into their reserved rows at the snapshot's fold position."""
-    big, c = o.Set(), o.Counter()
+    host and uploaded into their reserved rows at the snapshot's fold position; their member
+    byte references (kept in HBM with the rest until the dump asks) resolve to the oracle's
+    fold of the same snapshots."""
+    big, d, c = o.Set(), o.Dict(), o.Counter()
     for j in range(3000):
         big.set(b"m%d" % j, None, j % 17)
+        d.set(b"f%d" % j, b"v%d" % (j * 7), j % 11)
         if j % 5 == 0:
             big.dele[b"m%d" % j] = (j % 13) + 3
     for n in range(1500):
@@ -171,10 +177,33 @@ def test_device_decode_host_tier(ctx):
     c.cal_sum()
     db = o.DB()
     db.data.update({b"big": o.Object(1, 0, 0, o.OBJECT_ENC_SET, big),
+                    b"dict": o.Object(1, 0, 0, o.OBJECT_ENC_DICT, d),
                     b"cnt": o.Object(1, 0, 0, o.OBJECT_ENC_COUNTER, c)})
     snap = o.dump_all(db, o.NodeHeader())
-    _, din = _check(ctx, [gen_replicas(4, n_replicas=1)[0], snap, snap])
-    _release(din)
+    snaps = [gen_replicas(4, n_replicas=1)[0], snap, snap]
+    batches, din = _check(ctx, snaps)
+    try:
+        _dump_vs_oracle(ctx, snaps, batches, din)
+    finally:
+        _release(din)
+
+
+def _dump_vs_oracle(ctx, snaps, batches, din):
+    """cdb_merge_device over the device-decoded rows, then the canonical dump (its first call
+    downloads the batches' byte references) against the C++ oracle's fold."""
+    import cdb_oracle
+    from test_runs_oracle_gpu import _diff, _merge_device, _out_for
+    dout = _out_for(ctx, din)
+    try:
+        st = _merge_device(ctx, din, dout)
+        m = cdb.merged_from_device(ctx, dout, batches, stats=st)
+        got = m.canonical_dump()
+        assert m.canonical_dump() == got  # the references are on the host now
+        rc, want, _ = cdb_oracle.fold(snaps)
+        assert rc == 0
+        assert got == want, _diff(got, want)
+    finally:
+        _release(dout)
 
 
 def test_device_decode_c3_snapshots(ctx):
