@@ -551,10 +551,10 @@ cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, uint64_t nb, in
 }  // namespace
 
 namespace {
-// Stable LSD radix sort of n (u64 key, u32 value) pairs on bits [0, bits) (rounded up to whole
-// bytes); returns the buffers holding the result (the inputs or the spare pair).
+// Stable LSD radix sort of n (u64 key, u32 value) pairs on bits [lo, bits) in 8-bit passes from
+// lo; returns the buffers holding the result (the inputs or the spare pair).
 cdb_status radix_sort_pairs(cdb_ctx* ctx, uint64_t** k, uint32_t** v, uint64_t* k2, uint32_t* v2, uint64_t n,
-                            int bits, hipStream_t s) {
+                            int lo, int bits, hipStream_t s) {
   if (n == 0) return CDB_OK;
   const uint32_t tiles = (uint32_t)((n + kRadixTile - 1) / kRadixTile);
   cdb_status st = CDB_OK;
@@ -563,7 +563,7 @@ cdb_status radix_sort_pairs(cdb_ctx* ctx, uint64_t** k, uint32_t** v, uint64_t* 
   uint32_t* base = hist + 256ull * tiles;
   uint64_t *ka = *k, *kb = k2;
   uint32_t *va = *v, *vb = v2;
-  for (int sh = 0; sh < bits; sh += 8) {
+  for (int sh = lo; sh < bits; sh += 8) {
     radix_hist_kernel<<<tiles, kRadixThreads, 0, s>>>(ka, n, sh, hist, tiles);
     CDB_TRY(launch_check(ctx, s, "radix_hist_kernel"));
     CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, hist, 256ull * tiles, base, (uint32_t*)nullptr, nullptr, s));
@@ -582,7 +582,7 @@ cdb_status radix_sort_pairs(cdb_ctx* ctx, uint64_t** k, uint32_t** v, uint64_t* 
 // rows in the batch (the key table's index width in the sort tag and the child row indices).
 cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& wide_ids,
                      const std::vector<uint32_t>& hk_off, const std::vector<uint32_t>& c_off, uint64_t tk,
-                     uint64_t tc, uint64_t cmax, const RunView* rv, hipStream_t s) {
+                     uint64_t tc, uint64_t cmax, const RunView* rv, bool run_order, hipStream_t s) {
   cdb_status st = CDB_OK;
   const uint32_t H = (uint32_t)wide_ids.size();
   // device: ids[H] | hk_off[H + 1] | c_off[H + 1] | hk_kout[H] | run count
@@ -604,18 +604,23 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   uint64_t* d_runs = (uint64_t*)(((uintptr_t)(HA.hk_kout + H) + 7) & ~(uintptr_t)7);
   HA.H = H;
   HA.n_children = tc;
-  // Tag layout W = G << g_shift | id hash bits << 6 | pos, sorted on g_shift + gbits bits in 8-bit
-  // passes. The id bits only separate a key's children: ids sharing them take the successor-
-  // selection fold (exact, but slow for long runs), so a bucket of c children gets at least
-  // log2(c) + 9 of them (about c / 1024 rows sharing), and where fewer than 34 bits reach the
-  // next pass boundary they save whole passes: C3 (buckets of a few thousand children, a
-  // 400K-key table) sorts in 6 passes instead of 8; C5's hottest keys keep all 34.
+  // Tag layout W = G << g_shift | id hash bits << 6 | pos, sorted on bits [lo, g_shift + gbits) in
+  // 8-bit passes. On the sorted-run path (run_order) lo = 6: the pos bits are not sorted, the
+  // stable sort keeps a W-run's rows in flat order, which is run order there -- fold order when
+  // the runs are the fold positions (the fold checks, and takes the selection path where they
+  // are not); a partition leaves a bucket's rows in arbitrary order, so lo = 0. The id bits only
+  // separate a key's children: ids sharing them take the successor-selection fold (exact, but
+  // slow for long runs), so a bucket of c children gets at least log2(c) + 9 of them (about
+  // c / 1024 rows sharing), and where fewer than 34 bits reach the next pass boundary they save
+  // whole passes: C3 (buckets of a few thousand children, a 400K-key table) sorts in 5 passes
+  // instead of 8; C5's hottest keys keep all 34.
   int gbits = 0, cbits = 0;
   while (gbits < 32 && (tk >> gbits)) ++gbits;
   while (cbits < 40 && (cmax >> cbits)) ++cbits;
   const int min_id = std::max(kHotMinIdBits, cbits + 9);
-  const int passes = (gbits + 6 + std::min(min_id, kHotIdBits - 6) + 7) / 8;
-  int id_bits = std::min(kHotIdBits - 6, 8 * passes - 6 - gbits);
+  const int lo = run_order ? 6 : 0;
+  const int passes = (gbits + 6 - lo + std::min(min_id, kHotIdBits - 6) + 7) / 8;
+  int id_bits = std::min(kHotIdBits - 6, 8 * passes - 6 + lo - gbits);
   // test hook: fewer id bits force the collision (successor-selection) fold
   if (const char* e = std::getenv("CDB_HOT_ID_BITS")) {
     const int bits = std::atoi(e);
@@ -636,14 +641,15 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   HA.hk_tp = (uint32_t*)(HA.hk_sum + nk);
   HA.hk_cnt = HA.hk_tp + nk;
   HA.hk_cb = HA.hk_cnt + nk;
-  uint8_t* ct = (uint8_t*)ws_get(ctx, WS_HOTCH, nc * (2 * 8 + 2 * 4 + 2 * 4 + 5 * 4) + 64, &st);
+  uint8_t* ct = (uint8_t*)ws_get(ctx, WS_HOTCH, nc * (32 + 2 * 8 + 2 * 4 + 6 * 4) + 64, &st);
   if (!ct) return st;
+  HA.rec = (ulonglong2*)ct;  // (the workspace is 256-B aligned)
+  ct += nc * 32;
   uint64_t* w = (uint64_t*)ct;
   uint64_t* w2 = w + nc;
   uint32_t* v = (uint32_t*)(w2 + nc);
   uint32_t* v2 = v + nc;
-  HA.c_row = v2 + nc;
-  HA.c_h = HA.c_row + nc;
+  HA.c_h = v2 + nc;
   HA.emit_n = HA.c_h + nc;
   HA.emit_m = HA.emit_n + nc;
   uint32_t* rank_n = HA.emit_m + nc;
@@ -660,7 +666,7 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
     CDB_TRY(launch_check(ctx, s, "hot_tag_kernel"));
     // (per-bucket bitonic sorts in LDS measured slower than this global radix sort: C3 9.98 vs
     // 8.90 ms, C5 25.9 vs 24.3 ms; profiles/r03/experiments_r3.txt)
-    CDB_TRY(radix_sort_pairs(ctx, &HA.w, &HA.v, w2, v2, tc, HA.g_shift + gbits, s));
+    CDB_TRY(radix_sort_pairs(ctx, &HA.w, &HA.v, w2, v2, tc, lo, HA.g_shift + gbits, s));
   }
   if (tc) {
     // the sort's other buffers are free now: fold results per run start
@@ -724,7 +730,8 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   bool runs_batch = false;  // the batch being built reads its children from the runs
   auto flush = [&]() -> cdb_status {
     if (wide_ids.empty()) return CDB_OK;
-    const cdb_status r = chip_wide(ctx, A, wide_ids, hk_off, c_off, tk, tc, cmax, runs_batch ? rv : nullptr, s);
+    const cdb_status r =
+        chip_wide(ctx, A, wide_ids, hk_off, c_off, tk, tc, cmax, runs_batch ? rv : nullptr, rv != nullptr, s);
     wide_ids.clear();
     hk_off.assign(1, 0);
     c_off.assign(1, 0);

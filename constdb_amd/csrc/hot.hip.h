@@ -5,16 +5,19 @@
 // the whole chip instead:
 //   hot_keys_kernel : one workgroup per hot bucket: the key phase; the bucket's output keys go to
 //                     a global key table at hk_off[h] (G = hk_off[h] + rank is a chip-wide key id);
-//   hot_tag_kernel  : one thread per child: finds its key (binary search of the bucket's table),
+//   hot_tag_kernel  : one thread per child (flat order): finds its key (binary search of the
+//                     bucket's table), copies the fields the fold reads into a 32-B record,
 //                     decides whether it takes part (head type, element type, remote dels
 //                     ignored, exactly as the wave tier) and tags it with
-//                     W = G << g_shift | id-hash top (g_shift - 6) bits << 6 | pos, so that a
-//                     run's rows arrive in fold order unless two ids share those hash bits
-//                     (g_shift: 40, or less where that saves a sort pass -- see chip_wide); a
-//                     child that takes no part gets its bucket's marker (every W bit of the
-//                     bucket's last key set: pos 63, which no row has), so it sorts to the end of
-//                     its bucket's children and every bucket's children keep their flat range;
-//   radix sort of (W, child) pairs (radix.hip.h), stable, so equal W keep (bucket, row) order;
+//                     W = G << g_shift | id-hash top (g_shift - 6) bits << 6 | pos (g_shift:
+//                     40, or less where that saves a sort pass -- see chip_wide); a child that
+//                     takes no part gets its bucket's marker (every W bit of the bucket's last key
+//                     set: pos 63, which no row has, and an id field no child gets), so it sorts
+//                     to the end of its bucket's children and every bucket's children keep their
+//                     flat range;
+//   radix sort of (W, child) pairs (radix.hip.h) on W's bits above pos, stable, so equal W >> 6
+//                     keep (bucket, row) order: run order, which is fold order on the sorted-run
+//                     path unless two ids share the hash bits;
 //                     W orders the buckets, so bucket h's children (markers last) keep its flat
 //                     range [c_off[h], c_off[h + 1]);
 //   hot_fold_kernel : one thread per W-run (a (key, child id) group, ~ one row per replica):
@@ -48,7 +51,7 @@ struct HotArgs {
   // children
   uint64_t* w;               // W per flat child (then sorted)
   uint32_t* v;               // flat child index (then sorted)
-  uint32_t* c_row;           // physical row of flat child j
+  ulonglong2* rec;           // flat child j's fold fields: rec[2j] = (id1, id2), rec[2j + 1] = (t, meta)
   uint32_t* c_h;             // bucket h of flat child j, bit 31 = member
   uint32_t *emit_n, *emit_m; // per sorted position: outputs of the run starting there
   const uint32_t *rank_n, *rank_m;  // exclusive scans of emit_n / emit_m
@@ -61,7 +64,7 @@ struct HotArgs {
                              // (members: the winner; nodes: the head), kNone: selection path
   uint64_t* fold_v;          // per run start: a counter node's folded value
   // runs mode (sorted-run input, buckets of at most MatArgs::runs_child_max children): the
-  // children are read from the runs' columns (c_row = the absolute run row), not from copies
+  // tag pass reads the children from the runs' columns (the absolute run row), not from copies
   int runs;
   RunView V;
 };
@@ -143,6 +146,7 @@ __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
     }
     const uint64_t pkh = hot_col(A, H, isn, row, C_PKH), pkf = hot_col(A, H, isn, row, C_PKF);
     const uint64_t id1 = hot_col(A, H, isn, row, C_ID1), m = hot_col(A, H, isn, row, C_META);
+    const uint64_t id2 = hot_col(A, H, isn, row, C_ID2), t = hot_col(A, H, isn, row, C_T);
     // lower bound over the bucket's sorted output keys on (kh << shift, kh, kf)
     const uint32_t g0 = H.hk_off[h], kout = H.hk_kout[h];
     uint32_t lo = 0, hi = kout;
@@ -161,15 +165,19 @@ __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
       const bool elem_ok = (H.hk_vm[g0 + lo] >> p) & 1;
       const bool cand = isn || meta_tag(m) == KIND_ADD || p == hp;  // remote dels ignored
       if (type_ok && elem_ok && cand) {
-        const uint64_t ih = isn ? mix64(id1) : id1;
-        w = ((uint64_t)(g0 + lo) << H.g_shift) | ((ih >> H.id_shift) << 6) | p;
+        // (the id field stops one below all ones: the marker is above every W of the bucket in
+        // the sorted bits, which leave out the pos bits)
+        const uint64_t ih = isn ? mix64(id1) : id1, top = (1ull << (H.g_shift - 6)) - 2;
+        w = ((uint64_t)(g0 + lo) << H.g_shift) | (min(ih >> H.id_shift, top) << 6) | p;
       }
     } else {
       ++orph;
     }
     H.w[j] = w;
     H.v[j] = (uint32_t)j;
-    H.c_row[j] = row;
+    // the fold reads a child's four fields as one 32-B record (flat order: written in sequence)
+    H.rec[2 * j] = make_ulonglong2(id1, id2);
+    H.rec[2 * j + 1] = make_ulonglong2(t, m);
     H.c_h[j] = h | (isn ? 0u : 0x80000000u);
   }
   if (orph) atomicAdd(&stat_shard(A.stats)[ST_ORPHANS], orph);
@@ -180,13 +188,14 @@ struct HotChild {
   uint64_t id1, id2, t, meta;
   uint32_t j;
 };
-__device__ __forceinline__ HotChild hot_child(const BucketArgs& A, const HotArgs& H, uint64_t q, bool isn) {
-  const uint32_t j = H.v[q], row = H.c_row[j];
+__device__ __forceinline__ HotChild hot_child(const HotArgs& H, uint64_t q) {
+  const uint32_t j = H.v[q];
+  const ulonglong2 a = H.rec[2 * (uint64_t)j], b = H.rec[2 * (uint64_t)j + 1];
   HotChild c;
-  c.id1 = hot_col(A, H, isn, row, C_ID1);
-  c.id2 = hot_col(A, H, isn, row, C_ID2);
-  c.t = hot_col(A, H, isn, row, C_T);
-  c.meta = hot_col(A, H, isn, row, C_META);
+  c.id1 = a.x;
+  c.id2 = a.y;
+  c.t = b.x;
+  c.meta = b.y;
   c.j = j;
   return c;
 }
@@ -288,15 +297,16 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
       const bool fast = act && nrows <= kFoldFast;
       uint32_t rj[kFoldFast];
 #pragma unroll
-      for (uint32_t k = 0; k < kFoldFast; ++k) rj[k] = (fast && k < nrows) ? H.c_row[H.v[p + k]] : 0;
+      for (uint32_t k = 0; k < kFoldFast; ++k) rj[k] = (fast && k < nrows) ? H.v[p + k] : 0;
       uint64_t xi1[kFoldFast], xi2[kFoldFast], xt[kFoldFast], xm[kFoldFast];
 #pragma unroll
       for (uint32_t k = 0; k < kFoldFast; ++k) {
         if (fast && k < nrows) {
-          xi1[k] = hot_col(A, H, isn, rj[k], C_ID1);
-          xi2[k] = hot_col(A, H, isn, rj[k], C_ID2);
-          xt[k] = hot_col(A, H, isn, rj[k], C_T);
-          xm[k] = hot_col(A, H, isn, rj[k], C_META);
+          const ulonglong2 a = H.rec[2 * (uint64_t)rj[k]], c = H.rec[2 * (uint64_t)rj[k] + 1];
+          xi1[k] = a.x;
+          xi2[k] = a.y;
+          xt[k] = c.x;
+          xm[k] = c.y;
         } else {
           xi1[k] = xi2[k] = xt[k] = xm[k] = 0;
         }
@@ -339,7 +349,7 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
       if (q != kNone) {
         slow = false;
         if ((isn ? H.emit_n : H.emit_m)[p]) {
-          const HotChild x = hot_child(A, H, q, isn);
+          const HotChild x = hot_child(H, q);
           put(x.id1, x.id2, x.t, x.meta, H.fold_v[p]);
         }
       }
@@ -359,7 +369,7 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
       bool have = false;
       for (uint32_t k = 0; k < kslow; ++k) {
         if (slow && k < nrows && step < nrows) {
-          const HotChild x = hot_child(A, H, p + k, isn);
+          const HotChild x = hot_child(H, p + k);
           const bool after = step == 0 || hot_before(last, x, isn);
           const bool take = after && (!have || hot_before(x, c, isn));
           c.id1 = take ? x.id1 : c.id1;
