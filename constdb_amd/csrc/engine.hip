@@ -1068,10 +1068,12 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   CDB_HIP(hipStreamSynchronize(s), "sync");
   constexpr uint32_t kMidChipWide = 4096;  // mid-tier buckets from which they go chip-wide
   const bool mid_wide = A.force_tier == 0 && counts[1] >= kMidChipWide;
-  // Going chip-wide from sorted runs, buckets of at most kRunsChildMax children keep their
-  // children in the runs (only their keys are copied): the tag pass reads each bucket's run slices
-  // in order and the fold's reads stay inside a few hundred KB per bucket (C3: 1.35 ms of copies)
-  constexpr uint32_t kRunsChildMax = 16384;
+  // Going chip-wide from sorted runs, buckets keep their children in the runs (only their keys
+  // are copied): the tag pass reads each bucket's run slices in order and writes the fold's
+  // records, so a copy of the children first only costs (C3: 1.35 ms of copies; C5 with copies
+  // of the buckets over 16K children 21.5 ms, without 20.2). With fewer than kMidChipWide mid
+  // buckets the over-capacity ones still take the copy batch (children copied by mat_copy).
+  constexpr uint32_t kRunsChildMax = 0xFFFFFFFFu;
   const uint32_t runs_child_max = (use_runs && mid_wide) ? kRunsChildMax : 0;
   if (use_runs) {
     // the workgroup tiers' buckets: copied out of the runs into AoS rows + row indices
