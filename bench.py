@@ -298,7 +298,7 @@ def run_single(cdb, args):
         "stats": {"type_conflicts": st.type_conflicts, "dict_merges": st.dict_merges,
                   "deletes_gced": st.deletes_gced, "hot_buckets": st.hot_buckets,
                   "wide_buckets": st.wide_buckets, "mid_buckets": st.mid_buckets,
-                  "orphans": st.orphan_children},
+                  "orphans": st.orphan_children, "hot_slow_runs": st.hot_slow_runs},
     }
     if tr:
         res["roofline"]["traffic_per_kernel"] = tr["per_kernel"]

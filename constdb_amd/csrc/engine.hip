@@ -743,11 +743,17 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
     return rv && runs_child_max && !legacy_all && cnt3[3 * i] <= (uint32_t)kCapK &&
            cnt3[3 * i + 1] + cnt3[3 * i + 2] <= runs_child_max;
   };
-  for (int pass = 0; pass < 2; ++pass) {
-    runs_batch = pass == 0;
+  // Each kind in two size classes: the sort's id bits follow the batch's largest bucket and its
+  // key bits the batch's key count, so many small buckets and a few huge ones sorted together
+  // can take a pass more than either alone (C5: 20.1 -> 19.6 ms split).
+  constexpr uint32_t kBigBucket = 16384;
+  for (int pass = 0; pass < 4; ++pass) {
+    runs_batch = pass < 2;
+    const bool big = pass & 1;
     for (uint32_t i : order) {
       if (runs_mode(i) != runs_batch) continue;
       const uint32_t K = cnt3[3 * i], N = cnt3[3 * i + 1], M = cnt3[3 * i + 2];
+      if ((N + M > kBigBucket) != big) continue;
       if (legacy_all || K > (uint32_t)kCapK) {
         legacy.push_back(ids[i]);
         lk.push_back(K);
