@@ -123,9 +123,15 @@ __global__ void __launch_bounds__(kBktThreads) hot_keys_kernel(BucketArgs A, Hot
 __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
   const int ks = A.key_shift;
   unsigned long long orph = 0;
+  const uint32_t lane = threadIdx.x & 63;
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < H.n_children;
        j += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t h = hot_bucket_of(H, j), b = H.ids[h];
+    // the wave's children are consecutive: lane 0 (active whenever any lane is) searches the
+    // bucket of the first, the others step forward from it (buckets here hold hundreds of rows)
+    uint32_t h = lane == 0 ? hot_bucket_of(H, j) : 0;
+    h = (uint32_t)__shfl((int)h, 0);
+    while (h + 1 < H.H && H.c_off[h + 1] <= j) ++h;
+    const uint32_t b = H.ids[h];
     const uint32_t i = (uint32_t)(j - H.c_off[h]), N = A.ncnt[b];
     const bool isn = i < N;
     uint32_t row;
