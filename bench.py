@@ -29,7 +29,7 @@ sys.path.insert(0, ROOT)
 # SURVEY.md §8d algorithmic row widths (bytes): compulsory read + write per row
 W_KEY, W_NODE, W_SET, W_DICT = 50, 33, 34, 42
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")
 # the merge pipeline's kernels (everything cdb_merge_device launches; not the generator)
 MERGE_KERNEL_PREFIXES = ("part_", "bucket_", "compact", "scan_", "stats_reduce", "gc_lastbad", "set_dir",
                          "stamp_pos", "iota", "hot_", "sorted_", "seg_", "run_", "mat_", "radix_hist",
@@ -61,6 +61,12 @@ def parse():
     ap.add_argument("--no-general", action="store_true",
                     help="skip the general_input figures (the same rows merged unsorted, on the partition path)")
     ap.add_argument("--force-tier", type=int, default=0, help="testing: cdb_merge_opts.force_tier")
+    ap.add_argument("--layout", default="records", choices=["records", "columns"],
+                    help="input rows: records (the key-hash column + one record per row, cdb_dev_rows.stride) or "
+                         "plain columns")
+    ap.add_argument("--output", default="buckets", choices=["buckets", "dense"],
+                    help="merge result: the engine's bucket layout (cdb_dev_output.compact = 0, what the next merge, "
+                         "the canonical dump and encode read) or dense columns (compact = 1: one more pass)")
     ap.add_argument("--input-order", default="sorted", choices=["sorted", "hash-random"],
                     help="sorted: every replica's rows form one run in key-hash order (as this engine's merge "
                          "output and snapshots encoded from it are; the sorted-run path); hash-random: rows "
@@ -150,8 +156,10 @@ def setup(cdb, ctx, args):
     din = cdb.DevInput()
     opts = cdb.MergeOpts()
     c = args.config
+    rec_flag = cdb.GEN_ROWS_RECORDS if args.layout == "records" else 0
     if c == "c4":
         cfg = configs.c4(cdb, args.universe_per_gpu, args.replicas, args.seed)
+        cfg.flags |= rec_flag
         ctx.check(L.cdb_gen_device(ctx.handle, ctypes.byref(cfg), ctypes.byref(din)))
         work = (f"C4 anti-entropy shard: {args.universe_per_gpu} keys/GPU x {args.replicas} replicas "
                 f"(N=8 -> exactly C4's 500M keys)")
@@ -166,6 +174,7 @@ def setup(cdb, ctx, args):
                     f"C4 generator config, {args.cpu_universe} keys x {args.replicas} replicas")
     elif c == "c1":
         cfg = configs.c1(cdb)
+        cfg.flags |= rec_flag
         ctx.check(L.cdb_gen_device(ctx.handle, ctypes.byref(cfg), ctypes.byref(din)))
         work = "C1/C2 2-node MEET: 1M Bytes + 1M counters per node, 50 % key overlap, B merged into A"
 
@@ -173,6 +182,7 @@ def setup(cdb, ctx, args):
             return [cdb.gen_snapshot(cfg, r) for r in range(2)], "C1 at full size"
     elif c == "c5":
         cfg = configs.c5(cdb)
+        cfg.flags |= rec_flag
         ctx.check(L.cdb_gen_device(ctx.handle, ctypes.byref(cfg), ctypes.byref(din)))
         work = "C5 Zipf hot keys: 10M keys, children ~ rank^-1.1, 80M node/member rows over 8 replicas"
 
@@ -185,6 +195,9 @@ def setup(cdb, ctx, args):
         batches = [cdb.decode_snapshot(s) for s in snaps]
         arr = (ctypes.c_void_p * len(batches))(*[b.handle for b in batches])
         ctx.check(L.cdb_upload_batches(ctx.handle, arr, len(batches), ctypes.byref(din)))
+        if args.layout == "records":
+            from constdb_amd.runs import to_records
+            to_records(cdb, ctx, din)
         opts.flags = cdb.MERGE_GC_DELETES
         opts.gc_watermark = configs.median_member_time(cdb, batches)
         work = (f"C3 set/dict add-win merge: 4 replicas x {args.c3_ops} sadd/srem/hset/hdel replayed over "
@@ -203,13 +216,15 @@ def timed_merges(cdb, ctx, din, opts, args, steps):
     its stream before returning). Returns (ms per step, per-phase HIP-event ms, last stats)."""
     L = cdb.lib()
     dout = cdb.DevOutput()
-    ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.keys), din.keys.n, 8))
-    ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.nodes), din.nodes.n, 6))
-    ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.members), din.members.n, 6))
-    dout.compact = 1
+    dense = args.output == "dense"
+    if dense:  # caller-allocated dense columns; the bucket layout's rows are the library's
+        ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.keys), din.keys.n, 8))
+        ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.nodes), din.nodes.n, 6))
+        ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(dout.members), din.members.n, 6))
     st = cdb.MergeStats()
 
     def step():
+        dout.compact = 1 if dense else 0
         ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(din), ctypes.byref(opts), ctypes.byref(dout),
                                      ctypes.byref(st), None))
 
@@ -224,8 +239,9 @@ def timed_merges(cdb, ctx, din, opts, args, steps):
         acc["finish"] += st.finish_ms
         acc["device"] += st.device_ms
     t1 = time.perf_counter()
-    for fam in (dout.keys, dout.nodes, dout.members):
-        L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
+    if dense:
+        for fam in (dout.keys, dout.nodes, dout.members):
+            L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
     return (t1 - t0) * 1e3 / steps, {k: v / steps for k, v in acc.items()}, st
 
 
@@ -280,6 +296,7 @@ def run_single(cdb, args):
                    "member_rows_in": st.member_rows_in, "key_rows_out": st.key_rows_out,
                    "node_rows_out": st.node_rows_out, "member_rows_out": st.member_rows_out,
                    "gc_watermark": opts.gc_watermark, "input_order": args.input_order,
+                   "input_layout": args.layout, "output_layout": args.output,
                    "merge_path": "sorted runs" if st.sorted_runs else "partition", "parallelism": "single GPU"},
         "child_rows_per_s": (st.node_rows_in + st.member_rows_in) / (ms * 1e-3),
         "phases_ms": {"partition": per["partition"], "bucket_merge": per["bucket"], "finish": per["finish"],
@@ -287,7 +304,8 @@ def run_single(cdb, args):
         # achieved = B_alg / t_merge over the WHOLE merge (HIP events on the merge
         # stream around partition -> bucket merge -> compaction)
         "roofline": {"bound": "hbm",
-                     "kernel": "whole merge pipeline (partition + bucket merge + compaction), HIP events",
+                     "kernel": ("whole merge pipeline (run directories / partition + bucket merge + "
+                                + ("compaction" if args.output == "dense" else "bucket directory scans") + "), HIP events"),
                      "achieved": B / (per["device"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": B / (per["device"] * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "alg_bytes": B,

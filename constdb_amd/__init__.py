@@ -41,6 +41,8 @@ MERGE_GC_MEMBERS = 4
 GEN_NODE_PER_REPLICA = 1
 GEN_OPS_ZIPF_MEMBERS = 2
 GEN_OPS_TAGS_ONLY = 4
+GEN_ROWS_RECORDS = 8
+DECODE_ROWS_RECORDS = 2
 
 
 class CstError(Exception):
@@ -170,7 +172,16 @@ class ApplyStats(ctypes.Structure):
 
 
 class DevRows(ctypes.Structure):
-    _fields_ = [("col", ctypes.c_void_p * 8), ("n", ctypes.c_uint64)]
+    """cdb_dev_rows: plain columns (stride 0), the records layout (col[0] the hash column, fields
+    1.. one record of `stride` words per row), or a merge's bucket-layout rows (stride0 = stride)."""
+    _fields_ = [("col", ctypes.c_void_p * 8), ("n", ctypes.c_uint64), ("stride", ctypes.c_uint32),
+                ("stride0", ctypes.c_uint32)]
+
+
+class DevBuckets(ctypes.Structure):
+    """cdb_dev_buckets: a bucket-layout result's directory (library-owned)."""
+    _fields_ = [("nb", ctypes.c_uint64), ("first", ctypes.c_void_p * 3), ("count", ctypes.c_void_p * 3),
+                ("dense", ctypes.c_void_p * 3)]
 
 
 MAX_RUNS = 64
@@ -183,7 +194,7 @@ class DevInput(ctypes.Structure):
 
 class DevOutput(ctypes.Structure):
     _fields_ = [("keys", DevRows), ("nodes", DevRows), ("members", DevRows), ("compact", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("reserved", ctypes.c_uint32), ("buckets", DevBuckets)]
 
 
 class ExchangeStats(ctypes.Structure):
@@ -219,7 +230,8 @@ ABI_FUNCTIONS = (
     "cdb_encode_snapshot", "cdb_crc64_gpu", "cdb_upload_batches", "cdb_decode_snapshots_device",
     "cdb_decode_ops_gpu", "cdb_ops_column", "cdb_snapshot_index_selftest", "cdb_merge_into",
     "cdb_merged_from_device", "cdb_dev_state_rows", "cdb_ctx_create_multi", "cdb_ctx_device_count",
-    "cdb_ctx_shard", "cdb_merge_sharded")
+    "cdb_ctx_shard", "cdb_merge_sharded", "cdb_dev_rows_alloc_records", "cdb_dev_output_compact",
+    "cdb_dev_input_append")
 
 _lib = None
 
@@ -266,6 +278,9 @@ def lib():
         "cdb_merged_free": (None, [vp]),
         "cdb_free": (None, [vp]),
         "cdb_dev_rows_alloc": (c_st, [vp, P(DevRows), ctypes.c_uint64, ctypes.c_int]),
+        "cdb_dev_rows_alloc_records": (c_st, [vp, P(DevRows), ctypes.c_uint64, ctypes.c_int]),
+        "cdb_dev_output_compact": (c_st, [vp, P(DevOutput), P(DevOutput), vp]),
+        "cdb_dev_input_append": (c_st, [vp, P(DevInput), P(DevInput), ctypes.c_uint32, vp]),
         "cdb_dev_rows_release": (None, [vp, P(DevRows)]),
         "cdb_merge_device": (c_st, [vp, P(DevInput), P(MergeOpts), P(DevOutput), P(MergeStats), vp]),
         "cdb_partition_owner": (c_st, [vp, P(DevRows), ctypes.c_int, ctypes.c_int, P(DevRows), P(ctypes.c_uint64), vp]),
@@ -446,11 +461,12 @@ def decode_snapshot_gpu(ctx: "Context", data: bytes, reference_checksum: bool = 
 
 
 def decode_snapshots_device(ctx: "Context", snaps, reference_checksum: bool = False,
-                            timing: Optional[dict] = None):
+                            timing: Optional[dict] = None, records: bool = False):
     """GPU decode of several snapshots straight into HBM (cdb_decode_snapshots_device):
     returns (batches, DevInput) -- the rows of snapshot i at fold position i in one set of
     device columns (release each family with cdb_dev_rows_release), each batch holding the
-    host side (bytes, references, header). Errors are raised for the failing snapshot."""
+    host side (bytes, references, header). Errors are raised for the failing snapshot. records: the rows
+    in the records layout (cdb_dev_rows.stride) instead of columns."""
     n = len(snaps)
     datas = [bytes(x) for x in snaps]
     bufs = (ctypes.c_char_p * max(n, 1))(*datas)
@@ -460,7 +476,7 @@ def decode_snapshots_device(ctx: "Context", snaps, reference_checksum: bool = Fa
     failed = ctypes.c_uint32()
     off = ctypes.c_size_t()
     ims, dms = ctypes.c_double(), ctypes.c_double()
-    flags = DECODE_REFERENCE_CHECKSUM if reference_checksum else 0
+    flags = (DECODE_REFERENCE_CHECKSUM if reference_checksum else 0) | (DECODE_ROWS_RECORDS if records else 0)
     st = lib().cdb_decode_snapshots_device(ctx.handle, bufs, lens, n, flags, hs, ctypes.byref(din),
                                            ctypes.byref(failed), ctypes.byref(off), ctypes.byref(ims),
                                            ctypes.byref(dms))

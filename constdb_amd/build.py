@@ -13,20 +13,20 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libcdbmerge.so")
 OBJ = os.path.join(HERE, "build", "obj")
 SOURCES = ["engine.hip", "gen_device.hip", "decode_gpu.hip", "ops_apply.hip", "ops_gpu.hip", "encode_gpu.hip", "shard.hip",
-           "group.cpp", "capi.cpp", "decode.cpp", "gen.cpp", "ops.cpp"]
+           "capi.cpp", "decode.cpp", "gen.cpp", "ops.cpp"]
 HEADERS = ["common.h", "batch.h", "engine.h", "partition.hip.h", "bucket.hip.h", "bucket_wave.hip.h",
-           "gen_model.h", "ops.h", "runs.hip.h", "hot.hip.h", "radix.hip.h", "tile.hip.h"]
+           "gen_model.h", "ops.h", "runs.hip.h", "hot.hip.h", "radix.hip.h"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
          "-Wno-unused-variable", "-Wno-unused-value", "-I/opt/rocm/include"]
 LIBS = ["-ldl"]
 
 
 def _sources():
-    return [f for f in SOURCES if os.path.exists(os.path.join(CSRC, f))]
+    return list(SOURCES)
 
 
 def _deps_time():
-    deps = [os.path.join(CSRC, f) for f in HEADERS if os.path.exists(os.path.join(CSRC, f))]
+    deps = [os.path.join(CSRC, f) for f in HEADERS]
     deps.append(os.path.join(HERE, "..", "include", "cdb_merge.h"))
     deps.append(os.path.abspath(__file__))
     return max(os.path.getmtime(d) for d in deps)

@@ -135,6 +135,9 @@ struct RunView {
   const uint64_t* kin[kKeyCols];
   const uint64_t* nin[kNodeCols];
   const uint64_t* min[kMemberCols];
+  uint32_t ks, ns, ms;        // record strides of the families (1: plain columns; common.h row_field)
+  uint32_t staged;            // records layout of every family: a bucket's record bytes go to LDS
+                              // in 16-B pieces (load_runs_staged)
 };
 
 struct WaveArgs {

@@ -586,7 +586,21 @@ cdb_status cdb_merged_from_device(cdb_ctx* ctx, cdb_merged* state, cdb_batch* co
     if (!inputs[i]) return CDB_BAD_ARGUMENT;
   hipSetDevice(ctx->device);
   auto m = std::make_unique<cdb_merged>();
-  cdb_status st = download_result(ctx, *dout, m.get());
+  cdb_status st = CDB_OK;
+  if (dout->compact) {
+    st = download_result(ctx, *dout, m.get());
+  } else {  // the bucket layout: compacted into temporary columns first
+    cdb_dev_output dense;
+    std::memset(&dense, 0, sizeof dense);
+    st = cdb_dev_rows_alloc(ctx, &dense.keys, dout->keys.n, kKeyOutCols);
+    if (st == CDB_OK) st = cdb_dev_rows_alloc(ctx, &dense.nodes, dout->nodes.n, kNodeCols);
+    if (st == CDB_OK) st = cdb_dev_rows_alloc(ctx, &dense.members, dout->members.n, kMemberCols);
+    if (st == CDB_OK) st = cdb_dev_output_compact(ctx, dout, &dense, nullptr);
+    if (st == CDB_OK) st = download_result(ctx, dense, m.get());
+    cdb_dev_rows_release(ctx, &dense.keys);
+    cdb_dev_rows_release(ctx, &dense.nodes);
+    cdb_dev_rows_release(ctx, &dense.members);
+  }
   if (st != CDB_OK) return st;
   if (state) flatten_onto(m.get(), *state, n);
   for (uint32_t i = 0; i < n; ++i) m->inputs.push_back(inputs[i]->b);

@@ -60,6 +60,13 @@ CDB_HD uint64_t cref_pack(uint64_t begin, uint64_t count) {
   return (begin << 24) | (count & 0xFFFFFF);
 }
 
+// Input rows come in two layouts (cdb_dev_rows.stride): plain columns, or the (parent) key-hash
+// column col[0] plus one record of s = ncols - 1 words per row (col[c] = col[1] + c - 1). Field c
+// of row i in either (s = 1 for columns).
+CDB_HD uint64_t row_field(const uint64_t* const* col, uint32_t s, int c, uint64_t i) {
+  return col[c][c ? i * s : i];
+}
+
 // ---------------------------------------------------------------- hashing
 // splitmix64 finalizer: full-avalanche 64-bit mix.
 CDB_HD uint64_t mix64(uint64_t x) {

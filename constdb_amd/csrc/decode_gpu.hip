@@ -87,7 +87,12 @@ struct DecArgs {
   ulonglong2 *mref, *mvref;          // Batch::m_ref / m_vref
   uint32_t pos;                     // fold position stamped into meta (device-resident emit)
   const uint32_t* dest;             // device-resident emit: key row of entry i (null: row i)
+  uint32_t ks, cs;                  // record strides of k / nd, mb (1: columns; the records layout of
+                                    // cdb_dev_rows: field c >= 1 of row r at col[c][r * stride])
 };
+__device__ __forceinline__ uint64_t& dcell(uint64_t* const* col, uint32_t s, int c, uint64_t r) {
+  return col[c][c ? r * s : r];
+}
 
 struct Head {  // the part of a DATAS entry before the payload
   Span key;
@@ -200,11 +205,11 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
     const Span key = rd_span(p, o);
     const uint64_t t = (uint64_t)rd_int(p, o);
     const Hash128 h = hash_bytes(p + key.off, key.len, kDomainKey);
-    A.k[0][kr] = h.h;
-    A.k[1][kr] = h.f;
-    A.k[2][kr] = t;
-    A.k[3][kr] = A.k[4][kr] = A.k[5][kr] = 0;
-    A.k[6][kr] = meta_pack(A.kind[i] == 1 ? TAG_EXPIRE : TAG_DELETE, A.pos, i);
+    dcell(A.k, A.ks, 0, kr) = h.h;
+    dcell(A.k, A.ks, 1, kr) = h.f;
+    dcell(A.k, A.ks, 2, kr) = t;
+    dcell(A.k, A.ks, 3, kr) = dcell(A.k, A.ks, 4, kr) = dcell(A.k, A.ks, 5, kr) = 0;
+    dcell(A.k, A.ks, 6, kr) = meta_pack(A.kind[i] == 1 ? TAG_EXPIRE : TAG_DELETE, A.pos, i);
     A.kref[i] = make_ulonglong2(key.off, key.len);
     A.vref[i] = make_ulonglong2(0, 0);
     return;
@@ -234,12 +239,12 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
         (void)rd_int(p, r);
       }
       if (later) continue;
-      A.nd[0][row] = h.h;
-      A.nd[1][row] = h.f;
-      A.nd[2][row] = id;
-      A.nd[3][row] = v;
-      A.nd[4][row] = t;
-      A.nd[5][row] = meta_pack(0, A.pos, row);
+      dcell(A.nd, A.cs, 0, row) = h.h;
+      dcell(A.nd, A.cs, 1, row) = h.f;
+      dcell(A.nd, A.cs, 2, row) = id;
+      dcell(A.nd, A.cs, 3, row) = v;
+      dcell(A.nd, A.cs, 4, row) = t;
+      dcell(A.nd, A.cs, 5, row) = meta_pack(0, A.pos, row);
       ++row;
     }
   } else if ((hd.tag == TAG_SET || hd.tag == TAG_DICT) && A.mcount[i] != kHostTier) {
@@ -264,24 +269,24 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
       if (dict && j < na) v = rd_span(p, q);
       if (!((keep >> j) & 1)) continue;
       const Hash128 mh = hash_bytes(p + m.off, m.len, kDomainMember);
-      A.mb[0][row] = h.h;
-      A.mb[1][row] = h.f;
-      A.mb[2][row] = mh.h;
-      A.mb[3][row] = mh.f;
-      A.mb[4][row] = t;
-      A.mb[5][row] = meta_pack(j < na ? KIND_ADD : KIND_DEL, A.pos, row);
+      dcell(A.mb, A.cs, 0, row) = h.h;
+      dcell(A.mb, A.cs, 1, row) = h.f;
+      dcell(A.mb, A.cs, 2, row) = mh.h;
+      dcell(A.mb, A.cs, 3, row) = mh.f;
+      dcell(A.mb, A.cs, 4, row) = t;
+      dcell(A.mb, A.cs, 5, row) = meta_pack(j < na ? KIND_ADD : KIND_DEL, A.pos, row);
       A.mref[row] = make_ulonglong2(m.off, m.len);
       A.mvref[row] = make_ulonglong2(v.off, v.len);
       ++row;
     }
   }
-  A.k[0][kr] = h.h;
-  A.k[1][kr] = h.f;
-  A.k[2][kr] = hd.ct;
-  A.k[3][kr] = hd.ut;
-  A.k[4][kr] = hd.dt;
-  A.k[5][kr] = aux;
-  A.k[6][kr] = meta_pack(hd.tag, A.pos, i);
+  dcell(A.k, A.ks, 0, kr) = h.h;
+  dcell(A.k, A.ks, 1, kr) = h.f;
+  dcell(A.k, A.ks, 2, kr) = hd.ct;
+  dcell(A.k, A.ks, 3, kr) = hd.ut;
+  dcell(A.k, A.ks, 4, kr) = hd.dt;
+  dcell(A.k, A.ks, 5, kr) = aux;
+  dcell(A.k, A.ks, 6, kr) = meta_pack(hd.tag, A.pos, i);
   A.kref[i] = make_ulonglong2(hd.key.off, hd.key.len);
   A.vref[i] = make_ulonglong2(val.off, val.len);
 }
@@ -557,7 +562,8 @@ class GpuDecode {
   // everything after it (returns the index pass's status when the device part succeeds)
   int prepare_device(size_t* err_off);
   cdb_status emit_host(DecodeTiming* tm);
-  cdb_status emit_device(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t pos, bool run,
+  cdb_status emit_device(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t ks, uint32_t cs,
+                         uint32_t pos, bool run,
                          DecodeTiming* tm);
   // key-hash order (after prepare_device): queues the key-hash pass and the sections' order check
   // on the context's stream; the verdict reads after a synchronisation (read_order).
@@ -1062,6 +1068,7 @@ cdb_status GpuDecode::emit_host(DecodeTiming* tm) {
   uint64_t* const w0 = w;
   auto align16 = [&]() { w += (w - w0) & 1; };  // reference pairs are 16-B stores
   for (int c = 0; c < 7; ++c, w += n) A.k[c] = w;
+  A.ks = A.cs = 1;  // (the host batch's columns)
   align16();
   A.kref = (ulonglong2*)w; w += 2 * n;
   A.vref = (ulonglong2*)w; w += 2 * n;
@@ -1160,8 +1167,32 @@ cdb_status GpuDecode::order_check() {
   return st_;
 }
 
-cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t pos,
-                                  bool run, DecodeTiming* tm) {
+// Host-decoded child rows [at, at + n) of a 6-field family into device rows: one upload per column,
+// or (records, stride s) the hash column and the interleaved records.
+template <typename Val>
+static void up_rows(std::vector<ColVec>& up, std::vector<HostSeg>& segs, uint64_t* const* dst, uint32_t s,
+                    uint64_t at, uint64_t n, Val&& val) {
+  if (s <= 1) {
+    for (int c = 0; c < 6; ++c) {
+      up.emplace_back(n);
+      ColVec& v = up.back();
+      for (uint64_t j = 0; j < n; ++j) v[j] = val(c, j);
+      segs.push_back({v.data(), dst[c] + at, n * 8});
+    }
+    return;
+  }
+  up.emplace_back(n);
+  for (uint64_t j = 0; j < n; ++j) up.back()[j] = val(0, j);
+  segs.push_back({up.back().data(), dst[0] + at, n * 8});
+  up.emplace_back(n * s);
+  ColVec& r = up.back();
+  for (uint64_t j = 0; j < n; ++j)
+    for (int c = 1; c < 6; ++c) r[j * s + (c - 1)] = val(c, j);
+  segs.push_back({r.data(), dst[1] + at * s, n * s * 8});
+}
+
+cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t ks,
+                                  uint32_t cs, uint32_t pos, bool run, DecodeTiming* tm) {
   out_->rows_on_device = true;
   out_->dev_rows[0] = n_;
   out_->dev_rows[1] = nn_;
@@ -1184,6 +1215,8 @@ cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint6
   A.mref = (ulonglong2*)w; w += 2 * nm;
   A.mvref = (ulonglong2*)w; w += 2 * nm;
   A.pos = pos;
+  A.ks = ks;
+  A.cs = cs;
   A.dest = nullptr;
   if (run && n > 1 && sec_.b[1] != n) {  // side sections to merge into the DATAS order
     const uint64_t* kh = (const uint64_t*)d_ord_.p;
@@ -1204,22 +1237,15 @@ cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint6
     const uint64_t nr = r.n_pkh.size(), mr = r.m_pkh.size();
     if (nr) {
       const ColVec* src[6] = {&r.n_pkh, &r.n_pkf, &r.n_node, &r.n_v, &r.n_t, nullptr};
-      for (int c = 0; c < 6; ++c) {
-        up.emplace_back(nr);
-        ColVec& v = up.back();
-        for (uint64_t j = 0; j < nr; ++j) v[j] = c < 5 ? (*src[c])[j] : meta_pack(0, pos, noff_[he.i] + j);
-        segs.push_back({v.data(), nd[c] + noff_[he.i], nr * 8});
-      }
+      auto val = [&](int c, uint64_t j) { return c < 5 ? (*src[c])[j] : meta_pack(0, pos, noff_[he.i] + j); };
+      up_rows(up, segs, nd, cs, noff_[he.i], nr, val);
     }
     if (mr) {
       const ColVec* src[6] = {&r.m_pkh, &r.m_pkf, &r.m_h, &r.m_f, &r.m_t, nullptr};
-      for (int c = 0; c < 6; ++c) {
-        up.emplace_back(mr);
-        ColVec& v = up.back();
-        for (uint64_t j = 0; j < mr; ++j)
-          v[j] = c < 5 ? (*src[c])[j] : meta_pack(meta_tag(r.m_meta[j]), pos, moff_[he.i] + j);
-        segs.push_back({v.data(), mb[c] + moff_[he.i], mr * 8});
-      }
+      auto val = [&](int c, uint64_t j) {
+        return c < 5 ? (*src[c])[j] : meta_pack(meta_tag(r.m_meta[j]), pos, moff_[he.i] + j);
+      };
+      up_rows(up, segs, mb, cs, moff_[he.i], mr, val);
     }
   }
   if (!segs.empty() && (st_ = staged_copy(ctx_, segs.data(), segs.size(), true, s)) != CDB_OK) return st_;
@@ -1373,9 +1399,12 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     for (uint32_t i = 0; i < n; ++i) runs = runs && dec[i]->read_order();
   }
   std::memset(din, 0, sizeof *din);
-  if ((st = cdb_dev_rows_alloc(ctx, &din->keys, tot[0], kKeyCols)) != CDB_OK ||
-      (st = cdb_dev_rows_alloc(ctx, &din->nodes, tot[1], kNodeCols)) != CDB_OK ||
-      (st = cdb_dev_rows_alloc(ctx, &din->members, tot[2], kMemberCols)) != CDB_OK) {
+  const bool rec = flags & CDB_DECODE_ROWS_RECORDS;
+  auto alloc = [&](cdb_dev_rows* r, uint64_t rows, int nc) {
+    return rec ? cdb_dev_rows_alloc_records(ctx, r, rows, nc) : cdb_dev_rows_alloc(ctx, r, rows, nc);
+  };
+  if ((st = alloc(&din->keys, tot[0], kKeyCols)) != CDB_OK || (st = alloc(&din->nodes, tot[1], kNodeCols)) != CDB_OK ||
+      (st = alloc(&din->members, tot[2], kMemberCols)) != CDB_OK) {
     cdb_dev_rows_release(ctx, &din->keys);
     cdb_dev_rows_release(ctx, &din->nodes);
     cdb_dev_rows_release(ctx, &din->members);
@@ -1386,13 +1415,15 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     uint64_t* k[kKeyCols];
     uint64_t* nd[kNodeCols];
     uint64_t* mb[kMemberCols];
-    for (int c = 0; c < kKeyCols; ++c) k[c] = din->keys.col[c] + o[0];
-    for (int c = 0; c < kNodeCols; ++c) nd[c] = din->nodes.col[c] + o[1];
-    for (int c = 0; c < kMemberCols; ++c) mb[c] = din->members.col[c] + o[2];
+    // (records: field c >= 1 of row r at col[c][r * stride], so the offset scales by the stride)
+    const uint64_t ks = std::max<uint32_t>(din->keys.stride, 1), cs = std::max<uint32_t>(din->nodes.stride, 1);
+    for (int c = 0; c < kKeyCols; ++c) k[c] = din->keys.col[c] + o[0] * (c ? ks : 1);
+    for (int c = 0; c < kNodeCols; ++c) nd[c] = din->nodes.col[c] + o[1] * (c ? cs : 1);
+    for (int c = 0; c < kMemberCols; ++c) mb[c] = din->members.col[c] + o[2] * (c ? cs : 1);
     DecodeTiming t1;
     if (runs)
       for (int f = 0; f < 3; ++f) din->run_start[f][i] = o[f];
-    if ((st = dec[i]->emit_device(k, nd, mb, i, runs, &t1)) != CDB_OK) {
+    if ((st = dec[i]->emit_device(k, nd, mb, (uint32_t)ks, (uint32_t)cs, i, runs, &t1)) != CDB_OK) {
       cdb_dev_rows_release(ctx, &din->keys);
       cdb_dev_rows_release(ctx, &din->nodes);
       cdb_dev_rows_release(ctx, &din->members);

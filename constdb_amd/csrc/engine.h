@@ -59,6 +59,7 @@ enum WsSlot {
   WS_YK, WS_YN, WS_YM,                                  // sharded merge: this device's output rows
   WS_PK, WS_PN, WS_PM,                                  // sharded merge: owner-packed rows (inputs not in runs)
   WS_SPLIT,                                             // sharded merge: owner splits of the runs
+  WS_STATE,                                             // cdb_dev_state_rows: zero bases, error word
   WS_COUNT
 };
 static_assert(WS_COUNT <= 48, "cdb_ctx::ws has 48 slots");

@@ -110,12 +110,12 @@ __global__ void iota_kernel(uint32_t* p, uint64_t n) {
     p[i] = (uint32_t)i;
 }
 
-__global__ void gc_lastbad_kernel(const uint64_t* __restrict__ ct, const uint64_t* __restrict__ meta, uint64_t n,
-                                  uint64_t wm, unsigned long long* out) {
+__global__ void gc_lastbad_kernel(const uint64_t* __restrict__ ct, const uint64_t* __restrict__ meta, uint32_t stride,
+                                  uint64_t n, uint64_t wm, unsigned long long* out) {
   uint64_t best = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t m = meta[i];
-    if (meta_tag(m) == TAG_DELETE && ct[i] > wm) best = max(best, meta_order(m) + 1);
+    const uint64_t m = meta[i * stride];
+    if (meta_tag(m) == TAG_DELETE && ct[i * stride] > wm) best = max(best, meta_order(m) + 1);
   }
   for (int o = 32; o > 0; o >>= 1) best = max(best, (uint64_t)__shfl_xor((unsigned long long)best, o, 64));
   if ((threadIdx.x & 63) == 0 && best) atomicMax(out, (unsigned long long)best);
@@ -132,7 +132,45 @@ struct CompactArgs {
   uint32_t* err;                       // set when an index falls outside them
   const uint32_t* skip_if;             // pipelined ranges: nothing to do once a bucket went to a
                                        // workgroup tier (everything is compacted again at the end)
+  // state = 1 (cdb_dev_state_rows from the bucket layout): the destinations are the next merge's
+  // input rows -- keys kh kf ct ut dt aux meta, children unchanged, meta = tag | pos 0 | src = the
+  // dense index, aux = a counter's sum -- in columns or records (ds: record stride per family)
+  int state;
+  uint32_t ds[3];
 };
+
+// Writes dense row d of a result family as the next merge's input row (position 0): the reference
+// merges peer snapshots into its live server.db (replica/pull.rs:120-128, db.rs:31-43), whose rows
+// are what the previous merge produced. A counter's load-time total (aux) is its sum
+// (type_counter.rs:89-91, the result's win); src is the dense row, which resolves bytes.
+template <int FAM>
+__device__ __forceinline__ void put_state_row(uint64_t* const* dst, uint32_t ds, uint64_t d, const uint64_t* v) {
+  if constexpr (FAM == 0) {
+    const uint32_t T = meta_tag(v[O_META]);
+    const uint64_t f[kKeyCols] = {v[O_KH], v[O_KF], v[O_CT], v[O_UT], v[O_DT],
+                                  T == TAG_COUNTER ? v[O_WIN] : 0, meta_pack(T, 0, d)};
+#pragma unroll
+    for (int c = 0; c < kKeyCols; ++c) dst[c][c ? d * ds : d] = f[c];
+  } else {
+#pragma unroll
+    for (int c = 0; c < kChildStride; ++c)
+      dst[c][c ? d * ds : d] = c == C_META ? meta_pack(meta_tag(v[C_META]), 0, d) : v[c];
+  }
+}
+
+// The same from a dense (compacted) result: one thread per row.
+template <int FAM>
+__global__ void state_dense_kernel(const cdb_dev_rows src, cdb_dev_rows dst, uint32_t ds) {
+  constexpr int NW = FAM == 0 ? kKeyOutCols : kChildStride;
+  uint64_t* dc[8];
+  for (int c = 0; c < 8; ++c) dc[c] = dst.col[c];
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < src.n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t v[NW];
+#pragma unroll
+    for (int c = 0; c < NW; ++c) v[c] = src.col[c][i];
+    put_state_row<FAM>(dc, ds, i, v);
+  }
+}
 
 // Sparse-by-bucket outputs -> dense arrays; child ranges become absolute row indices.
 // A group of 64 consecutive buckets' dense output rows are one contiguous range (doff is an
@@ -163,6 +201,19 @@ __device__ __forceinline__ void compact_row(const CompactArgs& A, const CompactL
   const uint64_t dst = A.base_tot[FAM] + d0 + t;
   if (src >= A.cap[FAM] || dst >= A.cap[FAM]) {  // a broken directory: report, never touch memory
     atomicOr(A.err, 1u);
+    return;
+  }
+  if (A.state) {
+    constexpr int NW = FAM == 0 ? kKeyOutCols : kChildStride;
+    uint64_t v[NW];
+    const ulonglong2* row = (const ulonglong2*)((FAM == 0 ? A.ks : FAM == 1 ? A.ns : A.ms) + (uint64_t)src * NW);
+#pragma unroll
+    for (int c = 0; c < NW / 2; ++c) {
+      const ulonglong2 q = row[c];
+      v[2 * c] = q.x;
+      v[2 * c + 1] = q.y;
+    }
+    put_state_row<FAM>(FAM == 0 ? A.kd : FAM == 1 ? A.nd : A.md, A.ds[FAM], dst, v);
     return;
   }
   if constexpr (FAM == 0) {
@@ -377,7 +428,7 @@ Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
 // last level writes only `perm`, so bucket b's rows are rows[perm[base[b] .. base[b] +
 // hist[b])]. Returns the row buffer in `rows` and the other ping-pong buffer in `spare`.
 template <int NC, int W>
-cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const Plan& plan, int shift,
+cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint32_t in_stride, uint64_t n, const Plan& plan, int shift,
                             uint64_t* const* A, uint64_t* const* Bf, const Dir& d, uint64_t** rows,
                             uint64_t** spare, uint64_t* khcol, uint32_t* perm, hipStream_t s,
                             int scan_slot) {
@@ -417,9 +468,11 @@ cdb_status partition_family(cdb_ctx* ctx, uint64_t* const* in, uint64_t n, const
       CDB_TRY(launch_check(ctx, s, "partition (index level)"));
     } else {
       ColSet<NC> ci, co;
-      for (int c = 0; c < NC; ++c) {
+      for (int c = 0; c < NC; ++c) {  // the caller's rows (level 0) may be records, the workspace's are columns
         ci.c[c] = cur[c];
+        ci.s[c] = (cur == in && c) ? in_stride : 1;
         co.c[c] = dst[c];
+        co.s[c] = 1;
       }
       if (kind == 1) {
         // before a per-segment final level, leave each row's u16 digit in place of the key hash
@@ -458,11 +511,43 @@ cdb_status state_rows(cdb_ctx* ctx, uint64_t* meta, uint64_t* aux, uint64_t n, h
 }
 
 namespace {
+// The input families' layouts (cdb_dev_rows.stride): plain columns, or the hash column + records
+// of ncols - 1 words. staged: every family is in records with 16-B aligned record arrays, so the
+// sorted-run wave kernel copies a bucket's record bytes to LDS in 16-B pieces (runs.hip.h).
+struct InLayout {
+  uint32_t ks = 1, ns = 1, ms = 1;
+  bool staged = false;
+};
+cdb_status input_layout(cdb_ctx* ctx, const cdb_dev_input* in, InLayout* lay) {
+  const cdb_dev_rows* fam[3] = {&in->keys, &in->nodes, &in->members};
+  const int ncols[3] = {kKeyCols, kNodeCols, kMemberCols};
+  uint32_t* out[3] = {&lay->ks, &lay->ns, &lay->ms};
+  bool staged = true;
+  for (int f = 0; f < 3; ++f) {
+    const cdb_dev_rows& r = *fam[f];
+    if (r.stride0 > 1) return fail(ctx, CDB_BAD_ARGUMENT, "input rows: col[0] must be a plain column (stride0 0 or 1)");
+    if (r.stride <= 1) {
+      *out[f] = 1;
+      staged = staged && r.n == 0;
+      continue;
+    }
+    if (r.stride != (uint32_t)(ncols[f] - 1))
+      return fail(ctx, CDB_BAD_ARGUMENT, "input rows: records layout needs stride = ncols - 1 (6 keys, 5 children)");
+    for (int c = 2; c < ncols[f]; ++c)
+      if (r.n && r.col[c] != r.col[1] + (c - 1))
+        return fail(ctx, CDB_BAD_ARGUMENT, "input rows: records layout needs col[c] = col[1] + c - 1");
+    *out[f] = r.stride;
+    staged = staged && (r.n == 0 || ((uintptr_t)r.col[1] & 15) == 0);
+  }
+  lay->staged = staged;
+  return CDB_OK;
+}
+
 // Sorted-run input: checks the caller's run bounds, builds the run directories (run_mark_kernel)
 // and, when every run really is ordered, the bucket directories of the three families. *ok =
 // false sends the merge to the partition path (a run that decreases somewhere).
-cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, uint64_t nb, int shift, const Dir* dirs,
-                          RunView* V, bool* ok, hipStream_t s) {
+cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, const InLayout& lay, uint64_t nb, int shift,
+                          const Dir* dirs, RunView* V, bool* ok, hipStream_t s) {
   *ok = false;
   const uint32_t nr = in->n_runs;
   if (nr > (uint32_t)kMaxRuns) return fail(ctx, CDB_BAD_ARGUMENT, "n_runs > 64");
@@ -540,6 +625,10 @@ cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, uint64_t nb, in
   V->rbase = d_rbase;
   V->nr = nr;
   V->nbp1 = (uint32_t)row;
+  V->ks = lay.ks;
+  V->ns = lay.ns;
+  V->ms = lay.ms;
+  V->staged = lay.staged ? 1 : 0;
   for (int c = 0; c < kKeyCols; ++c) V->kin[c] = in->keys.col[c];
   for (int c = 0; c < kNodeCols; ++c) {
     V->nin[c] = in->nodes.col[c];
@@ -805,6 +894,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     return fail(ctx, CDB_BAD_ARGUMENT, "row counts must be < 2^32 per family per device");
   const uint32_t flags = opts ? opts->flags : 0;
   const uint64_t wm = opts ? opts->gc_watermark : 0;
+  InLayout lay;
+  CDB_TRY(input_layout(ctx, in, &lay));
   const Plan plan = make_plan(K, N, M);
   const int shift = opts ? (int)opts->key_shift : 0;
   if (shift < 0 || shift > 16) return fail(ctx, CDB_BAD_ARGUMENT, "key_shift");
@@ -873,7 +964,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   bool use_runs = false;
   if (in->n_runs) {
     const Dir dirs[3] = {dk, dnd, dm};
-    CDB_TRY(runs_directory(ctx, in, nb, shift, dirs, &RV, &use_runs, s));
+    CDB_TRY(runs_directory(ctx, in, lay, nb, shift, dirs, &RV, &use_runs, s));
   }
   if (use_runs) {  // rows stay in the runs; KA/NA/MA take the rows of the workgroup tiers
     krows = KA[0];
@@ -893,11 +984,11 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   CDB_HIP(hipEventRecord(ctx->ev_pfork, s), "event");
   CDB_HIP(hipStreamWaitEvent(sn, ctx->ev_pfork, 0), "wait");
   CDB_HIP(hipStreamWaitEvent(sm, ctx->ev_pfork, 0), "wait");
-  CDB_TRY(partition_family<kKeyCols, kKeyStride>(ctx, kin, K, plan, shift, KA, KB, dk, &krows, ksp, khcol, kperm, s,
-                                                 WS_SCAN));
-  CDB_TRY(partition_family<kNodeCols, kChildStride>(ctx, nin, N, plan, shift, NA, NB, dnd, &nrows, nsp, khcol + K,
-                                                    nperm, sn, WS_SCAN2));
-  CDB_TRY(partition_family<kMemberCols, kChildStride>(ctx, min_, M, plan, shift, MA, MBf, dm, &mrows, msp,
+  CDB_TRY(partition_family<kKeyCols, kKeyStride>(ctx, kin, lay.ks, K, plan, shift, KA, KB, dk, &krows, ksp, khcol,
+                                                 kperm, s, WS_SCAN));
+  CDB_TRY(partition_family<kNodeCols, kChildStride>(ctx, nin, lay.ns, N, plan, shift, NA, NB, dnd, &nrows, nsp,
+                                                    khcol + K, nperm, sn, WS_SCAN2));
+  CDB_TRY(partition_family<kMemberCols, kChildStride>(ctx, min_, lay.ms, M, plan, shift, MA, MBf, dm, &mrows, msp,
                                                       khcol + K + N, mperm, sm, WS_SCAN3));
   CDB_HIP(hipEventRecord(ctx->ev_pn, sn), "event");
   CDB_HIP(hipEventRecord(ctx->ev_pm, sm), "event");
@@ -912,7 +1003,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   CDB_HIP(hipEventRecord(ctx->ev_part, s), "event");
   // ---- 2. GC watermark scan (DB::gc's LIFO stop point)
   if ((flags & CDB_MERGE_GC_DELETES) && K) {
-    gc_lastbad_kernel<<<1024, 256, 0, s>>>(in->keys.col[K_CT], in->keys.col[K_META], K, wm, d_last_bad);
+    gc_lastbad_kernel<<<1024, 256, 0, s>>>(in->keys.col[K_CT], in->keys.col[K_META], lay.ks, K, wm, d_last_bad);
     CDB_TRY(launch_check(ctx, s, "gc_lastbad"));
   }
 
@@ -969,9 +1060,11 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   // A bucket beyond the wide tier's capacity goes to a workgroup tier, which adds outputs after
   // every range, so the range compactions would stand down and only their scans would run (C5:
   // 24 idle scans per step): such merges run as one range (one flag read before the bucket phase).
+  // The bucket layout (out->compact == 0) has no compaction to overlap: one range.
   constexpr uint32_t kPipeRanges = 8;
-  const uint32_t pipe_opt = opts ? opts->pipe_ranges : 0;
-  bool pipe_auto = !(K + N + M < (64ull << 20) || nb < 64ull * kPipeRanges);
+  const bool dense_out = out->compact != 0;
+  const uint32_t pipe_opt = (opts && dense_out) ? opts->pipe_ranges : 0;
+  bool pipe_auto = dense_out && !(K + N + M < (64ull << 20) || nb < 64ull * kPipeRanges);
   if (!pipe_opt && pipe_auto) {
     uint32_t* d_over = (uint32_t*)(misc + 112);  // zeroed with the misc header
     beyond_wide_kernel<<<(uint32_t)std::min<uint64_t>((nb + 255) / 256, 4096), 256, 0, s>>>(A, (uint32_t)nb, d_over);
@@ -1004,6 +1097,8 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   uint32_t* d_cerr_p = (uint32_t*)(misc + 108);  // the pipelined compaction's
   C.err = d_cerr;
   C.skip_if = nullptr;
+  C.state = 0;
+  C.ds[0] = C.ds[1] = C.ds[2] = 1;
   uint64_t* d_pipe = nullptr;  // [P + 1][3] dense bases | [P][3] range totals
   hipStream_t ws = ctx->side;
   hipStream_t cs = ctx->side2;
@@ -1135,12 +1230,14 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dk.out, nb, dk.doff, (uint32_t*)nullptr, d_totals + 0, s));
     CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dnd.out, nb, dnd.doff, (uint32_t*)nullptr, d_totals + 1, s));
     CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dm.out, nb, dm.doff, (uint32_t*)nullptr, d_totals + 2, s));
+  }
+  if (recompact && dense_out) {
     // one wave per 4096 output rows of a family (the kernel strides over any excess)
     const uint64_t tasks = (K + N + M) / kCompactChunk + 3;
     compact_kernel<<<(uint32_t)std::min<uint64_t>((tasks + kCompactWaves - 1) / kCompactWaves, 65536),
                      64 * kCompactWaves, 0, s>>>(C, (uint32_t)nb);
     CDB_TRY(launch_check(ctx, s, "compact_kernel"));
-  } else {
+  } else if (!recompact) {  // the pipelined ranges compacted everything: their totals
     CDB_HIP(hipMemcpyAsync(d_totals, d_pipe + 3 * P, 3 * sizeof(uint64_t), hipMemcpyDeviceToDevice, s), "d2d");
     CDB_HIP(hipMemcpyAsync(d_cerr, d_cerr_p, sizeof(uint32_t), hipMemcpyDeviceToDevice, s), "d2d");
   }
@@ -1157,6 +1254,21 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   CDB_HIP(hipMemcpyAsync(&cerr, d_cerr, sizeof cerr, hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipStreamSynchronize(s), "sync");
   if (cerr) return fail(ctx, CDB_DEVICE_ERROR, "compaction: a source or destination row fell outside the family's rows");
+  if (!dense_out) {  // the bucket layout: the rows stay in their slots, the directory says where
+    const Dir* dd[3] = {&dk, &dnd, &dm};
+    cdb_dev_rows* fam[3] = {&out->keys, &out->nodes, &out->members};
+    uint64_t* base[3] = {ksp[0], nsp[0], msp[0]};
+    for (int f = 0; f < 3; ++f) {
+      std::memset(fam[f], 0, sizeof *fam[f]);
+      const int w = f == 0 ? kKeyOutCols : kChildStride;
+      for (int c = 0; c < w; ++c) fam[f]->col[c] = base[f] + c;
+      fam[f]->stride = fam[f]->stride0 = (uint32_t)w;
+      out->buckets.first[f] = dd[f]->base;
+      out->buckets.count[f] = dd[f]->out;
+      out->buckets.dense[f] = dd[f]->doff;
+    }
+    out->buckets.nb = nb;
+  }
   out->keys.n = totals[0];
   out->nodes.n = totals[1];
   out->members.n = totals[2];
@@ -1258,10 +1370,28 @@ cdb_status cdb_dev_rows_alloc(cdb_ctx* ctx, cdb_dev_rows* r, uint64_t rows, int 
   hipSetDevice(ctx->device);
   const uint64_t n = std::max<uint64_t>(rows, 1);
   uint64_t* p = nullptr;
-  cdb_status st = hip_check(ctx, hipMalloc(&p, ncols * n * sizeof(uint64_t)), "hipMalloc(rows)");
+  // (+16 B: readable up to the 16-B boundary after the last row, cdb_merge.h)
+  cdb_status st = hip_check(ctx, hipMalloc(&p, ncols * n * sizeof(uint64_t) + 16), "hipMalloc(rows)");
   if (st != CDB_OK) return st;
   for (int c = 0; c < ncols; ++c) r->col[c] = p + c * n;
   r->n = rows;
+  return CDB_OK;
+}
+
+cdb_status cdb_dev_rows_alloc_records(cdb_ctx* ctx, cdb_dev_rows* r, uint64_t rows, int ncols) {
+  std::memset(r, 0, sizeof *r);
+  if (ncols != kKeyCols && ncols != kNodeCols) return fail(ctx, CDB_BAD_ARGUMENT, "records layout: ncols 6 or 7");
+  hipSetDevice(ctx->device);
+  const uint64_t n = std::max<uint64_t>(rows, 1);
+  const uint64_t hash_words = (n + 1) & ~1ull;  // records start 16-B aligned
+  uint64_t* p = nullptr;
+  cdb_status st =
+      hip_check(ctx, hipMalloc(&p, (hash_words + (uint64_t)(ncols - 1) * n) * sizeof(uint64_t) + 16), "hipMalloc(rows)");
+  if (st != CDB_OK) return st;
+  r->col[0] = p;
+  for (int c = 1; c < ncols; ++c) r->col[c] = p + hash_words + (c - 1);
+  r->n = rows;
+  r->stride = (uint32_t)(ncols - 1);
   return CDB_OK;
 }
 
@@ -1290,15 +1420,30 @@ cdb_status cdb_partition_owner(cdb_ctx* ctx, const cdb_dev_rows* in, int ncols, 
     CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, hist, nb, base, cursor, nullptr, s));
     if (ncols == 6) {
       ColSet<6> ci, co;
-      for (int c = 0; c < 6; ++c) { ci.c[c] = in->col[c]; co.c[c] = out->col[c]; }
+      for (int c = 0; c < 6; ++c) {
+        ci.c[c] = in->col[c];
+        ci.s[c] = c ? std::max<uint32_t>(in->stride, 1) : 1;
+        co.c[c] = out->col[c];
+        co.s[c] = c ? std::max<uint32_t>(out->stride, 1) : 1;
+      }
       part_scatter_kernel<6><<<tiles, kPartThreads, 0, s>>>(ci, co, n, 1, (uint32_t)nb, 0, cursor);
     } else if (ncols == 7) {
       ColSet<7> ci, co;
-      for (int c = 0; c < 7; ++c) { ci.c[c] = in->col[c]; co.c[c] = out->col[c]; }
+      for (int c = 0; c < 7; ++c) {
+        ci.c[c] = in->col[c];
+        ci.s[c] = c ? std::max<uint32_t>(in->stride, 1) : 1;
+        co.c[c] = out->col[c];
+        co.s[c] = c ? std::max<uint32_t>(out->stride, 1) : 1;
+      }
       part_scatter_kernel<7><<<tiles, kPartThreads, 0, s>>>(ci, co, n, 1, (uint32_t)nb, 0, cursor);
     } else {
       ColSet<8> ci, co;
-      for (int c = 0; c < 8; ++c) { ci.c[c] = in->col[c]; co.c[c] = out->col[c]; }
+      for (int c = 0; c < 8; ++c) {
+        ci.c[c] = in->col[c];
+        ci.s[c] = c ? std::max<uint32_t>(in->stride, 1) : 1;
+        co.c[c] = out->col[c];
+        co.s[c] = c ? std::max<uint32_t>(out->stride, 1) : 1;
+      }
       part_scatter_kernel<8><<<tiles, kPartThreads, 0, s>>>(ci, co, n, 1, (uint32_t)nb, 0, cursor);
     }
     CDB_TRY(launch_check(ctx, s, "partition_owner"));
@@ -1318,21 +1463,170 @@ cdb_status cdb_dev_state_rows(cdb_ctx* ctx, const cdb_dev_output* state, cdb_dev
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   const cdb_dev_rows* src[3] = {&state->keys, &state->nodes, &state->members};
   cdb_dev_rows* dst[3] = {keys, nodes, members};
+  const int ncols[3] = {kKeyCols, kNodeCols, kMemberCols};
+  uint32_t ds[3];
   for (int f = 0; f < 3; ++f) {
-    const uint64_t n = src[f]->n;
-    // key out kh kf ct ut dt meta win cref -> in kh kf ct ut dt aux(<- win) meta(<- meta);
-    // children keep their six columns
-    const int map_k[7] = {O_KH, O_KF, O_CT, O_UT, O_DT, O_WIN, O_META};
-    for (int c = 0; c < (f == 0 ? kKeyCols : kNodeCols); ++c) {
-      const uint64_t* from = src[f]->col[f == 0 ? map_k[c] : c];
-      if (n && (!from || !dst[f]->col[c])) return fail(ctx, CDB_BAD_ARGUMENT, "cdb_dev_state_rows: missing column");
-      if (n && from != dst[f]->col[c])
-        CDB_HIP(hipMemcpyAsync(dst[f]->col[c], from, n * 8, hipMemcpyDeviceToDevice, s), "d2d");
-    }
-    dst[f]->n = n;
-    CDB_TRY(state_rows(ctx, dst[f]->col[f == 0 ? K_META : C_META], f == 0 ? dst[f]->col[K_AUX] : nullptr, n, s));
+    ds[f] = std::max<uint32_t>(dst[f]->stride, 1);
+    if (dst[f]->stride0 > 1 || (ds[f] > 1 && ds[f] != (uint32_t)(ncols[f] - 1)))
+      return fail(ctx, CDB_BAD_ARGUMENT, "cdb_dev_state_rows: destination rows must be columns or records");
+    for (int c = 0; c < ncols[f]; ++c)
+      if (src[f]->n && !dst[f]->col[c]) return fail(ctx, CDB_BAD_ARGUMENT, "cdb_dev_state_rows: missing column");
   }
+  if (state->compact) {
+    for (int f = 0; f < 3; ++f) {
+      const uint64_t n = src[f]->n;
+      if (n == 0) continue;
+      const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
+      if (f == 0) state_dense_kernel<0><<<blocks, 256, 0, s>>>(*src[f], *dst[f], ds[f]);
+      else state_dense_kernel<1><<<blocks, 256, 0, s>>>(*src[f], *dst[f], ds[f]);
+      CDB_TRY(launch_check(ctx, s, "state_dense_kernel"));
+    }
+  } else {
+    const cdb_dev_buckets& B = state->buckets;
+    if (B.nb == 0 || B.nb >= (1ull << 32)) return fail(ctx, CDB_BAD_ARGUMENT, "cdb_dev_state_rows: no bucket directory");
+    cdb_status st = CDB_OK;
+    uint8_t* w = (uint8_t*)ws_get(ctx, WS_STATE, 64, &st);
+    if (!w) return st;
+    CDB_HIP(hipMemsetAsync(w, 0, 64, s), "memset");
+    CompactArgs C;
+    std::memset(&C, 0, sizeof C);
+    C.ks = src[0]->col[0];
+    C.ns = src[1]->col[0];
+    C.ms = src[2]->col[0];
+    for (int c = 0; c < kKeyCols; ++c) C.kd[c] = keys->col[c];
+    for (int c = 0; c < kNodeCols; ++c) {
+      C.nd[c] = nodes->col[c];
+      C.md[c] = members->col[c];
+    }
+    C.kbase = B.first[0]; C.nbase = B.first[1]; C.mbase = B.first[2];
+    C.kout = B.count[0]; C.nout = B.count[1]; C.mout = B.count[2];
+    C.kdoff = B.dense[0]; C.ndoff = B.dense[1]; C.mdoff = B.dense[2];
+    C.base_tot = (const unsigned long long*)w;  // zero bases
+    for (int f = 0; f < 3; ++f) C.cap[f] = std::max<uint64_t>(src[f]->n, 1) + (uint64_t)UINT32_MAX;  // slots: ours
+    C.err = (uint32_t*)(w + 32);
+    C.state = 1;
+    for (int f = 0; f < 3; ++f) C.ds[f] = ds[f];
+    const uint64_t tasks = (src[0]->n + src[1]->n + src[2]->n) / kCompactChunk + 3;
+    compact_kernel<<<(uint32_t)std::min<uint64_t>((tasks + kCompactWaves - 1) / kCompactWaves, 65536),
+                     64 * kCompactWaves, 0, s>>>(C, (uint32_t)B.nb);
+    CDB_TRY(launch_check(ctx, s, "compact_kernel(state)"));
+  }
+  for (int f = 0; f < 3; ++f) dst[f]->n = src[f]->n;
   return hip_check(ctx, hipStreamSynchronize(s), "cdb_dev_state_rows");
+}
+
+namespace {
+// Appends rows of one family (any input layout) behind `at` rows of dst (any input layout), the
+// meta word's fold position raised by dpos.
+struct AppendArgs {
+  const uint64_t* src[8];
+  uint64_t* dst[8];
+  uint32_t ss, ds;  // record strides (1: columns)
+  int ncols;
+  uint64_t n, at;
+  uint32_t dpos;
+};
+__global__ void append_rows_kernel(AppendArgs a) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t d = a.at + i;
+    for (int c = 0; c < a.ncols; ++c) {
+      uint64_t v = row_field(a.src, a.ss, c, i);
+      if (c == a.ncols - 1) v = meta_pack(meta_tag(v), meta_pos(v) + a.dpos, meta_src(v));
+      a.dst[c][c ? d * a.ds : d] = v;
+    }
+  }
+}
+}  // namespace
+
+cdb_status cdb_dev_input_append(cdb_ctx* ctx, cdb_dev_input* dst, const cdb_dev_input* src, uint32_t pos_offset,
+                                void* stream) {
+  if (!ctx || !dst || !src) return CDB_BAD_ARGUMENT;
+  if (src->n_pos + pos_offset > (uint32_t)kMaxPos) return fail(ctx, CDB_BAD_ARGUMENT, "at most 63 fold positions");
+  hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  cdb_dev_rows* D[3] = {&dst->keys, &dst->nodes, &dst->members};
+  const cdb_dev_rows* S[3] = {&src->keys, &src->nodes, &src->members};
+  const int ncols[3] = {kKeyCols, kNodeCols, kMemberCols};
+  const bool runs = dst->n_runs > 0 && src->n_runs > 0 && dst->n_runs + src->n_runs <= CDB_MAX_RUNS;
+  uint64_t at[3];
+  for (int f = 0; f < 3; ++f) {
+    const uint32_t ds = std::max<uint32_t>(D[f]->stride, 1), ss = std::max<uint32_t>(S[f]->stride, 1);
+    if (D[f]->stride0 > 1 || S[f]->stride0 > 1 || (ds > 1 && ds != (uint32_t)(ncols[f] - 1)) ||
+        (ss > 1 && ss != (uint32_t)(ncols[f] - 1)))
+      return fail(ctx, CDB_BAD_ARGUMENT, "cdb_dev_input_append: rows must be columns or records");
+    at[f] = D[f]->n;
+    if (!S[f]->n) continue;
+    AppendArgs a;
+    std::memset(&a, 0, sizeof a);
+    for (int c = 0; c < ncols[f]; ++c) {
+      a.src[c] = S[f]->col[c];
+      a.dst[c] = D[f]->col[c];
+      if (!a.src[c] || !a.dst[c]) return fail(ctx, CDB_BAD_ARGUMENT, "cdb_dev_input_append: missing column");
+    }
+    a.ss = ss;
+    a.ds = ds;
+    a.ncols = ncols[f];
+    a.n = S[f]->n;
+    a.at = at[f];
+    a.dpos = pos_offset;
+    append_rows_kernel<<<(uint32_t)std::min<uint64_t>((a.n + 255) / 256, 8192), 256, 0, s>>>(a);
+    CDB_TRY(launch_check(ctx, s, "append_rows_kernel"));
+    D[f]->n += S[f]->n;
+  }
+  if (runs) {
+    for (int f = 0; f < 3; ++f)
+      for (uint32_t r = 0; r <= src->n_runs; ++r) dst->run_start[f][dst->n_runs + r] = at[f] + src->run_start[f][r];
+    dst->n_runs += src->n_runs;
+  } else {
+    dst->n_runs = 0;
+  }
+  dst->n_pos = std::max(dst->n_pos, src->n_pos + pos_offset);
+  return hip_check(ctx, hipStreamSynchronize(s), "cdb_dev_input_append");
+}
+
+cdb_status cdb_dev_output_compact(cdb_ctx* ctx, const cdb_dev_output* src, cdb_dev_output* dst, void* stream) {
+  if (!ctx || !src || !dst) return CDB_BAD_ARGUMENT;
+  if (src->compact) return fail(ctx, CDB_BAD_ARGUMENT, "cdb_dev_output_compact: the source is already dense");
+  const cdb_dev_buckets& B = src->buckets;
+  if (B.nb == 0 || B.nb >= (1ull << 32)) return fail(ctx, CDB_BAD_ARGUMENT, "cdb_dev_output_compact: no bucket directory");
+  const cdb_dev_rows* from[3] = {&src->keys, &src->nodes, &src->members};
+  cdb_dev_rows* to[3] = {&dst->keys, &dst->nodes, &dst->members};
+  for (int f = 0; f < 3; ++f)
+    for (int c = 0; c < (f == 0 ? kKeyOutCols : kChildStride); ++c)
+      if (from[f]->n && !to[f]->col[c]) return fail(ctx, CDB_BAD_ARGUMENT, "cdb_dev_output_compact: missing column");
+  hipSetDevice(ctx->device);
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  cdb_status st = CDB_OK;
+  uint8_t* w = (uint8_t*)ws_get(ctx, WS_STATE, 64, &st);
+  if (!w) return st;
+  CDB_HIP(hipMemsetAsync(w, 0, 64, s), "memset");
+  CompactArgs C;
+  std::memset(&C, 0, sizeof C);
+  C.ks = from[0]->col[0];
+  C.ns = from[1]->col[0];
+  C.ms = from[2]->col[0];
+  for (int c = 0; c < kKeyOutCols; ++c) C.kd[c] = dst->keys.col[c];
+  for (int c = 0; c < kNodeCols; ++c) {
+    C.nd[c] = dst->nodes.col[c];
+    C.md[c] = dst->members.col[c];
+  }
+  C.kbase = B.first[0]; C.nbase = B.first[1]; C.mbase = B.first[2];
+  C.kout = B.count[0]; C.nout = B.count[1]; C.mout = B.count[2];
+  C.kdoff = B.dense[0]; C.ndoff = B.dense[1]; C.mdoff = B.dense[2];
+  C.base_tot = (const unsigned long long*)w;
+  for (int f = 0; f < 3; ++f) C.cap[f] = std::max<uint64_t>(from[f]->n, 1) + (uint64_t)UINT32_MAX;
+  C.err = (uint32_t*)(w + 32);
+  C.ds[0] = C.ds[1] = C.ds[2] = 1;
+  const uint64_t tasks = (from[0]->n + from[1]->n + from[2]->n) / kCompactChunk + 3;
+  compact_kernel<<<(uint32_t)std::min<uint64_t>((tasks + kCompactWaves - 1) / kCompactWaves, 65536),
+                   64 * kCompactWaves, 0, s>>>(C, (uint32_t)B.nb);
+  CDB_TRY(launch_check(ctx, s, "compact_kernel"));
+  for (int f = 0; f < 3; ++f) {
+    to[f]->n = from[f]->n;
+    to[f]->stride = to[f]->stride0 = 0;
+  }
+  dst->compact = 1;
+  return hip_check(ctx, hipStreamSynchronize(s), "cdb_dev_output_compact");
 }
 
 cdb_status cdb_merge_device(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts, cdb_dev_output* out,

@@ -35,7 +35,12 @@ struct GenArgs {
   uint64_t* k[kKeyCols];
   uint64_t* nd[kNodeCols];
   uint64_t* mb[kMemberCols];
+  uint32_t ks, cs;         // record strides (1: plain columns; the records layout, cdb_merge.h)
 };
+// field c of row i of a family (common.h row_field)
+__device__ __forceinline__ uint64_t& gcell(uint64_t* const* col, uint32_t s, int c, uint64_t i) {
+  return col[c][c ? i * s : i];
+}
 
 __global__ void gen_count_kernel(GenArgs a) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.g.universe;
@@ -68,23 +73,23 @@ __global__ void gen_count_kernel(GenArgs a) {
 
 __device__ __forceinline__ void gen_node_row(const GenArgs& a, const Hash128& h, const GenKey& k, uint64_t i,
                                              uint32_t r, uint32_t j, uint64_t pn, uint64_t v) {
-  a.nd[C_PKH][pn] = h.h;
-  a.nd[C_PKF][pn] = h.f;
-  a.nd[C_ID1][pn] = gen_node_id(a.g, k, j, r);
-  a.nd[C_ID2][pn] = v;
-  a.nd[C_T][pn] = gen_node_t(a.g, i, r, j);
-  a.nd[C_META][pn] = meta_pack(0, r, gen_node_src(a.g, i, j));
+  gcell(a.nd, a.cs, C_PKH, pn) = h.h;
+  gcell(a.nd, a.cs, C_PKF, pn) = h.f;
+  gcell(a.nd, a.cs, C_ID1, pn) = gen_node_id(a.g, k, j, r);
+  gcell(a.nd, a.cs, C_ID2, pn) = v;
+  gcell(a.nd, a.cs, C_T, pn) = gen_node_t(a.g, i, r, j);
+  gcell(a.nd, a.cs, C_META, pn) = meta_pack(0, r, gen_node_src(a.g, i, j));
 }
 __device__ __forceinline__ void gen_member_row(const GenArgs& a, const Hash128& h, const GenKey& k, uint64_t i,
                                                uint32_t r, uint32_t j, uint64_t pm) {
   const uint64_t mi = gen_member_index(a.g, k, j);
   const Hash128 mh = gen_member_hash(mi);
-  a.mb[C_PKH][pm] = h.h;
-  a.mb[C_PKF][pm] = h.f;
-  a.mb[C_ID1][pm] = mh.h;
-  a.mb[C_ID2][pm] = mh.f;
-  a.mb[C_T][pm] = gen_member_t(a.g, i, r, j);
-  a.mb[C_META][pm] = meta_pack(gen_member_is_del(a.g, i, r, j) ? KIND_DEL : KIND_ADD, r, gen_member_src(a.g, i, mi));
+  gcell(a.mb, a.cs, C_PKH, pm) = h.h;
+  gcell(a.mb, a.cs, C_PKF, pm) = h.f;
+  gcell(a.mb, a.cs, C_ID1, pm) = mh.h;
+  gcell(a.mb, a.cs, C_ID2, pm) = mh.f;
+  gcell(a.mb, a.cs, C_T, pm) = gen_member_t(a.g, i, r, j);
+  gcell(a.mb, a.cs, C_META, pm) = meta_pack(gen_member_is_del(a.g, i, r, j) ? KIND_DEL : KIND_ADD, r, gen_member_src(a.g, i, mi));
 }
 
 __global__ void gen_fill_kernel(GenArgs a, const uint32_t* __restrict__ ok, const uint32_t* __restrict__ on,
@@ -95,13 +100,13 @@ __global__ void gen_fill_kernel(GenArgs a, const uint32_t* __restrict__ ok, cons
     if (!gen_in_shard(a.g, h.h)) continue;
     uint64_t pk = ok[i], pn = on[i], pm = om[i];
     auto key_row = [&](uint64_t ct, uint64_t ut, uint64_t dt, uint64_t aux, uint64_t meta) {
-      a.k[K_KH][pk] = h.h;
-      a.k[K_KF][pk] = h.f;
-      a.k[K_CT][pk] = ct;
-      a.k[K_UT][pk] = ut;
-      a.k[K_DT][pk] = dt;
-      a.k[K_AUX][pk] = aux;
-      a.k[K_META][pk] = meta;
+      gcell(a.k, a.ks, K_KH, pk) = h.h;
+      gcell(a.k, a.ks, K_KF, pk) = h.f;
+      gcell(a.k, a.ks, K_CT, pk) = ct;
+      gcell(a.k, a.ks, K_UT, pk) = ut;
+      gcell(a.k, a.ks, K_DT, pk) = dt;
+      gcell(a.k, a.ks, K_AUX, pk) = aux;
+      gcell(a.k, a.ks, K_META, pk) = meta;
       ++pk;
     };
     for (uint32_t r = a.lo; r < a.hi; ++r) {
@@ -152,7 +157,7 @@ __global__ void __launch_bounds__(256) gen_big_kernel(GenArgs a, uint64_t n) {
       for (uint32_t j = threadIdx.x; j < k.n_members; j += blockDim.x) gen_member_row(a, h, k, B.i, r, j, B.child0 + j);
     }
     __syncthreads();
-    if (threadIdx.x == 0 && k.tag == TAG_COUNTER) a.k[K_AUX][B.key_row] += part;
+    if (threadIdx.x == 0 && k.tag == TAG_COUNTER) gcell(a.k, a.ks, K_AUX, B.key_row) += part;
     __syncthreads();
   }
 }
@@ -223,14 +228,19 @@ extern "C" cdb_status cdb_gen_device(cdb_ctx* ctx, const cdb_gen_config* cfg, cd
     return fail(ctx, CDB_BAD_ARGUMENT, "generated rows exceed 2^32 per family");
   }
   std::memset(in, 0, sizeof *in);
-  if ((st = cdb_dev_rows_alloc(ctx, &in->keys, t[0], kKeyCols)) != CDB_OK ||
-      (st = cdb_dev_rows_alloc(ctx, &in->nodes, t[1], kNodeCols)) != CDB_OK ||
-      (st = cdb_dev_rows_alloc(ctx, &in->members, t[2], kMemberCols)) != CDB_OK) {
+  const bool rec = cfg->flags & CDB_GEN_ROWS_RECORDS;
+  auto alloc = [&](cdb_dev_rows* r, uint64_t rows, int nc) {
+    return rec ? cdb_dev_rows_alloc_records(ctx, r, rows, nc) : cdb_dev_rows_alloc(ctx, r, rows, nc);
+  };
+  if ((st = alloc(&in->keys, t[0], kKeyCols)) != CDB_OK || (st = alloc(&in->nodes, t[1], kNodeCols)) != CDB_OK ||
+      (st = alloc(&in->members, t[2], kMemberCols)) != CDB_OK) {
     hipFree(cnt);
     hipFree(tot);
     if (big) hipFree(big);
     return st;
   }
+  a.ks = std::max<uint32_t>(in->keys.stride, 1);
+  a.cs = std::max<uint32_t>(in->nodes.stride, 1);
   for (int c = 0; c < kKeyCols; ++c) a.k[c] = in->keys.col[c];
   for (int c = 0; c < kNodeCols; ++c) {
     a.nd[c] = in->nodes.col[c];

@@ -71,7 +71,7 @@ struct HotArgs {
 
 // A child's columns: its copied AoS row, or (runs mode) the runs' SoA columns.
 __device__ __forceinline__ uint64_t hot_col(const BucketArgs& A, const HotArgs& H, bool isn, uint32_t row, int c) {
-  if (H.runs) return (isn ? H.V.nin : H.V.min)[c][row];
+  if (H.runs) return row_field(isn ? H.V.nin : H.V.min, isn ? H.V.ns : H.V.ms, c, row);
   return (isn ? A.nr : A.mr)[(uint64_t)row * kChildStride + c];
 }
 

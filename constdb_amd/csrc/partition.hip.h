@@ -27,6 +27,9 @@ constexpr int kPF = 2;                // partition scatter: columns prefetched a
 template <int NC>
 struct ColSet {
   uint64_t* c[NC];
+  uint32_t s[NC];  // row stride of column k in words (0 = 1: a plain column; records layout, common.h)
+  __device__ __forceinline__ uint64_t at(int k, uint64_t i) const { return c[k][s[k] ? i * s[k] : i]; }
+  __device__ __forceinline__ const uint64_t* ptr(int k, uint64_t i) const { return &c[k][s[k] ? i * s[k] : i]; }
 };
 
 // Bucket index of hash h among `nb` buckets: floor(h * nb / 2^64). Monotone in h, so for
@@ -111,20 +114,20 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
   const uint64_t tile1 = tile0 + kPartTile < n ? tile0 + kPartTile : n;
   const int rows = (int)(tile1 - tile0);
   const uint64_t ncur = nprev * d;
-  const uint64_t plo = bucket_of_n(in.c[0][tile0] << shift, nprev);
-  const uint64_t phi = bucket_of_n(in.c[0][tile1 - 1] << shift, nprev);
+  const uint64_t plo = bucket_of_n(in.at(0, tile0) << shift, nprev);
+  const uint64_t phi = bucket_of_n(in.at(0, tile1 - 1) << shift, nprev);
   const uint64_t glo = plo * d;
   const uint64_t span64 = (phi - plo + 1) * d;
 
   if (span64 > (uint64_t)kPartLocalMax) {  // wide tile: per-row global reservation
     for (int r = threadIdx.x; r < rows; r += kPartThreads) {
-      const uint64_t gb = bucket_of_n(in.c[0][tile0 + r] << shift, ncur);
+      const uint64_t gb = bucket_of_n(in.at(0, tile0 + r) << shift, ncur);
       const uint32_t p = atomicAdd(&cursor[gb], 1u);
       if (IDX) {
         perm[p] = (uint32_t)(tile0 + r);
       } else {
 #pragma unroll
-        for (int c = 0; c < NC; ++c) out.c[c][p] = in.c[c][tile0 + r];
+        for (int c = 0; c < NC; ++c) out.c[c][p] = in.at(c, tile0 + r);
       }
     }
     return;
@@ -137,7 +140,7 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
 #pragma unroll
     for (int k = 0; k < kPartRowsPerThread; ++k) {
       const int r = threadIdx.x + k * kPartThreads;
-      v[c][k] = r < rows ? __builtin_nontemporal_load(&in.c[c][tile0 + r]) : 0;
+      v[c][k] = r < rows ? __builtin_nontemporal_load(in.ptr(c, tile0 + r)) : 0;
     }
   };
 #pragma unroll
@@ -226,18 +229,18 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_aos_kernel(ColSet<N
   const uint64_t tile1 = tile0 + kAosTile < n ? tile0 + kAosTile : n;
   const int rows = (int)(tile1 - tile0);
   const uint64_t ncur = nprev * d;
-  const uint64_t plo = bucket_of_n(in.c[0][tile0] << shift, nprev);
-  const uint64_t phi = bucket_of_n(in.c[0][tile1 - 1] << shift, nprev);
+  const uint64_t plo = bucket_of_n(in.at(0, tile0) << shift, nprev);
+  const uint64_t phi = bucket_of_n(in.at(0, tile1 - 1) << shift, nprev);
   const uint64_t glo = plo * d;
   const uint64_t span64 = (phi - plo + 1) * d;
 
   if (span64 > (uint64_t)kLocal) {  // wide tile: per-row global reservation
     for (int r = threadIdx.x; r < rows; r += kPartThreads) {
-      const uint64_t h = in.c[0][tile0 + r];
+      const uint64_t h = in.at(0, tile0 + r);
       const uint64_t gb = bucket_of_n(h << shift, ncur);
       const uint32_t p = atomicAdd(&cursor[gb], 1u);
 #pragma unroll
-      for (int c = 0; c < W; ++c) aos[(uint64_t)p * W + c] = c < NC ? in.c[c < NC ? c : 0][tile0 + r] : 0;
+      for (int c = 0; c < W; ++c) aos[(uint64_t)p * W + c] = c < NC ? in.at(c < NC ? c : 0, tile0 + r) : 0;
       if (dig) dig[p] = (uint16_t)(bucket_of_n(h << shift, ncur * d1) - gb * d1);
       else khcol[p] = h;
     }
@@ -249,7 +252,7 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_aos_kernel(ColSet<N
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     const int r = threadIdx.x + k * kPartThreads;
-    v0[k] = r < rows ? __builtin_nontemporal_load(&in.c[0][tile0 + r]) : 0;
+    v0[k] = r < rows ? __builtin_nontemporal_load(in.ptr(0, tile0 + r)) : 0;
   }
   __syncthreads();
   uint16_t lb[RPT];
@@ -277,7 +280,7 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_aos_kernel(ColSet<N
       uint64_t* row = &stage[(uint32_t)s * W];
       row[0] = v0[k];
 #pragma unroll
-      for (int c = 1; c < W; ++c) row[c] = c < NC ? __builtin_nontemporal_load(&in.c[c < NC ? c : 0][tile0 + r]) : 0;
+      for (int c = 1; c < W; ++c) row[c] = c < NC ? __builtin_nontemporal_load(in.ptr(c < NC ? c : 0, tile0 + r)) : 0;
     }
   }
   __syncthreads();

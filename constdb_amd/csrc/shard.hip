@@ -159,6 +159,7 @@ struct Source {
   std::vector<uint64_t> sp;   // [3][R][N + 1] absolute rows of each owner slice
   unsigned long long bad = 0;
   const uint64_t* cols[3][8] = {};
+  uint32_t stride[3] = {1, 1, 1};  // record stride per family (1: columns)
   uint64_t split(int f, uint32_t r, int d, int N) const { return sp[((uint64_t)f * R + r) * (N + 1) + d]; }
 };
 
@@ -187,6 +188,26 @@ cdb_status ws_cols(cdb_ctx* c, int slot, int ncols, uint64_t rows, uint64_t** co
   for (int k = 0; k < ncols; ++k) col[k] = p + k * n;
   return CDB_OK;
 }
+
+// Rows of one family in workspace slot `slot` of c, in the given layout (stride 1: columns; else
+// the records layout: a hash column, then records of `stride` words starting 16-B aligned).
+cdb_status ws_rows(cdb_ctx* c, int slot, int ncols, uint64_t rows, uint32_t stride, cdb_dev_rows* r) {
+  std::memset(r, 0, sizeof *r);
+  if (stride <= 1) return ws_cols(c, slot, ncols, rows, r->col);
+  cdb_status st = CDB_OK;
+  const uint64_t n = std::max<uint64_t>(rows, 1), hw = (n + 1) & ~1ull;
+  uint64_t* p = (uint64_t*)ws_get(c, slot, (hw + (uint64_t)stride * n + 2) * sizeof(uint64_t), &st);
+  if (!p) return st;
+  r->col[0] = p;
+  for (int k = 1; k < ncols; ++k) r->col[k] = p + hw + (k - 1);
+  r->stride = stride;
+  return CDB_OK;
+}
+
+// Arrays a family's rows move as: columns, one per field; records, the hash column and the
+// records (so a slice of rows [a, e) is one contiguous range of each array).
+int fam_arrays(int f, uint32_t stride) { return stride > 1 ? 2 : kFamCols[f]; }
+uint64_t array_words(int k, uint32_t stride) { return (k > 0 && stride > 1) ? stride : 1; }
 
 double ms_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -292,14 +313,38 @@ cdb_status cdb_merge_sharded(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     return st;
   }
 
+  // Inputs must not live in this call's own workspace (a previous call's outputs or received rows):
+  // growing a slot would free them under the exchange. Chain through cdb_dev_state_rows instead.
+  for (int i = 0; i < N; ++i)
+    for (int f = 0; f < 3; ++f) {
+      const cdb_dev_rows& r = fam_rows(in[i], f);
+      for (int k = 0; k < kFamCols[f] && r.n; ++k)
+        for (int j = 0; j < N; ++j)
+          for (int slot = WS_XK; slot <= WS_PM; ++slot) {
+            const cdb_ctx::Buf& b = slot_ctx(ctx, j)->ws[slot];
+            const uintptr_t p = (uintptr_t)r.col[k], lo = (uintptr_t)b.p;
+            if (b.p && p >= lo && p < lo + b.bytes)
+              return fail(ctx, CDB_BAD_ARGUMENT,
+                          "cdb_merge_sharded: an input lies in the library's exchange/output workspace (a previous "
+                          "call's output); copy it with cdb_dev_state_rows first");
+          }
+    }
+
   // ---- 1. owner splits of every source (one synchronisation of every device)
   std::vector<Source> src(N);
   for (int i = 0; i < N; ++i) {
     cdb_ctx* c = slot_ctx(ctx, i);
     const cdb_dev_input& d = in[i];
     Source& S = src[i];
-    for (int f = 0; f < 3; ++f)
-      for (int k = 0; k < kFamCols[f]; ++k) S.cols[f][k] = fam_rows(d, f).col[k];
+    for (int f = 0; f < 3; ++f) {
+      const cdb_dev_rows& r = fam_rows(d, f);
+      for (int k = 0; k < kFamCols[f]; ++k) S.cols[f][k] = r.col[k];
+      S.stride[f] = std::max<uint32_t>(r.stride, 1);
+      if (r.stride0 > 1 || (S.stride[f] > 1 && S.stride[f] != (uint32_t)(kFamCols[f] - 1)))
+        return fail(ctx, CDB_BAD_ARGUMENT, "cdb_merge_sharded: input rows must be columns or records");
+      if (S.stride[f] != std::max<uint32_t>(fam_rows(in[0], f).stride, 1))
+        return fail(ctx, CDB_BAD_ARGUMENT, "cdb_merge_sharded: every device slot's rows must share one layout");
+    }
     if (d.keys.n >= (1ull << 32) || d.nodes.n >= (1ull << 32) || d.members.n >= (1ull << 32))
       return fail(ctx, CDB_BAD_ARGUMENT, "row counts must be < 2^32 per family per device");
     if (!runs_valid(d)) continue;
@@ -353,7 +398,7 @@ cdb_status cdb_merge_sharded(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     for (int f = 0; f < 3; ++f) {
       const cdb_dev_rows& rows = fam_rows(in[i], f);
       cdb_dev_rows packed{};
-      CDB_SHARD_TRY(ws_cols(c, slots[f], kFamCols[f], rows.n, packed.col));
+      CDB_SHARD_TRY(ws_rows(c, slots[f], kFamCols[f], rows.n, S.stride[f], &packed));
       std::vector<uint64_t> cnt(N, 0);
       if (rows.n && (st = cdb_partition_owner(c, &rows, kFamCols[f], bits, &packed, cnt.data(), c->stream)) != CDB_OK)
         return fail_from(c, st);
@@ -374,8 +419,10 @@ cdb_status cdb_merge_sharded(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     std::vector<uint64_t> start[3];
     uint64_t total[3] = {0, 0, 0};
     bool sorted = true;
-    uint64_t* cols[3][8] = {};
+    cdb_dev_rows rows[3];
   };
+  uint32_t lay[3];
+  for (int f = 0; f < 3; ++f) lay[f] = src[0].stride[f];
   std::vector<Recv> rv(N);
   for (int d = 0; d < N; ++d) {
     Recv& R = rv[d];
@@ -397,13 +444,23 @@ cdb_status cdb_merge_sharded(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     cdb_ctx* c = slot_ctx(ctx, d);
     hipSetDevice(c->device);
     const int slots[3] = {WS_XK, WS_XN, WS_XM};
-    for (int f = 0; f < 3; ++f) CDB_SHARD_TRY(ws_cols(c, slots[f], kFamCols[f], R.total[f], R.cols[f]));
+    for (int f = 0; f < 3; ++f) CDB_SHARD_TRY(ws_rows(c, slots[f], kFamCols[f], R.total[f], lay[f], &R.rows[f]));
     CDB_SHARD_TRY(outputs(d, R.total));
   }
 
-  // ---- 3. the exchange
+  // ---- 3. the exchange: per (source run, family) slice, one transfer per array of the layout
+  //         (records: the hash column and the records; columns: every column), in pieces of <= 1 GiB
   const auto t1 = std::chrono::steady_clock::now();
   if (rccl) CDB_SHARD_NCCL(node->group_start(), "ncclGroupStart");
+  // an error inside the group still closes it (a group left open would swallow the next call's
+  // transfers), and then waits for nothing it posted
+  struct GroupGuard {
+    const Node* n;
+    bool open;
+    ~GroupGuard() {
+      if (open) n->group_end();
+    }
+  } guard{node, rccl};
   for (int d = 0; d < N; ++d) {
     const Recv& R = rv[d];
     cdb_ctx* cd = slot_ctx(ctx, d);
@@ -421,20 +478,22 @@ cdb_status cdb_merge_sharded(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
           X.bytes_moved += bytes;
           X.link_bytes[i][d] += bytes;
         }
-        for (int col = 0; col < kFamCols[f]; ++col) {
-          const uint64_t* from = S.cols[f][col] + a;
-          uint64_t* to = R.cols[f][col] + R.start[f][k];
+        for (int col = 0; col < fam_arrays(f, lay[f]); ++col) {
+          const uint64_t w = array_words(col, lay[f]);
+          const uint64_t* from = S.cols[f][col] + a * w;
+          uint64_t* to = R.rows[f].col[col] + R.start[f][k] * w;
+          const uint64_t words = (e - a) * w;
           if (i == d || !rccl) {
             hipSetDevice(cd->device);
             const hipError_t e2 = i == d || ci->device == cd->device
-                                      ? hipMemcpyAsync(to, from, (e - a) * 8, hipMemcpyDeviceToDevice, cd->stream)
-                                      : hipMemcpyPeerAsync(to, cd->device, from, ci->device, (e - a) * 8, cd->stream);
+                                      ? hipMemcpyAsync(to, from, words * 8, hipMemcpyDeviceToDevice, cd->stream)
+                                      : hipMemcpyPeerAsync(to, cd->device, from, ci->device, words * 8, cd->stream);
             CDB_SHARD_HIP(cd, e2, "exchange copy");
             ++X.transfers;
             continue;
           }
-          for (uint64_t x = 0; x < e - a; x += kMaxPieceRows) {
-            const uint64_t cnt = std::min<uint64_t>(kMaxPieceRows, e - a - x);
+          for (uint64_t x = 0; x < words; x += kMaxPieceRows) {
+            const uint64_t cnt = std::min<uint64_t>(kMaxPieceRows, words - x);
             hipSetDevice(ci->device);
             CDB_SHARD_NCCL(node->send(from + x, cnt, ncclUint64, d, node->comms[i], ci->stream), "ncclSend");
             hipSetDevice(cd->device);
@@ -445,11 +504,26 @@ cdb_status cdb_merge_sharded(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
       }
     }
   }
-  if (rccl) CDB_SHARD_NCCL(node->group_end(), "ncclGroupEnd");
+  if (rccl) {
+    guard.open = false;
+    CDB_SHARD_NCCL(node->group_end(), "ncclGroupEnd");
+  }
+  // Wait with a deadline: a transfer that never completes (a peer that never posts its side, a
+  // link down) is reported instead of hanging the caller. The context is unusable afterwards.
+  const double deadline_ms = 60e3 + (double)(X.bytes_moved + X.bytes_local) / 1e6;  // + 1 ms per MB
   for (int d = 0; d < N; ++d) {
     cdb_ctx* c = slot_ctx(ctx, d);
     hipSetDevice(c->device);
-    CDB_SHARD_HIP(c, hipStreamSynchronize(c->stream), "sync(exchange)");
+    for (;;) {
+      const hipError_t q = hipStreamQuery(c->stream);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) CDB_SHARD_HIP(c, q, "sync(exchange)");
+      if (ms_since(t1) > deadline_ms)
+        return fail(ctx, CDB_DEVICE_ERROR, "cdb_merge_sharded: the row exchange did not complete within " +
+                                               std::to_string((long long)deadline_ms) + " ms (device slot " +
+                                               std::to_string(d) + ")");
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
   }
   X.exchange_ms = ms_since(t1);
 
@@ -464,7 +538,7 @@ cdb_status cdb_merge_sharded(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     std::memset(&din, 0, sizeof din);
     cdb_dev_rows* fam[3] = {&din.keys, &din.nodes, &din.members};
     for (int f = 0; f < 3; ++f) {
-      for (int k = 0; k < kFamCols[f]; ++k) fam[f]->col[k] = R.cols[f][k];
+      *fam[f] = R.rows[f];
       fam[f]->n = R.total[f];
     }
     din.n_pos = n_pos;

@@ -65,13 +65,22 @@ def sort_into_runs(din, n_runs: int | None = None, sections: bool = False) -> No
                 din.run_start[f][r] = 0
             continue
         kh = wrap(rows.col[0], n)
-        meta = wrap(rows.col[ncol - 1], n)
+        if rows.stride > 1:  # records layout: the hash column + one record of `stride` words per row
+            rec = wrap(rows.col[1], n * rows.stride).view(n, rows.stride)
+            meta = rec[:, rows.stride - 1].contiguous()
+        else:
+            rec = None
+            meta = wrap(rows.col[ncol - 1], n)
         o, run = run_order(kh, meta, sections, key_family=(f == 0))
         counts = torch.bincount(run, minlength=R).tolist()
-        del run
-        for c in range(ncol):
-            col = wrap(rows.col[c], n)
-            col.copy_(col[o])
+        del run, meta
+        if rec is not None:
+            kh.copy_(kh[o])
+            rec.copy_(rec[o])
+        else:
+            for c in range(ncol):
+                col = wrap(rows.col[c], n)
+                col.copy_(col[o])
         del o
         st = 0
         for r in range(R):
@@ -80,3 +89,26 @@ def sort_into_runs(din, n_runs: int | None = None, sections: bool = False) -> No
         din.run_start[f][R] = st
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+
+
+def to_records(cdb, ctx, din) -> None:
+    """Setup helper: moves every family of a cdb_dev_input from plain columns into the records layout
+    (cdb_dev_rows_alloc_records; the column memory is released)."""
+    import ctypes
+    import torch
+    L = cdb.lib()
+    for f, (name, ncol) in enumerate(zip(("keys", "nodes", "members"), FAMILY_COLS)):
+        rows = getattr(din, name)
+        if rows.stride > 1:
+            continue
+        n = rows.n
+        rec = cdb.DevRows()
+        ctx.check(L.cdb_dev_rows_alloc_records(ctx.handle, ctypes.byref(rec), n, ncol))
+        if n:
+            wrap(rec.col[0], n).copy_(wrap(rows.col[0], n))
+            r = wrap(rec.col[1], n * (ncol - 1)).view(n, ncol - 1)
+            for c in range(1, ncol):
+                r[:, c - 1].copy_(wrap(rows.col[c], n))
+            torch.cuda.synchronize()
+        L.cdb_dev_rows_release(ctx.handle, ctypes.byref(rows))
+        setattr(din, name, rec)

@@ -67,9 +67,11 @@ const char* cdb_last_error(const cdb_ctx* ctx);
  * merges every entry before it reaches the checksum, replica/pull.rs:64-79), so the
  * caller decides; for every other error *out is NULL and *err_offset = byte offset. */
 enum {
-  CDB_DECODE_REFERENCE_CHECKSUM = 1u << 0 /* reproduce snapshot.rs:207-213 exactly: read the
-                                             checksum as a varint and CRC it too (rejects
-                                             practically every well-formed dump) */
+  CDB_DECODE_REFERENCE_CHECKSUM = 1u << 0, /* reproduce snapshot.rs:207-213 exactly: read the
+                                              checksum as a varint and CRC it too (rejects
+                                              practically every well-formed dump) */
+  CDB_DECODE_ROWS_RECORDS = 1u << 1        /* cdb_decode_snapshots_device: emit the rows in the
+                                              records layout (cdb_dev_rows) instead of columns */
 };
 cdb_status cdb_decode_snapshot(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags,
                                cdb_batch** out, size_t* err_offset);
@@ -331,14 +333,27 @@ cdb_status cdb_apply_ops(cdb_ctx* ctx, cdb_merged* state, const cdb_ops* ops, cd
                          cdb_apply_stats* stats);
 
 /* ------------------------------------------------------------------ device level
- * The same merge over columnar rows already resident in HBM (what bench.py times, and
- * what a multi-GPU driver calls after its RCCL all-to-all). Every column is a u64 device
- * array; layouts are documented in DESIGN.md §Data layout and constdb_amd/csrc/common.h.
- * Rows may come in any order and from up to 63 fold positions (pos in the meta word). */
+ * The same merge over rows already resident in HBM (what bench.py times, and what a multi-GPU
+ * driver calls after its RCCL all-to-all). Every field is a u64; layouts are documented in
+ * DESIGN.md §Data layout and constdb_amd/csrc/common.h. Rows may come in any order and from up
+ * to 63 fold positions (pos in the meta word).
+ *
+ * Two input layouts (cdb_dev_rows.stride):
+ *   columns (stride 0): col[c] is a plain array, row i's field c = col[c][i];
+ *   records (stride = ncols - 1): col[0] is the (parent) key-hash column and the other fields of
+ *     row i are one record of `stride` words, col[c] = col[1] + (c - 1), field c = col[c][i * stride]
+ *     (keys: a 48-B record kf ct ut dt aux meta; nodes / members: a 40-B record). Same bytes per row
+ *     as columns, but a bucket's rows of one run are ONE contiguous byte range, which the merge
+ *     copies into LDS in 16-B pieces (the sorted-run path); the hash column alone is
+ *     what the run directories stream. Arrays 16-B aligned, readable up to the next 16-B boundary
+ *     (cdb_dev_rows_alloc* allocate so). */
 typedef struct cdb_dev_rows {
   uint64_t* col[8]; /* keys: kh kf ct ut dt aux meta | nodes: pkh pkf node v t meta |
                        members: pkh pkf mh mf t meta */
   uint64_t n;
+  uint32_t stride;  /* words from one row to the next in col[1..7]: 0 (or 1) plain columns */
+  uint32_t stride0; /* the same for col[0]; inputs: 0. A merge's own bucket-layout outputs
+                       (cdb_dev_output.compact = 0) are whole rows: stride0 = stride = row words */
 } cdb_dev_rows;
 #define CDB_MAX_RUNS 64
 typedef struct cdb_dev_input {
@@ -356,14 +371,34 @@ typedef struct cdb_dev_input {
                        result is the same. */
   uint64_t run_start[3][CDB_MAX_RUNS + 1];
 } cdb_dev_input;
-/* Outputs are written sparse-by-bucket: bucket b's rows start at the bucket's input
- * offset; dense compaction into *_dense happens when cdb_dev_output.compact != 0. */
+/* The merge's buckets (the engine's native result layout, cdb_dev_output.compact = 0): bucket b
+ * owns a hash range (ascending in b); its output rows of family f (0 keys, 1 nodes, 2 members) are
+ * count[f][b] whole rows at row slots first[f][b] ..; dense[f][b] is the index the bucket's first
+ * row has in the dense result (an exclusive scan of count). Library-owned, in the ctx workspace. */
+typedef struct cdb_dev_buckets {
+  uint64_t nb;
+  const uint32_t* first[3];
+  const uint32_t* count[3];
+  const uint32_t* dense[3];
+} cdb_dev_buckets;
+
+/* Merge outputs.
+ *   compact = 1: dense plain columns in caller-allocated keys / nodes / members (at least the
+ *     input row counts), keys in key-hash order, cref = (absolute child row, count);
+ *   compact = 0: the engine's bucket layout, no compaction pass: the merge points keys / nodes /
+ *     members at its own row slots (whole AoS rows: stride0 = stride = 8 words per key row, 6 per
+ *     child row; library-owned, valid until the next merge on the ctx) and fills `buckets`. Every row
+ *     of a bucket lies in its slot range, in key-hash order; a key row's cref child begin is relative
+ *     to its bucket's first child slot. ->n = the dense row counts. Consumers read this layout
+ *     directly: cdb_dev_state_rows (the next merge's position 0), cdb_merged_from_device (canonical
+ *     dump, encode, op apply, cdb_merge_into). */
 typedef struct cdb_dev_output {
   cdb_dev_rows keys;    /* kh kf ct ut dt meta win cref */
   cdb_dev_rows nodes;   /* pkh pkf node v t meta */
   cdb_dev_rows members; /* pkh pkf mh mf t meta */
   uint32_t compact;
   uint32_t reserved;
+  cdb_dev_buckets buckets; /* compact = 0 only */
 } cdb_dev_output;
 
 /* Multi-GPU pack step: groups the rows of one family by owner rank = the
@@ -389,16 +424,32 @@ cdb_status cdb_merged_from_device(cdb_ctx* ctx, cdb_merged* state, cdb_batch* co
                                   const cdb_dev_output* out, cdb_merged** m);
 
 /* A merge result kept in HBM as fold position 0 of the next cdb_merge_device (the reference's
- * persistent server.db, replica/pull.rs:120-128): the compacted `state` rows are copied into
- * caller-allocated input rows (7 / 6 / 6 columns, at least state's row counts; ->n is set) as
- * key rows kh kf ct ut dt aux meta (aux = a counter's sum) and children unchanged, every meta
- * word with pos 0 and src = the row in `state`. A merge result is in key-hash order, so these
- * rows are ONE run of every family for the next merge (run_start[f] = {0, n, ...}). */
+ * persistent server.db, replica/pull.rs:120-128): `state` rows (either output layout) are copied
+ * into caller-allocated input rows (columns or records, 7 / 6 / 6 fields, at least state's row
+ * counts; ->n is set) as key rows kh kf ct ut dt aux meta (aux = a counter's sum) and children
+ * unchanged, every meta word with pos 0 and src = the row's dense index in `state`. A merge
+ * result is in key-hash order, so these rows are ONE run of every family for the next merge
+ * (run_start[f] = {0, n, ...}). */
 cdb_status cdb_dev_state_rows(cdb_ctx* ctx, const cdb_dev_output* state, cdb_dev_rows* keys, cdb_dev_rows* nodes,
                               cdb_dev_rows* members, void* stream);
 
-/* Allocates device columns for `rows` rows of a family (8 u64 columns) in *r. */
+/* Appends every family of `src` (any input layout) behind dst's rows (dst->keys.n etc.; dst's
+ * columns must have room: the caller allocated them), converting to dst's layout and raising each
+ * row's fold position by pos_offset; dst's row counts, n_pos and runs follow (src's runs after dst's
+ * when both are in runs, else dst->n_runs = 0). With cdb_dev_state_rows this chains a merge result
+ * (position 0) and newly decoded snapshots (positions 1..) into the next cdb_merge_device input. */
+cdb_status cdb_dev_input_append(cdb_ctx* ctx, cdb_dev_input* dst, const cdb_dev_input* src, uint32_t pos_offset,
+                                void* stream);
+
+/* The dense form (compact = 1) of a bucket-layout result `src` in caller-allocated columns
+ * (8 / 6 / 6, at least src's row counts): what the compaction pass of a compact = 1 merge does. */
+cdb_status cdb_dev_output_compact(cdb_ctx* ctx, const cdb_dev_output* src, cdb_dev_output* dst, void* stream);
+
+/* Allocates device columns for `rows` rows of a family (ncols u64 columns, 1..8) in *r. */
 cdb_status cdb_dev_rows_alloc(cdb_ctx* ctx, cdb_dev_rows* r, uint64_t rows, int ncols);
+/* The records layout (above) for `rows` rows of an ncols-field family (6 or 7): a hash column and
+ * records of ncols - 1 words, in one allocation released by cdb_dev_rows_release. */
+cdb_status cdb_dev_rows_alloc_records(cdb_ctx* ctx, cdb_dev_rows* r, uint64_t rows, int ncols);
 void cdb_dev_rows_release(cdb_ctx* ctx, cdb_dev_rows* r);
 /* Runs the merge pipeline on the context's stream (or `stream` if non-NULL, a hipStream_t).
  * out->*.n receive the output row counts. Synchronises before returning. */
@@ -479,8 +530,9 @@ enum {
   CDB_GEN_NODE_PER_REPLICA = 1u << 0, /* counters carry one node, the replica's own id r + 1 (the
                                          2-node MEET shape of config C1, bin/test.rs:85-106) */
   CDB_GEN_OPS_ZIPF_MEMBERS = 1u << 1, /* cdb_gen_ops: zipf_milli skews member choice, keys uniform */
-  CDB_GEN_OPS_TAGS_ONLY = 1u << 2     /* cdb_gen_ops: only sadd/srem/hset/hdel (config C3): no
+  CDB_GEN_OPS_TAGS_ONLY = 1u << 2,    /* cdb_gen_ops: only sadd/srem/hset/hdel (config C3): no
                                          whole-key deletes, no other types */
+  CDB_GEN_ROWS_RECORDS = 1u << 3      /* cdb_gen_device: rows in the records layout (cdb_dev_rows) */
 };
 void cdb_gen_default(cdb_gen_config* cfg);
 /* Snapshot bytes of replica r (writer layout). *out released with cdb_free. */

@@ -28,11 +28,20 @@ def ctx():
 
 
 def _cols(din):
+    """Every field of every family as numpy columns, from either input layout."""
     from constdb_amd.runs import wrap
     out = []
     for f, rows in enumerate((din.keys, din.nodes, din.members)):
-        out.append([wrap(rows.col[c], rows.n).cpu().numpy().view(np.uint64) if rows.n else np.zeros(0, np.uint64)
-                    for c in range(NCOLS[f])])
+        if not rows.n:
+            out.append([np.zeros(0, np.uint64) for _ in range(NCOLS[f])])
+            continue
+        if rows.stride > 1:
+            assert rows.stride == NCOLS[f] - 1
+            rec = wrap(rows.col[1], rows.n * rows.stride).view(rows.n, rows.stride).cpu().numpy().view(np.uint64)
+            out.append([wrap(rows.col[0], rows.n).cpu().numpy().view(np.uint64)] +
+                       [rec[:, c - 1].copy() for c in range(1, NCOLS[f])])
+        else:
+            out.append([wrap(rows.col[c], rows.n).cpu().numpy().view(np.uint64) for c in range(NCOLS[f])])
     return out
 
 
@@ -42,8 +51,10 @@ def _release(din):
         L.cdb_dev_rows_release(None, ctypes.byref(fam))
 
 
-def _check(ctx, snaps):
-    batches, din = cdb.decode_snapshots_device(ctx, snaps)
+def _check(ctx, snaps, records=False):
+    batches, din = cdb.decode_snapshots_device(ctx, snaps, records=records)
+    if records:
+        assert din.keys.stride == 6 and din.nodes.stride == 5 and din.members.stride == 5
     try:
         host = [cdb.decode_snapshot(s) for s in snaps]
         up = cdb.DevInput()
@@ -69,10 +80,11 @@ def _check(ctx, snaps):
         raise
 
 
+@pytest.mark.parametrize("records", [False, True])
 @pytest.mark.parametrize("seed", range(6))
-def test_device_decode_random(ctx, seed):
+def test_device_decode_random(ctx, seed, records):
     snaps = gen_replicas(seed, n_replicas=1 + seed % 4, n_keys=40 + 7 * seed, p_conflict=0.1, p_side=0.3)
-    _, din = _check(ctx, snaps)
+    _, din = _check(ctx, snaps, records)
     _release(din)
 
 
@@ -181,11 +193,12 @@ def test_device_decode_host_tier(ctx):
                     b"cnt": o.Object(1, 0, 0, o.OBJECT_ENC_COUNTER, c)})
     snap = o.dump_all(db, o.NodeHeader())
     snaps = [gen_replicas(4, n_replicas=1)[0], snap, snap]
-    batches, din = _check(ctx, snaps)
-    try:
-        _dump_vs_oracle(ctx, snaps, batches, din)
-    finally:
-        _release(din)
+    for records in (False, True):  # (records: the host tier's rows go up as the hash column + records)
+        batches, din = _check(ctx, snaps, records)
+        try:
+            _dump_vs_oracle(ctx, snaps, batches, din)
+        finally:
+            _release(din)
 
 
 def _dump_vs_oracle(ctx, snaps, batches, din):
