@@ -105,6 +105,10 @@ __global__ void beyond_wide_kernel(BucketArgs A, uint32_t nb, uint32_t* flag) {
   if (__ballot(any) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
 }
 
+__global__ void add_stat_kernel(unsigned long long* stats, int which, unsigned long long v) {
+  atomicAdd(&stats[which], v);
+}
+
 __global__ void iota_kernel(uint32_t* p, uint64_t n) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     p[i] = (uint32_t)i;
@@ -815,7 +819,7 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   std::vector<uint32_t> wide_ids, legacy;  // wide: the chip-wide child path
   std::vector<uint32_t> hk_off(1, 0), c_off(1, 0);
   std::vector<uint32_t> lk, ln, lm;
-  uint64_t tk = 0, tc = 0, cmax = 0;
+  uint64_t tk = 0, tc = 0, cmax = 0, orphans = 0;
   bool runs_batch = false;  // the batch being built reads its children from the runs
   auto flush = [&]() -> cdb_status {
     if (wide_ids.empty()) return CDB_OK;
@@ -843,6 +847,10 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
       if (runs_mode(i) != runs_batch) continue;
       const uint32_t K = cnt3[3 * i], N = cnt3[3 * i + 1], M = cnt3[3 * i + 2];
       if ((N + M > kBigBucket) != big) continue;
+      if (K == 0) {  // no key rows: every child is an orphan and nothing is output (the bucket's
+        orphans += N + M;  // counts were zeroed when it was listed); kept off the chip-wide path,
+        continue;          // whose per-bucket marker needs a key row
+      }
       if (legacy_all || K > (uint32_t)kCapK) {
         legacy.push_back(ids[i]);
         lk.push_back(K);
@@ -859,6 +867,10 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
       c_off.push_back((uint32_t)tc);
     }
     CDB_TRY(flush());
+  }
+  if (orphans) {
+    add_stat_kernel<<<1, 1, 0, s>>>(A.stats, ST_ORPHANS, orphans);
+    CDB_TRY(launch_check(ctx, s, "add_stat_kernel"));
   }
   if (!legacy.empty()) {
     const uint32_t nl = (uint32_t)legacy.size();

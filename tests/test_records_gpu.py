@@ -302,3 +302,58 @@ def test_decode_records_runs_vs_oracle(ctx, seed):
             assert st.type_conflicts == ost.type_conflicts
         finally:
             _release(ctx, din)
+
+
+def _filtered(ctx, batches, key_lo, child_lo):
+    """The batches uploaded as columns, keeping key rows with unsigned hash >= key_lo and child rows
+    with unsigned parent hash >= child_lo (rows keep their meta, so bytes still resolve)."""
+    L = cdb.lib()
+    din = _upload(ctx, batches, False)
+    out = cdb.DevInput()
+    out.n_pos = din.n_pos
+    keep = []
+    for name, nc, lo in (("keys", 7, key_lo), ("nodes", 6, child_lo), ("members", 6, child_lo)):
+        rows = getattr(din, name)
+        cols = [wrap(rows.col[c], rows.n) for c in range(nc)] if rows.n else []
+        sel = ((cols[0] ^ (-(1 << 63))) >= (lo - (1 << 63))) if rows.n else None
+        r = cdb.DevRows()
+        n = int(sel.sum()) if rows.n else 0
+        ctx.check(L.cdb_dev_rows_alloc(ctx.handle, ctypes.byref(r), n, nc))
+        for c in range(nc):
+            if n:
+                wrap(r.col[c], n).copy_(cols[c][sel])
+        keep.append(r)
+        setattr(out, name, r)
+    torch.cuda.synchronize()
+    _release(ctx, din)
+    return out
+
+
+def test_keyless_buckets_first_in_chip_wide_batches(ctx, monkeypatch):
+    """buckets holding children but no key rows (orphans), placed first in chip-wide
+    batches (every bucket chip-wide, small key-table batches): nothing is output for them, every
+    child counts as an orphan, and the rest of the result equals the merge of the same input without
+    those children (which the oracle tests pin)."""
+    cfg = _small(611, 20000, 4, mix_set=40, mix_dict=30, mean_members=6, side_permille=100)
+    batches = [cdb.decode_snapshot(cdb.gen_snapshot(cfg, r)) for r in range(4)]
+    lo = 1 << 58  # the lowest 1/64 of the hash space: several buckets, no key rows left in them
+    orphan_in = _filtered(ctx, batches, lo, 0)
+    clean = _filtered(ctx, batches, lo, lo)
+    try:
+        n_orphans = (orphan_in.nodes.n - clean.nodes.n) + (orphan_in.members.n - clean.members.n)
+        assert n_orphans > 0
+        sort_into_runs(orphan_in)
+        sort_into_runs(clean)
+        monkeypatch.setenv("CDB_HOT_KEY_CAP", "1500")
+        o1 = cdb.DevOutput()
+        st1 = _merge(ctx, orphan_in, o1, force_tier=2)
+        got = cdb.merged_from_device(ctx, o1, batches, stats=st1).canonical_dump()
+        monkeypatch.delenv("CDB_HOT_KEY_CAP")
+        o2 = cdb.DevOutput()
+        st2 = _merge(ctx, clean, o2)
+        want = cdb.merged_from_device(ctx, o2, batches, stats=st2).canonical_dump()
+        assert got == want, _diff(got, want)
+        assert st1.orphan_children == n_orphans and st2.orphan_children == 0
+        assert st1.key_rows_out == st2.key_rows_out
+    finally:
+        _release(ctx, orphan_in, clean)
