@@ -43,6 +43,7 @@ GEN_OPS_ZIPF_MEMBERS = 2
 GEN_OPS_TAGS_ONLY = 4
 GEN_ROWS_RECORDS = 8
 DECODE_ROWS_RECORDS = 2
+DECODE_STREAM_ORDER = 4
 
 
 class CstError(Exception):
@@ -461,7 +462,7 @@ def decode_snapshot_gpu(ctx: "Context", data: bytes, reference_checksum: bool = 
 
 
 def decode_snapshots_device(ctx: "Context", snaps, reference_checksum: bool = False,
-                            timing: Optional[dict] = None, records: bool = False):
+                            timing: Optional[dict] = None, records: bool = False, stream_order: bool = False):
     """GPU decode of several snapshots straight into HBM (cdb_decode_snapshots_device):
     returns (batches, DevInput) -- the rows of snapshot i at fold position i in one set of
     device columns (release each family with cdb_dev_rows_release), each batch holding the
@@ -476,7 +477,8 @@ def decode_snapshots_device(ctx: "Context", snaps, reference_checksum: bool = Fa
     failed = ctypes.c_uint32()
     off = ctypes.c_size_t()
     ims, dms = ctypes.c_double(), ctypes.c_double()
-    flags = (DECODE_REFERENCE_CHECKSUM if reference_checksum else 0) | (DECODE_ROWS_RECORDS if records else 0)
+    flags = ((DECODE_REFERENCE_CHECKSUM if reference_checksum else 0) | (DECODE_ROWS_RECORDS if records else 0)
+             | (DECODE_STREAM_ORDER if stream_order else 0))
     st = lib().cdb_decode_snapshots_device(ctx.handle, bufs, lens, n, flags, hs, ctypes.byref(din),
                                            ctypes.byref(failed), ctypes.byref(off), ctypes.byref(ims),
                                            ctypes.byref(dms))

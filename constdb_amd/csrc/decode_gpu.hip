@@ -569,6 +569,10 @@ class GpuDecode {
   // on the context's stream; the verdict reads after a synchronisation (read_order).
   cdb_status order_check();
   bool read_order() const { return ordered_ && !order_flag_; }
+  // a snapshot not in key-hash order (the reference's HashMap order) made ONE run anyway (after
+  // read_order): its entries sorted by key hash on the device, children laid out in that order
+  cdb_status sort_to_run();
+  bool sorted() const { return sorted_; }
   unsigned long long order_flag_ = 0;  // written by the D2H copy queued in order_check
   uint64_t keys() const { return n_; }
   uint64_t nodes() const { return nn_; }
@@ -637,6 +641,9 @@ class GpuDecode {
   } cursor_free_{&cursor_};
   uint64_t dev_datas_ = 0;  // leading entries (the DATAS section) whose offsets are only in di_.offs
   bool ordered_ = false;  // the sections are contiguous, in DATAS, EXPIRES, DELETES order
+  bool sorted_ = false;   // sort_to_run placed the rows: sort_dest_ is every entry's key row
+  uint32_t* sort_dest_ = nullptr;
+  DevBuf d_sort_;
   Sections sec_{};
   DecArgs A_;
   uint32_t grid_ = 0;
@@ -1167,6 +1174,77 @@ cdb_status GpuDecode::order_check() {
   return st_;
 }
 
+// ---- a snapshot in the reference's HashMap order made one run (sort_to_run)
+// perm: sorted position -> entry. dest[entry] = its key row; the children counts in sorted order.
+__global__ void __launch_bounds__(kDecThreads) sort_perm_kernel(const uint32_t* __restrict__ perm, uint64_t n,
+                                                                const uint32_t* __restrict__ ncnt,
+                                                                const uint32_t* __restrict__ mcnt,
+                                                                uint32_t* __restrict__ dest, uint32_t* __restrict__ ns,
+                                                                uint32_t* __restrict__ ms) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t e = perm[j];
+    dest[e] = (uint32_t)j;
+    ns[j] = ncnt[e];
+    ms[j] = mcnt[e];
+  }
+}
+// every entry's first child rows: the scans in sorted order, back to entry order
+__global__ void __launch_bounds__(kDecThreads) sort_off_kernel(const uint32_t* __restrict__ perm, uint64_t n,
+                                                               const uint64_t* __restrict__ nso,
+                                                               const uint64_t* __restrict__ mso,
+                                                               uint64_t* __restrict__ noff, uint64_t* __restrict__ moff) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t e = perm[j];
+    noff[e] = nso[j];
+    moff[e] = mso[j];
+  }
+}
+__global__ void __launch_bounds__(kDecThreads) iota32_kernel(uint32_t* __restrict__ v, uint64_t n) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x)
+    v[j] = (uint32_t)j;
+}
+
+// The reference dumps its DB by iterating a HashMap (db.rs:122-136), so a peer running it sends
+// DATAS, EXPIRES and DELETES in no key order. Such a snapshot still becomes ONE sorted run: a stable
+// radix sort of (key hash, entry) pairs over all its entries (8 passes of 8 bits; equal hashes keep
+// stream order, so DATAS precede EXPIRES precede DELETES, as dest_kernel orders a hash-ordered
+// snapshot), then every entry's key row is its sorted position and its children are laid out in
+// that order (the count scans redone in sorted order). Entries left to the host tier keep the
+// snapshot in stream order (no run).
+cdb_status GpuDecode::sort_to_run() {
+  sorted_ = false;
+  const uint64_t n = n_;
+  if (!ordered_ || !hosted_.empty() || n < 2 || n >= (1ull << 32)) return CDB_OK;
+  uint64_t* kh = (uint64_t*)d_ord_.p;
+  uint32_t* dest = (uint32_t*)(kh + n + 8);
+  if ((st_ = alloc(&d_sort_.p, n * (8 + 4 + 4 + 4 + 4 + 8 + 8) + 64, "decode: key-hash sort scratch")) != CDB_OK)
+    return st_;
+  uint64_t* k2 = (uint64_t*)d_sort_.p;
+  uint64_t* nso = k2 + n;
+  uint64_t* mso = nso + n;
+  uint32_t* v = (uint32_t*)(mso + n);
+  uint32_t* v2 = v + n;
+  uint32_t* ns = v2 + n;
+  uint32_t* ms = ns + n;
+  const uint32_t g = (uint32_t)std::min<uint64_t>(grid_, 4096);
+  iota32_kernel<<<g, kDecThreads, 0, s_>>>(v, n);
+  ck(hipGetLastError(), "iota32_kernel");
+  uint64_t* kk = kh;
+  uint32_t* vv = v;
+  if (st_ == CDB_OK) st_ = radix_sort_pairs(ctx_, &kk, &vv, k2, v2, n, 0, 64, s_);
+  if (st_ != CDB_OK) return st_;
+  sort_perm_kernel<<<g, kDecThreads, 0, s_>>>(vv, n, A_.ncount, A_.mcount, dest, ns, ms);
+  ck(hipGetLastError(), "sort_perm_kernel");
+  if (st_ == CDB_OK) st_ = exclusive_scan_u32(ctx_, ns, n, nso, nullptr, s_);
+  if (st_ == CDB_OK) st_ = exclusive_scan_u32(ctx_, ms, n, mso, nullptr, s_);
+  if (st_ != CDB_OK) return st_;
+  sort_off_kernel<<<g, kDecThreads, 0, s_>>>(vv, n, nso, mso, (uint64_t*)A_.noff, (uint64_t*)A_.moff);
+  ck(hipGetLastError(), "sort_off_kernel");
+  sort_dest_ = dest;
+  sorted_ = st_ == CDB_OK;
+  return st_;
+}
+
 // Host-decoded child rows [at, at + n) of a 6-field family into device rows: one upload per column,
 // or (records, stride s) the hash column and the interleaved records.
 template <typename Val>
@@ -1218,7 +1296,9 @@ cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint6
   A.ks = ks;
   A.cs = cs;
   A.dest = nullptr;
-  if (run && n > 1 && sec_.b[1] != n) {  // side sections to merge into the DATAS order
+  if (run && sorted_) {
+    A.dest = sort_dest_;
+  } else if (run && n > 1 && sec_.b[1] != n) {  // side sections to merge into the DATAS order
     const uint64_t* kh = (const uint64_t*)d_ord_.p;
     uint32_t* dest = (uint32_t*)(kh + n + 8);
     dest_kernel<<<grid_, kDecThreads, 0, s>>>(kh, sec_, dest);
@@ -1396,7 +1476,12 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     if ((st = dec[i]->order_check()) != CDB_OK) return st;
   if (runs) {
     if ((st = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync(decode order)")) != CDB_OK) return st;
-    for (uint32_t i = 0; i < n; ++i) runs = runs && dec[i]->read_order();
+    for (uint32_t i = 0; i < n && runs; ++i) {
+      if (dec[i]->read_order()) continue;
+      // the reference's HashMap order: sorted into a run unless the caller keeps stream order
+      if (!(flags & CDB_DECODE_STREAM_ORDER) && (st = dec[i]->sort_to_run()) != CDB_OK) return st;
+      runs = dec[i]->sorted();
+    }
   }
   std::memset(din, 0, sizeof *din);
   const bool rec = flags & CDB_DECODE_ROWS_RECORDS;

@@ -98,6 +98,13 @@ void advise_huge(void* p, size_t bytes);
 uint64_t crc_tile_bytes();
 cdb_status crc64_device(cdb_ctx* ctx, const uint8_t* dev, uint64_t padded, uint64_t* d_crc, hipStream_t s);
 cdb_status stamp_pos(cdb_ctx* ctx, uint64_t* meta, uint64_t n, uint32_t pos, hipStream_t s);
+// Stable LSD radix sort of n (u64 key, u32 value) pairs on key bits [lo, bits) (radix.hip.h; workspace
+// slots WS_RADIX, WS_SCAN); *k / *v receive whichever buffers hold the result.
+cdb_status radix_sort_pairs(cdb_ctx* ctx, uint64_t** k, uint32_t** v, uint64_t* k2, uint32_t* v2, uint64_t n,
+                            int lo, int bits, hipStream_t s);
+// Exclusive scan of n u32 into u64 (workspace slot WS_SCAN); *d_total (device, may be null) = the sum.
+cdb_status exclusive_scan_u32(cdb_ctx* ctx, const uint32_t* in, uint64_t n, uint64_t* out, uint64_t* d_total,
+                              hipStream_t s);
 // A merge result's family as fold position 0 of the next merge, in place in the input rows:
 // meta <- tag | pos 0 | src = row; for keys (aux != null) also aux <- the counter sum (the
 // result's win, staged in aux) for counters, 0 otherwise.

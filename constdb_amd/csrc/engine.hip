@@ -643,7 +643,6 @@ cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, const InLayout&
 }
 }  // namespace
 
-namespace {
 // Stable LSD radix sort of n (u64 key, u32 value) pairs on bits [lo, bits) in 8-bit passes from
 // lo; returns the buffers holding the result (the inputs or the spare pair).
 cdb_status radix_sort_pairs(cdb_ctx* ctx, uint64_t** k, uint32_t** v, uint64_t* k2, uint32_t* v2, uint64_t n,
@@ -669,6 +668,13 @@ cdb_status radix_sort_pairs(cdb_ctx* ctx, uint64_t** k, uint32_t** v, uint64_t* 
   *v = va;
   return CDB_OK;
 }
+
+cdb_status exclusive_scan_u32(cdb_ctx* ctx, const uint32_t* in, uint64_t n, uint64_t* out, uint64_t* d_total,
+                              hipStream_t s) {
+  return exclusive_scan<uint32_t, uint64_t>(ctx, in, n, out, (uint64_t*)nullptr, d_total, s);
+}
+
+namespace {
 
 // The chip-wide child path (hot.hip.h) over one batch of buckets: ids in ascending order, their
 // key rows (prefix hk_off) and child rows (prefix c_off); tk < 2^23 key rows and tc < 2^32 child

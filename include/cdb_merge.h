@@ -70,8 +70,11 @@ enum {
   CDB_DECODE_REFERENCE_CHECKSUM = 1u << 0, /* reproduce snapshot.rs:207-213 exactly: read the
                                               checksum as a varint and CRC it too (rejects
                                               practically every well-formed dump) */
-  CDB_DECODE_ROWS_RECORDS = 1u << 1        /* cdb_decode_snapshots_device: emit the rows in the
+  CDB_DECODE_ROWS_RECORDS = 1u << 1,       /* cdb_decode_snapshots_device: emit the rows in the
                                               records layout (cdb_dev_rows) instead of columns */
+  CDB_DECODE_STREAM_ORDER = 1u << 2        /* cdb_decode_snapshots_device: leave a snapshot that is not
+                                              in key-hash order in stream order (n_runs = 0) instead
+                                              of sorting it into a run */
 };
 cdb_status cdb_decode_snapshot(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags,
                                cdb_batch** out, size_t* err_offset);
@@ -96,12 +99,15 @@ cdb_status cdb_decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len,
  * stay in HBM, so cdb_merge, cdb_upload_batches and cdb_batch_column reject it. Its byte
  * references stay in HBM too, until the first cdb_merged_canonical_dump or cdb_encode_snapshot
  * of a result behind it downloads them (on that call's ctx, which must be this ctx's device).
- * Sorted runs: when every snapshot's DATAS, EXPIRES and DELETES sections are each in key-hash
- * order (a snapshot cdb_encode_snapshot wrote from a merge result), snapshot i's key rows are
- * placed as ONE run in key-hash order (the three sections merged, DATAS first on equal hashes;
- * meta src still names the entry), its node and member rows are one run each, and out->n_runs = n
- * with run_start set: cdb_merge_device then takes the sorted-run path. Otherwise (the
- * reference's HashMap order) rows keep stream order and n_runs = 0. Errors: *failed
+ * Sorted runs: snapshot i's key rows are placed as ONE run in key-hash order (meta src still names
+ * the entry), its node and member rows as one run each in their parents' order, and out->n_runs = n
+ * with run_start set, so cdb_merge_device takes the sorted-run path. A snapshot whose DATAS, EXPIRES
+ * and DELETES sections are each in key-hash order (one cdb_encode_snapshot wrote from a merge
+ * result) is placed by merging the three sections (DATAS first on equal hashes); one in the
+ * reference's HashMap order (db.rs:122-136) is sorted on the device (a stable radix sort of its
+ * entries' key hashes: the same order). Snapshots with entries left to the host decoder (objects
+ * past 3000 members or 1500 nodes), or CDB_DECODE_STREAM_ORDER, keep stream order: n_runs = 0 (the
+ * partition path; the same result). Errors: *failed
  * is the snapshot, *err_offset the byte offset in it, and nothing is allocated; a checksum
  * mismatch (CDB_INVALID_SNAPSHOT_CHECKSUM) still returns every batch and the rows, as the
  * reference merges a snapshot's entries before it reaches the checksum. */

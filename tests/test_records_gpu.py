@@ -278,19 +278,21 @@ def test_bucket_layout_state_chain_vs_oracle(ctx, records):
 
 @pytest.mark.parametrize("seed", [0, 1])
 def test_decode_records_runs_vs_oracle(ctx, seed):
-    """Snapshots this engine encoded (key-hash order), decoded straight into HBM as records
-    (CDB_DECODE_ROWS_RECORDS: one run per snapshot), merged into the bucket layout: the decoder's own
-    runs through the staged loads, equal to the oracle; the same snapshots in generator order take
-    the partition path from records."""
+    """Snapshots this engine encoded (key-hash order) and the same replicas in generator order (the
+    reference's HashMap order: no key order), decoded straight into HBM as records
+    (CDB_DECODE_ROWS_RECORDS) -- the first placed as one run per snapshot by merging its sections, the
+    second sorted into one run per snapshot on the device -- merged into the bucket layout on the
+    sorted-run path through the staged loads: equal to the oracle. With CDB_DECODE_STREAM_ORDER the
+    generator-order rows take the partition path from records."""
     cfg = _small(600 + seed, 30000, 4 + seed, conflict_ppm=20000, tie_permille=100, side_permille=300,
                  mix_set=20, mix_dict=20, del_permille=300)
     raw = [cdb.gen_snapshot(cfg, r) for r in range(cfg.n_replicas)]
     db = cdb.DB(ctx)
     encs = [db.merge_snapshots([x]).encode_snapshot(replicas=None)[0] for x in raw]
-    for snaps, want_runs in ((encs, True), (raw, False)):
+    for snaps, want_runs in ((encs, True), (raw, True), (raw, False)):
         rc, want, ost = cdb_oracle.fold(snaps)
         assert rc == 0
-        batches, din = cdb.decode_snapshots_device(ctx, snaps, records=True)
+        batches, din = cdb.decode_snapshots_device(ctx, snaps, records=True, stream_order=not want_runs)
         try:
             assert din.keys.stride == 6 and (din.n_runs == len(snaps)) == want_runs
             out = cdb.DevOutput()
@@ -357,3 +359,30 @@ def test_keyless_buckets_first_in_chip_wide_batches(ctx, monkeypatch):
         assert st1.key_rows_out == st2.key_rows_out
     finally:
         _release(ctx, orphan_in, clean)
+
+
+@pytest.mark.parametrize("records", [False, True])
+def test_decode_reference_order_sorted_vs_oracle(ctx, records):
+    """The reference's HashMap-order dumps (the Python oracle's writer iterates its dict in insertion
+    order, not key order) with every kind of entry, expires and deletes, decoded into HBM: every
+    snapshot becomes one run (sorted on the device), the merge takes the sorted-run path, and the
+    result -- with DB::gc -- equals the oracle's fold; C4's shape at 200K keys too."""
+    from snapgen import gen_replicas
+    snaps = gen_replicas(31, n_replicas=5, n_keys=3000, p_conflict=0.05, p_side=0.3)
+    cfg = configs.c4(cdb, 200_000)
+    for group, wm in ((snaps, None), (snaps, (configs.T0_MS + (1 << 30)) << 22),
+                      ([cdb.gen_snapshot(cfg, r) for r in range(8)], None)):
+        flags = cdb_oracle.FLAG_GC if wm is not None else 0
+        rc, want, ost = cdb_oracle.fold(group, flags=flags, gc_watermark=wm or 0)
+        assert rc == 0
+        batches, din = cdb.decode_snapshots_device(ctx, group, records=records)
+        try:
+            assert din.n_runs == len(group)
+            out = cdb.DevOutput()
+            st = _merge(ctx, din, out, gc_watermark=wm)
+            assert st.sorted_runs == 1
+            got = cdb.merged_from_device(ctx, out, batches, stats=st).canonical_dump()
+            assert got == want, _diff(got, want)
+            assert st.type_conflicts == ost.type_conflicts
+        finally:
+            _release(ctx, din)

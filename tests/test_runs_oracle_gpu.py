@@ -299,11 +299,11 @@ def test_encode_decode_device_runs_vs_oracle(ctx, seed, gc):
     """encode -> GPU decode into HBM -> cdb_merge_device: the decoder places each snapshot's key rows
     as one key-hash-ordered run (its three sections merged), so the merge takes the sorted-run path
     with no setup sort; the result equals the oracle's fold of the same snapshots. Snapshots in
-    generator order (not hash-ordered) get no runs."""
+    generator order decoded with CDB_DECODE_STREAM_ORDER get no runs."""
     cfg = _small(300 + seed, 20000 + 10000 * seed, 3 + 2 * seed, conflict_ppm=20000, tie_permille=100,
                  side_permille=300, mix_set=20, mix_dict=20, del_permille=300)
     raw = [cdb.gen_snapshot(cfg, r) for r in range(cfg.n_replicas)]
-    batches, din = cdb.decode_snapshots_device(ctx, raw)
+    batches, din = cdb.decode_snapshots_device(ctx, raw, stream_order=True)
     assert din.n_runs == 0
     _release(ctx, din)
     encs = _hash_ordered_snapshots(ctx, raw)
