@@ -232,7 +232,7 @@ ABI_FUNCTIONS = (
     "cdb_decode_ops_gpu", "cdb_ops_column", "cdb_snapshot_index_selftest", "cdb_merge_into",
     "cdb_merged_from_device", "cdb_dev_state_rows", "cdb_ctx_create_multi", "cdb_ctx_device_count",
     "cdb_ctx_shard", "cdb_merge_sharded", "cdb_dev_rows_alloc_records", "cdb_dev_output_compact",
-    "cdb_dev_input_append")
+    "cdb_dev_input_append", "cdb_shard_splits", "cdb_shard_recv_plan")
 
 _lib = None
 
@@ -282,6 +282,11 @@ def lib():
         "cdb_dev_rows_alloc_records": (c_st, [vp, P(DevRows), ctypes.c_uint64, ctypes.c_int]),
         "cdb_dev_output_compact": (c_st, [vp, P(DevOutput), P(DevOutput), vp]),
         "cdb_dev_input_append": (c_st, [vp, P(DevInput), P(DevInput), ctypes.c_uint32, vp]),
+        "cdb_shard_splits": (c_st, [P(ctypes.c_uint64), P(ctypes.c_uint64), ctypes.c_uint32, ctypes.c_uint32,
+                                    P(ctypes.c_uint64)]),
+        "cdb_shard_recv_plan": (c_st, [ctypes.c_uint32, P(ctypes.c_uint32), P(ctypes.c_uint64), ctypes.c_uint32,
+                                       P(ctypes.c_uint32), P(ctypes.c_uint32), P(ctypes.c_uint32),
+                                       P(ctypes.c_uint64), P(ctypes.c_uint64)]),
         "cdb_dev_rows_release": (None, [vp, P(DevRows)]),
         "cdb_merge_device": (c_st, [vp, P(DevInput), P(MergeOpts), P(DevOutput), P(MergeStats), vp]),
         "cdb_partition_owner": (c_st, [vp, P(DevRows), ctypes.c_int, ctypes.c_int, P(DevRows), P(ctypes.c_uint64), vp]),

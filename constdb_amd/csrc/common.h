@@ -103,6 +103,18 @@ CDB_HD Hash128 hash_bytes(const uint8_t* p, uint64_t n, uint64_t domain) {
 }
 constexpr uint64_t kDomainKey = 0x4B4559ull, kDomainMember = 0x4D454Dull;
 
+// Multi-GPU owner of a (parent) key hash: its top `bits` bits. In a run (rows in
+// key-hash order) the rows owned by device d are one slice: this is its first row in [lo, hi).
+CDB_HD uint64_t owner_lower_bound(const uint64_t* kh, uint64_t lo, uint64_t hi, uint32_t d, int bits) {
+  uint64_t x = lo, y = hi;
+  while (x < y) {
+    const uint64_t m = (x + y) >> 1;
+    if ((bits ? kh[m] >> (64 - bits) : 0) < d) x = m + 1;
+    else y = m;
+  }
+  return x;
+}
+
 // Bucket hash of every row family: the parent KEY hash, so that a key and all its
 // children land in the same bucket (the fused bucket kernel needs no lookups).
 CDB_HD uint64_t bucket_of(uint64_t kh, int bits) { return bits ? kh >> (64 - bits) : 0; }

@@ -116,21 +116,7 @@ __global__ void owner_split_kernel(SplitArgs a) {
   if (i >= 3 * per_f) return;
   const uint32_t f = i / per_f, rem = i - f * per_f, r = rem / (a.world + 1), d = rem - r * (a.world + 1);
   const uint64_t lo = a.rs[f * (a.R + 1) + r], hi = a.rs[f * (a.R + 1) + r + 1];
-  uint64_t v;
-  if (d == 0) {
-    v = lo;
-  } else if (d == a.world) {
-    v = hi;
-  } else {
-    uint64_t x = lo, y = hi;
-    while (x < y) {
-      const uint64_t m = (x + y) >> 1;
-      if ((a.kh[f][m] >> (64 - a.bits)) < d) x = m + 1;
-      else y = m;
-    }
-    v = x;
-  }
-  a.out[i] = v;
+  a.out[i] = d == 0 ? lo : d == a.world ? hi : owner_lower_bound(a.kh[f], lo, hi, d, a.bits);
 }
 
 // Every run must be non-decreasing in the key hash. A decreasing adjacent pair is a violation
@@ -208,6 +194,60 @@ cdb_status ws_rows(cdb_ctx* c, int slot, int ncols, uint64_t rows, uint32_t stri
 // records (so a slice of rows [a, e) is one contiguous range of each array).
 int fam_arrays(int f, uint32_t stride) { return stride > 1 ? 2 : kFamCols[f]; }
 uint64_t array_words(int k, uint32_t stride) { return (k > 0 && stride > 1) ? stride : 1; }
+
+}  // namespace
+}  // namespace cdb
+
+extern "C" cdb_status cdb_shard_recv_plan(uint32_t n_sources, const uint32_t* n_runs, const uint64_t* counts,
+                                          uint32_t cap, uint32_t* n_recv_runs, uint32_t* recv_src,
+                                          uint32_t* recv_run, uint64_t* run_start, uint64_t* totals) {
+  if (!n_runs || !counts || !n_recv_runs || !totals || (cap && (!recv_src || !recv_run || !run_start)))
+    return CDB_BAD_ARGUMENT;
+  uint32_t k = 0;
+  uint64_t acc[3] = {0, 0, 0};
+  const uint64_t* c = counts;  // source i's [3][R_i]
+  for (uint32_t i = 0; i < n_sources; ++i) {
+    const uint32_t R = n_runs[i];
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint64_t n0 = c[r], n1 = c[R + r], n2 = c[2 * R + r];
+      if (!(n0 | n1 | n2)) continue;
+      if (k < cap) {
+        recv_src[k] = i;
+        recv_run[k] = r;
+        run_start[k] = acc[0];
+        run_start[(cap + 1) + k] = acc[1];
+        run_start[2 * (cap + 1) + k] = acc[2];
+      }
+      acc[0] += n0;
+      acc[1] += n1;
+      acc[2] += n2;
+      ++k;
+    }
+    c += 3ull * R;
+  }
+  if (k <= cap)
+    for (int f = 0; f < 3; ++f) run_start[f * (uint64_t)(cap + 1) + k] = acc[f];
+  *n_recv_runs = k;
+  for (int f = 0; f < 3; ++f) totals[f] = acc[f];
+  return k <= cap ? CDB_OK : CDB_BAD_ARGUMENT;
+}
+
+extern "C" cdb_status cdb_shard_splits(const uint64_t* kh, const uint64_t* run_start, uint32_t n_runs,
+                                       uint32_t n_devices, uint64_t* out) {
+  if (!run_start || !out || n_devices < 1 || n_devices > 256 || (n_devices & (n_devices - 1))) return CDB_BAD_ARGUMENT;
+  int bits = 0;
+  while ((1u << bits) < n_devices) ++bits;
+  for (uint32_t r = 0; r < n_runs; ++r) {
+    const uint64_t lo = run_start[r], hi = run_start[r + 1];
+    if (hi < lo || (hi > lo && !kh)) return CDB_BAD_ARGUMENT;
+    for (uint32_t d = 0; d <= n_devices; ++d)
+      out[(uint64_t)r * (n_devices + 1) + d] = d == 0 ? lo : d == n_devices ? hi : cdb::owner_lower_bound(kh, lo, hi, d, bits);
+  }
+  return CDB_OK;
+}
+
+namespace cdb {
+namespace {
 
 double ms_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
@@ -424,23 +464,28 @@ cdb_status cdb_merge_sharded(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   uint32_t lay[3];
   for (int f = 0; f < 3; ++f) lay[f] = src[0].stride[f];
   std::vector<Recv> rv(N);
+  std::vector<uint32_t> nruns(N);
+  uint32_t cap = 0;
+  for (int i = 0; i < N; ++i) cap += (nruns[i] = src[i].R);
   for (int d = 0; d < N; ++d) {
     Recv& R = rv[d];
-    for (int i = 0; i < N; ++i) {
-      const Source& S = src[i];
-      for (uint32_t r = 0; r < S.R; ++r) {
-        uint64_t rows = 0;
-        for (int f = 0; f < 3; ++f) rows += S.split(f, r, d + 1, N) - S.split(f, r, d, N);
-        if (!rows) continue;
-        R.runs.emplace_back(i, r);
-        R.sorted = R.sorted && S.sorted;
-        for (int f = 0; f < 3; ++f) {
-          R.start[f].push_back(R.total[f]);
-          R.total[f] += S.split(f, r, d + 1, N) - S.split(f, r, d, N);
-        }
-      }
+    // the receive layout (cdb_shard_recv_plan, the one plan dist.py uses too): one run per (source,
+    // source run) with rows for d, in (source, run) order
+    std::vector<uint64_t> counts;
+    for (int i = 0; i < N; ++i)
+      for (int f = 0; f < 3; ++f)
+        for (uint32_t r = 0; r < src[i].R; ++r) counts.push_back(src[i].split(f, r, d + 1, N) - src[i].split(f, r, d, N));
+    std::vector<uint32_t> rs(cap + 1), rr(cap + 1);
+    std::vector<uint64_t> starts(3ull * (cap + 1));
+    uint32_t k = 0;
+    if ((st = cdb_shard_recv_plan((uint32_t)N, nruns.data(), counts.data(), cap, &k, rs.data(), rr.data(),
+                                  starts.data(), R.total)) != CDB_OK)
+      return fail(ctx, st, "cdb_merge_sharded: receive plan");
+    for (uint32_t j = 0; j < k; ++j) {
+      R.runs.emplace_back((int)rs[j], rr[j]);
+      R.sorted = R.sorted && src[rs[j]].sorted;
     }
-    for (int f = 0; f < 3; ++f) R.start[f].push_back(R.total[f]);
+    for (int f = 0; f < 3; ++f) R.start[f].assign(starts.begin() + f * (cap + 1), starts.begin() + f * (cap + 1) + k + 1);
     cdb_ctx* c = slot_ctx(ctx, d);
     hipSetDevice(c->device);
     const int slots[3] = {WS_XK, WS_XN, WS_XM};

@@ -1,16 +1,19 @@
 """Multi-GPU snapshot merge: key-hash sharding with RCCL point-to-point over xGMI.
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL). Replica r lives on rank
-r*N/R, as one run: its rows in key-hash order (runs.py). Every key has ONE owner rank: the
-top log2(N) bits of its key hash (children use their parent's hash, so a key and its children
-travel together). Because a run is in hash order, the rows a rank owes owner d are ONE
-contiguous slice of every run -- there is no pack pass. A merge step:
-  1. splits : per (family, run), the owner boundaries by binary search (torch.searchsorted);
+r*N/R, as one run: its rows in key-hash order (runs.py), in the records layout (the key-hash
+column plus one record per row, cdb_merge.h). Every key has ONE owner rank: the top log2(N) bits
+of its key hash (children use their parent's hash, so a key and its children travel together).
+Because a run is in hash order, the rows a rank owes owner d are ONE contiguous slice of every run
+-- of the hash column and of the records alike -- so there is no pack pass. A merge step:
+  1. splits : per (family, run), the owner boundaries by binary search (torch.searchsorted; the
+              same search as cdb_shard_splits, which cdb_merge_sharded runs on the devices);
   2. counts : one all_to_all of the (family, run) row counts, then ONE host copy of the
-              split table and the received counts (the step's only host synchronisation);
+              split table and the received counts (the step's only host synchronisation); the
+              receive layout is cdb_shard_recv_plan's (the one plan both drivers use);
   3. rows   : one batch of point-to-point transfers (dist.batch_isend_irecv -> one RCCL
-              group): per (peer, family, run, column) a contiguous slice, pieces of at most
-              max_piece_bytes; this rank's own slices are device copies;
+              group): per (peer, family, run) two contiguous slices -- hash column and records --
+              in pieces of at most max_piece_bytes; this rank's own slices are device copies;
   4. merge  : the received slices are again runs in key-hash order (one per source run), so
               cdb_merge_device takes the sorted-run path (no partition pass) with
               key_shift = log2(N). Outputs stay sharded.
@@ -25,6 +28,7 @@ from typing import Sequence
 from .runs import FAMILY_COLS, SIGN, sort_into_runs, wrap
 
 OUT_COLS = (8, 6, 6)
+REC_WORDS = tuple(c - 1 for c in FAMILY_COLS)  # record words per family (7 - 1, 6 - 1, 6 - 1)
 
 # Largest single transfer. A 2.2 GB (2.2e9-byte, 2.75e8-element) RCCL transfer never completed
 # on MI355X in round 1 while every transfer below 2^31 bytes did: the limit is a byte count
@@ -81,34 +85,41 @@ def _pieces(a: int, e: int, piece_rows: int):
 
 
 class Plan:
-    """Who sends what to whom in one step (host integers, from the one synchronised copy)."""
+    """Who sends what to whom in one step (host integers, from the one synchronised copy). The
+    receive layout is cdb_shard_recv_plan's: one run per (source rank, source run) with rows, in
+    (source, run) order."""
 
     def __init__(self, splits, recv, world: int, rank: int, n_runs: int):
+        import constdb_amd as cdb
         self.world, self.rank, self.R = world, rank, n_runs
         self.splits = splits      # [3][R][world + 1] absolute offsets in this rank's rows
         self.recv = recv          # [world(src)][3][R] rows this rank receives
-        # receiver runs: (source run r, source s) pairs that carry rows, in (r, s) order
-        self.runs = [(r, s) for r in range(n_runs) for s in range(world)
-                     if any(recv[s][f][r] for f in range(3))]
-        self.run_start = []       # [3][len(runs) + 1]
-        self.total = []
-        for f in range(3):
-            st, acc = [], 0
-            for r, s in self.runs:
-                st.append(acc)
-                acc += recv[s][f][r]
-            st.append(acc)
-            self.run_start.append(st)
-            self.total.append(acc)
+        cap = world * n_runs
+        counts = (ctypes.c_uint64 * max(1, 3 * cap))(*[recv[s][f][r] for s in range(world) for f in range(3)
+                                                      for r in range(n_runs)])
+        nruns = (ctypes.c_uint32 * world)(*([n_runs] * world))
+        k = ctypes.c_uint32()
+        src = (ctypes.c_uint32 * max(1, cap))()
+        run = (ctypes.c_uint32 * max(1, cap))()
+        starts = (ctypes.c_uint64 * (3 * (cap + 1)))()
+        tot = (ctypes.c_uint64 * 3)()
+        st = cdb.lib().cdb_shard_recv_plan(world, nruns, counts, cap, ctypes.byref(k), src, run, starts, tot)
+        if st != cdb.OK:
+            raise RuntimeError(f"cdb_shard_recv_plan: status {st}")
+        n = k.value
+        self.runs = [(src[i], run[i]) for i in range(n)]   # receiver runs: (source rank, source run)
+        self.run_start = [[starts[f * (cap + 1) + i] for i in range(n + 1)] for f in range(3)]
+        self.total = [tot[f] for f in range(3)]
+        self._index = {sr: i for i, sr in enumerate(self.runs)}
 
     def dest(self, f: int, r: int, s: int) -> int:
         """First receive-buffer row of source s's run r in family f."""
-        return self.run_start[f][self.runs.index((r, s))]
+        return self.run_start[f][self._index[(s, r)]]
 
 
 def make_plan(fams, starts, world: int, rank: int, device=None) -> Plan:
-    """fams: three [ncols, n] int64 tensors (this rank's rows as runs); starts: three lists of
-    R + 1 run offsets. One all_to_all of the counts, one host copy."""
+    """fams: this rank's three families as (hash [n], records [n, w]) tensor pairs, rows as runs;
+    starts: three lists of R + 1 run offsets. One all_to_all of the counts, one host copy."""
     import torch
     import torch.distributed as dist
     R = len(starts[0]) - 1
@@ -130,35 +141,45 @@ def make_plan(fams, starts, world: int, rank: int, device=None) -> Plan:
 
 
 def exchange_runs(fams, plan: Plan, recv_bufs, max_piece_bytes: int = MAX_PIECE_BYTES) -> int:
-    """Moves every owed slice into recv_bufs (three [ncols, >= total] tensors on the same
-    device as fams) at the plan's run offsets. One batch of point-to-point operations; own
-    slices are local copies. Returns the number of point-to-point operations posted."""
+    """Moves every owed slice into recv_bufs (three (hash [>= total], records [>= total, w]) tensor
+    pairs on the same device as fams) at the plan's run offsets: per (peer, family, run) the hash
+    slice and the record slice, each one contiguous range. One batch of point-to-point operations;
+    own slices are local copies. Returns the number of point-to-point operations posted."""
     import torch.distributed as dist
     world, me = plan.world, plan.rank
     ops = []
     for peer in range(world):
         for f in range(3):
-            t, buf = fams[f], recv_bufs[f]
-            piece = max(1, max_piece_bytes // t.element_size())
             for r in range(plan.R):
                 # what I send to peer: my run r's slice owned by peer
                 a, e = plan.splits[f][r][peer], plan.splits[f][r][peer + 1]
                 # what I receive from peer: peer's run r's slice owned by me
                 n_in = plan.recv[peer][f][r]
                 d0 = plan.dest(f, r, peer) if n_in else 0
-                if peer == me:
-                    if e > a:
-                        buf[:, d0:d0 + (e - a)].copy_(t[:, a:e])
-                    continue
-                for c in range(t.shape[0]):
-                    for x, y in _pieces(a, e, piece):
-                        ops.append(dist.P2POp(dist.isend, t[c, x:y], peer))
-                    for x, y in _pieces(d0, d0 + n_in, piece):
-                        ops.append(dist.P2POp(dist.irecv, buf[c, x:y], peer))
+                for t, buf in zip(fams[f], recv_bufs[f]):
+                    if peer == me:
+                        if e > a:
+                            buf[d0:d0 + (e - a)].copy_(t[a:e])
+                        continue
+                    src, dst = t[a:e].reshape(-1), buf[d0:d0 + n_in].reshape(-1)
+                    piece = max(1, max_piece_bytes // t.element_size())
+                    for x, y in _pieces(0, src.numel(), piece):
+                        ops.append(dist.P2POp(dist.isend, src[x:y], peer))
+                    for x, y in _pieces(0, dst.numel(), piece):
+                        ops.append(dist.P2POp(dist.irecv, dst[x:y], peer))
     if ops:
         for w in dist.batch_isend_irecv(ops):
             w.wait()
     return len(ops)
+
+
+def recv_buffers(totals, device, pad: int = 2):
+    """Receive buffers of the three families: (hash, records) tensor pairs for `totals` rows (plus
+    `pad` rows: the merge may read up to the next 16 B past the last row)."""
+    import torch
+    return [(torch.empty(max(totals[f], 1) + pad, dtype=torch.int64, device=device),
+             torch.empty((max(totals[f], 1) + pad, REC_WORDS[f]), dtype=torch.int64, device=device))
+            for f in range(3)]
 
 
 def _rows_from_tensor(cdb, t, n):
@@ -170,22 +191,39 @@ def _rows_from_tensor(cdb, t, n):
     return r
 
 
+def _rows_from_records(cdb, pair, n):
+    """cdb_dev_rows view (records layout) of a (hash [cap], records [cap, w]) tensor pair."""
+    h, rec = pair
+    r = cdb.DevRows()
+    r.col[0] = h.data_ptr()
+    for c in range(1, rec.shape[1] + 1):
+        r.col[c] = rec.data_ptr() + 8 * (c - 1)
+    r.n = n
+    r.stride = rec.shape[1]
+    return r
+
+
 def _input_tensors(din):
-    """The input families as three [ncols, n] torch tensors (copies: the library's columns
-    are separate allocations; setup, outside any timed step)."""
+    """The input families as (hash [n], records [n, w]) torch tensor pairs (copies, from either
+    input layout; setup, outside any timed step)."""
     import torch
     out = []
     for rows, nc in zip((din.keys, din.nodes, din.members), FAMILY_COLS):
-        if rows.n:
-            out.append(torch.stack([wrap(rows.col[c], rows.n) for c in range(nc)]))
+        n = rows.n
+        if not n:
+            out.append((torch.zeros(0, dtype=torch.int64, device="cuda"),
+                        torch.zeros((0, nc - 1), dtype=torch.int64, device="cuda")))
+        elif rows.stride > 1:
+            out.append((wrap(rows.col[0], n).clone(), wrap(rows.col[1], n * (nc - 1)).view(n, nc - 1).clone()))
         else:
-            out.append(torch.zeros((nc, 0), dtype=torch.int64, device="cuda"))
+            out.append((wrap(rows.col[0], n).clone(),
+                        torch.stack([wrap(rows.col[c], n) for c in range(1, nc)], dim=1).contiguous()))
     return out
 
 
 def _merge_input(cdb, recv, plan: Plan, n_pos: int):
     d = cdb.DevInput()
-    d.keys, d.nodes, d.members = (_rows_from_tensor(cdb, recv[f], plan.total[f]) for f in range(3))
+    d.keys, d.nodes, d.members = (_rows_from_records(cdb, recv[f], plan.total[f]) for f in range(3))
     d.n_pos = n_pos
     if len(plan.runs) <= cdb.MAX_RUNS:
         d.n_runs = len(plan.runs)
@@ -214,6 +252,7 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
     lo, hi = rank * R // world, (rank + 1) * R // world
     universe = args.universe_per_gpu * world
     cfg = c4_config(cdb, universe, R, args.seed, lo, hi)
+    cfg.flags |= cdb.GEN_ROWS_RECORDS
     din = cdb.DevInput()
     ctx.check(L.cdb_gen_device(ctx.handle, ctypes.byref(cfg), ctypes.byref(din)))
     din.n_pos = R
@@ -233,11 +272,11 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
     # library would read as "use the context's own stream" -- unordered with the exchange).
     cs = torch.cuda.Stream(device=dev)
 
-    def buf(key, ncols, need):
-        b = state.get(key)
-        if b is None or b.shape[1] < need:
-            b = torch.empty((ncols, need + need // 8), dtype=torch.int64, device=dev)
-            state[key] = b
+    def bufs(totals):
+        b = state.get("recv")
+        if b is None or any(b[f][0].shape[0] < totals[f] + 2 for f in range(3)):
+            b = recv_buffers([t + t // 8 for t in totals], dev)
+            state["recv"] = b
         return b
 
     ev = []  # per timed step: (start, exchanged) events on the step's stream
@@ -249,7 +288,7 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
                 e0.record(cs)
             if world == 1:  # every row is this rank's own: the runs are the merge input as they lie
                 d2 = cdb.DevInput()
-                d2.keys, d2.nodes, d2.members = (_rows_from_tensor(cdb, fams[f], n_in[f]) for f in range(3))
+                d2.keys, d2.nodes, d2.members = (_rows_from_records(cdb, fams[f], n_in[f]) for f in range(3))
                 d2.n_pos = R
                 d2.n_runs = R
                 for f in range(3):
@@ -260,7 +299,7 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
                 total = n_in
             else:
                 plan = make_plan(fams, starts, world, rank)
-                recv = [buf(("recv", f), FAMILY_COLS[f], max(plan.total[f], 1)) for f in range(3)]
+                recv = bufs(plan.total)
                 state["ops"] = exchange_runs(fams, plan, recv)
                 state["runs"] = len(plan.runs)
                 state["sent"] = sent_bytes(plan, fams)
@@ -270,9 +309,7 @@ def run_bench(cdb, args, rank, world, local_rank, c4_config, alg_bytes):
                 e1.record(cs)
                 ev.append((e0, e1))
             dout = cdb.DevOutput()
-            outs = [buf(("out", f), OUT_COLS[f], max(total[f], 1)) for f in range(3)]
-            dout.keys, dout.nodes, dout.members = (_rows_from_tensor(cdb, t, 0) for t in outs)
-            dout.compact = 1
+            dout.compact = 0  # the bucket layout (as the N = 1 line): rows stay in the rank's workspace
             stream = torch.cuda.current_stream().cuda_stream
             assert stream, "the merge must run on the exchange's (non-default) stream"
             ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(d2), ctypes.byref(opts), ctypes.byref(dout),
@@ -355,7 +392,7 @@ def sent_bytes(plan: Plan, fams):
         if peer == plan.rank:
             continue
         for f in range(3):
-            nc = fams[f].shape[0]
+            nc = 1 + fams[f][1].shape[1]  # the hash word + the record
             for r in range(plan.R):
                 out[peer] += (plan.splits[f][r][peer + 1] - plan.splits[f][r][peer]) * nc * 8
     return out
@@ -380,12 +417,11 @@ def sharded_merge(cdb, ctx, din, n_pos: int, stream=None, max_piece_bytes: int =
     starts = [[din.run_start[f][r] for r in range(R + 1)] for f in range(3)]
     fams = _input_tensors(din)
     if on_host:
-        fams = [t.cpu() for t in fams]
+        fams = [(h.cpu(), r.cpu()) for h, r in fams]
     plan = make_plan(fams, starts, world, rank)
-    recv = [torch.empty((FAMILY_COLS[f], max(plan.total[f], 1)), dtype=torch.int64, device=fams[f].device)
-            for f in range(3)]
+    recv = recv_buffers(plan.total, fams[0][0].device)
     exchange_runs(fams, plan, recv, max_piece_bytes)
-    recv = [t.to(dev) for t in recv]
+    recv = [(h.to(dev), r.to(dev)) for h, r in recv]
     torch.cuda.synchronize()
     d2 = _merge_input(cdb, recv, plan, n_pos)
     dout = cdb.DevOutput()

@@ -505,6 +505,24 @@ typedef struct cdb_exchange_stats {
 cdb_status cdb_merge_sharded(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts, cdb_dev_output* out,
                              cdb_merge_stats* stats, cdb_exchange_stats* xs);
 
+/* The exchange plan of a sharded merge, as host functions (cdb_merge_sharded computes the splits on
+ * the devices; constdb_amd/dist.py, one process per GPU, with torch.searchsorted, and takes its
+ * receive layout from cdb_shard_recv_plan: one plan for both drivers). No device needed.
+ * cdb_shard_splits: the owner slices of n_runs key-hash-ordered runs of one family (rows
+ * [run_start[r], run_start[r + 1]) of the hash column kh, a host array): out[r * (n_devices + 1) + d]
+ * = the first row of run r owned by device d or later (owner = the top log2(n_devices) hash bits).
+ * cdb_shard_recv_plan: the receive layout of one destination. counts = every source's rows for it,
+ * source after source, each as [3][n_runs[i]] (family-major). The destination receives one run per
+ * (source, source run) with rows in any family, in that order: recv_src / recv_run name them and
+ * run_start[f * (cap + 1) + k] is run k's first row of family f (run_start[f * (cap + 1) + n] the
+ * family's total, also in totals[f]). CDB_BAD_ARGUMENT (with *n_recv_runs set) when more than cap
+ * runs. */
+cdb_status cdb_shard_splits(const uint64_t* kh, const uint64_t* run_start, uint32_t n_runs, uint32_t n_devices,
+                            uint64_t* out);
+cdb_status cdb_shard_recv_plan(uint32_t n_sources, const uint32_t* n_runs, const uint64_t* counts, uint32_t cap,
+                               uint32_t* n_recv_runs, uint32_t* recv_src, uint32_t* recv_run, uint64_t* run_start,
+                               uint64_t* totals);
+
 /* ------------------------------------------------------------------ synthetic inputs
  * Seeded generator of replica states. Writes snapshot bytes
  * (for the decode path and the oracle) or device rows (for HBM-resident benches). */
