@@ -44,6 +44,7 @@ GEN_OPS_TAGS_ONLY = 4
 GEN_ROWS_RECORDS = 8
 DECODE_ROWS_RECORDS = 2
 DECODE_STREAM_ORDER = 4
+DECODE_KEEP_BYTES = 8
 
 
 class CstError(Exception):
@@ -228,7 +229,7 @@ ABI_FUNCTIONS = (
     "cdb_merged_free", "cdb_free",
     "cdb_dev_rows_alloc", "cdb_dev_rows_release", "cdb_merge_device", "cdb_partition_owner", "cdb_gen_default",
     "cdb_gen_snapshot", "cdb_gen_device", "cdb_decode_ops", "cdb_ops_info_get", "cdb_ops_free", "cdb_apply_ops", "cdb_gen_ops",
-    "cdb_encode_snapshot", "cdb_crc64_gpu", "cdb_upload_batches", "cdb_decode_snapshots_device",
+    "cdb_encode_snapshot", "cdb_encode_device", "cdb_crc64_gpu", "cdb_upload_batches", "cdb_decode_snapshots_device",
     "cdb_decode_ops_gpu", "cdb_ops_column", "cdb_snapshot_index_selftest", "cdb_merge_into",
     "cdb_merged_from_device", "cdb_dev_state_rows", "cdb_ctx_create_multi", "cdb_ctx_device_count",
     "cdb_ctx_shard", "cdb_merge_sharded", "cdb_dev_rows_alloc_records", "cdb_dev_output_compact",
@@ -306,6 +307,8 @@ def lib():
                                P(ctypes.c_size_t)]),
         "cdb_apply_ops": (c_st, [vp, vp, vp, P(vp), P(ApplyStats)]),
         "cdb_encode_snapshot": (c_st, [vp, vp, P(EncodeHeader), P(vp), P(ctypes.c_size_t), P(EncodeStats)]),
+        "cdb_encode_device": (c_st, [vp, P(DevOutput), P(vp), ctypes.c_uint32, P(EncodeHeader), P(vp),
+                                     P(ctypes.c_size_t), P(EncodeStats)]),
         "cdb_crc64_gpu": (c_st, [vp, ctypes.c_char_p, ctypes.c_size_t, P(ctypes.c_uint64)]),
         "cdb_upload_batches": (c_st, [vp, P(vp), ctypes.c_uint32, P(DevInput)]),
         "cdb_decode_snapshots_device": (c_st, [vp, P(ctypes.c_char_p), P(ctypes.c_size_t), ctypes.c_uint32,
@@ -467,12 +470,14 @@ def decode_snapshot_gpu(ctx: "Context", data: bytes, reference_checksum: bool = 
 
 
 def decode_snapshots_device(ctx: "Context", snaps, reference_checksum: bool = False,
-                            timing: Optional[dict] = None, records: bool = False, stream_order: bool = False):
+                            timing: Optional[dict] = None, records: bool = False, stream_order: bool = False,
+                            keep_bytes: bool = False):
     """GPU decode of several snapshots straight into HBM (cdb_decode_snapshots_device):
     returns (batches, DevInput) -- the rows of snapshot i at fold position i in one set of
     device columns (release each family with cdb_dev_rows_release), each batch holding the
     host side (bytes, references, header). Errors are raised for the failing snapshot. records: the rows
-    in the records layout (cdb_dev_rows.stride) instead of columns."""
+    in the records layout (cdb_dev_rows.stride) instead of columns; keep_bytes: the snapshot bytes
+    stay in HBM with the batches (cdb_encode_device)."""
     n = len(snaps)
     datas = [bytes(x) for x in snaps]
     bufs = (ctypes.c_char_p * max(n, 1))(*datas)
@@ -483,7 +488,7 @@ def decode_snapshots_device(ctx: "Context", snaps, reference_checksum: bool = Fa
     off = ctypes.c_size_t()
     ims, dms = ctypes.c_double(), ctypes.c_double()
     flags = ((DECODE_REFERENCE_CHECKSUM if reference_checksum else 0) | (DECODE_ROWS_RECORDS if records else 0)
-             | (DECODE_STREAM_ORDER if stream_order else 0))
+             | (DECODE_STREAM_ORDER if stream_order else 0) | (DECODE_KEEP_BYTES if keep_bytes else 0))
     st = lib().cdb_decode_snapshots_device(ctx.handle, bufs, lens, n, flags, hs, ctypes.byref(din),
                                            ctypes.byref(failed), ctypes.byref(off), ctypes.byref(ims),
                                            ctypes.byref(dms))
@@ -494,6 +499,58 @@ def decode_snapshots_device(ctx: "Context", snaps, reference_checksum: bool = Fa
     if st not in (OK, INVALID_SNAPSHOT_CHECKSUM):
         _raise(st, ctx.last_error(), offset=off.value)
     return batches, din
+
+
+def _encode_header(node_id, alias, addr, last_uuid, replicas, keep, rep=None):
+    """A cdb_encode_header; `replicas` None or a list of dicts in the shape Merged.replicas()
+    returns, or `rep` = (ReplicaEntry pointer, count) as cdb_merged_replicas gives. `keep` holds the
+    buffers the header points into."""
+    if rep is None:
+        if not replicas:
+            rep = (ctypes.POINTER(ReplicaEntry)(), 0)
+        else:
+            arr = (ReplicaEntry * len(replicas))()
+            for i, d in enumerate(replicas):
+                e = arr[i]
+                a = d["addr"].encode()
+                keep.append(a)
+                e.addr = a
+                if "add" in d:
+                    t, nid, al, uuid = d["add"]
+                    al = al.encode()
+                    keep.append(al)
+                    e.has_add, e.add_time, e.node_id, e.alias, e.uuid_he_sent = 1, t, nid, al, uuid
+                else:
+                    e.alias = b""
+                if "del" in d:
+                    e.has_del, e.del_time = 1, d["del"]
+            keep.append(arr)
+            rep = (ctypes.cast(arr, ctypes.POINTER(ReplicaEntry)), len(replicas))
+    a, ad = alias.encode(), addr.encode()
+    keep += [a, ad]
+    return EncodeHeader(node_id, a, len(a), ad, len(ad), last_uuid, rep[0], rep[1])
+
+
+def _take_bytes(out, n):
+    try:
+        return ctypes.string_at(out.value, n.value)
+    finally:
+        lib().cdb_free(out)
+
+
+def encode_device(ctx: "Context", out: "DevOutput", batches, node_id: int = 1, alias: str = "n1",
+                  addr: str = "127.0.0.1:9001", last_uuid: int = 0, replicas=None):
+    """cdb_encode_device: a cdb_merge_device result (either output layout) written as a snapshot
+    from HBM, fold position i resolving through batches[i]. Returns (bytes, EncodeStats)."""
+    keep = []
+    hdr = _encode_header(node_id, alias, addr, last_uuid, replicas, keep)
+    hs = (ctypes.c_void_p * max(len(batches), 1))(*[b.handle for b in batches])
+    o = ctypes.c_void_p()
+    n = ctypes.c_size_t()
+    st = EncodeStats()
+    ctx.check(lib().cdb_encode_device(ctx.handle, ctypes.byref(out), hs, len(batches), ctypes.byref(hdr),
+                                      ctypes.byref(o), ctypes.byref(n), ctypes.byref(st)))
+    return _take_bytes(o, n), st
 
 
 # ----------------------------------------------------------------- op stream (SURVEY §8f.2)
@@ -626,38 +683,15 @@ class Merged:
             ptr = ctypes.POINTER(ReplicaEntry)()
             n = ctypes.c_size_t()
             self._ctx.check(lib().cdb_merged_replicas(self._h, ctypes.byref(ptr), ctypes.byref(n)))
-            rep, nrep = ptr, n.value
-        elif not replicas:
-            rep, nrep = ctypes.POINTER(ReplicaEntry)(), 0
+            hdr = _encode_header(node_id, alias, addr, last_uuid, None, keep, rep=(ptr, n.value))
         else:
-            arr = (ReplicaEntry * len(replicas))()
-            for i, d in enumerate(replicas):
-                e = arr[i]
-                a = d["addr"].encode()
-                keep.append(a)
-                e.addr = a
-                if "add" in d:
-                    t, nid, al, uuid = d["add"]
-                    al = al.encode()
-                    keep.append(al)
-                    e.has_add, e.add_time, e.node_id, e.alias, e.uuid_he_sent = 1, t, nid, al, uuid
-                else:
-                    e.alias = b""
-                if "del" in d:
-                    e.has_del, e.del_time = 1, d["del"]
-            rep, nrep = ctypes.cast(arr, ctypes.POINTER(ReplicaEntry)), len(replicas)
-            keep.append(arr)
-        a, ad = alias.encode(), addr.encode()
-        hdr = EncodeHeader(node_id, a, len(a), ad, len(ad), last_uuid, rep, nrep)
+            hdr = _encode_header(node_id, alias, addr, last_uuid, replicas, keep)
         out = ctypes.c_void_p()
         n = ctypes.c_size_t()
         st = EncodeStats()
         self._ctx.check(lib().cdb_encode_snapshot(self._ctx.handle, self._h, ctypes.byref(hdr), ctypes.byref(out),
                                                   ctypes.byref(n), ctypes.byref(st)))
-        try:
-            return ctypes.string_at(out.value, n.value), st
-        finally:
-            lib().cdb_free(out)
+        return _take_bytes(out, n), st
 
     def apply_ops(self, ops: "Ops") -> "Merged":
         """cdb_apply_ops: the op stream applied on the device on top of this result (SURVEY

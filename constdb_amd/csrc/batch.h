@@ -85,6 +85,10 @@ struct DeviceRefs {
   void* dev = nullptr;
   uint64_t n = 0, nm = 0;
   std::vector<Patch> patch;
+  // CDB_DECODE_KEEP_BYTES: the snapshot bytes stay in HBM too (raw + raw_off = byte 0), for
+  // cdb_encode_device; freed with the batch
+  void* raw = nullptr;
+  uint64_t raw_off = 0;
   std::mutex mu;
   ~DeviceRefs();
 };

@@ -22,6 +22,8 @@
 namespace cdb {
 cdb_status encode_snapshot_impl(cdb_ctx* ctx, const cdb_merged& m, const cdb_encode_header& hdr, uint8_t** out,
                                 size_t* out_len, cdb_encode_stats* stats);
+cdb_status encode_device_impl(cdb_ctx* ctx, const cdb_dev_output& dout, const std::vector<Batch*>& inputs,
+                              const cdb_encode_header& hdr, uint8_t** out, size_t* out_len, cdb_encode_stats* stats);
 cdb_status crc64_gpu_impl(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t* crc);
 cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts,
                              cdb_dev_output* out, cdb_merge_stats* stats, hipStream_t s);
@@ -935,6 +937,23 @@ cdb_status cdb_encode_snapshot(cdb_ctx* ctx, cdb_merged* m, const cdb_encode_hea
   for (const auto& b : m->inputs)
     if (cdb_status st = refs_ready(ctx, b.get()); st != CDB_OK) return st;
   return encode_snapshot_impl(ctx, *m, *hdr, out, len, stats);
+}
+
+cdb_status cdb_encode_device(cdb_ctx* ctx, const cdb_dev_output* dout, cdb_batch* const* inputs, uint32_t n,
+                             const cdb_encode_header* hdr, uint8_t** out, size_t* len, cdb_encode_stats* stats) {
+  if (!ctx || !dout || !hdr || !out || !len || (n && !inputs)) return CDB_BAD_ARGUMENT;
+  if ((hdr->alias_len && !hdr->alias) || (hdr->addr_len && !hdr->addr) || (hdr->n_replicas && !hdr->replicas))
+    return CDB_BAD_ARGUMENT;
+  if (n > 255) return fail(ctx, CDB_BAD_ARGUMENT, "at most 255 inputs behind one result");
+  std::vector<Batch*> in(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!inputs[i]) return CDB_BAD_ARGUMENT;
+    in[i] = inputs[i]->b.get();
+  }
+  *out = nullptr;
+  *len = 0;
+  hipSetDevice(ctx->device);
+  return encode_device_impl(ctx, *dout, in, *hdr, out, len, stats);
 }
 
 cdb_status cdb_crc64_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t* crc) {

@@ -631,6 +631,7 @@ class GpuDecode {
   std::vector<uint64_t> noff_, moff_;
   std::vector<HostEntry> hosted_;
   DevBuf d_raw_, d_meta_, d_crc_, d_rows_, d_ord_, d_idx_raw_;
+  uint64_t raw_pad_ = 0;  // d_raw_ + raw_pad_ = byte 0 of the snapshot
   DeferredDatas defer_;
   IndexCursor* cursor_ = nullptr;
   struct CursorFree {
@@ -859,6 +860,7 @@ int GpuDecode::prepare_device(size_t* err_off) {
   const uint64_t tile = crc_tile_bytes();
   const uint64_t pad = dcrc_.pending ? (tile - dcrc_.len % tile) % tile : 0;
   if ((st_ = alloc(&d_raw_.p, pad + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK) return st_;
+  raw_pad_ = pad;
   // small device words: crc | node-row total | member-row total | host-tier flag
   if ((st_ = alloc(&d_crc_.p, 32, "decode: device checksum word")) != CDB_OK) return st_;
   uint64_t* d_small = (uint64_t*)d_crc_.p;
@@ -1022,11 +1024,12 @@ cdb_status GpuDecode::refs_to_batch(const DecArgs& A) {
 }
 
 DeviceRefs::~DeviceRefs() {
-  if (!dev) return;
+  if (!dev && !raw) return;
   int cur = 0;
   (void)hipGetDevice(&cur);
   (void)hipSetDevice(device);
-  (void)hipFree(dev);
+  if (dev) (void)hipFree(dev);
+  if (raw) (void)hipFree(raw);
   (void)hipSetDevice(cur);
 }
 
@@ -1348,6 +1351,11 @@ cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint6
   }
   r->dev = d_rows_.p;
   d_rows_.p = nullptr;
+  if (flags_ & CDB_DECODE_KEEP_BYTES) {
+    r->raw = d_raw_.p;
+    r->raw_off = raw_pad_;
+    d_raw_.p = nullptr;
+  }
   out_->dev_refs = std::move(r);
   (void)nn;
   return CDB_OK;

@@ -245,8 +245,9 @@ __global__ void __launch_bounds__(kST) tscan_apply(Tr tr, uint64_t n, const type
 }
 
 // ------------------------------------------------------------------ encode inputs in HBM
-struct PosBase {  // per fold position: where its arena and ref tables start
-  uint64_t arena, krow, mrow;
+struct EncPos {  // per fold position: its snapshot bytes and byte-reference tables (device pointers)
+  const uint8_t* raw;
+  const ByteRef *kref, *vref, *mref, *mvref;  // key/value refs by key src; member/value refs by member src
 };
 struct EncIn {
   // result rows (cdb_merged): key out meta ct ut dt win cref; node out node v t; member out t meta
@@ -254,34 +255,43 @@ struct EncIn {
   const uint64_t *nnode, *nv, *nt;
   const uint64_t *mt, *mmeta;
   uint64_t nk, nn, nm;
-  const uint8_t* arena;
-  const PosBase* pb;
-  const ByteRef *kref, *vref, *mref, *mvref;  // key/value refs by key src; member/value refs by member src
+  const EncPos* pos;
 };
 
 __device__ __forceinline__ ByteRef key_span(const EncIn& E, uint64_t meta, const uint8_t** p) {
-  const PosBase b = E.pb[meta_pos(meta)];
-  const ByteRef r = E.kref[b.krow + meta_src(meta)];
-  *p = E.arena + b.arena + r.off;
+  const EncPos& b = E.pos[meta_pos(meta)];
+  const ByteRef r = b.kref[meta_src(meta)];
+  *p = b.raw + r.off;
   return r;
 }
 __device__ __forceinline__ ByteRef val_span(const EncIn& E, uint64_t win, const uint8_t** p) {
-  const PosBase b = E.pb[meta_pos(win)];
-  const ByteRef r = E.vref[b.krow + meta_src(win)];
-  *p = E.arena + b.arena + r.off;
+  const EncPos& b = E.pos[meta_pos(win)];
+  const ByteRef r = b.vref[meta_src(win)];
+  *p = b.raw + r.off;
   return r;
 }
 __device__ __forceinline__ ByteRef mem_span(const EncIn& E, uint64_t meta, const uint8_t** p) {
-  const PosBase b = E.pb[meta_pos(meta)];
-  const ByteRef r = E.mref[b.mrow + meta_src(meta)];
-  *p = E.arena + b.arena + r.off;
+  const EncPos& b = E.pos[meta_pos(meta)];
+  const ByteRef r = b.mref[meta_src(meta)];
+  *p = b.raw + r.off;
   return r;
 }
 __device__ __forceinline__ ByteRef mval_span(const EncIn& E, uint64_t meta, const uint8_t** p) {
-  const PosBase b = E.pb[meta_pos(meta)];
-  const ByteRef r = E.mvref[b.mrow + meta_src(meta)];
-  *p = E.arena + b.arena + r.off;
+  const EncPos& b = E.pos[meta_pos(meta)];
+  const ByteRef r = b.mvref[meta_src(meta)];
+  *p = b.raw + r.off;
   return r;
+}
+
+// host-tier member refs of a device-decoded batch, written into its HBM tables (refs_ready's
+// patch step, on the device)
+struct RefPatch { uint64_t row; ByteRef m, mv; };
+__global__ void patch_refs_kernel(const RefPatch* pt, uint64_t n, ByteRef* mref, ByteRef* mvref) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const RefPatch q = pt[i];
+  mref[q.row] = q.m;
+  mvref[q.row] = q.mv;
 }
 
 // 1. first child row of each key -> key index + 1 (counter keys into nhead, set/dict into mhead)
@@ -709,6 +719,15 @@ cdb_status crc64_gpu_impl(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint64_t
   return hip_check(ctx, hipMemcpy(crc, dc.p, 8, hipMemcpyDeviceToHost), "d2h crc");
 }
 
+namespace {
+
+// Steps 1-6 of the encoder over result rows and byte tables already in HBM (E; E.pos set).
+// ev.e[0] / e[1] were recorded by the caller around its uploads.
+cdb_status encode_rows(cdb_ctx* ctx, const EncIn& E, const cdb_encode_header& hdr, uint8_t** out, size_t* out_len,
+                       cdb_encode_stats* stats, Events& ev);
+
+}  // namespace
+
 cdb_status encode_snapshot_impl(cdb_ctx* ctx, const cdb_merged& m, const cdb_encode_header& hdr, uint8_t** out,
                                 size_t* out_len, cdb_encode_stats* stats) {
   hipStream_t s = ctx->stream;
@@ -716,20 +735,21 @@ cdb_status encode_snapshot_impl(cdb_ctx* ctx, const cdb_merged& m, const cdb_enc
   if (nk >= 0xFFFFFFFFull) return fail(ctx, CDB_BAD_ARGUMENT, "encode: more than 2^32-2 key rows");
   Events ev;
   (void)hipEventRecord(ev.e[0], s);
-  // ---- uploads: result rows, per-position bases, ref tables, byte arenas
-  std::vector<PosBase> pb(m.inputs.size());
+  // ---- uploads: result rows, byte arenas and ref tables (one allocation each), position table
+  struct Base { uint64_t arena, krow, mrow; };
+  std::vector<Base> pb(m.inputs.size());
   uint64_t arena = 0, krow = 0, mrow = 0;
   for (size_t p = 0; p < m.inputs.size(); ++p) {
     const Batch& b = *m.inputs[p];
-    pb[p] = PosBase{arena, krow, mrow};
+    pb[p] = Base{arena, krow, mrow};
     arena += b.raw.size();
     krow += b.key_ref.size();
     mrow += b.m_ref.size();
   }
-  DevMem dk, dn, dm, dpb, dar, dkr, dvr, dmr, dmvr;
+  DevMem dk, dn, dm, dpos, dar, dkr, dvr, dmr, dmvr;
   cdb_status st;
   if ((st = dalloc(ctx, dk, 6 * nk * 8)) != CDB_OK || (st = dalloc(ctx, dn, 3 * nn * 8)) != CDB_OK ||
-      (st = dalloc(ctx, dm, 2 * nm * 8)) != CDB_OK || (st = dalloc(ctx, dpb, pb.size() * sizeof(PosBase))) != CDB_OK ||
+      (st = dalloc(ctx, dm, 2 * nm * 8)) != CDB_OK || (st = dalloc(ctx, dpos, pb.size() * sizeof(EncPos))) != CDB_OK ||
       (st = dalloc(ctx, dar, arena + 8)) != CDB_OK || (st = dalloc(ctx, dkr, krow * sizeof(ByteRef))) != CDB_OK ||
       (st = dalloc(ctx, dvr, krow * sizeof(ByteRef))) != CDB_OK ||
       (st = dalloc(ctx, dmr, mrow * sizeof(ByteRef))) != CDB_OK ||
@@ -762,27 +782,151 @@ cdb_status encode_snapshot_impl(cdb_ctx* ctx, const cdb_merged& m, const cdb_enc
   E.nk = nk;
   E.nn = nn;
   E.nm = nm;
-  if ((st = h2d(ctx, dpb.p, pb.data(), pb.size() * sizeof(PosBase), s)) != CDB_OK) return st;
+  std::vector<EncPos> pos(m.inputs.size());
   for (size_t p = 0; p < m.inputs.size(); ++p) {
     const Batch& b = *m.inputs[p];
-    if ((st = h2d(ctx, (uint8_t*)dar.p + pb[p].arena, b.raw.data(), b.raw.size(), s)) != CDB_OK ||
-        (st = h2d(ctx, (ByteRef*)dkr.p + pb[p].krow, b.key_ref.data(), b.key_ref.size() * sizeof(ByteRef), s)) !=
-            CDB_OK ||
-        (st = h2d(ctx, (ByteRef*)dvr.p + pb[p].krow, b.val_ref.data(), b.val_ref.size() * sizeof(ByteRef), s)) !=
-            CDB_OK ||
-        (st = h2d(ctx, (ByteRef*)dmr.p + pb[p].mrow, b.m_ref.data(), b.m_ref.size() * sizeof(ByteRef), s)) !=
-            CDB_OK ||
-        (st = h2d(ctx, (ByteRef*)dmvr.p + pb[p].mrow, b.m_vref.data(), b.m_vref.size() * sizeof(ByteRef), s)) !=
-            CDB_OK)
+    pos[p] = EncPos{(const uint8_t*)dar.p + pb[p].arena, (const ByteRef*)dkr.p + pb[p].krow,
+                    (const ByteRef*)dvr.p + pb[p].krow, (const ByteRef*)dmr.p + pb[p].mrow,
+                    (const ByteRef*)dmvr.p + pb[p].mrow};
+    if ((st = h2d(ctx, (void*)pos[p].raw, b.raw.data(), b.raw.size(), s)) != CDB_OK ||
+        (st = h2d(ctx, (void*)pos[p].kref, b.key_ref.data(), b.key_ref.size() * sizeof(ByteRef), s)) != CDB_OK ||
+        (st = h2d(ctx, (void*)pos[p].vref, b.val_ref.data(), b.val_ref.size() * sizeof(ByteRef), s)) != CDB_OK ||
+        (st = h2d(ctx, (void*)pos[p].mref, b.m_ref.data(), b.m_ref.size() * sizeof(ByteRef), s)) != CDB_OK ||
+        (st = h2d(ctx, (void*)pos[p].mvref, b.m_vref.data(), b.m_vref.size() * sizeof(ByteRef), s)) != CDB_OK)
       return st;
   }
-  E.arena = (const uint8_t*)dar.p;
-  E.pb = (const PosBase*)dpb.p;
-  E.kref = (const ByteRef*)dkr.p;
-  E.vref = (const ByteRef*)dvr.p;
-  E.mref = (const ByteRef*)dmr.p;
-  E.mvref = (const ByteRef*)dmvr.p;
+  if ((st = h2d(ctx, dpos.p, pos.data(), pos.size() * sizeof(EncPos), s)) != CDB_OK) return st;
+  E.pos = (const EncPos*)dpos.p;
   (void)hipEventRecord(ev.e[1], s);
+  return encode_rows(ctx, E, hdr, out, out_len, stats, ev);
+}
+
+cdb_status encode_device_impl(cdb_ctx* ctx, const cdb_dev_output& dout, const std::vector<Batch*>& inputs,
+                              const cdb_encode_header& hdr, uint8_t** out, size_t* out_len, cdb_encode_stats* stats) {
+  hipStream_t s = ctx->stream;
+  const uint64_t nk = dout.keys.n, nn = dout.nodes.n, nm = dout.members.n;
+  if (nk >= 0xFFFFFFFFull) return fail(ctx, CDB_BAD_ARGUMENT, "encode: more than 2^32-2 key rows");
+  if (dout.compact && (dout.keys.stride > 1 || dout.nodes.stride > 1 || dout.members.stride > 1))
+    return fail(ctx, CDB_BAD_ARGUMENT, "encode: a compacted result is in plain columns");
+  // the byte tables of device-decoded batches stay in HBM for the whole call (refs_ready and
+  // another encoder wait); a batch at several positions is locked once
+  std::vector<std::shared_ptr<DeviceRefs>> held;
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (Batch* b : inputs)
+    if (b->dev_refs && std::find(held.begin(), held.end(), b->dev_refs) == held.end()) held.push_back(b->dev_refs);
+  std::sort(held.begin(), held.end());  // (one lock order for every caller)
+  for (auto& r : held) locks.emplace_back(r->mu);
+  for (auto& r : held)
+    if ((r->dev || r->raw) && r->device != ctx->device)
+      return fail(ctx, CDB_BAD_ARGUMENT, "encode: byte references live on another device");
+  Events ev;
+  (void)hipEventRecord(ev.e[0], s);
+  cdb_status st;
+  // ---- result rows: the bucket layout compacted into temporary columns, dense columns as they are
+  cdb_dev_output dense;
+  std::memset(&dense, 0, sizeof dense);
+  struct Release {
+    cdb_ctx* c;
+    cdb_dev_output* d;
+    ~Release() {
+      cdb_dev_rows_release(c, &d->keys);
+      cdb_dev_rows_release(c, &d->nodes);
+      cdb_dev_rows_release(c, &d->members);
+    }
+  } release{ctx, &dense};
+  const cdb_dev_output* rows = &dout;
+  if (!dout.compact) {
+    if ((st = cdb_dev_rows_alloc(ctx, &dense.keys, nk, kKeyOutCols)) != CDB_OK ||
+        (st = cdb_dev_rows_alloc(ctx, &dense.nodes, nn, kNodeCols)) != CDB_OK ||
+        (st = cdb_dev_rows_alloc(ctx, &dense.members, nm, kMemberCols)) != CDB_OK ||
+        (st = cdb_dev_output_compact(ctx, &dout, &dense, s)) != CDB_OK)
+      return st;
+    rows = &dense;
+  }
+  EncIn E{};
+  E.kmeta = rows->keys.col[O_META];
+  E.kct = rows->keys.col[O_CT];
+  E.kut = rows->keys.col[O_UT];
+  E.kdt = rows->keys.col[O_DT];
+  E.kwin = rows->keys.col[O_WIN];
+  E.kcref = rows->keys.col[O_CREF];
+  E.nnode = rows->nodes.col[C_ID1];
+  E.nv = rows->nodes.col[C_ID2];
+  E.nt = rows->nodes.col[C_T];
+  E.mt = rows->members.col[C_T];
+  E.mmeta = rows->members.col[C_META];
+  E.nk = nk;
+  E.nn = nn;
+  E.nm = nm;
+  // ---- per position: snapshot bytes and byte references from HBM where the decode left them,
+  // else uploaded (host tables: one allocation per batch)
+  std::vector<EncPos> pos(inputs.size());
+  std::vector<std::unique_ptr<DevMem>> tmp;
+  for (size_t p = 0; p < inputs.size(); ++p) {
+    Batch& b = *inputs[p];
+    DeviceRefs* r = b.dev_refs.get();
+    if (r && r->raw) {
+      pos[p].raw = (const uint8_t*)r->raw + r->raw_off;
+    } else {
+      tmp.emplace_back(new DevMem);
+      if ((st = dalloc(ctx, *tmp.back(), b.raw.size() + 8)) != CDB_OK ||
+          (st = h2d(ctx, tmp.back()->p, b.raw.data(), b.raw.size(), s)) != CDB_OK)
+        return st;
+      pos[p].raw = (const uint8_t*)tmp.back()->p;
+    }
+    if (r && r->dev) {
+      ByteRef* d = (ByteRef*)r->dev;
+      if (!r->patch.empty()) {  // host-tier member refs: into the HBM tables once
+        static_assert(sizeof(RefPatch) == sizeof(DeviceRefs::Patch), "patch layout");
+        DevMem dp;
+        const uint64_t np = r->patch.size();
+        if ((st = dalloc(ctx, dp, np * sizeof(RefPatch))) != CDB_OK ||
+            (st = hip_check(ctx, hipMemcpyAsync(dp.p, r->patch.data(), np * sizeof(RefPatch), hipMemcpyHostToDevice, s),
+                            "h2d(patch)")) != CDB_OK)
+          return st;
+        patch_refs_kernel<<<(np + 255) / 256, 256, 0, s>>>((const RefPatch*)dp.p, np, d + 2 * r->n,
+                                                            d + 2 * r->n + r->nm);
+        if ((st = launch_check(ctx, s, "patch_refs")) != CDB_OK ||
+            (st = hip_check(ctx, hipStreamSynchronize(s), "sync(patch)")) != CDB_OK)
+          return st;
+        r->patch.clear();
+      }
+      pos[p].kref = d;
+      pos[p].vref = d + r->n;
+      pos[p].mref = d + 2 * r->n;
+      pos[p].mvref = d + 2 * r->n + r->nm;
+    } else {
+      const uint64_t n = b.key_ref.size(), mn = b.m_ref.size();
+      tmp.emplace_back(new DevMem);
+      if ((st = dalloc(ctx, *tmp.back(), (2 * n + 2 * mn) * sizeof(ByteRef))) != CDB_OK) return st;
+      ByteRef* d = (ByteRef*)tmp.back()->p;
+      if ((st = h2d(ctx, d, b.key_ref.data(), n * sizeof(ByteRef), s)) != CDB_OK ||
+          (st = h2d(ctx, d + n, b.val_ref.data(), n * sizeof(ByteRef), s)) != CDB_OK ||
+          (st = h2d(ctx, d + 2 * n, b.m_ref.data(), mn * sizeof(ByteRef), s)) != CDB_OK ||
+          (st = h2d(ctx, d + 2 * n + mn, b.m_vref.data(), mn * sizeof(ByteRef), s)) != CDB_OK)
+        return st;
+      pos[p].kref = d;
+      pos[p].vref = d + n;
+      pos[p].mref = d + 2 * n;
+      pos[p].mvref = d + 2 * n + mn;
+    }
+  }
+  DevMem dpos;
+  if ((st = dalloc(ctx, dpos, pos.size() * sizeof(EncPos))) != CDB_OK ||
+      (st = h2d(ctx, dpos.p, pos.data(), pos.size() * sizeof(EncPos), s)) != CDB_OK)
+    return st;
+  E.pos = (const EncPos*)dpos.p;
+  (void)hipEventRecord(ev.e[1], s);
+  return encode_rows(ctx, E, hdr, out, out_len, stats, ev);
+}
+
+namespace {
+
+cdb_status encode_rows(cdb_ctx* ctx, const EncIn& E, const cdb_encode_header& hdr, uint8_t** out, size_t* out_len,
+                       cdb_encode_stats* stats, Events& ev) {
+  hipStream_t s = ctx->stream;
+  const uint64_t nk = E.nk, nn = E.nn, nm = E.nm;
+  cdb_status st;
 
   // ---- 1-3. sizing scans
   DevMem dnh, dmh, dpn, dpa, dpd, dpc, dko, dtot, dcb;
@@ -912,6 +1056,8 @@ cdb_status encode_snapshot_impl(cdb_ctx* ctx, const cdb_merged& m, const cdb_enc
   }
   return CDB_OK;
 }
+
+}  // namespace
 
 // CRC-64/Jones of a device buffer whose length is a multiple of crc_tile_bytes() (leading
 // zero bytes do not change it); the result lands in d_crc. Synchronises the stream.

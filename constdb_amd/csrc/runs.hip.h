@@ -405,7 +405,8 @@ __device__ __forceinline__ uint32_t xcd_bucket(uint32_t blk, uint32_t G, int wv)
 __global__ void __launch_bounds__(kWavesPerWG * 64, 5) bucket_wave_runs_kernel(WaveArgs W) {
   __shared__ WaveLds<1> lds_all[kWavesPerWG];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t b = W.blo + xcd_bucket(blockIdx.x, gridDim.x, wv);
+  // (wave-uniform: scalar loads of the bucket's directory entry)
+  const uint32_t b = __builtin_amdgcn_readfirstlane(W.blo + xcd_bucket(blockIdx.x, gridDim.x, wv));
   if (b >= W.bhi) return;
   const WaveDir d = load_dir(W.A, b);
   if (d.N + d.M <= 64) {  // (wave-uniform) one child slot per lane

@@ -72,9 +72,12 @@ enum {
                                               practically every well-formed dump) */
   CDB_DECODE_ROWS_RECORDS = 1u << 1,       /* cdb_decode_snapshots_device: emit the rows in the
                                               records layout (cdb_dev_rows) instead of columns */
-  CDB_DECODE_STREAM_ORDER = 1u << 2        /* cdb_decode_snapshots_device: leave a snapshot that is not
+  CDB_DECODE_STREAM_ORDER = 1u << 2,       /* cdb_decode_snapshots_device: leave a snapshot that is not
                                               in key-hash order in stream order (n_runs = 0) instead
                                               of sorting it into a run */
+  CDB_DECODE_KEEP_BYTES = 1u << 3          /* cdb_decode_snapshots_device: keep the snapshot bytes in
+                                              HBM with the batch (for cdb_encode_device; the host
+                                              copy stays too) */
 };
 cdb_status cdb_decode_snapshot(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags,
                                cdb_batch** out, size_t* err_offset);
@@ -428,6 +431,18 @@ cdb_status cdb_upload_batches(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n
  * (canonical dump, replicas, encode, op apply, cdb_merge_into). */
 cdb_status cdb_merged_from_device(cdb_ctx* ctx, cdb_merged* state, cdb_batch* const* inputs, uint32_t n,
                                   const cdb_dev_output* out, cdb_merged** m);
+
+/* cdb_encode_snapshot of a cdb_merge_device result without its host view (server.rs:183-215 for a
+ * node whose state is in HBM): the result rows (either output layout) are read where the merge left
+ * them, fold position i resolves through inputs[i] -- their byte references from HBM while a device
+ * decode still holds them there (cdb_decode_snapshots_device; host-tier member references are
+ * patched into those tables), their snapshot bytes from HBM when decoded with
+ * CDB_DECODE_KEEP_BYTES, everything else uploaded. No result row crosses PCIe; the stream comes
+ * back once. Byte for byte the stream cdb_encode_snapshot writes for
+ * cdb_merged_from_device(ctx, NULL, inputs, n, out). A result whose position 0 was a previous
+ * result (cdb_dev_state_rows) needs that chain's host view: use cdb_merged_from_device. */
+cdb_status cdb_encode_device(cdb_ctx* ctx, const cdb_dev_output* out, cdb_batch* const* inputs, uint32_t n,
+                             const cdb_encode_header* hdr, uint8_t** bytes, size_t* len, cdb_encode_stats* stats);
 
 /* A merge result kept in HBM as fold position 0 of the next cdb_merge_device (the reference's
  * persistent server.db, replica/pull.rs:120-128): `state` rows (either output layout) are copied
