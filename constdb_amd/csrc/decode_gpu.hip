@@ -22,6 +22,7 @@
 #include <atomic>
 #include <chrono>
 #include <thread>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -1381,6 +1382,33 @@ int decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t f
   return st != CDB_OK ? (int)st : rc;
 }
 
+namespace {
+struct PhaseClock {
+  const char* path = std::getenv("CDB_DECODE_TRACE");
+  std::chrono::steady_clock::time_point last;
+  std::string json;
+  explicit PhaseClock(std::chrono::steady_clock::time_point t0) : last(t0) {}
+  void mark(const char* name) {
+    if (!path) return;
+    const auto now = std::chrono::steady_clock::now();
+    char b[96];
+    std::snprintf(b, sizeof b, "%s\"%s_ms\": %.3f", json.empty() ? "" : ", ", name,
+                  std::chrono::duration<double, std::milli>(now - last).count());
+    json += b;
+    last = now;
+  }
+  void write(uint32_t n, uint64_t bytes, const uint64_t* rows, bool runs) {
+    if (!path) return;
+    if (FILE* f = std::fopen(path, "a")) {
+      std::fprintf(f, "{\"snapshots\": %u, \"bytes\": %llu, \"rows\": [%llu, %llu, %llu], \"runs\": %d, %s}\n", n,
+                   (unsigned long long)bytes, (unsigned long long)rows[0], (unsigned long long)rows[1],
+                   (unsigned long long)rows[2], runs ? 1 : 0, json.c_str());
+      std::fclose(f);
+    }
+  }
+};
+}  // namespace
+
 int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, uint32_t n,
                                 uint32_t flags, Batch* const* outs, cdb_dev_input* din, uint32_t* failed,
                                 size_t* err_off, DecodeTiming* tm) {
@@ -1410,6 +1438,9 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     for (auto& t : th) t.join();
   }
   if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+  // CDB_DECODE_TRACE=<file>: one JSON line of phase times (host clock, ms) appended per call
+  PhaseClock clk(t_start);
+  clk.mark("index");
   {
     // the deferred DATAS sections, side by side: every snapshot's bytes go up (one after another
     // through the staging ring) with its speculative walk queued behind them on its own stream,
@@ -1457,6 +1488,7 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
       if (k) (void)hipStreamDestroy(k);
     if (st != CDB_OK) return st;
   }
+  clk.mark("deferred_datas");
   for (uint32_t i = 0; i < n; ++i) {
     size_t eo = ieo[i];
     int rc = irc[i];
@@ -1477,6 +1509,7 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
   }
   if (tot[0] >= (1ull << 32) || tot[1] >= (1ull << 32) || tot[2] >= (1ull << 32))
     return fail(ctx, CDB_BAD_ARGUMENT, "decoded rows exceed 2^32 per family");
+  clk.mark("prepare_device");
   cdb_status st;
   // one run per snapshot when every snapshot is in key-hash order (written from a merge result)
   bool runs = n <= CDB_MAX_RUNS;
@@ -1491,6 +1524,7 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
       runs = dec[i]->sorted();
     }
   }
+  clk.mark("order_sort");
   std::memset(din, 0, sizeof *din);
   const bool rec = flags & CDB_DECODE_ROWS_RECORDS;
   auto alloc = [&](cdb_dev_rows* r, uint64_t rows, int nc) {
@@ -1531,6 +1565,12 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
   if (runs) {
     din->n_runs = n;
     for (int f = 0; f < 3; ++f) din->run_start[f][n] = o[f];
+  }
+  clk.mark("alloc_emit");
+  {
+    uint64_t bytes = 0;
+    for (uint32_t i = 0; i < n; ++i) bytes += lens[i];
+    clk.write(n, bytes, tot, runs);
   }
   if (tm)  // everything but the host index passes (the snapshots' device work overlaps)
     tm->device_ms =

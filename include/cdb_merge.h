@@ -410,11 +410,14 @@ typedef struct cdb_dev_output {
   cdb_dev_buckets buckets; /* compact = 0 only */
 } cdb_dev_output;
 
-/* Multi-GPU pack step: groups the rows of one family by owner rank = the
- * top `owner_bits` bits of column 0 (key hash, or parent key hash for children, so a key and
- * its children go to the same rank) into `out` (caller-allocated, >= in->n rows, same
- * columns), and writes the 2^owner_bits per-owner row counts to the host array `counts`.
- * The caller then exchanges the rows with an RCCL all-to-all (constdb_amd/dist.py). */
+/* Owner grouping for inputs that are not in runs: a counting-sort scatter of one
+ * family's rows by owner = the top `owner_bits` bits (0..9) of column 0 (key hash, or parent key
+ * hash for children, so a key and its children share an owner) into `out` (caller-allocated,
+ * >= in->n rows, `ncols` = 6, 7 or 8 fields, either input layout on either side); the 2^owner_bits
+ * per-owner row counts go to the host array `counts`, so owner d's rows are out's rows
+ * [sum(counts[<d]), sum(counts[<=d])). cdb_merge_sharded calls it for such inputs (their owner
+ * slices then travel as one unsorted run each); inputs in runs need no grouping: their owner
+ * slices are found by binary search (cdb_shard_splits). */
 cdb_status cdb_partition_owner(cdb_ctx* ctx, const cdb_dev_rows* in, int ncols, int owner_bits,
                                cdb_dev_rows* out, uint64_t* counts, void* stream);
 

@@ -1,6 +1,10 @@
 """Snapshot decode bench: one seeded replica snapshot decoded by the host decoder
 (cdb_decode_snapshot) and by the GPU path (cdb_decode_snapshot_gpu: host entry index, HIP
-count/emit kernels, staged download into the host batch). Prints one JSON line, best of --reps."""
+count/emit kernels, staged download into the host batch); then R replica snapshots (generator
+order: the reference's unordered HashMap layout, sorted into runs on the device) decoded straight
+into HBM, with the library's phase clock (CDB_DECODE_TRACE), and that decode followed by the
+cdb_merge_device of its rows (bucket layout) beside the merge alone. Prints one JSON line, best of
+--reps."""
 import argparse
 import json
 import os
@@ -19,7 +23,7 @@ def main():
     ap.add_argument("--universe", type=int, default=8_000_000)
     ap.add_argument("--replicas", type=int, default=8)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--device-snapshots", type=int, default=4,
+    ap.add_argument("--device-snapshots", type=int, default=8,
                     help="replica snapshots decoded straight into HBM (0: skip)")
     a = ap.parse_args()
     cfg = cdb.gen_config(seed=4, universe=a.universe, n_replicas=a.replicas, replica_hi=a.replicas)
@@ -58,17 +62,37 @@ def main():
         def release(din):
             for fam in (din.keys, din.nodes, din.members):
                 L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
-        bs, din = cdb.decode_snapshots_device(ctx, snaps)  # warm-up
+        import tempfile
+        trace = os.path.join(tempfile.mkdtemp(), "decode_trace.jsonl")
+        os.environ["CDB_DECODE_TRACE"] = trace
+
+        def merge(din):
+            dout = cdb.DevOutput()
+            dout.compact = 0
+            opts = cdb.merge_opts()
+            st = cdb.MergeStats()
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(din), ctypes.byref(opts), ctypes.byref(dout),
+                                         ctypes.byref(st), None))
+            torch.cuda.synchronize()
+            return time.perf_counter() - t, st
+        bs, din = cdb.decode_snapshots_device(ctx, snaps, records=True)  # warm-up
+        merge(din)
         release(din)
         del bs
-        dev = up = None
+        dev = up = mrg = None
         for _ in range(a.reps):
             tm = {}
             t = time.perf_counter()
-            bs, din = cdb.decode_snapshots_device(ctx, snaps, timing=tm)
+            bs, din = cdb.decode_snapshots_device(ctx, snaps, timing=tm, records=True)
             dt = time.perf_counter() - t
+            with open(trace) as f:
+                phases = json.loads(f.read().strip().split("\n")[-1])
+            mt, mst = merge(din)
             if dev is None or dt < dev[0]:
-                dev = (dt, tm)
+                dev = (dt, tm, phases, din.n_runs)
+            mrg = (mt, mst) if mrg is None or mt < mrg[0] else mrg
             release(din)
             del bs
             t = time.perf_counter()
@@ -80,10 +104,16 @@ def main():
             up = dt if up is None else min(up, dt)
             release(din)
             del hb
-        out["device_resident"] = {"snapshots": R, "bytes": sum(len(x) for x in snaps),
+        nbytes = sum(len(x) for x in snaps)
+        out["device_resident"] = {"snapshots": R, "bytes": nbytes, "layout": "records", "runs": dev[3],
                                   "decode_to_hbm_ms": dev[0] * 1e3, "index_ms": dev[1]["index_ms"],
-                                  "device_ms": dev[1]["device_ms"],
+                                  "device_ms": dev[1]["device_ms"], "phases": dev[2],
+                                  "effective_gbs": nbytes / dev[0] / 1e9,
                                   "host_decode_plus_upload_ms": up * 1e3}
+        out["decode_plus_merge"] = {"decode_ms": dev[0] * 1e3, "merge_ms": mrg[0] * 1e3,
+                                    "total_ms": (dev[0] + mrg[0]) * 1e3,
+                                    "total_over_merge": (dev[0] + mrg[0]) / mrg[0],
+                                    "sorted_runs": mrg[1].sorted_runs, "key_rows_out": mrg[1].key_rows_out}
     print(json.dumps(out))
 
 

@@ -60,7 +60,17 @@ def _roundtrip_vs_oracle(stream, snaps):
     assert rc2 == 0 and got == want
 
 
-def _case(ctx, snaps, records=True, compact=False, keep_bytes=True, host_refs_first=False, device_decode=True):
+def _writer_check(stream):
+    """The oracle's writer restatement (db.rs:122-136, object.rs:85-108, replica.rs:100-119) over the
+    oracle's load of the stream reproduces it byte for byte (the order is the stream's)."""
+    h = o.NodeHeader(node_id=5, alias="a5", addr="10.0.0.5:9001", last_uuid=1234)
+    h.replicas_add = [(7, 2, "n2", "10.0.0.2:9001", 99)]
+    h.replicas_del = [("10.0.0.3:9001", 11)]
+    assert o.dump_all(o.fold_snapshots([stream]), h) == stream
+
+
+def _case(ctx, snaps, records=True, compact=False, keep_bytes=True, host_refs_first=False, device_decode=True,
+          writer=False):
     if device_decode:
         batches, din = cdb.decode_snapshots_device(ctx, snaps, records=records, keep_bytes=keep_bytes)
     else:
@@ -82,6 +92,8 @@ def _case(ctx, snaps, records=True, compact=False, keep_bytes=True, host_refs_fi
         assert (est.bytes, est.checksum, est.data_entries, est.expires, est.deletes) == \
             (wst.bytes, wst.checksum, wst.data_entries, wst.expires, wst.deletes)
         _roundtrip_vs_oracle(got, snaps)
+        if writer:
+            _writer_check(got)
         return est
     finally:
         _release(ctx, din)
@@ -94,7 +106,7 @@ def _case(ctx, snaps, records=True, compact=False, keep_bytes=True, host_refs_fi
 @pytest.mark.parametrize("seed", range(3))
 def test_encode_device_random(ctx, seed, records, compact, keep_bytes):
     snaps = gen_replicas(seed, n_replicas=2 + seed, n_keys=60 + 11 * seed, p_conflict=0.1, p_side=0.3)
-    _case(ctx, snaps, records=records, compact=compact, keep_bytes=keep_bytes)
+    _case(ctx, snaps, records=records, compact=compact, keep_bytes=keep_bytes, writer=True)
 
 
 def test_encode_device_after_refs_downloaded(ctx):
@@ -152,3 +164,13 @@ def test_encode_device_rejects_bad_arguments(ctx):
                                None) == cdb.BAD_ARGUMENT
     assert L.cdb_encode_device(ctx.handle, ctypes.byref(dout), None, 1, ctypes.byref(hdr), ctypes.byref(o_),
                                ctypes.byref(n), None) == cdb.BAD_ARGUMENT
+
+
+def test_encode_device_c4_1m(ctx):
+    """C4's shape (the bench's generator config) at 1M keys x 8 replicas: decoded into HBM with the
+    bytes kept, merged into the bucket layout, encoded from HBM; equal to the host view's stream, and
+    the C++ oracle's load + fold of that stream equals its fold of the eight snapshots."""
+    from constdb_amd import configs
+    cfg = configs.c4(cdb, 1_000_000)
+    est = _case(ctx, [cdb.gen_snapshot(cfg, r) for r in range(8)])
+    assert est.data_entries > 900_000
