@@ -136,8 +136,6 @@ struct RunView {
   const uint64_t* nin[kNodeCols];
   const uint64_t* min[kMemberCols];
   uint32_t ks, ns, ms;        // record strides of the families (1: plain columns; common.h row_field)
-  uint32_t staged;            // records layout of every family: a bucket's record bytes go to LDS
-                              // in 16-B pieces (load_runs_staged)
 };
 
 struct WaveArgs {
@@ -634,21 +632,10 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     En[e] = __ballot(cemit[e] && knode[e]);
     Em[e] = __ballot(cemit[e] && !knode[e]);
   }
-  // output positions: the bucket's row slots (its input offsets). The rows are assembled in LDS (the
-  // sort words and the row union are dead from here on) and leave as whole 16-B pieces, 64 of them
-  // per store instruction over the bucket's contiguous output range -- not one scattered 16-B piece
-  // per lane and row.
+  // output positions: the bucket's row slots (its input offsets); each lane stores its rows whole
+  // (16-B pieces). Staging the rows in LDS for wave-contiguous stores was measured slower (C4:
+  // 20.5 -> 21.3 ms with per-lane record loads, the extra LDS round trip and VALU outweigh it).
   const uint64_t xk = kb, xn = nb0, xm = mb0;
-  // (addressed from the struct's base: the stage spans the sort words and the union behind them)
-  char* const stage = reinterpret_cast<char*>(&L) + offsetof(WaveLds<KE>, sw);
-  constexpr uint32_t kOutStage = (uint32_t)(sizeof(WaveLds<KE>) - offsetof(WaveLds<KE>, sw));
-  uint32_t NN = 0, NM = 0;
-#pragma unroll
-  for (int e = 0; e < CE; ++e) {
-    NN += __popcll(En[e]);
-    NM += __popcll(Em[e]);
-  }
-  const bool cstaged = (NN + NM) * 48 <= kOutStage;
   uint32_t nbase = 0, mbase = 0;
 #pragma unroll
   for (int e = 0; e < CE; ++e) {
@@ -656,9 +643,8 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
       const uint32_t crank = (knode[e] ? nbase : mbase) + lane_rank(knode[e] ? En[e] : Em[e]);
       const uint32_t k = (uint32_t)(sw_[e] >> 56) & (KC - 1);
       const uint64_t id2 = knode[e] ? c_v[e] : sid2[e];
-      {  // one whole 48-B AoS row: node rows first, then member rows
-        ulonglong2* row = cstaged ? (ulonglong2*)(stage + 48 * (knode[e] ? crank : NN + crank))
-                                  : (ulonglong2*)((knode[e] ? A.nos : A.mos) + ((knode[e] ? xn : xm) + crank) * kChildStride);
+      {  // one whole 48-B AoS row
+        ulonglong2* row = (ulonglong2*)((knode[e] ? A.nos : A.mos) + ((knode[e] ? xn : xm) + crank) * kChildStride);
         row[0] = make_ulonglong2(L.okh[k], L.okf[k]);
         row[1] = make_ulonglong2(sid1[e], id2);
         row[2] = make_ulonglong2(c_t[e], c_m[e]);
@@ -672,20 +658,8 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     mbase += __popcll(Em[e]);
   }
   wave_sync();
-  if (cstaged) {  // (wave-uniform)
-    ulonglong2* const nos = reinterpret_cast<ulonglong2*>(A.nos + xn * kChildStride);
-    ulonglong2* const mos = reinterpret_cast<ulonglong2*>(A.mos + xm * kChildStride);
-    const ulonglong2* const src = reinterpret_cast<const ulonglong2*>(stage);
-    for (uint32_t p = lane; p < 3 * (NN + NM); p += 64) {
-      const ulonglong2 v = src[p];
-      if (p < 3 * NN) nos[p] = v;
-      else mos[p - 3 * NN] = v;
-    }
-    wave_sync();  // (the key rows are staged over the same bytes next)
-  }
 
   // ------------------------------------------------------------ 5. key outputs
-  static_assert(64 * KE * 64 <= kOutStage, "a bucket's key rows fit the output stage");
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
     if (emit[e]) {
@@ -693,20 +667,14 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
       const uint64_t win = (fam[e] == 0 && o_T[e] == TAG_COUNTER) ? L.osum[r] : o_win[e];
       // child ranges: bucket-relative (compaction makes them absolute)
       const uint64_t cref = cref_pack(L.ocnt[r] ? L.ocb[r] : 0, L.ocnt[r]);
-      {  // one whole 64-B AoS row, staged at its output rank
-        ulonglong2* row = (ulonglong2*)(stage + 64 * r);
+      {  // one whole 64-B AoS row
+        ulonglong2* row = (ulonglong2*)(A.kos + (xk + r) * kKeyOutCols);
         row[0] = make_ulonglong2(kh[e], kf[e]);
         row[1] = make_ulonglong2(o_ct[e], o_ut[e]);
         row[2] = make_ulonglong2(o_dt[e], o_meta[e]);
         row[3] = make_ulonglong2(win, cref);
       }
     }
-  }
-  wave_sync();
-  {
-    ulonglong2* const kos = reinterpret_cast<ulonglong2*>(A.kos + xk * kKeyOutCols);
-    const ulonglong2* const src = reinterpret_cast<const ulonglong2*>(stage);
-    for (uint32_t p = lane; p < 4 * kout; p += 64) kos[p] = src[p];
   }
   if (lane == 0) {
     A.kout[b] = kout;

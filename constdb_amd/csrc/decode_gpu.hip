@@ -362,18 +362,31 @@ constexpr uint64_t kIdxChunk = 8192;
 constexpr uint32_t kIdxSync = 16;
 constexpr uint32_t kIdxSyncTries = 256;  // offsets tried per chunk (4 rounds of 64 lanes)
 constexpr uint64_t kIdxEntryMax = 1u << 16;
+// The walk reads its chunk and the first kIdxTail bytes after it from LDS (one copy per wave).
+constexpr uint64_t kIdxTail = 4096, kIdxWin = kIdxChunk + kIdxTail;
+// Entries starting in one chunk: a DATAS entry takes at least 6 bytes (key length, three times,
+// the tag, one payload length), so at most kIdxChunk / 6 + 1 start in a chunk.
+constexpr uint32_t kIdxRelCap = (uint32_t)(kIdxChunk / 6 + 2);
 
+// A cursor over the stream; bytes [wlo, wlo + wlen) come from an LDS copy (the walk's window),
+// the rest from global memory.
 struct DCur {
   const uint8_t* p;
   uint64_t n, off;
+  const uint8_t* lds = nullptr;
+  uint64_t wlo = 0, wlen = 0;
+  __device__ __forceinline__ uint32_t at(uint64_t i) const {
+    const uint64_t r = i - wlo;
+    return r < wlen ? lds[r] : p[i];
+  }
 };
 __device__ __forceinline__ bool dc_int(DCur& c, int64_t* v) {
   if (c.off >= c.n) return false;
-  const uint32_t f = c.p[c.off++];
+  const uint32_t f = c.at(c.off++);
   const uint32_t sz = (f >> 6) == 0 ? 0 : (f >> 6) == 1 ? 1 : (f >> 6) == 2 ? 3 : 8;
   if (sz > c.n - c.off) return false;
   uint64_t x = sz == 8 ? 0 : (f & 0x3F);
-  for (uint32_t i = 0; i < sz; ++i) x = (x << 8) | c.p[c.off + i];
+  for (uint32_t i = 0; i < sz; ++i) x = (x << 8) | c.at(c.off + i);
   c.off += sz;
   *v = (int64_t)x;
   return true;
@@ -395,7 +408,7 @@ __device__ bool dc_data_entry(DCur& c, uint64_t lim) {
   int64_t v;
   if (!dc_span(c, lim) || !dc_int(c, &v) || !dc_int(c, &v) || !dc_int(c, &v)) return false;
   if (c.off >= c.n) return false;
-  const uint32_t tag = c.p[c.off++];
+  const uint32_t tag = c.at(c.off++);
   uint64_t cnt;
   switch (tag) {
     case TAG_COUNTER:
@@ -434,26 +447,42 @@ struct IdxArgs {
   const uint64_t* tbase;   // record pass: index of that entry in the section
   const uint32_t* tcount;  // record pass: entries of the true chain in chunk t
   uint64_t* out;           // record pass: entry offsets
+  uint16_t* rel;           // per chunk: the walked chain's entry offsets relative to the chunk start
+                           // (kIdxRelCap slots per chunk; the record pass expands the true chain's)
 };
 
 // One wave per chunk. req == null: the speculative pass (sync search by the 64 lanes, then the
 // walk by lane 0); req[t] != ~0: lane 0 walks chunk t again from req[t] (the offset at which the
 // true chain enters it), other chunks keep their results.
 __global__ void __launch_bounds__(256) idx_walk_kernel(IdxArgs a, const uint64_t* __restrict__ req) {
-  const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  __shared__ __attribute__((aligned(16))) uint8_t win_all[4][kIdxWin];
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t t = blockIdx.x * 4 + wv;
   if (t >= a.T) return;
   const uint64_t lo = a.S + (uint64_t)t * kIdxChunk, hi = min(a.n, lo + kIdxChunk);
   uint64_t o = lo;
   if (req) {
     if (req[t] == ~0ull) return;
     o = req[t];
-  } else if (t > 0) {
+  }
+  // the window: [lo16, lo16 + kIdxWin) with lo16 = lo rounded down to 16 B, copied in 16-B pieces
+  // (a piece that starts before the end of the stream may read up to 15 bytes past it: the device
+  // copy has 16 bytes of slack)
+  uint8_t* win = win_all[wv];
+  const uint64_t lo16 = lo & ~15ull;
+  const uint64_t wend = min(lo16 + kIdxWin, (a.n + 15) & ~15ull);
+  for (uint64_t q = lo16 + 16ull * lane; q < wend; q += 16 * 64)
+    *reinterpret_cast<uint4*>(win + (q - lo16)) = *reinterpret_cast<const uint4*>(a.raw + q);
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  const uint64_t wlen = min(wend, a.n) > lo16 ? min(wend, a.n) - lo16 : 0;
+  if (!req && t > 0) {
     uint64_t found = ~0ull;
     for (uint32_t k = 0; k < kIdxSyncTries && found == ~0ull; k += 64) {  // (wave-uniform)
       const uint64_t at0 = lo + k + lane;
       bool ok = false;
       if (at0 < hi) {
-        DCur s{a.raw, a.n, at0};
+        DCur s{a.raw, a.n, at0, win, lo16, wlen};
         uint32_t q = 0;
         for (; q < kIdxSync && s.off < a.n; ++q) {
           const uint64_t at = s.off;
@@ -476,11 +505,13 @@ __global__ void __launch_bounds__(256) idx_walk_kernel(IdxArgs a, const uint64_t
     o = found;
   }
   if (lane != 0) return;
-  DCur c{a.raw, a.n, o};
+  DCur c{a.raw, a.n, o, win, lo16, wlen};
+  uint16_t* rel = a.rel + (uint64_t)t * kIdxRelCap;
   uint32_t k = 0;
   bool good = true;
   while (c.off < hi) {
     const uint64_t at = c.off;
+    if (k < kIdxRelCap) rel[k] = (uint16_t)(at - lo);
     if (!dc_data_entry(c, ~0ull)) {
       c.off = at;
       good = false;
@@ -494,16 +525,15 @@ __global__ void __launch_bounds__(256) idx_walk_kernel(IdxArgs a, const uint64_t
   a.ok[t] = good ? 1 : 0;
 }
 
+// Every offset of the true chain: chunk t's walk started where the chain enters it (the stitch
+// re-walks every chunk for which that was not so), so its first tcount[t] relative offsets are the
+// chain's. One wave per chunk, coalesced.
 __global__ void __launch_bounds__(256) idx_record_kernel(IdxArgs a) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (t >= a.T || a.tstart[t] == ~0ull) return;
-  DCur c{a.raw, a.n, a.tstart[t]};
-  const uint64_t b = a.tbase[t];
-  const uint32_t m = a.tcount[t];
-  for (uint32_t k = 0; k < m; ++k) {
-    a.out[b + k] = c.off;
-    if (!dc_data_entry(c, ~0ull)) return;  // (cannot fail: the same chain parsed in the walk)
-  }
+  const uint64_t lo = a.S + (uint64_t)t * kIdxChunk, b = a.tbase[t];
+  const uint16_t* rel = a.rel + (uint64_t)t * kIdxRelCap;
+  for (uint32_t k = lane; k < a.tcount[t]; k += 64) a.out[b + k] = lo + rel[k];
 }
 
 // Any entry left to the host tier (its count is the kHostTier marker)?
@@ -671,7 +701,7 @@ int GpuDecode::dd_launch(hipStream_t ks) {
   ck(hipEventRecord(d.up.a, s), "event(index)");
   ck(hipStreamWaitEvent(ks, d.up.a, 0), "wait(index)");
   const uint32_t T = d.T = (uint32_t)((len - S + kIdxChunk - 1) / kIdxChunk);
-  const size_t wbytes = (size_t)T * (8 + 4 + 8 + 1 + 8 + 8 + 4 + 8) + 64;
+  const size_t wbytes = (size_t)T * (8 + 4 + 8 + 1 + 8 + 8 + 4 + 8) + 64 + (size_t)T * kIdxRelCap * 2 + 16;
   if ((st_ = alloc(&d.work.p, wbytes, "decode: device entry index scratch")) != CDB_OK) return -1;
   IdxArgs& a = d.a;
   std::memset(&a, 0, sizeof a);
@@ -688,6 +718,7 @@ int GpuDecode::dd_launch(hipStream_t ks) {
   a.count = (uint32_t*)(d.d_req + T);
   uint32_t* d_tcount = a.count + T;
   a.ok = (uint8_t*)(d_tcount + T);
+  a.rel = (uint16_t*)(((uintptr_t)(a.ok + T) + 15) & ~(uintptr_t)15);
   a.tstart = d_tstart;
   a.tbase = d_tbase;
   a.tcount = d_tcount;
@@ -775,6 +806,7 @@ int GpuDecode::dd_step(size_t* err_off) {
       const uint64_t hi = std::min<uint64_t>(len, S + (uint64_t)(t + 1) * kIdxChunk);
       if (cur >= hi) continue;
       const uint32_t m = (uint32_t)std::min<uint64_t>(d.count[t], cnt - got);
+      if (m > kIdxRelCap) return dd_done(1, 0, err_off);  // (no valid entry is that short)
       tstart[t] = cur;
       tbase[t] = got;
       tcount[t] = m;
@@ -791,7 +823,7 @@ int GpuDecode::dd_step(size_t* err_off) {
   // the last one (where the section ends) unless an entry falls to the host tier
   if ((st_ = alloc(&d.offs.p, cnt * 8, "decode: device entry offsets")) != CDB_OK) return dd_done(-1, 0, err_off);
   d.a.out = (uint64_t*)d.offs.p;
-  idx_record_kernel<<<(T + 255) / 256, 256, 0, d.ks>>>(d.a);
+  idx_record_kernel<<<(T + 3) / 4, 256, 0, d.ks>>>(d.a);
   ck(hipGetLastError(), "idx_record_kernel");
   ck(hipMemcpyAsync(&d.last, d.a.out + (cnt - 1), 8, hipMemcpyDeviceToHost, d.ks), "d2h(index)");
   ck(hipStreamSynchronize(d.ks), "sync(index)");  // (the host vectors above are copy sources)

@@ -516,23 +516,19 @@ cdb_status state_rows(cdb_ctx* ctx, uint64_t* meta, uint64_t* aux, uint64_t n, h
 
 namespace {
 // The input families' layouts (cdb_dev_rows.stride): plain columns, or the hash column + records
-// of ncols - 1 words. staged: every family is in records with 16-B aligned record arrays, so the
-// sorted-run wave kernel copies a bucket's record bytes to LDS in 16-B pieces (runs.hip.h).
+// of ncols - 1 words.
 struct InLayout {
   uint32_t ks = 1, ns = 1, ms = 1;
-  bool staged = false;
 };
 cdb_status input_layout(cdb_ctx* ctx, const cdb_dev_input* in, InLayout* lay) {
   const cdb_dev_rows* fam[3] = {&in->keys, &in->nodes, &in->members};
   const int ncols[3] = {kKeyCols, kNodeCols, kMemberCols};
   uint32_t* out[3] = {&lay->ks, &lay->ns, &lay->ms};
-  bool staged = true;
   for (int f = 0; f < 3; ++f) {
     const cdb_dev_rows& r = *fam[f];
     if (r.stride0 > 1) return fail(ctx, CDB_BAD_ARGUMENT, "input rows: col[0] must be a plain column (stride0 0 or 1)");
     if (r.stride <= 1) {
       *out[f] = 1;
-      staged = staged && r.n == 0;
       continue;
     }
     if (r.stride != (uint32_t)(ncols[f] - 1))
@@ -541,9 +537,7 @@ cdb_status input_layout(cdb_ctx* ctx, const cdb_dev_input* in, InLayout* lay) {
       if (r.n && r.col[c] != r.col[1] + (c - 1))
         return fail(ctx, CDB_BAD_ARGUMENT, "input rows: records layout needs col[c] = col[1] + c - 1");
     *out[f] = r.stride;
-    staged = staged && (r.n == 0 || ((uintptr_t)r.col[1] & 15) == 0);
   }
-  lay->staged = staged;
   return CDB_OK;
 }
 
@@ -632,7 +626,6 @@ cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, const InLayout&
   V->ks = lay.ks;
   V->ns = lay.ns;
   V->ms = lay.ms;
-  V->staged = lay.staged ? 1 : 0;
   for (int c = 0; c < kKeyCols; ++c) V->kin[c] = in->keys.col[c];
   for (int c = 0; c < kNodeCols; ++c) {
     V->nin[c] = in->nodes.col[c];

@@ -30,6 +30,7 @@ struct ColSet {
   uint32_t s[NC];  // row stride of column k in words (0 = 1: a plain column; records layout, common.h)
   __device__ __forceinline__ uint64_t at(int k, uint64_t i) const { return c[k][s[k] ? i * s[k] : i]; }
   __device__ __forceinline__ const uint64_t* ptr(int k, uint64_t i) const { return &c[k][s[k] ? i * s[k] : i]; }
+  __device__ __forceinline__ uint64_t& ref(int k, uint64_t i) const { return c[k][s[k] ? i * s[k] : i]; }
 };
 
 // Bucket index of hash h among `nb` buckets: floor(h * nb / 2^64). Monotone in h, so for
@@ -127,7 +128,7 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
         perm[p] = (uint32_t)(tile0 + r);
       } else {
 #pragma unroll
-        for (int c = 0; c < NC; ++c) out.c[c][p] = in.at(c, tile0 + r);
+        for (int c = 0; c < NC; ++c) out.ref(c, p) = in.at(c, tile0 + r);
       }
     }
     return;
@@ -193,7 +194,7 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
       if (r < rows) stage[slot[k]] = v[c][k];
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < rows; j += kPartThreads) out.c[c][delta[slot_lb[j]] + j] = stage[j];
+    for (int j = threadIdx.x; j < rows; j += kPartThreads) out.ref(c, delta[slot_lb[j]] + j) = stage[j];
     __syncthreads();
   }
 }

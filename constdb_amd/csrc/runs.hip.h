@@ -186,12 +186,19 @@ __device__ __forceinline__ RunMap run_map(const RunView& V, uint32_t b, int lane
     rb = V.rbase[f * (kMaxRuns + 1) + r];
   }
   uint32_t incl = n;
+  if (q.L <= 16) {  // (wave-uniform) the slices sit in lanes 0..15: a row scan by DPP, no LDS trips
+    incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x111, 0xF, 0xF, false);  // row_shr:1
+    incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x112, 0xF, 0xF, false);  // row_shr:2
+    incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x114, 0xF, 0xF, false);  // row_shr:4
+    incl += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x118, 0xF, 0xF, false);  // row_shr:8
+  } else {
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += t;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
   }
-  q.incl = incl;
+  q.incl = incl;  // (lanes >= L: unused; lane_slice reads lanes < L only)
   q.off = rb + s - (incl - n);
   return q;
 }
@@ -221,10 +228,9 @@ __device__ __forceinline__ uint64_t run_row(const RunMap& q, uint32_t c) {
 // The columns of bucket b (KE key rows and CE child rows per lane) from the runs, field by field
 // (either input layout: a lane reads its row's fields with one 8-B load each).
 template <int KE, int CE = 2 * KE>
-__device__ __forceinline__ void load_runs(const WaveArgs& W, const WaveDir& d, uint32_t b, int lane,
-                                          WaveIn<KE, CE>& in) {
+__device__ __forceinline__ void load_runs(const WaveArgs& W, const WaveDir& d, const RunMap& qk, const RunMap& qc,
+                                          int lane, WaveIn<KE, CE>& in) {
   const RunView& V = W.V;
-  const RunMap qk = run_map(V, b, lane, false), qc = run_map(V, b, lane, true);
   in.d = d;
   const uint32_t C = d.N + d.M;
 #pragma unroll
@@ -262,139 +268,6 @@ __device__ __forceinline__ void load_runs(const WaveArgs& W, const WaveDir& d, u
   }
 }
 
-// ---------------------------------------------------------------- staged loads (records layout)
-// A bucket's records of one run are one contiguous byte range. The wave copies the ranges of all
-// its slices into LDS with LDS-DMA (global_load_lds_dwordx4: 64 lanes x 16 B = 1 KB per
-// instruction, no VGPR destination): each range is widened to whole 16-B granules and the
-// granules of all slices are numbered in slice order, piece p landing at stage + 16 p. Slot c's
-// record then sits at stage + E[slice] + 8 W c. The hash columns (8 B per row, what the sort
-// words need first) are read straight into registers, one load per family.
-typedef __attribute__((address_space(3))) void* lds_void_ptr;
-
-struct PieceMap {
-  uint32_t incl;  // inclusive prefix of granule counts over the slices (lanes)
-  uint32_t excl;  // pieces before my slice (within this family's pieces)
-  uint64_t g0;    // my slice's first granule (byte address >> 4)
-  int32_t E;      // LDS byte offset of my slice's slot 0 record (relative to the stage)
-  uint32_t total; // pieces of this family
-};
-
-// rec0: byte address of record 0 of the family's array (whole-array, run-absolute rows);
-// q: the slot map of the slices (run_map), n: my slice's rows; `first`: pieces before this family.
-template <int W>
-__device__ __forceinline__ PieceMap piece_map(uint64_t rec0, const RunMap& q, uint32_t n, int lane, uint32_t first) {
-  PieceMap m;
-  uint32_t cnt = 0;
-  m.g0 = 0;
-  uint32_t mis = 0;
-  if ((uint32_t)lane < q.L && n) {
-    const uint64_t slot0 = q.incl - n;
-    const uint64_t a = rec0 + (q.off + slot0) * (8 * W), e = a + (uint64_t)n * (8 * W);
-    m.g0 = a >> 4;
-    mis = (uint32_t)(a & 15);
-    cnt = (uint32_t)(((e + 15) >> 4) - m.g0);
-  }
-  uint32_t incl = cnt;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(incl, o, 64);
-    if (lane >= o) incl += t;
-  }
-  m.incl = incl;
-  m.excl = incl - cnt;
-  m.total = (uint32_t)__shfl((int)incl, 63, 64);
-  const uint32_t slot0 = q.incl - n;  // (lanes past L: unused)
-  m.E = (int32_t)(16 * (first + m.excl) + mis) - (int32_t)(8 * W * slot0);
-  return m;
-}
-
-// Issues the family's pieces: instruction i covers pieces [64 i, 64 i + 64) into stage + 16 (first + 64 i).
-__device__ __forceinline__ void stage_pieces(const PieceMap& m, uint32_t L, char* stage, uint32_t first, int lane) {
-  const uint32_t ni = (m.total + 63) / 64;
-  for (uint32_t i = 0; i < ni; ++i) {
-    const uint32_t p = 64 * i + lane;
-    const uint32_t r = lane_slice(m.incl, L, p);
-    const uint64_t g = shfl_u64(m.g0, r) + (p - (uint32_t)__shfl((int)m.excl, (int)r, 64));
-    if (p < m.total)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(g << 4),
-                                       (lds_void_ptr)(stage + 16 * (first + 64 * i)), 16, 0, 0);
-  }
-}
-
-// Bucket b (at most 64 KE key and 64 CE child rows) through LDS; returns false (nothing issued)
-// when its pieces do not fit the wave's LDS -- the caller then loads field by field.
-template <int KE, int CE>
-__device__ __forceinline__ bool load_runs_staged(const WaveArgs& W, const WaveDir& d, uint32_t b, int lane,
-                                                 WaveLds<KE>& L, WaveIn<KE, CE>& in) {
-  constexpr uint32_t kStagePieces = sizeof(WaveLds<KE>) / 16;
-  const RunView& V = W.V;
-  const RunMap qk = run_map(V, b, lane, false), qc = run_map(V, b, lane, true);
-  // my slice's row count (lanes < L)
-  const uint32_t nk = qk.incl - (uint32_t)__shfl_up((int)qk.incl, 1, 64) * (lane > 0);
-  const uint32_t nc = qc.incl - (uint32_t)__shfl_up((int)qc.incl, 1, 64) * (lane > 0);
-  const bool node_slice = (uint32_t)lane < V.nr;
-  const PieceMap pk = piece_map<kKeyCols - 1>((uint64_t)V.kin[1], qk, nk, lane, 0);
-  // node slices then member slices: two arrays, so two record bases (slot order is node rows first)
-  const uint64_t crec0 = node_slice ? (uint64_t)V.nin[1] : (uint64_t)V.min[1];
-  const PieceMap pc = piece_map<kNodeCols - 1>(crec0, qc, nc, lane, pk.total);
-  in.d = d;
-  if (pk.total + pc.total > kStagePieces) return false;
-  char* stage = reinterpret_cast<char*>(&L);
-  stage_pieces(pk, qk.L, stage, 0, lane);
-  stage_pieces(pc, qc.L, stage, pk.total, lane);
-  const uint32_t C = d.N + d.M;
-  // hash columns straight to registers while the pieces are in flight
-  int32_t Ek[KE], Ec[CE];
-#pragma unroll
-  for (int e = 0; e < KE; ++e) {
-    const uint32_t c = lane + 64 * e;
-    const uint32_t rk = lane_slice(qk.incl, qk.L, c);
-    const uint64_t krow = shfl_u64(qk.off, rk) + c;
-    Ek[e] = __shfl(pk.E, (int)rk, 64);
-    in.kh[e] = c < d.K ? V.kin[K_KH][krow] : 0;
-  }
-#pragma unroll
-  for (int e = 0; e < CE; ++e) {
-    const uint32_t c = lane + 64 * e;
-    const uint32_t rc = lane_slice(qc.incl, qc.L, c);
-    const uint64_t crow = shfl_u64(qc.off, rc) + c;
-    Ec[e] = __shfl(pc.E, (int)rc, 64);
-    in.cpkh[e] = c < C ? (c < d.N ? V.nin[C_PKH] : V.min[C_PKH])[crow] : 0;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-#pragma unroll
-  for (int e = 0; e < KE; ++e) {
-    const uint32_t c = lane + 64 * e;
-    in.kf[e] = in.kct[e] = in.kut[e] = in.kdt[e] = in.kaux[e] = in.kmeta[e] = 0;
-    if (c < d.K) {  // 48-B record, 16-B aligned (stage and record array are)
-      const ulonglong2* r = reinterpret_cast<const ulonglong2*>(stage + Ek[e] + 48 * c);
-      const ulonglong2 q0 = r[0], q1 = r[1], q2 = r[2];
-      in.kf[e] = q0.x;
-      in.kct[e] = q0.y;
-      in.kut[e] = q1.x;
-      in.kdt[e] = q1.y;
-      in.kaux[e] = q2.x;
-      in.kmeta[e] = q2.y;
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < CE; ++e) {
-    const uint32_t c = lane + 64 * e;
-    in.cpkf[e] = in.cid1[e] = in.cid2[e] = in.ct[e] = in.cm[e] = 0;
-    if (c < C) {  // 40-B record, 8-B aligned
-      const uint64_t* r = reinterpret_cast<const uint64_t*>(stage + Ec[e] + 40 * c);
-      in.cpkf[e] = r[0];
-      in.cid1[e] = r[1];
-      in.cid2[e] = r[2];
-      in.ct[e] = r[3];
-      in.cm[e] = r[4];
-    }
-  }
-  wave_sync();  // every read of the stage is done before the bucket reuses the LDS
-  return true;
-}
-
 // Workgroups are dispatched round-robin over the 8 XCDs; XCD x takes one contiguous range of
 // buckets, so neighbouring buckets (which share the runs' cache lines) meet in one L2.
 __device__ __forceinline__ uint32_t xcd_bucket(uint32_t blk, uint32_t G, int wv) {
@@ -408,16 +281,17 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, 5) bucket_wave_runs_kernel(W
   // (wave-uniform: scalar loads of the bucket's directory entry)
   const uint32_t b = __builtin_amdgcn_readfirstlane(W.blo + xcd_bucket(blockIdx.x, gridDim.x, wv));
   if (b >= W.bhi) return;
+  // the directory entry (scalar loads) and the bucket's run slices (vector loads) do not depend on
+  // each other: both are in flight before either is used
   const WaveDir d = load_dir(W.A, b);
+  const RunMap qk = run_map(W.V, b, lane, false), qc = run_map(W.V, b, lane, true);
   if (d.N + d.M <= 64) {  // (wave-uniform) one child slot per lane
     WaveIn<1, 1> in;
-    if (!(W.V.staged && d.K <= 64 && load_runs_staged<1, 1>(W, d, b, lane, lds_all[wv], in)))
-      load_runs<1, 1>(W, d, b, lane, in);
+    load_runs<1, 1>(W, d, qk, qc, lane, in);
     wave_bucket<1>(W, lds_all[wv], b, lane, in, []() {});
   } else {
     WaveIn<1> in;
-    if (!(W.V.staged && d.K <= 64 && d.N + d.M <= 128 && load_runs_staged<1, 2>(W, d, b, lane, lds_all[wv], in)))
-      load_runs<1>(W, d, b, lane, in);
+    load_runs<1>(W, d, qk, qc, lane, in);
     wave_bucket<1>(W, lds_all[wv], b, lane, in, []() {});
   }
 }
@@ -437,11 +311,11 @@ __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_runs_kernel(Wave
       m &= m - 1;
       const uint32_t bb = W.blo + g * 64 + i;
       const WaveDir d = load_dir(W.A, bb);
+      const RunMap qk = run_map(W.V, bb, lane, false), qc = run_map(W.V, bb, lane, true);
       WaveIn<2> in;
-      if (!(W.V.staged && d.K <= 128 && d.N + d.M <= 256 && load_runs_staged<2, 4>(W, d, bb, lane, lds_all[wv], in)))
-        load_runs<2>(W, d, bb, lane, in);
+      load_runs<2>(W, d, qk, qc, lane, in);
       wave_bucket<2>(W, lds_all[wv], bb, lane, in, []() {});
-      wave_sync();  // (the next bucket's pieces overwrite this one's LDS)
+      wave_sync();  // (the next bucket reuses this one's LDS)
     }
   }
   if (lane == 0 && found) atomicAdd(&stat_shard(W.A.stats)[ST_WIDE], found);

@@ -31,11 +31,13 @@ def ctx():
     return cdb.Context(0)
 
 
-def _gen(c, cfg, lo, hi):
+def _gen(c, cfg, lo, hi, records=False):
     L = cdb.lib()
     g = cdb.GenConfig()
     ctypes.memmove(ctypes.byref(g), ctypes.byref(cfg), ctypes.sizeof(g))
     g.replica_lo, g.replica_hi = lo, hi
+    if records:
+        g.flags |= cdb.GEN_ROWS_RECORDS
     din = cdb.DevInput()
     c.check(L.cdb_gen_device(c.handle, ctypes.byref(g), ctypes.byref(din)))
     din.n_pos = cfg.n_replicas
@@ -92,12 +94,12 @@ def _concat(outs):
     return fam
 
 
-def _sharded(mctx, cfg, runs=True, scramble=None):
+def _sharded(mctx, cfg, runs=True, scramble=None, records=False):
     N = mctx.n_devices
     R = cfg.n_replicas
     ins = []
     for i in range(N):
-        d = _gen(mctx.shard(i), cfg, i * R // N, (i + 1) * R // N)
+        d = _gen(mctx.shard(i), cfg, i * R // N, (i + 1) * R // N, records)
         if runs:
             sort_into_runs(d, R)
         ins.append(d)
@@ -143,6 +145,23 @@ def test_sharded_equals_single_merge(ctx, slots, runs):
         if slots > 1:
             moved = sum(xs.link_bytes[i][j] for i in range(slots) for j in range(slots) if i != j)
             assert moved == xs.bytes_moved > 0 and xs.bytes_local > 0
+    finally:
+        mctx.close()
+
+
+@pytest.mark.parametrize("slots,runs", [(2, True), (4, True), (2, False)])
+def test_sharded_records_equals_single_merge(ctx, slots, runs):
+    """Records inputs (hash column + records, cdb_dev_rows.stride): the exchange moves two arrays per
+    slice, the received rows are records, and the result equals the single-device merge."""
+    cfg = configs.c4(cdb, 300_000)
+    want, _ = _single(ctx, cfg)
+    mctx = cdb.Context(devices=[0] * slots)
+    try:
+        got, sts, xs = _sharded(mctx, cfg, runs=runs, records=True)
+        for g, w in zip(got, want):
+            assert g.shape == w.shape and torch.equal(g, w)
+        if runs:
+            assert all(s.sorted_runs == 1 for s in sts) and xs.packed == 0
     finally:
         mctx.close()
 
