@@ -44,6 +44,7 @@ constexpr int kWavesPerWG = 4;
 #endif
 constexpr uint64_t kM44 = (1ull << 44) - 1, kM42 = (1ull << 42) - 1;
 
+
 // Per-wave LDS. KE = key rows per lane (1 or 2); child rows per lane CE = 2 KE.
 template <int KE>
 struct WaveLds {

@@ -361,7 +361,11 @@ __global__ void __launch_bounds__(kDecThreads) dest_kernel(const uint64_t* __res
 constexpr uint64_t kIdxChunk = 8192;
 constexpr uint32_t kIdxSync = 16;
 constexpr uint32_t kIdxSyncTries = 256;  // offsets tried per chunk (4 rounds of 64 lanes)
-constexpr uint64_t kIdxEntryMax = 1u << 16;
+// The sync search bounds every length it meets by kIdxSyncEntryMax: a wrong offset often reads a
+// huge member count or length, and one lane parsing thousands of bogus members held its whole wave
+// (and, by the walks' serial order, the snapshot) for milliseconds. A chunk whose entries near its
+// start are longer finds its sync later or not at all; the stitch re-walks it from the true chain.
+constexpr uint64_t kIdxEntryMax = 1u << 10;
 // The walk reads its chunk and the first kIdxTail bytes after it from LDS (one copy per wave).
 constexpr uint64_t kIdxTail = 4096, kIdxWin = kIdxChunk + kIdxTail;
 // Entries starting in one chunk: a DATAS entry takes at least 6 bytes (key length, three times,
@@ -451,89 +455,95 @@ struct IdxArgs {
                            // (kIdxRelCap slots per chunk; the record pass expands the true chain's)
 };
 
-// One wave per chunk. req == null: the speculative pass (sync search by the 64 lanes, then the
-// walk by lane 0); req[t] != ~0: lane 0 walks chunk t again from req[t] (the offset at which the
-// true chain enters it), other chunks keep their results.
-__global__ void __launch_bounds__(256) idx_walk_kernel(IdxArgs a, const uint64_t* __restrict__ req) {
+// One wave per chunk, persistent over the chunks (a launch of one workgroup per 4 chunks spent its
+// time dispatching workgroups that had little to do). list == null: the speculative pass over every
+// chunk (sync search by the 64 lanes, then the walk by lane 0); else the nlist chunks of `list`,
+// walked again by lane 0 from req[t] (the offset at which the true chain enters chunk t).
+constexpr uint32_t kIdxWalkBlocks = 768;  // 3 workgroups of 4 waves per CU (48 KB of LDS each)
+__global__ void __launch_bounds__(256) idx_walk_kernel(IdxArgs a, const uint64_t* __restrict__ req,
+                                                       const uint32_t* __restrict__ list, uint32_t nlist) {
   __shared__ __attribute__((aligned(16))) uint8_t win_all[4][kIdxWin];
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint32_t t = blockIdx.x * 4 + wv;
-  if (t >= a.T) return;
-  const uint64_t lo = a.S + (uint64_t)t * kIdxChunk, hi = min(a.n, lo + kIdxChunk);
-  uint64_t o = lo;
-  if (req) {
-    if (req[t] == ~0ull) return;
-    o = req[t];
-  }
-  // the window: [lo16, lo16 + kIdxWin) with lo16 = lo rounded down to 16 B, copied in 16-B pieces
-  // (a piece that starts before the end of the stream may read up to 15 bytes past it: the device
-  // copy has 16 bytes of slack)
   uint8_t* win = win_all[wv];
-  const uint64_t lo16 = lo & ~15ull;
-  const uint64_t wend = min(lo16 + kIdxWin, (a.n + 15) & ~15ull);
-  for (uint64_t q = lo16 + 16ull * lane; q < wend; q += 16 * 64)
-    *reinterpret_cast<uint4*>(win + (q - lo16)) = *reinterpret_cast<const uint4*>(a.raw + q);
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-  const uint64_t wlen = min(wend, a.n) > lo16 ? min(wend, a.n) - lo16 : 0;
-  if (!req && t > 0) {
-    uint64_t found = ~0ull;
-    for (uint32_t k = 0; k < kIdxSyncTries && found == ~0ull; k += 64) {  // (wave-uniform)
-      const uint64_t at0 = lo + k + lane;
-      bool ok = false;
-      if (at0 < hi) {
-        DCur s{a.raw, a.n, at0, win, lo16, wlen};
-        uint32_t q = 0;
-        for (; q < kIdxSync && s.off < a.n; ++q) {
-          const uint64_t at = s.off;
-          if (!dc_data_entry(s, kIdxEntryMax) || s.off - at > kIdxEntryMax) break;
+  const uint32_t total = list ? nlist : a.T;
+  for (uint32_t i = blockIdx.x * 4 + wv; i < total; i += gridDim.x * 4) {  // (wave-uniform)
+    const uint32_t t = list ? list[i] : i;
+    const uint64_t lo = a.S + (uint64_t)t * kIdxChunk, hi = min(a.n, lo + kIdxChunk);
+    uint64_t o = list ? req[t] : lo;
+    // the window: [lo16, lo16 + kIdxWin) with lo16 = lo rounded down to 16 B, copied in 16-B pieces
+    // (a piece that starts before the end of the stream may read up to 15 bytes past it: the device
+    // copy has 16 bytes of slack)
+    const uint64_t lo16 = lo & ~15ull;
+    const uint64_t wend = min(lo16 + kIdxWin, (a.n + 15) & ~15ull);
+    __builtin_amdgcn_wave_barrier();  // (the previous chunk's readers are done with the window)
+    for (uint64_t q = lo16 + 16ull * lane; q < wend; q += 16 * 64)
+      *reinterpret_cast<uint4*>(win + (q - lo16)) = *reinterpret_cast<const uint4*>(a.raw + q);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t wlen = min(wend, a.n) > lo16 ? min(wend, a.n) - lo16 : 0;
+    if (!list && t > 0) {
+      uint64_t found = ~0ull;
+      for (uint32_t k = 0; k < kIdxSyncTries && found == ~0ull; k += 64) {  // (wave-uniform)
+        const uint64_t at0 = lo + k + lane;
+        bool ok = false;
+        if (at0 < hi) {
+          DCur s{a.raw, a.n, at0, win, lo16, wlen};
+          uint32_t q = 0;
+          for (; q < kIdxSync && s.off < a.n; ++q) {
+            const uint64_t at = s.off;
+            if (!dc_data_entry(s, kIdxEntryMax) || s.off - at > kIdxEntryMax) break;
+          }
+          ok = q == kIdxSync;
         }
-        ok = q == kIdxSync;
+        const uint64_t m = __ballot(ok);
+        if (m) found = lo + k + __builtin_ctzll(m);
       }
-      const uint64_t m = __ballot(ok);
-      if (m) found = lo + k + __builtin_ctzll(m);
-    }
-    if (found == ~0ull) {
-      if (lane == 0) {
-        a.sync[t] = ~0ull;
-        a.count[t] = 0;
-        a.stop[t] = lo;
-        a.ok[t] = 0;
+      if (found == ~0ull) {
+        if (lane == 0) {
+          a.sync[t] = ~0ull;
+          a.count[t] = 0;
+          a.stop[t] = lo;
+          a.ok[t] = 0;
+        }
+        continue;
       }
-      return;
+      o = found;
     }
-    o = found;
-  }
-  if (lane != 0) return;
-  DCur c{a.raw, a.n, o, win, lo16, wlen};
-  uint16_t* rel = a.rel + (uint64_t)t * kIdxRelCap;
-  uint32_t k = 0;
-  bool good = true;
-  while (c.off < hi) {
-    const uint64_t at = c.off;
-    if (k < kIdxRelCap) rel[k] = (uint16_t)(at - lo);
-    if (!dc_data_entry(c, ~0ull)) {
-      c.off = at;
-      good = false;
-      break;
+    if (lane == 0) {
+      DCur c{a.raw, a.n, o, win, lo16, wlen};
+      uint16_t* rel = a.rel + (uint64_t)t * kIdxRelCap;
+      uint32_t k = 0;
+      bool good = true;
+      while (c.off < hi) {
+        const uint64_t at = c.off;
+        if (k < kIdxRelCap) rel[k] = (uint16_t)(at - lo);
+        if (!dc_data_entry(c, ~0ull)) {
+          c.off = at;
+          good = false;
+          break;
+        }
+        ++k;
+      }
+      a.sync[t] = o;
+      a.count[t] = k;
+      a.stop[t] = c.off;
+      a.ok[t] = good ? 1 : 0;
     }
-    ++k;
   }
-  a.sync[t] = o;
-  a.count[t] = k;
-  a.stop[t] = c.off;
-  a.ok[t] = good ? 1 : 0;
 }
 
 // Every offset of the true chain: chunk t's walk started where the chain enters it (the stitch
 // re-walks every chunk for which that was not so), so its first tcount[t] relative offsets are the
 // chain's. One wave per chunk, coalesced.
 __global__ void __launch_bounds__(256) idx_record_kernel(IdxArgs a) {
-  const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (t >= a.T || a.tstart[t] == ~0ull) return;
-  const uint64_t lo = a.S + (uint64_t)t * kIdxChunk, b = a.tbase[t];
-  const uint16_t* rel = a.rel + (uint64_t)t * kIdxRelCap;
-  for (uint32_t k = lane; k < a.tcount[t]; k += 64) a.out[b + k] = lo + rel[k];
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6); t < a.T; t += gridDim.x * 4) {
+    if (a.tstart[t] == ~0ull) continue;
+    const uint64_t lo = a.S + (uint64_t)t * kIdxChunk, b = a.tbase[t];
+    const uint16_t* rel = a.rel + (uint64_t)t * kIdxRelCap;
+    const uint32_t m = a.tcount[t];
+    for (uint32_t k = lane; k < m; k += 64) a.out[b + k] = lo + rel[k];
+  }
 }
 
 // Any entry left to the host tier (its count is the kHostTier marker)?
@@ -641,6 +651,8 @@ class GpuDecode {
     int round = 0;
     IdxArgs a;
     uint64_t* d_req = nullptr;
+    uint32_t* d_list = nullptr;  // re-walk rounds: the requested chunks
+    std::vector<uint32_t> list;
     uint64_t last = 0;  // the section's last entry
     DevBuf work, offs;
     EvPair up;  // (a: the snapshot's bytes are on the device)
@@ -662,7 +674,16 @@ class GpuDecode {
   std::vector<uint64_t> noff_, moff_;
   std::vector<HostEntry> hosted_;
   DevBuf d_raw_, d_meta_, d_crc_, d_rows_, d_ord_, d_idx_raw_;
+  struct HostReg {  // the batch's bytes, page-locked for a direct upload (unlocked after every sync)
+    void* p = nullptr;
+    ~HostReg() {
+      if (p) (void)hipHostUnregister(p);
+    }
+  } reg_;
   uint64_t raw_pad_ = 0;  // d_raw_ + raw_pad_ = byte 0 of the snapshot
+ public:
+  double lt_[4] = {0, 0, 0, 0};  // dd_launch host time (ms): bytes buffer, upload call, scratch, walk launch
+ private:
   DeferredDatas defer_;
   IndexCursor* cursor_ = nullptr;
   struct CursorFree {
@@ -686,6 +707,13 @@ int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTimi
   const auto t0 = std::chrono::steady_clock::now();
   rc_ = index_snapshot(buf, len, flags_, out_, &idx_, err_off, &dcrc_, index_threads_, &defer_, &cursor_);
   if (rc_ == kIndexDeferred) rc_ = CDB_OK;  // the DATAS section is indexed in prepare_device
+  // a deferred section's snapshot goes up whole right after: page-lock the batch's bytes here, on
+  // this thread (the index passes of several snapshots run side by side, and so do the page-locks;
+  // one after another they cost as much as the uploads). CDB_H2D_STAGED=1: through the staging ring.
+  static const bool staged = std::getenv("CDB_H2D_STAGED") != nullptr;
+  if (!staged && cursor_ && out_->raw.size() >= (size_t(64) << 20) && hipSetDevice(ctx_->device) == hipSuccess &&
+      hipHostRegister(out_->raw.data(), out_->raw.size(), hipHostRegisterDefault) == hipSuccess)
+    reg_.p = out_->raw.data();
   if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return rc_;
 }
@@ -696,13 +724,28 @@ int GpuDecode::dd_launch(hipStream_t ks) {
   d.ks = ks;
   const uint64_t len = out_->raw.size(), S = defer_.start;
   hipStream_t s = ctx_->stream;
+  auto lap = [t = std::chrono::steady_clock::now()](double* acc) mutable {
+    const auto now = std::chrono::steady_clock::now();
+    *acc += std::chrono::duration<double, std::milli>(now - t).count();
+    t = now;
+  };
   if ((st_ = alloc(&d_idx_raw_.p, len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK) return -1;
-  if ((st_ = staged_h2d(ctx_, d_idx_raw_.p, out_->raw.data(), len, s)) != CDB_OK) return -1;
+  lap(&lt_[0]);
+  // bytes page-locked by the index pass go up directly (no second host copy through the staging
+  // ring, and this thread does not wait for the upload)
+  if (reg_.p) {
+    ck(hipMemcpyAsync(d_idx_raw_.p, out_->raw.data(), len, hipMemcpyHostToDevice, s), "h2d(index)");
+    if (st_ != CDB_OK) return -1;
+  } else if ((st_ = staged_h2d(ctx_, d_idx_raw_.p, out_->raw.data(), len, s)) != CDB_OK) {
+    return -1;
+  }
   ck(hipEventRecord(d.up.a, s), "event(index)");
   ck(hipStreamWaitEvent(ks, d.up.a, 0), "wait(index)");
+  lap(&lt_[1]);
   const uint32_t T = d.T = (uint32_t)((len - S + kIdxChunk - 1) / kIdxChunk);
-  const size_t wbytes = (size_t)T * (8 + 4 + 8 + 1 + 8 + 8 + 4 + 8) + 64 + (size_t)T * kIdxRelCap * 2 + 16;
+  const size_t wbytes = (size_t)T * (8 + 4 + 8 + 1 + 8 + 8 + 4 + 8) + 64 + (size_t)T * kIdxRelCap * 2 + 16 + (size_t)T * 4;
   if ((st_ = alloc(&d.work.p, wbytes, "decode: device entry index scratch")) != CDB_OK) return -1;
+  lap(&lt_[2]);
   IdxArgs& a = d.a;
   std::memset(&a, 0, sizeof a);
   a.raw = (const uint8_t*)d_idx_raw_.p;
@@ -719,6 +762,7 @@ int GpuDecode::dd_launch(hipStream_t ks) {
   uint32_t* d_tcount = a.count + T;
   a.ok = (uint8_t*)(d_tcount + T);
   a.rel = (uint16_t*)(((uintptr_t)(a.ok + T) + 15) & ~(uintptr_t)15);
+  d.d_list = (uint32_t*)(a.rel + (size_t)T * kIdxRelCap);
   a.tstart = d_tstart;
   a.tbase = d_tbase;
   a.tcount = d_tcount;
@@ -728,14 +772,14 @@ int GpuDecode::dd_launch(hipStream_t ks) {
   d.count.assign(T, 0);
   d.ok.assign(T, 0);
   d.round = 0;
-  idx_walk_kernel<<<(T + 3) / 4, 256, 0, ks>>>(a, nullptr);
+  idx_walk_kernel<<<std::min<uint32_t>((T + 3) / 4, kIdxWalkBlocks), 256, 0, ks>>>(a, nullptr, nullptr, 0);
   ck(hipGetLastError(), "idx_walk_kernel");
-  dd_download();
+  lap(&lt_[3]);
   d.active = true;
   return st_ == CDB_OK ? 0 : -1;
 }
 
-void GpuDecode::dd_download() {  // the walk's results to the host, queued on ks
+void GpuDecode::dd_download() {  // the walk's results to the host (after the walk: see dd_step)
   DevIndex& d = di_;
   const uint32_t T = d.T;
   ck(hipMemcpyAsync(d.sync.data(), d.a.sync, T * 8ull, hipMemcpyDeviceToHost, d.ks), "d2h(index)");
@@ -750,6 +794,10 @@ void GpuDecode::dd_download() {  // the walk's results to the host, queued on ks
 int GpuDecode::dd_step(size_t* err_off) {
   DevIndex& d = di_;
   if (!d.active) return 0;
+  // the walk's results come down only now: a copy into pageable host memory queued behind the walk
+  // would hold the launching thread until the walk ends (and with it every later snapshot's launch)
+  ck(hipStreamSynchronize(d.ks), "sync(index)");
+  dd_download();
   ck(hipStreamSynchronize(d.ks), "sync(index)");
   if (st_ != CDB_OK) return dd_done(-1, 0, err_off);
   const uint64_t len = out_->raw.size(), S = defer_.start, cnt = defer_.count;
@@ -791,10 +839,14 @@ int GpuDecode::dd_step(size_t* err_off) {
   }
   if (!consistent) {
     if (++d.round >= 16) return dd_done(1, 0, err_off);  // (3-4 rounds on the generator's streams)
+    d.list.clear();
+    for (uint32_t t = 0; t < T; ++t)
+      if (d.req[t] != ~0ull) d.list.push_back(t);
+    const uint32_t nl = (uint32_t)d.list.size();
     ck(hipMemcpyAsync(d.d_req, d.req.data(), T * 8ull, hipMemcpyHostToDevice, d.ks), "h2d(index)");
-    idx_walk_kernel<<<(T + 3) / 4, 256, 0, d.ks>>>(d.a, d.d_req);
+    ck(hipMemcpyAsync(d.d_list, d.list.data(), nl * 4ull, hipMemcpyHostToDevice, d.ks), "h2d(index)");
+    idx_walk_kernel<<<std::min<uint32_t>((nl + 3) / 4, kIdxWalkBlocks), 256, 0, d.ks>>>(d.a, d.d_req, d.d_list, nl);
     ck(hipGetLastError(), "idx_walk_kernel");
-    dd_download();
     return st_ == CDB_OK ? 1 : dd_done(-1, 0, err_off);
   }
   std::vector<uint64_t> tstart(T, ~0ull), tbase(T, 0);
@@ -823,7 +875,7 @@ int GpuDecode::dd_step(size_t* err_off) {
   // the last one (where the section ends) unless an entry falls to the host tier
   if ((st_ = alloc(&d.offs.p, cnt * 8, "decode: device entry offsets")) != CDB_OK) return dd_done(-1, 0, err_off);
   d.a.out = (uint64_t*)d.offs.p;
-  idx_record_kernel<<<(T + 3) / 4, 256, 0, d.ks>>>(d.a);
+  idx_record_kernel<<<std::min<uint32_t>((T + 3) / 4, 2048), 256, 0, d.ks>>>(d.a);
   ck(hipGetLastError(), "idx_record_kernel");
   ck(hipMemcpyAsync(&d.last, d.a.out + (cnt - 1), 8, hipMemcpyDeviceToHost, d.ks), "d2h(index)");
   ck(hipStreamSynchronize(d.ks), "sync(index)");  // (the host vectors above are copy sources)
@@ -1429,6 +1481,16 @@ struct PhaseClock {
     json += b;
     last = now;
   }
+  void add(const char* key, const std::vector<double>& v) {
+    if (!path) return;
+    std::string a;
+    for (double x : v) {
+      char b[32];
+      std::snprintf(b, sizeof b, "%s%.3f", a.empty() ? "" : ", ", x);
+      a += b;
+    }
+    json += std::string(json.empty() ? "" : ", ") + "\"" + key + "\": [" + a + "]";
+  }
   void write(uint32_t n, uint64_t bytes, const uint64_t* rows, bool runs) {
     if (!path) return;
     if (FILE* f = std::fopen(path, "a")) {
@@ -1521,6 +1583,12 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     if (st != CDB_OK) return st;
   }
   clk.mark("deferred_datas");
+  for (int k = 0; k < 4; ++k) {
+    static const char* names[4] = {"dd_alloc_bytes_ms", "dd_upload_call_ms", "dd_alloc_scratch_ms", "dd_walk_launch_ms"};
+    std::vector<double> v;
+    for (uint32_t i = 0; i < n; ++i) v.push_back(dec[i]->lt_[k]);
+    clk.add(names[k], v);
+  }
   for (uint32_t i = 0; i < n; ++i) {
     size_t eo = ieo[i];
     int rc = irc[i];

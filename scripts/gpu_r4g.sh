@@ -10,6 +10,8 @@ timeout -k 10 600 python -u -m pytest tests/test_decode_device_gpu.py tests/test
 rc=$?; tail -4 $O/pytest_r4g.log
 [ $rc -eq 0 ] || { echo "pytest ended with $rc"; exit 1; }
 for lay in records columns; do
+  CDB_LIB=$PWD/variants/lib_nounroll.so timeout -k 10 200 python bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-general --layout $lay > $O/g_nounroll_$lay.json 2> $O/g_nounroll_$lay.err || { echo "bench nounroll $lay failed"; tail -5 $O/g_nounroll_$lay.err; exit 2; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['ms_per_step'],2), 'ms', {k: round(v,2) for k,v in d['phases_ms'].items()})" $O/g_nounroll_$lay.json "nounroll $lay"
   timeout -k 10 200 python bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-general --layout $lay > $O/g_$lay.json 2> $O/g_$lay.err || { echo "bench $lay failed"; tail -5 $O/g_$lay.err; exit 2; }
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['ms_per_step'],2), 'ms', {k: round(v,2) for k,v in d['phases_ms'].items()})" $O/g_$lay.json "$lay"
 done
