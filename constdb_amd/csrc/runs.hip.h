@@ -25,6 +25,11 @@
 
 namespace cdb {
 
+// 16 bytes at an 8-byte aligned address (records rows): one 16-B load per piece
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2), aligned(8)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2), aligned(4)));
+
+
 constexpr int kMaxRuns = 64;          // runs per family (cdb_dev_input.run_start rows)
 constexpr uint32_t kGapInline = 32;  // longer directory gaps go to the gap list
 
@@ -181,8 +186,9 @@ __device__ __forceinline__ RunMap run_map(const RunView& V, uint32_t b, int lane
     const int f = children ? 1 + (lane >= (int)V.nr) : 0;
     const uint32_t r = (uint32_t)lane - (f == 2 ? V.nr : 0);
     const uint32_t* row = V.rdir[f] + (uint64_t)r * V.nbp1;
-    s = row[b];
-    n = row[b + 1] - s;
+    const u32x2 se = *reinterpret_cast<const u32x2*>(row + b);  // row[b], row[b + 1]: one load
+    s = se.x;
+    n = se.y - s;
     rb = V.rbase[f * (kMaxRuns + 1) + r];
   }
   uint32_t incl = n;
@@ -240,12 +246,23 @@ __device__ __forceinline__ void load_runs(const WaveArgs& W, const WaveDir& d, c
     const uint64_t row = run_row(qk, c);
     if (c < d.K) {
       in.kh[e] = V.kin[K_KH][row];
-      in.kf[e] = row_field(V.kin, V.ks, K_KF, row);
-      in.kct[e] = row_field(V.kin, V.ks, K_CT, row);
-      in.kut[e] = row_field(V.kin, V.ks, K_UT, row);
-      in.kdt[e] = row_field(V.kin, V.ks, K_DT, row);
-      in.kaux[e] = row_field(V.kin, V.ks, K_AUX, row);
-      in.kmeta[e] = row_field(V.kin, V.ks, K_META, row);
+      if (V.ks == kKeyCols - 1) {  // (uniform) records: the 48-B record as three 16-B pieces
+        const u64x2* r = reinterpret_cast<const u64x2*>(V.kin[1] + row * (kKeyCols - 1));
+        const u64x2 q0 = r[0], q1 = r[1], q2 = r[2];
+        in.kf[e] = q0.x;
+        in.kct[e] = q0.y;
+        in.kut[e] = q1.x;
+        in.kdt[e] = q1.y;
+        in.kaux[e] = q2.x;
+        in.kmeta[e] = q2.y;
+      } else {
+        in.kf[e] = V.kin[K_KF][row];
+        in.kct[e] = V.kin[K_CT][row];
+        in.kut[e] = V.kin[K_UT][row];
+        in.kdt[e] = V.kin[K_DT][row];
+        in.kaux[e] = V.kin[K_AUX][row];
+        in.kmeta[e] = V.kin[K_META][row];
+      }
     }
   }
 #pragma unroll
@@ -259,11 +276,21 @@ __device__ __forceinline__ void load_runs(const WaveArgs& W, const WaveDir& d, c
       const uint64_t* const* col = isn ? V.nin : V.min;
       const uint32_t s = isn ? V.ns : V.ms;
       in.cpkh[e] = col[C_PKH][row];
-      in.cpkf[e] = row_field(col, s, C_PKF, row);
-      in.cid1[e] = row_field(col, s, C_ID1, row);
-      in.cid2[e] = row_field(col, s, C_ID2, row);
-      in.ct[e] = row_field(col, s, C_T, row);
-      in.cm[e] = row_field(col, s, C_META, row);
+      if (s == kNodeCols - 1) {  // records: the 40-B record as two 16-B pieces and a word (8-B aligned)
+        const uint64_t* rec = col[1] + row * (kNodeCols - 1);
+        const u64x2 q0 = reinterpret_cast<const u64x2*>(rec)[0], q1 = reinterpret_cast<const u64x2*>(rec + 2)[0];
+        in.cpkf[e] = q0.x;
+        in.cid1[e] = q0.y;
+        in.cid2[e] = q1.x;
+        in.ct[e] = q1.y;
+        in.cm[e] = rec[4];
+      } else {
+        in.cpkf[e] = col[C_PKF][row];
+        in.cid1[e] = col[C_ID1][row];
+        in.cid2[e] = col[C_ID2][row];
+        in.ct[e] = col[C_T][row];
+        in.cm[e] = col[C_META][row];
+      }
     }
   }
 }
