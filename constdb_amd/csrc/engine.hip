@@ -579,9 +579,10 @@ cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, const InLayout&
   for (int f = 0; f < 3; ++f) {
     hipStream_t fs = f == 0 ? s : f == 1 ? ctx->side : ctx->side2;
     uint32_t* rd = rdir + f * per_fam;
-    for (uint32_t r = 0; r < nr; ++r)  // empty runs: every bucket starts at row 0
+    for (uint32_t r = 0; r < nr; ++r)  // empty runs: every bucket starts at the run's (absolute) first row
       if (in->run_start[f][r + 1] == in->run_start[f][r])
-        CDB_HIP(hipMemsetAsync(rd + r * row, 0, row * sizeof(uint32_t), fs), "memset run");
+        CDB_HIP(hipMemsetD32Async((hipDeviceptr_t)(rd + r * row), (int)(uint32_t)in->run_start[f][r], row, fs),
+                "memset run");
     const uint64_t n = fam[f]->n;
     if (n) {
       RunMarkArgs a;
@@ -617,7 +618,9 @@ cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, const InLayout&
   if (ctx->runs_err) return CDB_OK;  // a run is not ordered (or the gap list overflowed)
   for (int f = 0; f < 3; ++f) {
     const uint64_t blocks = std::min<uint64_t>((nb + 255) / 256, 8192);
-    run_reduce_kernel<<<(uint32_t)blocks, 256, 0, s>>>(V->rdir[f], nr, nb, dirs[f].base, dirs[f].hist);
+    uint64_t rs_sum = 0;
+    for (uint32_t r = 0; r < nr; ++r) rs_sum += ctx->runs_host[f * (kMaxRuns + 1) + r];
+    run_reduce_kernel<<<(uint32_t)blocks, 256, 0, s>>>(V->rdir[f], nr, nb, rs_sum, dirs[f].base, dirs[f].hist);
     CDB_TRY(launch_check(ctx, s, "run_reduce_kernel"));
   }
   V->rbase = d_rbase;

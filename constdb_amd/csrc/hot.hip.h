@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
         const uint32_t* d = H.V.rdir[f] + (uint64_t)r * H.V.nbp1 + b;
         const uint32_t len = d[1] - d[0];
         if (k < len || r + 1 >= H.V.nr) {
-          row = (uint32_t)(H.V.rbase[f * (kMaxRuns + 1) + r] + d[0] + k);
+          row = d[0] + k;  // (absolute rows)
           break;
         }
         k -= len;

@@ -87,8 +87,8 @@ __global__ void __launch_bounds__(256) run_mark_kernel(RunMarkArgs a, uint64_t n
       if (hp > h) atomicOr(a.err, 1u);
       c0 = __umul64hi(hp, a.nb) + 1;
     }
-    run_fill(a, r, c0, b, (uint32_t)rel);
-    if (rel + 1 == len) run_fill(a, r, b + 1, a.nb, (uint32_t)len);
+    run_fill(a, r, c0, b, (uint32_t)i);
+    if (rel + 1 == len) run_fill(a, r, b + 1, a.nb, (uint32_t)rs[r + 1]);
   }
 }
 
@@ -135,8 +135,8 @@ __global__ void __launch_bounds__(256) run_mark4_kernel(RunMarkArgs a, uint64_t 
         if (hp > hk) atomicOr(a.err, 1u);
         c0 = __umul64hi(hp, a.nb) + 1;
       }
-      run_fill(a, r, c0, b, (uint32_t)rel);
-      if (rel + 1 == len) run_fill(a, r, b + 1, a.nb, (uint32_t)len);
+      run_fill(a, r, c0, b, (uint32_t)i);
+      if (rel + 1 == len) run_fill(a, r, b + 1, a.nb, (uint32_t)rs[r + 1]);
       prev = h[k];
     }
   }
@@ -154,17 +154,19 @@ __global__ void __launch_bounds__(256) run_gap_kernel(const uint32_t* __restrict
 }
 
 // Bucket directory of the family from its run directory: count[b] and the exclusive prefix
-// base[b] = sum over runs of the run-relative first row of b.
+// base[b] = sum over runs of the run-relative first row of b (the directory holds absolute rows:
+// rs_sum = the sum of the runs' first rows).
 __global__ void __launch_bounds__(256) run_reduce_kernel(const uint32_t* __restrict__ rdir, uint32_t nr, uint64_t nb,
-                                                         uint32_t* __restrict__ base, uint32_t* __restrict__ cnt) {
+                                                         uint64_t rs_sum, uint32_t* __restrict__ base,
+                                                         uint32_t* __restrict__ cnt) {
   for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb; b += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t s0 = 0, s1 = 0;
+    uint64_t s0 = 0, s1 = 0;
     for (uint32_t r = 0; r < nr; ++r) {
       s0 += rdir[(uint64_t)r * (nb + 1) + b];
       s1 += rdir[(uint64_t)r * (nb + 1) + b + 1];
     }
-    base[b] = s0;
-    cnt[b] = s1 - s0;
+    base[b] = (uint32_t)(s0 - rs_sum);
+    cnt[b] = (uint32_t)(s1 - s0);
   }
 }
 
@@ -172,6 +174,7 @@ __global__ void __launch_bounds__(256) run_reduce_kernel(const uint32_t* __restr
 // keys: the nr key runs; children: the nr node runs, then the nr member runs (child slots are
 // node rows first, then member rows). incl = inclusive prefix of the slice lengths over lanes;
 // off = absolute row of the slice's first row minus its first slot (row of slot c = off + c).
+// (The run directory holds absolute rows, so no per-run base is loaded.)
 struct RunMap {
   uint32_t incl, L;
   uint64_t off;
@@ -181,7 +184,6 @@ __device__ __forceinline__ RunMap run_map(const RunView& V, uint32_t b, int lane
   RunMap q;
   q.L = children ? 2 * V.nr : V.nr;
   uint32_t s = 0, n = 0;
-  uint64_t rb = 0;
   if ((uint32_t)lane < q.L) {
     const int f = children ? 1 + (lane >= (int)V.nr) : 0;
     const uint32_t r = (uint32_t)lane - (f == 2 ? V.nr : 0);
@@ -189,7 +191,6 @@ __device__ __forceinline__ RunMap run_map(const RunView& V, uint32_t b, int lane
     const u32x2 se = *reinterpret_cast<const u32x2*>(row + b);  // row[b], row[b + 1]: one load
     s = se.x;
     n = se.y - s;
-    rb = V.rbase[f * (kMaxRuns + 1) + r];
   }
   uint32_t incl = n;
   if (q.L <= 16) {  // (wave-uniform) the slices sit in lanes 0..15: a row scan by DPP, no LDS trips
@@ -205,7 +206,7 @@ __device__ __forceinline__ RunMap run_map(const RunView& V, uint32_t b, int lane
     }
   }
   q.incl = incl;  // (lanes >= L: unused; lane_slice reads lanes < L only)
-  q.off = rb + s - (incl - n);
+  q.off = (uint64_t)s - (incl - n);
   return q;
 }
 
@@ -425,7 +426,7 @@ __global__ void __launch_bounds__(256) mat_copy_kernel(WaveArgs W, MatArgs M, co
       const uint32_t* row = V.rdir[f] + (uint64_t)r * V.nbp1;
       rs[r] = row[b];
       pre[r + 1] = row[b + 1] - row[b];
-      rb[r] = V.rbase[f * (kMaxRuns + 1) + r];
+      rb[r] = 0;  // (the directory holds absolute rows)
     }
     __syncthreads();
     if (threadIdx.x == 0) {
