@@ -24,6 +24,9 @@ constexpr int kPartRowsPerThread = kPartTile / kPartThreads;
 constexpr int kPartLocalMax = 2048;   // local (tile) bucket slots held in LDS
 constexpr int kPF = 2;                // partition scatter: columns prefetched ahead
 
+// 16 bytes at an 8-byte aligned address (records rows)
+typedef unsigned long long ul2a8 __attribute__((ext_vector_type(2), aligned(8)));
+
 template <int NC>
 struct ColSet {
   uint64_t* c[NC];
@@ -31,6 +34,12 @@ struct ColSet {
   __device__ __forceinline__ uint64_t at(int k, uint64_t i) const { return c[k][s[k] ? i * s[k] : i]; }
   __device__ __forceinline__ const uint64_t* ptr(int k, uint64_t i) const { return &c[k][s[k] ? i * s[k] : i]; }
   __device__ __forceinline__ uint64_t& ref(int k, uint64_t i) const { return c[k][s[k] ? i * s[k] : i]; }
+  // a streamed read of column k: non-temporal for a plain column (each line is read once); a
+  // records field shares its line with the record's other fields, read by the next loads, so that
+  // line must stay cached
+  __device__ __forceinline__ uint64_t stream(int k, uint64_t i) const {
+    return s[k] > 1 ? *ptr(k, i) : __builtin_nontemporal_load(ptr(k, i));
+  }
 };
 
 // Bucket index of hash h among `nb` buckets: floor(h * nb / 2^64). Monotone in h, so for
@@ -141,7 +150,7 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_kernel(ColSet<NC> i
 #pragma unroll
     for (int k = 0; k < kPartRowsPerThread; ++k) {
       const int r = threadIdx.x + k * kPartThreads;
-      v[c][k] = r < rows ? __builtin_nontemporal_load(in.ptr(c, tile0 + r)) : 0;
+      v[c][k] = r < rows ? in.stream(c, tile0 + r) : 0;
     }
   };
 #pragma unroll
@@ -280,8 +289,21 @@ __global__ void __launch_bounds__(kPartThreads) part_scatter_aos_kernel(ColSet<N
       slot_lb[s] = lb[k];
       uint64_t* row = &stage[(uint32_t)s * W];
       row[0] = v0[k];
+      if (in.s[1] > 1) {  // (uniform) records: the row's NC - 1 record words in 16-B pieces (8-B aligned)
+        const uint64_t* rec = in.ptr(1, tile0 + r);
 #pragma unroll
-      for (int c = 1; c < W; ++c) row[c] = c < NC ? __builtin_nontemporal_load(in.ptr(c < NC ? c : 0, tile0 + r)) : 0;
+        for (int c = 1; c + 1 < NC; c += 2) {
+          const ul2a8 q = *reinterpret_cast<const ul2a8*>(rec + (c - 1));
+          row[c] = q.x;
+          row[c + 1] = q.y;
+        }
+        if ((NC - 1) & 1) row[NC - 1] = rec[NC - 2];
+#pragma unroll
+        for (int c = NC; c < W; ++c) row[c] = 0;
+      } else {
+#pragma unroll
+        for (int c = 1; c < W; ++c) row[c] = c < NC ? __builtin_nontemporal_load(in.ptr(c < NC ? c : 0, tile0 + r)) : 0;
+      }
     }
   }
   __syncthreads();
