@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--no-general", action="store_true",
                     help="skip the general_input figures (the same rows merged unsorted, on the partition path)")
     ap.add_argument("--force-tier", type=int, default=0, help="testing: cdb_merge_opts.force_tier")
+    ap.add_argument("--no-decode-leg", action="store_true",
+                    help="c4 at N=1: skip the decode_leg sub-object (the same replicas as snapshots in the "
+                         "reference's HashMap order, decoded into HBM and merged)")
     ap.add_argument("--layout", default="records", choices=["records", "columns"],
                     help="input rows: records (the key-hash column + one record per row, cdb_dev_rows.stride) or "
                          "plain columns")
@@ -324,8 +327,50 @@ def run_single(cdb, args):
         res["general_input"] = general
     for fam in (din.keys, din.nodes, din.members):
         L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
+    if args.config == "c4" and not args.no_decode_leg and args.input_order == "sorted":
+        res["decode_leg"] = decode_leg(cdb, ctx, args, ms)
     res["_sample"] = info["sample"]
     return res
+
+
+def decode_leg(cdb, ctx, args, merge_ms):
+    """The same replicas as snapshots in the reference's HashMap order (the generator's writer
+    layout, no key order: db.rs:122-136), host-resident as a peer would send them, decoded straight
+    into HBM (cdb_decode_snapshots_device: validation, entry index, parse, each snapshot sorted into
+    one run) and merged into the bucket layout (pull.rs:64-79 then :120-128). Not `value`: the
+    snapshot bytes cross PCIe, so the copy floor is reported beside it."""
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    cfg = c4_config(cdb, args.universe_per_gpu, args.replicas, args.seed, 0, args.replicas)
+    log("decode leg: generating the replicas' snapshots")
+    with ThreadPoolExecutor(min(args.replicas, 16)) as ex:  # (the generator releases the GIL)
+        snaps = list(ex.map(lambda r: cdb.gen_snapshot(cfg, r), range(args.replicas)))
+    nbytes = sum(len(x) for x in snaps)
+    trace = os.path.join(tempfile.mkdtemp(), "decode_trace.jsonl")
+    os.environ["CDB_DECODE_TRACE"] = trace
+    L = cdb.lib()
+    log(f"decode leg: {nbytes / 1e9:.2f} GB of snapshots into HBM")
+    t = time.perf_counter()
+    batches, din = cdb.decode_snapshots_device(ctx, snaps, records=True)
+    dec_ms = (time.perf_counter() - t) * 1e3
+    del os.environ["CDB_DECODE_TRACE"]
+    with open(trace) as fh:
+        phases = json.loads(fh.read().strip().split("\n")[-1])
+    out = cdb.DevOutput()
+    out.compact = 0
+    st = cdb.MergeStats()
+    t = time.perf_counter()
+    ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(din), ctypes.byref(cdb.merge_opts()), ctypes.byref(out),
+                                 ctypes.byref(st), None))
+    mms = (time.perf_counter() - t) * 1e3
+    for fam in (din.keys, din.nodes, din.members):
+        L.cdb_dev_rows_release(ctx.handle, ctypes.byref(fam))
+    del batches, snaps
+    return {"snapshots": args.replicas, "bytes": nbytes, "order": "generator (HashMap-like, no key order)",
+            "decode_ms": dec_ms, "merge_ms": mms, "total_ms": dec_ms + mms,
+            "total_over_merge_step": (dec_ms + mms) / merge_ms, "sorted_runs": st.sorted_runs,
+            "pcie_floor_ms": nbytes / 56e9 * 1e3, "phases": phases,
+            "note": "host-resident snapshot bytes; PCIe-inclusive, never `value`"}
 
 
 def run_single_process(cdb, args):

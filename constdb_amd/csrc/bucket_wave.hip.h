@@ -432,7 +432,12 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
         o_win[e] = T == TAG_BYTES ? win : 0;
         vm |= (T == TAG_COUNTER && nvalid >= 2) ? kVmaskMerged : 0;
         // a counter that was never merged keeps its load-time total (aux, head row)
-        sum = (T == TAG_COUNTER && nvalid < 2) ? L.col[KS_AUX][hl] : 0;
+        // (sorted-run path, W.V.nr > 0: the aux slot holds the head row's index, its aux word is
+        // read from the runs only here)
+        if (T == TAG_COUNTER && nvalid < 2) {
+          const uint64_t a = L.col[KS_AUX][hl];
+          sum = W.V.nr ? row_field(W.V.kin, W.V.ks, K_AUX, a) : a;
+        }
         emit[e] = true;
       } else {  // expires / deletes: plain overwrite, the last (pos, src) wins
         const bool removed = fm == 2 && (A.flags & F_GC_DELETES) && gc_hit;

@@ -673,7 +673,8 @@ class GpuDecode {
   uint64_t n_ = 0, nn_ = 0, nm_ = 0;
   std::vector<uint64_t> noff_, moff_;
   std::vector<HostEntry> hosted_;
-  DevBuf d_raw_, d_meta_, d_crc_, d_rows_, d_ord_, d_idx_raw_;
+  DevBuf d_raw_, d_meta_, d_crc_, d_rows_, d_ord_;
+  uint64_t raw_front_ = 0;  // the deferred index uploaded the bytes to d_raw_ + raw_front_
   struct HostReg {  // the batch's bytes, page-locked for a direct upload (unlocked after every sync)
     void* p = nullptr;
     ~HostReg() {
@@ -729,14 +730,19 @@ int GpuDecode::dd_launch(hipStream_t ks) {
     *acc += std::chrono::duration<double, std::milli>(now - t).count();
     t = now;
   };
-  if ((st_ = alloc(&d_idx_raw_.p, len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK) return -1;
+  // the bytes go to their final place: one CRC tile of room in front, so prepare_device zero-fills
+  // the checksum's leading pad there instead of moving the stream
+  const uint64_t front = crc_tile_bytes();
+  if ((st_ = alloc(&d_raw_.p, front + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK) return -1;
+  raw_front_ = front;
+  uint8_t* const dst = (uint8_t*)d_raw_.p + front;
   lap(&lt_[0]);
   // bytes page-locked by the index pass go up directly (no second host copy through the staging
   // ring, and this thread does not wait for the upload)
   if (reg_.p) {
-    ck(hipMemcpyAsync(d_idx_raw_.p, out_->raw.data(), len, hipMemcpyHostToDevice, s), "h2d(index)");
+    ck(hipMemcpyAsync(dst, out_->raw.data(), len, hipMemcpyHostToDevice, s), "h2d(index)");
     if (st_ != CDB_OK) return -1;
-  } else if ((st_ = staged_h2d(ctx_, d_idx_raw_.p, out_->raw.data(), len, s)) != CDB_OK) {
+  } else if ((st_ = staged_h2d(ctx_, dst, out_->raw.data(), len, s)) != CDB_OK) {
     return -1;
   }
   ck(hipEventRecord(d.up.a, s), "event(index)");
@@ -748,7 +754,7 @@ int GpuDecode::dd_launch(hipStream_t ks) {
   lap(&lt_[2]);
   IdxArgs& a = d.a;
   std::memset(&a, 0, sizeof a);
-  a.raw = (const uint8_t*)d_idx_raw_.p;
+  a.raw = dst;
   a.n = len;
   a.S = S;
   a.T = T;
@@ -904,8 +910,9 @@ int GpuDecode::dd_done(int dv, uint64_t end, size_t* err_off) {
   } else if (dv > 0) {
     if (d.offs.p) (void)hipFree(d.offs.p);
     d.offs.p = nullptr;  // the host index pass over the whole stream: its statuses and offsets
-    if (d_idx_raw_.p) (void)hipFree(d_idx_raw_.p);
-    d_idx_raw_.p = nullptr;
+    if (d_raw_.p) (void)hipFree(d_raw_.p);
+    d_raw_.p = nullptr;
+    raw_front_ = 0;
     idx_ = EntryIndex{};
     dcrc_ = DeferredCrc{};
     *out_ = Batch{std::move(out_->raw)};
@@ -944,8 +951,11 @@ int GpuDecode::prepare_device(size_t* err_off) {
   // the raw stream sits after `pad` zero bytes, so the checksummed prefix ends on a CRC tile
   const uint64_t tile = crc_tile_bytes();
   const uint64_t pad = dcrc_.pending ? (tile - dcrc_.len % tile) % tile : 0;
-  if ((st_ = alloc(&d_raw_.p, pad + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK) return st_;
-  raw_pad_ = pad;
+  // (the deferred DATAS index already put the bytes on the device, raw_front_ bytes into d_raw_)
+  if (!raw_front_ && (st_ = alloc(&d_raw_.p, pad + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK)
+    return st_;
+  raw_pad_ = raw_front_ ? raw_front_ : pad;
+  uint8_t* const crc_base = (uint8_t*)d_raw_.p + raw_pad_ - pad;  // pad zero bytes, then the stream
   // small device words: crc | node-row total | member-row total | host-tier flag
   if ((st_ = alloc(&d_crc_.p, 32, "decode: device checksum word")) != CDB_OK) return st_;
   uint64_t* d_small = (uint64_t*)d_crc_.p;
@@ -962,16 +972,10 @@ int GpuDecode::prepare_device(size_t* err_off) {
   uint32_t* d_mcnt = d_ncnt + n;
   uint8_t* d_kind = (uint8_t*)(d_mcnt + n);
   ck(hipEventRecord(ev_.a, s), "event");
-  if (pad) ck(hipMemsetAsync(d_raw_.p, 0, pad, s), "memset(decode)");
+  if (pad) ck(hipMemsetAsync(crc_base, 0, pad, s), "memset(decode)");
   ck(hipMemsetAsync(d_small, 0, 32, s), "memset(decode)");
-  const uint8_t* raw_dev = (const uint8_t*)d_raw_.p + pad;
-  if (st_ == CDB_OK && d_idx_raw_.p) {  // already on the device (the DATAS index): moved to its CRC place
-    ck(hipMemcpyAsync((void*)raw_dev, d_idx_raw_.p, len, hipMemcpyDeviceToDevice, s), "d2d(decode)");
-    ck(hipStreamSynchronize(s), "sync(decode)");
-    (void)hipFree(d_idx_raw_.p);
-    d_idx_raw_.p = nullptr;
-  } else if (st_ == CDB_OK)
-    st_ = staged_h2d(ctx_, (void*)raw_dev, out_->raw.data(), len, s);
+  const uint8_t* raw_dev = (const uint8_t*)d_raw_.p + raw_pad_;
+  if (st_ == CDB_OK && !raw_front_) st_ = staged_h2d(ctx_, (void*)raw_dev, out_->raw.data(), len, s);
   if (dd) {  // the DATAS section's offsets from the device index, then the side sections'
     ck(hipMemcpyAsync(d_off, di_.offs.p, dd * 8, hipMemcpyDeviceToDevice, s), "d2d(decode)");
     ck(hipMemsetAsync(d_kind, 0, dd, s), "memset(decode)");
@@ -1006,7 +1010,7 @@ int GpuDecode::prepare_device(size_t* err_off) {
                                                                                (uint64_t*)nullptr);
   ck(hipGetLastError(), "decode scans");
   if (dcrc_.pending && st_ == CDB_OK)  // the index pass left the stream checksum to the GPU
-    st_ = crc64_device(ctx_, (const uint8_t*)d_raw_.p, pad + dcrc_.len, d_small, s);
+    st_ = crc64_device(ctx_, crc_base, pad + dcrc_.len, d_small, s);
   uint64_t small[4] = {0, 0, 0, 0};
   ck(hipMemcpyAsync(small, d_small, 32, hipMemcpyDeviceToHost, s), "d2h(decode)");
   ck(hipStreamSynchronize(s), "sync(decode)");
@@ -1630,6 +1634,7 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
   auto alloc = [&](cdb_dev_rows* r, uint64_t rows, int nc) {
     return rec ? cdb_dev_rows_alloc_records(ctx, r, rows, nc) : cdb_dev_rows_alloc(ctx, r, rows, nc);
   };
+  clk.mark("order_sort_sync");
   if ((st = alloc(&din->keys, tot[0], kKeyCols)) != CDB_OK || (st = alloc(&din->nodes, tot[1], kNodeCols)) != CDB_OK ||
       (st = alloc(&din->members, tot[2], kMemberCols)) != CDB_OK) {
     cdb_dev_rows_release(ctx, &din->keys);
@@ -1637,6 +1642,7 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     cdb_dev_rows_release(ctx, &din->members);
     return st;
   }
+  clk.mark("alloc_rows");
   uint64_t o[3] = {0, 0, 0};
   for (uint32_t i = 0; i < n; ++i) {
     uint64_t* k[kKeyCols];
@@ -1666,7 +1672,7 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     din->n_runs = n;
     for (int f = 0; f < 3; ++f) din->run_start[f][n] = o[f];
   }
-  clk.mark("alloc_emit");
+  clk.mark("emit");
   {
     uint64_t bytes = 0;
     for (uint32_t i = 0; i < n; ++i) bytes += lens[i];

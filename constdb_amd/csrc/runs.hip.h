@@ -247,21 +247,22 @@ __device__ __forceinline__ void load_runs(const WaveArgs& W, const WaveDir& d, c
     const uint64_t row = run_row(qk, c);
     if (c < d.K) {
       in.kh[e] = V.kin[K_KH][row];
-      if (V.ks == kKeyCols - 1) {  // (uniform) records: the 48-B record as three 16-B pieces
-        const u64x2* r = reinterpret_cast<const u64x2*>(V.kin[1] + row * (kKeyCols - 1));
-        const u64x2 q0 = r[0], q1 = r[1], q2 = r[2];
+      // aux (a counter's load-time total) is read only by a counter key no other replica holds:
+      // the fold fetches it then, by the row index kept in its place (wave_bucket, RunView)
+      in.kaux[e] = row;
+      if (V.ks == kKeyCols - 1) {  // (uniform) records: kf ct | ut dt as two 16-B pieces, then meta
+        const uint64_t* rec = V.kin[1] + row * (kKeyCols - 1);
+        const u64x2 q0 = reinterpret_cast<const u64x2*>(rec)[0], q1 = reinterpret_cast<const u64x2*>(rec)[1];
         in.kf[e] = q0.x;
         in.kct[e] = q0.y;
         in.kut[e] = q1.x;
         in.kdt[e] = q1.y;
-        in.kaux[e] = q2.x;
-        in.kmeta[e] = q2.y;
+        in.kmeta[e] = rec[K_META - 1];
       } else {
         in.kf[e] = V.kin[K_KF][row];
         in.kct[e] = V.kin[K_CT][row];
         in.kut[e] = V.kin[K_UT][row];
         in.kdt[e] = V.kin[K_DT][row];
-        in.kaux[e] = V.kin[K_AUX][row];
         in.kmeta[e] = V.kin[K_META][row];
       }
     }

@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
 O=gpurun_out
 mkdir -p $O
-timeout -k 10 700 python -u -m pytest tests/test_records_gpu.py tests/test_golden.py tests/test_runs_oracle_gpu.py tests/test_sorted_runs_gpu.py tests/test_shard_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread > $O/pytest_r4l.log 2>&1
+timeout -k 10 700 python -u -m pytest tests/test_records_gpu.py tests/test_golden.py tests/test_runs_oracle_gpu.py tests/test_sorted_runs_gpu.py tests/test_gpu_parity.py tests/test_configs_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread > $O/pytest_r4l.log 2>&1
 rc=$?; tail -2 $O/pytest_r4l.log
 [ $rc -eq 0 ] || { echo "pytest ended with $rc"; exit 1; }
 for lay in records columns; do
