@@ -94,6 +94,27 @@ struct DecArgs {
 __device__ __forceinline__ uint64_t& dcell(uint64_t* const* col, uint32_t s, int c, uint64_t r) {
   return col[c][c ? r * s : r];
 }
+// A whole row: the hash word, then fields 1.. -- in the records layout (s = ncols - 1) as 16-B
+// pieces of the record (8-B aligned), not one partial-line store per field.
+typedef unsigned long long dec_u64x2 __attribute__((ext_vector_type(2), aligned(8)));
+template <int NC>
+__device__ __forceinline__ void put_row(uint64_t* const* col, uint32_t s, uint64_t r, const uint64_t (&f)[NC]) {
+  col[0][r] = f[0];
+  if (s == NC - 1) {
+    uint64_t* rec = col[1] + r * (NC - 1);
+#pragma unroll
+    for (int c = 1; c + 1 < NC; c += 2) {
+      dec_u64x2 q;
+      q.x = f[c];
+      q.y = f[c + 1];
+      *reinterpret_cast<dec_u64x2*>(rec + (c - 1)) = q;
+    }
+    if ((NC - 1) & 1) rec[NC - 2] = f[NC - 1];
+  } else {
+#pragma unroll
+    for (int c = 1; c < NC; ++c) col[c][r] = f[c];
+  }
+}
 
 struct Head {  // the part of a DATAS entry before the payload
   Span key;
@@ -206,11 +227,8 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
     const Span key = rd_span(p, o);
     const uint64_t t = (uint64_t)rd_int(p, o);
     const Hash128 h = hash_bytes(p + key.off, key.len, kDomainKey);
-    dcell(A.k, A.ks, 0, kr) = h.h;
-    dcell(A.k, A.ks, 1, kr) = h.f;
-    dcell(A.k, A.ks, 2, kr) = t;
-    dcell(A.k, A.ks, 3, kr) = dcell(A.k, A.ks, 4, kr) = dcell(A.k, A.ks, 5, kr) = 0;
-    dcell(A.k, A.ks, 6, kr) = meta_pack(A.kind[i] == 1 ? TAG_EXPIRE : TAG_DELETE, A.pos, i);
+    const uint64_t f[7] = {h.h, h.f, t, 0, 0, 0, meta_pack(A.kind[i] == 1 ? TAG_EXPIRE : TAG_DELETE, A.pos, i)};
+    put_row<7>(A.k, A.ks, kr, f);
     A.kref[i] = make_ulonglong2(key.off, key.len);
     A.vref[i] = make_ulonglong2(0, 0);
     return;
@@ -240,12 +258,8 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
         (void)rd_int(p, r);
       }
       if (later) continue;
-      dcell(A.nd, A.cs, 0, row) = h.h;
-      dcell(A.nd, A.cs, 1, row) = h.f;
-      dcell(A.nd, A.cs, 2, row) = id;
-      dcell(A.nd, A.cs, 3, row) = v;
-      dcell(A.nd, A.cs, 4, row) = t;
-      dcell(A.nd, A.cs, 5, row) = meta_pack(0, A.pos, row);
+      const uint64_t f[6] = {h.h, h.f, id, v, t, meta_pack(0, A.pos, row)};
+      put_row<6>(A.nd, A.cs, row, f);
       ++row;
     }
   } else if ((hd.tag == TAG_SET || hd.tag == TAG_DICT) && A.mcount[i] != kHostTier) {
@@ -270,24 +284,15 @@ __global__ void __launch_bounds__(kDecThreads) emit_kernel(DecArgs A) {
       if (dict && j < na) v = rd_span(p, q);
       if (!((keep >> j) & 1)) continue;
       const Hash128 mh = hash_bytes(p + m.off, m.len, kDomainMember);
-      dcell(A.mb, A.cs, 0, row) = h.h;
-      dcell(A.mb, A.cs, 1, row) = h.f;
-      dcell(A.mb, A.cs, 2, row) = mh.h;
-      dcell(A.mb, A.cs, 3, row) = mh.f;
-      dcell(A.mb, A.cs, 4, row) = t;
-      dcell(A.mb, A.cs, 5, row) = meta_pack(j < na ? KIND_ADD : KIND_DEL, A.pos, row);
+      const uint64_t f[6] = {h.h, h.f, mh.h, mh.f, t, meta_pack(j < na ? KIND_ADD : KIND_DEL, A.pos, row)};
+      put_row<6>(A.mb, A.cs, row, f);
       A.mref[row] = make_ulonglong2(m.off, m.len);
       A.mvref[row] = make_ulonglong2(v.off, v.len);
       ++row;
     }
   }
-  dcell(A.k, A.ks, 0, kr) = h.h;
-  dcell(A.k, A.ks, 1, kr) = h.f;
-  dcell(A.k, A.ks, 2, kr) = hd.ct;
-  dcell(A.k, A.ks, 3, kr) = hd.ut;
-  dcell(A.k, A.ks, 4, kr) = hd.dt;
-  dcell(A.k, A.ks, 5, kr) = aux;
-  dcell(A.k, A.ks, 6, kr) = meta_pack(hd.tag, A.pos, i);
+  const uint64_t f[7] = {h.h, h.f, hd.ct, hd.ut, hd.dt, aux, meta_pack(hd.tag, A.pos, i)};
+  put_row<7>(A.k, A.ks, kr, f);
   A.kref[i] = make_ulonglong2(hd.key.off, hd.key.len);
   A.vref[i] = make_ulonglong2(val.off, val.len);
 }
@@ -315,12 +320,17 @@ struct Sections {
   uint64_t b[4];  // section s = entries [b[s], b[s + 1]): DATAS, EXPIRES, DELETES
 };
 
+// Grid-stride with a bounded grid, one flag update per wave at the end, skipped once the flag is
+// set: a snapshot in HashMap order has a descent at every other entry, and one atomic per wave on
+// the one flag word serialised ~500K atomics per 34M entries (6 ms).
 __global__ void __launch_bounds__(kDecThreads) order_check_kernel(const uint64_t* __restrict__ kh, Sections S,
                                                                   unsigned long long* flag) {
-  const uint64_t i = (uint64_t)blockIdx.x * kDecThreads + threadIdx.x;
   const uint64_t n = S.b[3];
-  const bool bad = i + 1 < n && i + 1 != S.b[1] && i + 1 != S.b[2] && kh[i] > kh[i + 1];
-  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1ull);
+  bool bad = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * kDecThreads + threadIdx.x; i + 1 < n && !bad;
+       i += (uint64_t)gridDim.x * kDecThreads)
+    bad = i + 1 != S.b[1] && i + 1 != S.b[2] && kh[i] > kh[i + 1];
+  if (__ballot(bad) && (threadIdx.x & 63) == 0 && *(volatile unsigned long long*)flag == 0) atomicOr(flag, 1ull);
 }
 
 __device__ __forceinline__ uint64_t count_below(const uint64_t* kh, uint64_t lo, uint64_t hi, uint64_t v, bool ties) {
@@ -1259,7 +1269,7 @@ cdb_status GpuDecode::order_check() {
   ck(hipMemsetAsync(flag, 0, 8, s_), "memset(decode order)");
   key_hash_kernel<<<grid_, kDecThreads, 0, s_>>>(A_, kh);
   ck(hipGetLastError(), "key_hash_kernel");
-  order_check_kernel<<<grid_, kDecThreads, 0, s_>>>(kh, sec_, flag);
+  order_check_kernel<<<std::min<uint32_t>(grid_, 2048), kDecThreads, 0, s_>>>(kh, sec_, flag);
   ck(hipGetLastError(), "order_check_kernel");
   ck(hipMemcpyAsync(&order_flag_, flag, 8, hipMemcpyDeviceToHost, s_), "d2h(decode order)");
   ordered_ = st_ == CDB_OK;
