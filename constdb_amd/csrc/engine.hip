@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <map>
 #include <cstdlib>
 #include <cstring>
@@ -716,10 +717,16 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   const int lo = run_order ? 6 : 0;
   const int passes = (gbits + 6 - lo + std::min(min_id, kHotIdBits - 6) + 7) / 8;
   int id_bits = std::min(kHotIdBits - 6, 8 * passes - 6 + lo - gbits);
+  // Run order and buckets of at most kSortCap children: the per-bucket LDS path
+  // (hot_sortfold_kernel), whose 32-bit tags take kSortIdBits id bits (test hook CDB_HOT_LDS=0:
+  // the global sort for every batch).
+  const char* lds_env = std::getenv("CDB_HOT_LDS");
+  const bool lds = run_order && cmax <= kSortCap && !(lds_env && lds_env[0] == '0');
+  if (lds) id_bits = kSortIdBits;
   // test hook: fewer id bits force the collision (successor-selection) fold
   if (const char* e = std::getenv("CDB_HOT_ID_BITS")) {
     const int bits = std::atoi(e);
-    if (bits >= 1 && bits <= kHotIdBits - 6) id_bits = bits;
+    if (bits >= 1 && bits <= (lds ? kSortIdBits : kHotIdBits - 6)) id_bits = bits;
   }
   HA.g_shift = 6 + id_bits;
   HA.id_shift = 64 - id_bits;
@@ -755,6 +762,29 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   HA.v = v;
   hot_keys_kernel<<<H, kBktThreads, 0, s>>>(A, HA);
   CDB_TRY(launch_check(ctx, s, "hot_keys_kernel"));
+  if (lds) {  // fold results per run go to the (unused) tag arrays
+    HA.fold_v = w;
+    HA.fold_q = v;
+    const bool prof = std::getenv("CDB_HOT_PROF") != nullptr;  // test hook: phase clocks to stderr
+    if (prof) {
+      HA.prof = nc >= 8 ? (unsigned long long*)w2 : nullptr;  // (the global sort's spare keys)
+      if (HA.prof) CDB_HIP(hipMemsetAsync(HA.prof, 0, 64, s), "memset");
+    }
+    hot_sortfold_kernel<<<H, kSortThreads, 0, s>>>(A, HA, id_bits);
+    CDB_TRY(launch_check(ctx, s, "hot_sortfold_kernel"));
+    CDB_HIP(hipStreamSynchronize(s), "sync");  // the host vectors are copy sources
+    if (prof && HA.prof) {
+      uint64_t t[8];
+      CDB_HIP(hipMemcpy(t, HA.prof, 64, hipMemcpyDeviceToHost), "d2h");
+      const char* names[6] = {"tag", "sort", "runs", "fold0+scan", "fold1", "finish"};
+      double tot = 0;
+      for (int i = 0; i < 6; ++i) tot += (double)t[i];
+      std::fprintf(stderr, "hot_sortfold H=%u tc=%llu:", H, (unsigned long long)tc);
+      for (int i = 0; i < 6; ++i) std::fprintf(stderr, " %s %.1f%%", names[i], 100.0 * t[i] / std::max(tot, 1.0));
+      std::fprintf(stderr, " (%.3f ms summed over workgroups / 256)\n", tot / 100e3 / 256);
+    }
+    return CDB_OK;
+  }
   const uint32_t grid = (uint32_t)std::min<uint64_t>((tc + 255) / 256, 16384);
   if (tc) {
     hot_tag_kernel<<<grid, 256, 0, s>>>(A, HA);
@@ -841,7 +871,8 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   // Each kind in two size classes: the sort's id bits follow the batch's largest bucket and its
   // key bits the batch's key count, so many small buckets and a few huge ones sorted together
   // can take a pass more than either alone (C5: 20.1 -> 19.6 ms split).
-  constexpr uint32_t kBigBucket = 16384;
+  // (On run order the small class is the LDS path's: at most kSortCap children.)
+  const uint32_t kBigBucket = rv ? kSortCap : 16384;
   for (int pass = 0; pass < 4; ++pass) {
     runs_batch = pass < 2;
     const bool big = pass & 1;

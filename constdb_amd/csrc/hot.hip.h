@@ -60,13 +60,14 @@ struct HotArgs {
   int g_shift;               // W's key-id bits start here (kHotIdBits or less)
   uint32_t* run_list;        // sorted position of every run's first row, ascending
   const uint64_t* run_count; // runs in run_list (device)
-  uint32_t* fold_q;          // per run start: the sorted position whose row is the output
+  uint32_t* fold_q;          // per run: the row of the run (k from its start) that is the output
                              // (members: the winner; nodes: the head), kNone: selection path
-  uint64_t* fold_v;          // per run start: a counter node's folded value
+  uint64_t* fold_v;          // per run: a counter node's folded value
   // runs mode (sorted-run input, buckets of at most MatArgs::runs_child_max children): the
   // tag pass reads the children from the runs' columns (the absolute run row), not from copies
   int runs;
   RunView V;
+  unsigned long long* prof;  // test hook (CDB_HOT_PROF): hot_sortfold_kernel's phase clocks, or null
 };
 
 // A child's columns: its copied AoS row, or (runs mode) the runs' SoA columns.
@@ -120,8 +121,66 @@ __global__ void __launch_bounds__(kBktThreads) hot_keys_kernel(BucketArgs A, Hot
     if (S.st[i]) atomicAdd(&stat_shard(A.stats)[i], S.st[i]);
 }
 
-__global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
+// Flat child j of hot bucket h: its fold fields into rec[j] and its tag W (the bucket's marker when
+// it takes no part; orph counts children whose key is not in the bucket).
+__device__ __forceinline__ uint64_t hot_tag_child(const BucketArgs& A, const HotArgs& H, uint32_t h, uint64_t j,
+                                                  unsigned long long& orph) {
   const int ks = A.key_shift;
+  const uint32_t b = H.ids[h];
+  const uint32_t i = (uint32_t)(j - H.c_off[h]), N = A.ncnt[b];
+  const bool isn = i < N;
+  uint32_t row;
+  if (H.runs) {  // the bucket's slices of the family's runs, in run order (as mat_copy lays them)
+    const int f = isn ? 1 : 2;
+    uint32_t k = isn ? i : i - N, r = 0;
+    for (;; ++r) {
+      const uint32_t* d = H.V.rdir[f] + (uint64_t)r * H.V.nbp1 + b;
+      const uint32_t len = d[1] - d[0];
+      if (k < len || r + 1 >= H.V.nr) {
+        row = d[0] + k;  // (absolute rows)
+        break;
+      }
+      k -= len;
+    }
+  } else {
+    row = isn ? A.np[A.nbase[b] + i] : A.mp[A.mbase[b] + (i - N)];
+  }
+  const uint64_t pkh = hot_col(A, H, isn, row, C_PKH), pkf = hot_col(A, H, isn, row, C_PKF);
+  const uint64_t id1 = hot_col(A, H, isn, row, C_ID1), m = hot_col(A, H, isn, row, C_META);
+  const uint64_t id2 = hot_col(A, H, isn, row, C_ID2), t = hot_col(A, H, isn, row, C_T);
+  // lower bound over the bucket's sorted output keys on (kh << shift, kh, kf)
+  const uint32_t g0 = H.hk_off[h], kout = H.hk_kout[h];
+  uint32_t lo = 0, hi = kout;
+  const uint64_t sp = pkh << ks;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const uint64_t kh = H.hk_h[g0 + mid], sm = kh << ks;
+    const bool less = sm < sp || (sm == sp && (kh < pkh || (kh == pkh && H.hk_f[g0 + mid] < pkf)));
+    lo = less ? mid + 1 : lo;
+    hi = less ? hi : mid;
+  }
+  uint64_t w = hot_marker(H, h);
+  if (lo < kout && H.hk_h[g0 + lo] == pkh && H.hk_f[g0 + lo] == pkf && (H.hk_tp[g0 + lo] & 0xFF) <= TAG_SET) {
+    const uint32_t T = H.hk_tp[g0 + lo] & 0xFF, hp = H.hk_tp[g0 + lo] >> 8, p = meta_pos(m);
+    const bool type_ok = isn ? T == TAG_COUNTER : (T == TAG_SET || T == TAG_DICT);
+    const bool elem_ok = (H.hk_vm[g0 + lo] >> p) & 1;
+    const bool cand = isn || meta_tag(m) == KIND_ADD || p == hp;  // remote dels ignored
+    if (type_ok && elem_ok && cand) {
+      // (the id field stops one below all ones: the marker is above every W of the bucket in
+      // the sorted bits, which leave out the pos bits)
+      const uint64_t ih = isn ? mix64(id1) : id1, top = (1ull << (H.g_shift - 6)) - 2;
+      w = ((uint64_t)(g0 + lo) << H.g_shift) | (min(ih >> H.id_shift, top) << 6) | p;
+    }
+  } else {
+    ++orph;
+  }
+  // the fold reads a child's four fields as one 32-B record (flat order: written in sequence)
+  H.rec[2 * j] = make_ulonglong2(id1, id2);
+  H.rec[2 * j + 1] = make_ulonglong2(t, m);
+  return w;
+}
+
+__global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
   unsigned long long orph = 0;
   const uint32_t lane = threadIdx.x & 63;
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < H.n_children;
@@ -131,71 +190,19 @@ __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
     uint32_t h = lane == 0 ? hot_bucket_of(H, j) : 0;
     h = (uint32_t)__shfl((int)h, 0);
     while (h + 1 < H.H && H.c_off[h + 1] <= j) ++h;
-    const uint32_t b = H.ids[h];
-    const uint32_t i = (uint32_t)(j - H.c_off[h]), N = A.ncnt[b];
-    const bool isn = i < N;
-    uint32_t row;
-    if (H.runs) {  // the bucket's slices of the family's runs, in run order (as mat_copy lays them)
-      const int f = isn ? 1 : 2;
-      uint32_t k = isn ? i : i - N, r = 0;
-      for (;; ++r) {
-        const uint32_t* d = H.V.rdir[f] + (uint64_t)r * H.V.nbp1 + b;
-        const uint32_t len = d[1] - d[0];
-        if (k < len || r + 1 >= H.V.nr) {
-          row = d[0] + k;  // (absolute rows)
-          break;
-        }
-        k -= len;
-      }
-    } else {
-      row = isn ? A.np[A.nbase[b] + i] : A.mp[A.mbase[b] + (i - N)];
-    }
-    const uint64_t pkh = hot_col(A, H, isn, row, C_PKH), pkf = hot_col(A, H, isn, row, C_PKF);
-    const uint64_t id1 = hot_col(A, H, isn, row, C_ID1), m = hot_col(A, H, isn, row, C_META);
-    const uint64_t id2 = hot_col(A, H, isn, row, C_ID2), t = hot_col(A, H, isn, row, C_T);
-    // lower bound over the bucket's sorted output keys on (kh << shift, kh, kf)
-    const uint32_t g0 = H.hk_off[h], kout = H.hk_kout[h];
-    uint32_t lo = 0, hi = kout;
-    const uint64_t sp = pkh << ks;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      const uint64_t kh = H.hk_h[g0 + mid], sm = kh << ks;
-      const bool less = sm < sp || (sm == sp && (kh < pkh || (kh == pkh && H.hk_f[g0 + mid] < pkf)));
-      lo = less ? mid + 1 : lo;
-      hi = less ? hi : mid;
-    }
-    uint64_t w = hot_marker(H, h);
-    if (lo < kout && H.hk_h[g0 + lo] == pkh && H.hk_f[g0 + lo] == pkf && (H.hk_tp[g0 + lo] & 0xFF) <= TAG_SET) {
-      const uint32_t T = H.hk_tp[g0 + lo] & 0xFF, hp = H.hk_tp[g0 + lo] >> 8, p = meta_pos(m);
-      const bool type_ok = isn ? T == TAG_COUNTER : (T == TAG_SET || T == TAG_DICT);
-      const bool elem_ok = (H.hk_vm[g0 + lo] >> p) & 1;
-      const bool cand = isn || meta_tag(m) == KIND_ADD || p == hp;  // remote dels ignored
-      if (type_ok && elem_ok && cand) {
-        // (the id field stops one below all ones: the marker is above every W of the bucket in
-        // the sorted bits, which leave out the pos bits)
-        const uint64_t ih = isn ? mix64(id1) : id1, top = (1ull << (H.g_shift - 6)) - 2;
-        w = ((uint64_t)(g0 + lo) << H.g_shift) | (min(ih >> H.id_shift, top) << 6) | p;
-      }
-    } else {
-      ++orph;
-    }
-    H.w[j] = w;
+    H.w[j] = hot_tag_child(A, H, h, j, orph);
     H.v[j] = (uint32_t)j;
-    // the fold reads a child's four fields as one 32-B record (flat order: written in sequence)
-    H.rec[2 * j] = make_ulonglong2(id1, id2);
-    H.rec[2 * j + 1] = make_ulonglong2(t, m);
-    H.c_h[j] = h | (isn ? 0u : 0x80000000u);
+    H.c_h[j] = h | ((uint32_t)(j - H.c_off[h]) < A.ncnt[H.ids[h]] ? 0u : 0x80000000u);
   }
   if (orph) atomicAdd(&stat_shard(A.stats)[ST_ORPHANS], orph);
 }
 
-// One child of a W-run, by sorted position q (j: its flat index, the last tie-break).
+// One child of a W-run, by flat index j (the last tie-break).
 struct HotChild {
   uint64_t id1, id2, t, meta;
   uint32_t j;
 };
-__device__ __forceinline__ HotChild hot_child(const HotArgs& H, uint64_t q) {
-  const uint32_t j = H.v[q];
+__device__ __forceinline__ HotChild hot_child(const HotArgs& H, uint32_t j) {
   const ulonglong2 a = H.rec[2 * (uint64_t)j], b = H.rec[2 * (uint64_t)j + 1];
   HotChild c;
   c.id1 = a.x;
@@ -234,15 +241,167 @@ __global__ void __launch_bounds__(256) hot_runlist_kernel(HotArgs H, const uint3
 
 constexpr uint32_t kFoldFast = 8;  // runs up to this many rows: rows in registers, loads overlapped
 
-// One thread per run. Pass 0: the run's output count (emit_n / emit_m at its first position)
-// and, for a run of one exact id whose rows arrive in strictly increasing (pos, src) order (the
-// tag's low bits are the position) and no longer than kFoldFast, the output row's position and
-// value (fold_q / fold_v); pass 1 writes outputs at their rank. Other runs (ids sharing the
-// tag's id-hash bits -- g_shift - 6 of them, 20 to 34 -- and long runs) fold by successor selection in both passes: each step selects the successor
-// of the last visited row (O(run^2) over rows in L2, no per-thread arrays), so rows are folded
-// in order whatever order the sort left them in. Loops have wave-uniform trip counts with
-// per-lane predicates: a loop-carried row must not be a live-out of a loop with divergent exits
-// (gfx950 compilers have produced the first candidate instead of the smallest there).
+// One run's contribution to its key's row: outputs, first output slot, counter sum.
+struct HotAcc {
+  uint32_t nout = 0, k_cnt = 0, k_cb = kNone;
+  unsigned long long k_sum = 0;
+};
+
+// The fold of one W-run: its rows k = 0 .. nrows - 1 in sorted order, flat index jat(k), key G,
+// bucket b. Pass 0 counts the run's outputs (acc.nout) and, for a run of one exact id whose rows
+// arrive in strictly increasing (pos, src) order (the tag's low bits are the position) and no
+// longer than kFoldFast, keeps the fold: *fq = the output row's k (members: the winner; nodes: the
+// head), *fv = a counter node's folded value; *fq = kNone sends the run to the selection path.
+// Pass 1 (emitted: pass 0 counted outputs) writes the outputs at rows obase.. of the bucket's
+// family and sums them into acc. Other runs (ids sharing the tag's id-hash bits, and long runs)
+// fold by successor selection in both passes: each step selects the successor of the last visited
+// row (O(run^2) over rows in L2, no per-thread arrays), so rows are folded in order whatever order
+// the sort left them in. Every lane of the wave calls this (act false for idle lanes): loops have
+// wave-uniform trip counts with per-lane predicates -- a loop-carried row must not be a live-out
+// of a loop with divergent exits (gfx950 compilers have produced the first candidate instead of
+// the smallest there).
+template <class JAt>
+__device__ __forceinline__ void hot_fold_run(const BucketArgs& A, const HotArgs& H, int pass, bool act, bool isn,
+                                             uint32_t b, uint32_t G, uint32_t nrows, JAt jat, uint64_t obase,
+                                             bool emitted, uint32_t* fq, uint64_t* fv, HotAcc& acc,
+                                             unsigned long long& gcm, unsigned long long& nslow) {
+  auto put = [&](uint64_t id1, uint64_t id2, uint64_t t, uint64_t meta, uint64_t v) {
+    const uint32_t o = (uint32_t)(obase + acc.nout);
+    uint64_t* row = (isn ? A.nos + (uint64_t)(A.nbase[b] + o) * kChildStride
+                         : A.mos + (uint64_t)(A.mbase[b] + o) * kChildStride);
+    row[C_PKH] = H.hk_h[G];
+    row[C_PKF] = H.hk_f[G];
+    row[C_ID1] = id1;
+    row[C_ID2] = isn ? v : id2;
+    row[C_T] = t;
+    row[C_META] = isn ? meta_pack(0, meta_pos(meta), meta_src(meta)) : meta;
+    acc.k_cb = min(acc.k_cb, o);
+    ++acc.k_cnt;
+    acc.k_sum += isn ? v : 0;
+  };
+  auto emit_id = [&](const HotChild& hd, uint64_t v, uint64_t tw, uint64_t wmeta) {
+    if (!isn && (A.flags & F_GC_MEMBERS) && meta_tag(wmeta) == KIND_DEL && tw < A.gc_wm) {
+      ++gcm;
+      return;
+    }
+    if (pass == 1) put(hd.id1, hd.id2, isn ? hd.t : tw, isn ? hd.meta : wmeta, v);
+    ++acc.nout;
+  };
+  bool slow = act;
+  if (pass == 0) {
+    // fast path: up to kFoldFast rows, their loads issued together
+    const bool fast = act && nrows <= kFoldFast;
+    uint32_t rj[kFoldFast];
+#pragma unroll
+    for (uint32_t k = 0; k < kFoldFast; ++k) rj[k] = (fast && k < nrows) ? jat(k) : 0;
+    uint64_t xi1[kFoldFast], xi2[kFoldFast], xt[kFoldFast], xm[kFoldFast];
+#pragma unroll
+    for (uint32_t k = 0; k < kFoldFast; ++k) {
+      if (fast && k < nrows) {
+        const ulonglong2 a = H.rec[2 * (uint64_t)rj[k]], c = H.rec[2 * (uint64_t)rj[k] + 1];
+        xi1[k] = a.x;
+        xi2[k] = a.y;
+        xt[k] = c.x;
+        xm[k] = c.y;
+      } else {
+        xi1[k] = xi2[k] = xt[k] = xm[k] = 0;
+      }
+    }
+    bool simple = fast;
+    uint64_t v = xi2[0], tw = xt[0];
+    uint32_t qw = 0;  // winner (members)
+#pragma unroll
+    for (uint32_t k = 1; k < kFoldFast; ++k) {
+      if (k < nrows) {
+        simple = simple && xi1[k] == xi1[0] && (isn || xi2[k] == xi2[0]) &&
+                 meta_order(xm[k]) > meta_order(xm[k - 1]);
+        if (isn) {  // Counter::merge (type_counter.rs:60-84): the head's t is kept
+          v = xt[k] > xt[0] ? xi2[k] : (xt[k] == xt[0] ? imax64(v, xi2[k]) : v);
+        } else if (!(tw > xt[k])) {  // LWWHash::set (lwwhash.rs:87-107): later wins ties
+          tw = xt[k];
+          qw = k;
+        }
+      }
+    }
+    if (simple) {
+      uint64_t wm = xm[0];
+#pragma unroll
+      for (uint32_t k = 1; k < kFoldFast; ++k) wm = (k == qw) ? xm[k] : wm;
+      HotChild hd;
+      hd.id1 = xi1[0];
+      hd.id2 = xi2[0];
+      hd.t = xt[0];
+      hd.meta = xm[0];
+      hd.j = 0;
+      emit_id(hd, v, tw, wm);
+      *fq = isn ? 0u : qw;
+      *fv = v;
+      slow = false;
+    } else if (act) {
+      *fq = kNone;
+    }
+  } else if (act) {  // pass 1, fold kept by pass 0
+    const uint32_t q = *fq;
+    if (q != kNone) {
+      slow = false;
+      if (emitted) {
+        const HotChild x = hot_child(H, jat(q));
+        put(x.id1, x.id2, x.t, x.meta, *fv);
+      }
+    }
+  }
+  // selection path
+  nslow += (pass == 0 && slow) ? 1 : 0;
+  uint32_t kslow = slow ? nrows : 0;
+  for (int off = 32; off > 0; off >>= 1) kslow = max(kslow, (uint32_t)__shfl_xor((int)kslow, off));
+  HotChild last, head;  // last visited row; first row of the id being folded
+  last.id1 = last.id2 = last.t = last.meta = 0;
+  last.j = 0;
+  head = last;
+  uint64_t v = 0, tw = 0, wmeta = 0;  // the fold of head's id so far
+  bool open = false;                  // head's id has rows not yet emitted
+  for (uint32_t step = 0; step < kslow + 1 && kslow; ++step) {
+    HotChild c = last;
+    bool have = false;
+    for (uint32_t k = 0; k < kslow; ++k) {
+      if (slow && k < nrows && step < nrows) {
+        const HotChild x = hot_child(H, jat(k));
+        const bool after = step == 0 || hot_before(last, x, isn);
+        const bool take = after && (!have || hot_before(x, c, isn));
+        c.id1 = take ? x.id1 : c.id1;
+        c.id2 = take ? x.id2 : c.id2;
+        c.t = take ? x.t : c.t;
+        c.meta = take ? x.meta : c.meta;
+        c.j = take ? x.j : c.j;
+        have = have || take;
+      }
+    }
+    const bool new_id = !have || !open || c.id1 != head.id1 || (!isn && c.id2 != head.id2);
+    if (slow && open && new_id) {  // head's id is complete: emit it
+      emit_id(head, v, tw, wmeta);
+      open = false;
+    }
+    if (slow && have) {
+      if (new_id) {  // c opens an id
+        head = c;
+        v = c.id2;
+        tw = c.t;
+        wmeta = c.meta;
+        open = true;
+      } else if (isn) {
+        v = c.t > head.t ? c.id2 : (c.t == head.t ? imax64(v, c.id2) : v);
+      } else if (!(tw > c.t)) {
+        tw = c.t;
+        wmeta = c.meta;
+      }
+      last = c;
+    }
+  }
+}
+
+// One thread per W-run of the global sort (a (key, child id) group, ~ one row per replica): pass
+// 0 counts (emit_n / emit_m at the run's first position), pass 1 writes at the run's rank in its
+// bucket (after scans of the counts) and adds the run to its key row.
 __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, int pass) {
   unsigned long long gcm = 0, nslow = 0;
   const uint64_t nruns = *H.run_count;
@@ -270,148 +429,18 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
       G = (uint32_t)(W >> H.g_shift);
       if (pass == 1) obase = (isn ? H.rank_n[p] - H.rank_n[H.c_off[h]] : H.rank_m[p] - H.rank_m[H.c_off[h]]);
     }
-    uint32_t nout = 0;
-    // this run's contribution to its key's row: outputs, first output slot, counter sum (one
-    // atomic per key and wave below, not per output: a hot key owns up to millions of them)
-    uint32_t k_cnt = 0, k_cb = kNone;
-    unsigned long long k_sum = 0;
-    auto put = [&](uint64_t id1, uint64_t id2, uint64_t t, uint64_t meta, uint64_t v) {
-      const uint32_t o = (uint32_t)(obase + nout);
-      uint64_t* row = (isn ? A.nos + (uint64_t)(A.nbase[b] + o) * kChildStride
-                           : A.mos + (uint64_t)(A.mbase[b] + o) * kChildStride);
-      row[C_PKH] = H.hk_h[G];
-      row[C_PKF] = H.hk_f[G];
-      row[C_ID1] = id1;
-      row[C_ID2] = isn ? v : id2;
-      row[C_T] = t;
-      row[C_META] = isn ? meta_pack(0, meta_pos(meta), meta_src(meta)) : meta;
-      k_cb = min(k_cb, o);
-      ++k_cnt;
-      k_sum += isn ? v : 0;
-    };
-    auto emit_id = [&](const HotChild& hd, uint64_t v, uint64_t tw, uint64_t wmeta) {
-      if (!isn && (A.flags & F_GC_MEMBERS) && meta_tag(wmeta) == KIND_DEL && tw < A.gc_wm) {
-        ++gcm;
-        return;
-      }
-      if (pass == 1) put(hd.id1, hd.id2, isn ? hd.t : tw, isn ? hd.meta : wmeta, v);
-      ++nout;
-    };
-    bool slow = act;
-    if (pass == 0) {
-      // fast path: up to kFoldFast rows, their loads issued together
-      const bool fast = act && nrows <= kFoldFast;
-      uint32_t rj[kFoldFast];
-#pragma unroll
-      for (uint32_t k = 0; k < kFoldFast; ++k) rj[k] = (fast && k < nrows) ? H.v[p + k] : 0;
-      uint64_t xi1[kFoldFast], xi2[kFoldFast], xt[kFoldFast], xm[kFoldFast];
-#pragma unroll
-      for (uint32_t k = 0; k < kFoldFast; ++k) {
-        if (fast && k < nrows) {
-          const ulonglong2 a = H.rec[2 * (uint64_t)rj[k]], c = H.rec[2 * (uint64_t)rj[k] + 1];
-          xi1[k] = a.x;
-          xi2[k] = a.y;
-          xt[k] = c.x;
-          xm[k] = c.y;
-        } else {
-          xi1[k] = xi2[k] = xt[k] = xm[k] = 0;
-        }
-      }
-      bool simple = fast;
-      uint64_t v = xi2[0], tw = xt[0];
-      uint32_t qw = 0;  // winner (members)
-#pragma unroll
-      for (uint32_t k = 1; k < kFoldFast; ++k) {
-        if (k < nrows) {
-          simple = simple && xi1[k] == xi1[0] && (isn || xi2[k] == xi2[0]) &&
-                   meta_order(xm[k]) > meta_order(xm[k - 1]);
-          if (isn) {  // Counter::merge (type_counter.rs:60-84): the head's t is kept
-            v = xt[k] > xt[0] ? xi2[k] : (xt[k] == xt[0] ? imax64(v, xi2[k]) : v);
-          } else if (!(tw > xt[k])) {  // LWWHash::set (lwwhash.rs:87-107): later wins ties
-            tw = xt[k];
-            qw = k;
-          }
-        }
-      }
-      if (simple) {
-        uint64_t wm = xm[0];
-#pragma unroll
-        for (uint32_t k = 1; k < kFoldFast; ++k) wm = (k == qw) ? xm[k] : wm;
-        HotChild hd;
-        hd.id1 = xi1[0];
-        hd.id2 = xi2[0];
-        hd.t = xt[0];
-        hd.meta = xm[0];
-        hd.j = 0;
-        emit_id(hd, v, tw, wm);
-        H.fold_q[p] = (uint32_t)(p + (isn ? 0 : qw));
-        H.fold_v[p] = v;
-        slow = false;
-      } else if (act) {
-        H.fold_q[p] = kNone;
-      }
-    } else if (act) {  // pass 1, fold kept by pass 0
-      const uint32_t q = H.fold_q[p];
-      if (q != kNone) {
-        slow = false;
-        if ((isn ? H.emit_n : H.emit_m)[p]) {
-          const HotChild x = hot_child(H, q);
-          put(x.id1, x.id2, x.t, x.meta, H.fold_v[p]);
-        }
-      }
-    }
-    // selection path
-    nslow += (pass == 0 && slow) ? 1 : 0;
-    uint32_t kslow = slow ? nrows : 0;
-    for (int off = 32; off > 0; off >>= 1) kslow = max(kslow, (uint32_t)__shfl_xor((int)kslow, off));
-    HotChild last, head;  // last visited row; first row of the id being folded
-    last.id1 = last.id2 = last.t = last.meta = 0;
-    last.j = 0;
-    head = last;
-    uint64_t v = 0, tw = 0, wmeta = 0;  // the fold of head's id so far
-    bool open = false;                  // head's id has rows not yet emitted
-    for (uint32_t step = 0; step < kslow + 1 && kslow; ++step) {
-      HotChild c = last;
-      bool have = false;
-      for (uint32_t k = 0; k < kslow; ++k) {
-        if (slow && k < nrows && step < nrows) {
-          const HotChild x = hot_child(H, p + k);
-          const bool after = step == 0 || hot_before(last, x, isn);
-          const bool take = after && (!have || hot_before(x, c, isn));
-          c.id1 = take ? x.id1 : c.id1;
-          c.id2 = take ? x.id2 : c.id2;
-          c.t = take ? x.t : c.t;
-          c.meta = take ? x.meta : c.meta;
-          c.j = take ? x.j : c.j;
-          have = have || take;
-        }
-      }
-      const bool new_id = !have || !open || c.id1 != head.id1 || (!isn && c.id2 != head.id2);
-      if (slow && open && new_id) {  // head's id is complete: emit it
-        emit_id(head, v, tw, wmeta);
-        open = false;
-      }
-      if (slow && have) {
-        if (new_id) {  // c opens an id
-          head = c;
-          v = c.id2;
-          tw = c.t;
-          wmeta = c.meta;
-          open = true;
-        } else if (isn) {
-          v = c.t > head.t ? c.id2 : (c.t == head.t ? imax64(v, c.id2) : v);
-        } else if (!(tw > c.t)) {
-          tw = c.t;
-          wmeta = c.meta;
-        }
-        last = c;
-      }
-    }
-    if (pass == 0 && act) (isn ? H.emit_n : H.emit_m)[p] = nout;
+    const bool emitted = act && pass == 1 && (isn ? H.emit_n : H.emit_m)[p] != 0;
+    HotAcc acc;
+    hot_fold_run(A, H, pass, act, isn, b, G, nrows, [&](uint32_t k) { return H.v[p + k]; }, obase, emitted,
+                 &H.fold_q[p], &H.fold_v[p], acc, gcm, nslow);
+    if (pass == 0 && act) (isn ? H.emit_n : H.emit_m)[p] = acc.nout;
     if (pass == 1) {
       // runs are in sorted order, so the wave's active lanes hold non-decreasing keys G:
-      // a segmented reduction per key, and the segment's last lane does the atomics
+      // a segmented reduction per key, and the segment's last lane does the atomics (one per key
+      // and wave, not per output: a hot key owns up to millions of them)
       const uint32_t key = act ? G : kNone;  // inactive lanes only at the tail: segments are contiguous
+      uint32_t k_cnt = acc.k_cnt, k_cb = acc.k_cb;
+      unsigned long long k_sum = acc.k_sum;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
         const uint32_t gk = (uint32_t)__shfl_up((int)key, d);
@@ -463,6 +492,286 @@ __global__ void __launch_bounds__(256) hot_finish_kernel(BucketArgs A, HotArgs H
     A.nout[b] = tot[0];
     A.mout[b] = tot[1];
   }
+}
+
+// ---- Run-order batches of buckets of at most kSortCap children: one workgroup per bucket does the
+// whole child path in LDS (hot_sortfold_kernel) instead of the global tag sort and its scans. The
+// tag of a child is key32 = W >> 6 less the bucket's first key id: (G - hk_off[h]) << id_bits | id
+// bits (G - hk_off[h] < kCapK = 2^10, id_bits <= kSortIdBits, so it fits 32 bits; the bucket's
+// marker is the largest, (K << id_bits) - 1). A stable LDS radix sort of (key32, flat index) is
+// then the global sort's permutation restricted to the bucket (the global one sorts W's bits from
+// 6 on and keeps buckets apart), so runs, their fold order and the outputs' order are the ones
+// the global path gives for the same id_bits. Runs are folded by hot_fold_run, ranked by a
+// workgroup scan, and the key rows finished from LDS accumulators.
+constexpr uint32_t kSortCap = 8192;
+constexpr int kSortThreads = 1024;
+constexpr int kSortWaves = kSortThreads / 64;
+constexpr int kSortIdBits = 22;
+
+struct SortLds {
+  uint32_t key[2][kSortCap];        // key32 (ping-pong); after the sort: run list, then run offsets
+  uint16_t ix[2][kSortCap];         // flat index - c_off[h] (ping-pong); then outputs per run
+  uint16_t wc[kSortWaves][256];     // a tile's digit counts per wave, then their prefixes
+  uint32_t dbase[256];              // digit histogram, then the digits' next output slot
+  uint32_t kcnt[kCapK], kcb[kCapK];  // per output key: children out, first child slot
+  unsigned long long ksum[kCapK];   // per output key: counter sum
+  uint32_t wsum[kSortWaves];
+  uint32_t misc[8];                 // AND / OR of the keys, first marker position, totals
+};
+
+// Exclusive scan of one value per thread over the workgroup (total in *total).
+__device__ __forceinline__ uint32_t sort_block_scan(uint32_t x, uint32_t* wsum, uint32_t* total) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t inc = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)inc, d);
+    if (lane >= (uint32_t)d) inc += y;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kSortWaves; ++k) {
+    const uint32_t v = wsum[k];
+    pre += (uint32_t)k < wv ? v : 0;
+    tot += v;
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + inc - x;
+}
+
+// One stable pass of the LDS radix sort on key bits [sh, sh + 8): key[s] / ix[s] -> key[s ^ 1] /
+// ix[s ^ 1], in tiles of one element per thread ranked with wave ballots.
+__device__ __forceinline__ void sort_pass(SortLds& L, int s, int sh, uint32_t n) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid < 256) L.dbase[tid] = 0;
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += kSortThreads) atomicAdd(&L.dbase[(L.key[s][i] >> sh) & 255], 1u);
+  __syncthreads();
+  if (wv == 0) {  // exclusive scan of the 256 digit counts, 4 per lane
+    uint32_t c[4], t = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c[k] = L.dbase[lane * 4 + k];
+      t += c[k];
+    }
+    uint32_t inc = t;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)inc, d);
+      if (lane >= (uint32_t)d) inc += y;
+    }
+    uint32_t ex = inc - t;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      L.dbase[lane * 4 + k] = ex;
+      ex += c[k];
+    }
+  }
+  const uint64_t lt = (1ull << lane) - 1;
+  for (uint32_t base = 0; base < n; base += kSortThreads) {  // (uniform)
+    uint16_t* wcf = &L.wc[0][0];
+    for (uint32_t k = tid; k < kSortWaves * 256; k += kSortThreads) wcf[k] = 0;
+    __syncthreads();
+    const uint32_t i = base + tid;
+    const bool valid = i < n;
+    const uint32_t key = valid ? L.key[s][i] : 0;
+    const uint16_t ix = valid ? L.ix[s][i] : 0;
+    const uint32_t d = (key >> sh) & 255;
+    uint64_t peers = __ballot(valid);  // the wave's valid lanes with this lane's digit
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const uint64_t bb = __ballot((d >> bit) & 1);
+      peers &= ((d >> bit) & 1) ? bb : ~bb;
+    }
+    const uint32_t rank = (uint32_t)__popcll(peers & lt);
+    if (valid && rank == 0) L.wc[wv][d] = (uint16_t)__popcll(peers);
+    __syncthreads();
+    uint32_t tot = 0;
+    if (tid < 256) {
+#pragma unroll
+      for (int w = 0; w < kSortWaves; ++w) {
+        const uint32_t c = L.wc[w][tid];
+        L.wc[w][tid] = (uint16_t)tot;
+        tot += c;
+      }
+    }
+    __syncthreads();
+    if (valid) {
+      const uint32_t dst = L.dbase[d] + L.wc[wv][d] + rank;
+      L.key[s ^ 1][dst] = key;
+      L.ix[s ^ 1][dst] = ix;
+    }
+    __syncthreads();
+    if (tid < 256) L.dbase[tid] += tot;
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A, HotArgs H, int id_bits) {
+  __shared__ SortLds L;
+  const uint32_t h = blockIdx.x, b = H.ids[h], tid = threadIdx.x;
+  const uint32_t c0 = H.c_off[h], n = H.c_off[h + 1] - c0, g0 = H.hk_off[h];
+  const uint32_t K = H.hk_off[h + 1] - g0, kout = H.hk_kout[h], N = A.ncnt[b];
+  const uint32_t mk = (K << id_bits) - 1;  // the marker's key32
+  unsigned long long orph = 0, gcm = 0, nslow = 0;
+  uint64_t clk = H.prof ? wall_clock64() : 0;
+  auto phase = [&](int i) {  // (after a barrier)
+    if (H.prof && tid == 0) {
+      const uint64_t now = wall_clock64();
+      atomicAdd(&H.prof[i], (unsigned long long)(now - clk));
+      clk = now;
+    }
+  };
+  for (uint32_t o = tid; o < kout; o += kSortThreads) {
+    L.kcnt[o] = 0;
+    L.kcb[o] = kNone;
+    L.ksum[o] = H.hk_sum[g0 + o];
+  }
+  if (tid == 0) {
+    L.misc[0] = ~0u;  // AND of the keys
+    L.misc[1] = 0;    // OR of the keys
+    L.misc[2] = n;    // first marker position after the sort
+    L.misc[3] = L.misc[4] = 0;
+  }
+  __syncthreads();
+  // 1. tags (rec[j] written as on the global path)
+  uint32_t kand = ~0u, kor = 0;
+  for (uint32_t i = tid; i < n; i += kSortThreads) {
+    const uint64_t W = hot_tag_child(A, H, h, (uint64_t)c0 + i, orph);
+    const uint32_t k32 = (uint32_t)((W >> 6) - ((uint64_t)g0 << id_bits));
+    L.key[0][i] = k32;
+    L.ix[0][i] = (uint16_t)i;
+    kand &= k32;
+    kor |= k32;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    kand &= (uint32_t)__shfl_xor((int)kand, off);
+    kor |= (uint32_t)__shfl_xor((int)kor, off);
+  }
+  if ((tid & 63) == 0) {
+    atomicAnd(&L.misc[0], kand);
+    atomicOr(&L.misc[1], kor);
+  }
+  __syncthreads();
+  phase(0);
+  // 2. stable LDS radix sort; digits equal in every key are skipped
+  const uint32_t vary = L.misc[0] ^ L.misc[1];
+  int s = 0;
+  for (int sh = 0; sh < 32; sh += 8) {
+    if (((vary >> sh) & 255) == 0) continue;
+    sort_pass(L, s, sh, n);
+    s ^= 1;
+  }
+  phase(1);
+  const uint32_t* sk = L.key[s];
+  const uint16_t* sx = L.ix[s];
+  // 3. runs (equal key32; markers, sorted last, start none): list in key[s ^ 1] as
+  //    start | (G - g0) << 16, in chunks of consecutive positions per thread
+  uint32_t* rl = L.key[s ^ 1];
+  const uint32_t per = (n + kSortThreads - 1) / kSortThreads;
+  const uint32_t q0 = min(n, tid * per), q1 = min(n, q0 + per);
+  uint32_t cnt = 0;
+  for (uint32_t q = q0; q < q1; ++q) {
+    const uint32_t k = sk[q];
+    const bool prev_same = q > 0 && sk[q - 1] == k;
+    cnt += (k != mk && !prev_same) ? 1 : 0;
+    if (k == mk && !prev_same) L.misc[2] = q;
+  }
+  uint32_t nruns = 0;
+  uint32_t ex = sort_block_scan(cnt, L.wsum, &nruns);
+  for (uint32_t q = q0; q < q1; ++q) {
+    const uint32_t k = sk[q];
+    if (k != mk && !(q > 0 && sk[q - 1] == k)) rl[ex++] = q | ((k >> id_bits) << 16);
+  }
+  __syncthreads();
+  const uint32_t m = L.misc[2];  // rows taking part
+  phase(2);
+  // 4. fold, pass 0: outputs per run into ix[s ^ 1]
+  uint16_t* no = L.ix[s ^ 1];
+  uint32_t* fq = H.fold_q + c0;
+  uint64_t* fv = H.fold_v + c0;
+  for (uint32_t base = 0; base < nruns; base += kSortThreads) {  // (uniform)
+    const uint32_t r = base + tid;
+    const bool act = r < nruns;
+    const uint32_t e = act ? rl[r] : 0, q = e & 0xFFFF;
+    const uint32_t nrows = act ? (r + 1 < nruns ? (rl[r + 1] & 0xFFFF) : m) - q : 0;
+    const bool isn = act && sx[q] < N;
+    HotAcc acc;
+    hot_fold_run(A, H, 0, act, isn, b, g0 + (e >> 16), nrows, [&](uint32_t k) { return c0 + sx[q + k]; }, 0,
+                 false, fq + r, fv + r, acc, gcm, nslow);
+    if (act) no[r] = (uint16_t)acc.nout;
+  }
+  __syncthreads();
+  // ranks: one scan of (member outputs << 16 | node outputs) over the runs, into key[s]
+  uint32_t* ro = L.key[s];
+  const uint32_t pr = (nruns + kSortThreads - 1) / kSortThreads;
+  const uint32_t r0 = min(nruns, tid * pr), r1 = min(nruns, r0 + pr);
+  uint32_t c = 0;
+  for (uint32_t r = r0; r < r1; ++r) c += sx[rl[r] & 0xFFFF] < N ? (uint32_t)no[r] : (uint32_t)no[r] << 16;
+  uint32_t tot = 0;
+  ex = sort_block_scan(c, L.wsum, &tot);
+  for (uint32_t r = r0; r < r1; ++r) {
+    ro[r] = ex;
+    ex += sx[rl[r] & 0xFFFF] < N ? (uint32_t)no[r] : (uint32_t)no[r] << 16;
+  }
+  __syncthreads();
+  phase(3);
+  // 5. fold, pass 1: outputs at their rank, their key rows' counts, first slots and sums in LDS
+  for (uint32_t base = 0; base < nruns; base += kSortThreads) {  // (uniform)
+    const uint32_t r = base + tid;
+    const bool act = r < nruns;
+    const uint32_t e = act ? rl[r] : 0, q = e & 0xFFFF, gr = e >> 16;
+    const uint32_t nrows = act ? (r + 1 < nruns ? (rl[r + 1] & 0xFFFF) : m) - q : 0;
+    const bool isn = act && sx[q] < N;
+    const uint32_t off = act ? ro[r] : 0;
+    HotAcc acc;
+    hot_fold_run(A, H, 1, act, isn, b, g0 + gr, nrows, [&](uint32_t k) { return c0 + sx[q + k]; },
+                 isn ? (off & 0xFFFF) : (off >> 16), act && no[r] != 0, fq + r, fv + r, acc, gcm, nslow);
+    if (act && acc.k_cnt) {
+      atomicAdd(&L.kcnt[gr], acc.k_cnt);
+      atomicMin(&L.kcb[gr], acc.k_cb);
+      if (isn && (H.hk_vm[g0 + gr] & kVmaskMerged)) atomicAdd(&L.ksum[gr], acc.k_sum);
+    }
+  }
+  __syncthreads();
+  phase(4);
+  // 6. key rows (as hot_finish_kernel)
+  const uint32_t kb = A.kbase[b];
+  uint32_t nn = 0, nm = 0;
+  for (uint32_t o = tid; o < kout; o += kSortThreads) {
+    const uint32_t T = H.hk_tp[g0 + o] & 0xFF, kc = L.kcnt[o];
+    if (T == TAG_COUNTER) {
+      A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_WIN] = L.ksum[o];
+      nn += kc;
+    } else if (T == TAG_SET || T == TAG_DICT) {
+      nm += kc;
+    }
+    A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_CREF] = cref_pack(kc ? L.kcb[o] : 0, kc);
+  }
+  if (nn) atomicAdd(&L.misc[3], nn);
+  if (nm) atomicAdd(&L.misc[4], nm);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    orph += __shfl_xor(orph, off);
+    gcm += __shfl_xor(gcm, off);
+    nslow += __shfl_xor(nslow, off);
+  }
+  if ((tid & 63) == 0) {
+    if (orph) atomicAdd(&stat_shard(A.stats)[ST_ORPHANS], orph);
+    if (gcm) atomicAdd(&stat_shard(A.stats)[ST_MEMBERS_GCED], gcm);
+    if (nslow) atomicAdd(&stat_shard(A.stats)[ST_HOT_SLOW], nslow);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    A.kout[b] = kout;
+    A.nout[b] = L.misc[3];
+    A.mout[b] = L.misc[4];
+  }
+  phase(5);
 }
 
 // Row counts of the listed buckets, for the host's plan of the over-capacity path.

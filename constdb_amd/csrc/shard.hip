@@ -338,21 +338,6 @@ cdb_status cdb_merge_sharded(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     return CDB_OK;
   };
 
-  if (N == 1) {  // one device: the rows are merged where they lie
-    hipSetDevice(ctx->device);
-    const uint64_t rows[3] = {in[0].keys.n, in[0].nodes.n, in[0].members.n};
-    CDB_SHARD_TRY(outputs(0, rows));
-    const auto t1 = std::chrono::steady_clock::now();
-    cdb_merge_stats ms{};
-    st = merge_device_impl(ctx, &in[0], &o, &out[0], &ms, ctx->stream);
-    if (stats) stats[0] = ms;
-    X.merge_ms = ms.device_ms;
-    X.split_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-    X.total_ms = ms_since(t0);
-    if (xs) *xs = X;
-    return st;
-  }
-
   // Inputs must not live in this call's own workspace (a previous call's outputs or received rows):
   // growing a slot would free them under the exchange. Chain through cdb_dev_state_rows instead.
   for (int i = 0; i < N; ++i)
@@ -369,6 +354,21 @@ cdb_status cdb_merge_sharded(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
                           "call's output); copy it with cdb_dev_state_rows first");
           }
     }
+
+  if (N == 1) {  // one device: the rows are merged where they lie
+    hipSetDevice(ctx->device);
+    const uint64_t rows[3] = {in[0].keys.n, in[0].nodes.n, in[0].members.n};
+    CDB_SHARD_TRY(outputs(0, rows));
+    const auto t1 = std::chrono::steady_clock::now();
+    cdb_merge_stats ms{};
+    st = merge_device_impl(ctx, &in[0], &o, &out[0], &ms, ctx->stream);
+    if (stats) stats[0] = ms;
+    X.merge_ms = ms.device_ms;
+    X.split_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    X.total_ms = ms_since(t0);
+    if (xs) *xs = X;
+    return st;
+  }
 
   // ---- 1. owner splits of every source (one synchronisation of every device)
   std::vector<Source> src(N);

@@ -511,7 +511,9 @@ typedef struct cdb_exchange_stats {
 } cdb_exchange_stats;
 
 /* One sharded merge step over every device of ctx (replica/pull.rs:120-128 for a whole node):
- * in[i] are the rows resident on device slot i (any fold positions; n_runs >= 1 for key-hash-
+ * in[i] are the rows resident on device slot i (fold positions are global across slots: slot i's
+ * replicas must not reuse a position another slot's rows carry, or the merge folds them as one
+ * replica; n_runs >= 1 for key-hash-
  * ordered runs, each run's owner slices then move as they are; n_runs = 0, or runs found out of
  * order, are grouped by owner on that device first). Each device receives the rows it owns -- as
  * runs when every source was in runs, so its merge takes the sorted-run path -- and merges them

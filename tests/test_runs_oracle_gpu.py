@@ -137,6 +137,36 @@ def test_chip_wide_in_batches_vs_oracle(ctx, monkeypatch):
     check_runs(ctx, [cdb.gen_snapshot(cfg, r) for r in range(4)], force_tier=2)
 
 
+@pytest.mark.parametrize("lds,id_bits", [("1", None), ("0", None), ("1", "6"), ("1", "12")])
+def test_chip_wide_lds_and_global_sort_vs_oracle(ctx, monkeypatch, lds, id_bits):
+    """Run-order batches of buckets of at most 8192 children take the per-bucket LDS sort and fold
+    (hot_sortfold_kernel); CDB_HOT_LDS=0 sends them through the global tag sort instead. Both equal
+    the oracle on every bucket forced through the chip-wide path (force_tier 2), with counters,
+    sets and dicts, GC of member deletes, and -- with few id-hash bits (CDB_HOT_ID_BITS) -- runs
+    holding several exact ids, folded by successor selection."""
+    monkeypatch.setenv("CDB_HOT_LDS", lds)
+    if id_bits:
+        monkeypatch.setenv("CDB_HOT_ID_BITS", id_bits)
+    cfg = _small(91, 40000, 5, mix_set=25, mix_dict=25, mean_members=20, side_permille=150, conflict_ppm=10000,
+                 tie_permille=100, del_permille=300)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(5)]
+    wm = (configs.T0_MS + (1 << 19)) << 22
+    m = check_runs(ctx, snaps, force_tier=2, gc=wm, gc_members=True)
+    assert m.stats.hot_buckets > 0
+    if id_bits == "6":
+        assert m.stats.hot_slow_runs > 0
+
+
+def test_c5_hot_lds_vs_global_sort_identical(ctx, monkeypatch):
+    """C5 at 300K keys on the sorted-run path: the LDS path (buckets of at most 8192 children) and
+    the global sort give the same dump (the oracle's), and the big buckets stay on the global sort."""
+    cfg = configs.c5(cdb, universe=300_000, events=3_000_000)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(8)]
+    a = check_runs(ctx, snaps).canonical_dump()
+    monkeypatch.setenv("CDB_HOT_LDS", "0")
+    assert runs_merge(ctx, snaps).canonical_dump() == a
+
+
 def test_runs_gc_vs_oracle(ctx):
     cfg = _small(7, 20000, 4, mix_set=40, mix_dict=40, side_permille=300, del_permille=400)
     wm = (configs.T0_MS + (1 << 19)) << 22

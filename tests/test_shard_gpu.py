@@ -222,3 +222,30 @@ def test_sharded_vs_oracle(ctx):
         assert m.canonical_dump() == want
     finally:
         mctx.close()
+
+
+@pytest.mark.parametrize("slots", [1, 2])
+def test_sharded_output_passed_back_is_rejected(ctx, slots):
+    """A previous call's outputs live in the library's workspace, which the next call may regrow:
+    passing them back as inputs is refused (CDB_BAD_ARGUMENT), at one slot as at several."""
+    cfg = configs.c4(cdb, 50_000)
+    mctx = cdb.Context(devices=[0] * slots)
+    try:
+        ins = []
+        for i in range(slots):
+            d = _gen(mctx.shard(i), cfg, i * cfg.n_replicas // slots, (i + 1) * cfg.n_replicas // slots, False)
+            sort_into_runs(d, cfg.n_replicas)
+            ins.append(d)
+        outs, _, _ = cdb.merge_sharded(mctx, ins)
+        back = []
+        for o in outs:
+            d = cdb.DevInput()
+            d.keys, d.nodes, d.members = o.keys, o.nodes, o.members
+            d.n_pos = cfg.n_replicas
+            back.append(d)
+        with pytest.raises(ValueError, match="workspace"):
+            cdb.merge_sharded(mctx, back)
+        for i in range(slots):
+            _release(mctx.shard(i), ins[i])
+    finally:
+        mctx.close()
