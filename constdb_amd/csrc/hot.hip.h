@@ -121,49 +121,99 @@ __global__ void __launch_bounds__(kBktThreads) hot_keys_kernel(BucketArgs A, Hot
     if (S.st[i]) atomicAdd(&stat_shard(A.stats)[i], S.st[i]);
 }
 
-// Flat child j of hot bucket h: its fold fields into rec[j] and its tag W (the bucket's marker when
-// it takes no part; orph counts children whose key is not in the bucket).
-__device__ __forceinline__ uint64_t hot_tag_child(const BucketArgs& A, const HotArgs& H, uint32_t h, uint64_t j,
-                                                  unsigned long long& orph) {
-  const int ks = A.key_shift;
-  const uint32_t b = H.ids[h];
-  const uint32_t i = (uint32_t)(j - H.c_off[h]), N = A.ncnt[b];
+// Bucket h's output keys: the global key table (from hk_off[h]), or a workgroup's copy in LDS.
+struct HotKeyTab {
+  const uint64_t *kh, *kf, *vm;
+  const uint32_t* tp;
+};
+__device__ __forceinline__ HotKeyTab hot_key_tab(const HotArgs& H, uint32_t g0) {
+  HotKeyTab T;
+  T.kh = H.hk_h + g0;
+  T.kf = H.hk_f + g0;
+  T.vm = H.hk_vm + g0;
+  T.tp = H.hk_tp + g0;
+  return T;
+}
+
+// Row of child i (flat order: nodes, then members) of bucket b: the bucket's slices of the family's
+// runs, in run order (as mat_copy lays them), or its partitioned row list.
+__device__ __forceinline__ uint32_t hot_row(const BucketArgs& A, const HotArgs& H, uint32_t b, uint32_t i,
+                                            uint32_t N) {
   const bool isn = i < N;
-  uint32_t row;
-  if (H.runs) {  // the bucket's slices of the family's runs, in run order (as mat_copy lays them)
-    const int f = isn ? 1 : 2;
-    uint32_t k = isn ? i : i - N, r = 0;
-    for (;; ++r) {
-      const uint32_t* d = H.V.rdir[f] + (uint64_t)r * H.V.nbp1 + b;
-      const uint32_t len = d[1] - d[0];
-      if (k < len || r + 1 >= H.V.nr) {
-        row = d[0] + k;  // (absolute rows)
-        break;
-      }
-      k -= len;
+  if (!H.runs) return isn ? A.np[A.nbase[b] + i] : A.mp[A.mbase[b] + (i - N)];
+  const int f = isn ? 1 : 2;
+  uint32_t k = isn ? i : i - N;
+  for (uint32_t r = 0;; ++r) {
+    const uint32_t* d = H.V.rdir[f] + (uint64_t)r * H.V.nbp1 + b;
+    const uint32_t len = d[1] - d[0];
+    if (k < len || r + 1 >= H.V.nr) return d[0] + k;  // (absolute rows)
+    k -= len;
+  }
+}
+
+// The fields of a child row the tag and the fold read: 16-B loads where two are adjacent (records
+// pkf id1 id2 t meta at 8-B alignment; copied rows pkh pkf id1 id2 t meta, 16-B aligned).
+struct HotFields {
+  uint64_t pkh, pkf, id1, id2, t, m;
+};
+__device__ __forceinline__ HotFields hot_fields(const BucketArgs& A, const HotArgs& H, bool isn, uint32_t row) {
+  HotFields F;
+  if (H.runs) {
+    const uint64_t* const* col = isn ? H.V.nin : H.V.min;
+    const uint32_t st = isn ? H.V.ns : H.V.ms;
+    F.pkh = col[C_PKH][row];
+    if (st > 1) {
+      const uint64_t* r = col[1] + (uint64_t)row * st;
+      const u64x2 a = *(const u64x2*)(r + 1), c = *(const u64x2*)(r + 3);
+      F.pkf = r[0];
+      F.id1 = a.x;
+      F.id2 = a.y;
+      F.t = c.x;
+      F.m = c.y;
+    } else {
+      F.pkf = col[C_PKF][row];
+      F.id1 = col[C_ID1][row];
+      F.id2 = col[C_ID2][row];
+      F.t = col[C_T][row];
+      F.m = col[C_META][row];
     }
   } else {
-    row = isn ? A.np[A.nbase[b] + i] : A.mp[A.mbase[b] + (i - N)];
+    const ulonglong2* r = (const ulonglong2*)((isn ? A.nr : A.mr) + (uint64_t)row * kChildStride);
+    const ulonglong2 a = r[0], b = r[1], c = r[2];
+    F.pkh = a.x;
+    F.pkf = a.y;
+    F.id1 = b.x;
+    F.id2 = b.y;
+    F.t = c.x;
+    F.m = c.y;
   }
-  const uint64_t pkh = hot_col(A, H, isn, row, C_PKH), pkf = hot_col(A, H, isn, row, C_PKF);
-  const uint64_t id1 = hot_col(A, H, isn, row, C_ID1), m = hot_col(A, H, isn, row, C_META);
-  const uint64_t id2 = hot_col(A, H, isn, row, C_ID2), t = hot_col(A, H, isn, row, C_T);
+  return F;
+}
+
+// Flat child j of hot bucket h (fields F, a node when isn): its fold fields into rec[j] and its tag
+// W (the bucket's marker when it takes no part; orph counts children whose key is not in the
+// bucket). T: the bucket's kout output keys.
+__device__ __forceinline__ uint64_t hot_tag_row(const BucketArgs& A, const HotArgs& H, uint32_t h, uint64_t j,
+                                                bool isn, const HotFields& F, const HotKeyTab& T, uint32_t kout,
+                                                unsigned long long& orph) {
+  const int ks = A.key_shift;
+  const uint64_t pkh = F.pkh, pkf = F.pkf, id1 = F.id1, id2 = F.id2, t = F.t, m = F.m;
   // lower bound over the bucket's sorted output keys on (kh << shift, kh, kf)
-  const uint32_t g0 = H.hk_off[h], kout = H.hk_kout[h];
+  const uint32_t g0 = H.hk_off[h];
   uint32_t lo = 0, hi = kout;
   const uint64_t sp = pkh << ks;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    const uint64_t kh = H.hk_h[g0 + mid], sm = kh << ks;
-    const bool less = sm < sp || (sm == sp && (kh < pkh || (kh == pkh && H.hk_f[g0 + mid] < pkf)));
+    const uint64_t kh = T.kh[mid], sm = kh << ks;
+    const bool less = sm < sp || (sm == sp && (kh < pkh || (kh == pkh && T.kf[mid] < pkf)));
     lo = less ? mid + 1 : lo;
     hi = less ? hi : mid;
   }
   uint64_t w = hot_marker(H, h);
-  if (lo < kout && H.hk_h[g0 + lo] == pkh && H.hk_f[g0 + lo] == pkf && (H.hk_tp[g0 + lo] & 0xFF) <= TAG_SET) {
-    const uint32_t T = H.hk_tp[g0 + lo] & 0xFF, hp = H.hk_tp[g0 + lo] >> 8, p = meta_pos(m);
-    const bool type_ok = isn ? T == TAG_COUNTER : (T == TAG_SET || T == TAG_DICT);
-    const bool elem_ok = (H.hk_vm[g0 + lo] >> p) & 1;
+  if (lo < kout && T.kh[lo] == pkh && T.kf[lo] == pkf && (T.tp[lo] & 0xFF) <= TAG_SET) {
+    const uint32_t TT = T.tp[lo] & 0xFF, hp = T.tp[lo] >> 8, p = meta_pos(m);
+    const bool type_ok = isn ? TT == TAG_COUNTER : (TT == TAG_SET || TT == TAG_DICT);
+    const bool elem_ok = (T.vm[lo] >> p) & 1;
     const bool cand = isn || meta_tag(m) == KIND_ADD || p == hp;  // remote dels ignored
     if (type_ok && elem_ok && cand) {
       // (the id field stops one below all ones: the marker is above every W of the bucket in
@@ -178,6 +228,15 @@ __device__ __forceinline__ uint64_t hot_tag_child(const BucketArgs& A, const Hot
   H.rec[2 * j] = make_ulonglong2(id1, id2);
   H.rec[2 * j + 1] = make_ulonglong2(t, m);
   return w;
+}
+
+__device__ __forceinline__ uint64_t hot_tag_child(const BucketArgs& A, const HotArgs& H, uint32_t h, uint64_t j,
+                                                  unsigned long long& orph) {
+  const uint32_t b = H.ids[h];
+  const uint32_t i = (uint32_t)(j - H.c_off[h]), N = A.ncnt[b];
+  const bool isn = i < N;
+  return hot_tag_row(A, H, h, j, isn, hot_fields(A, H, isn, hot_row(A, H, b, i, N)), hot_key_tab(H, H.hk_off[h]),
+                     H.hk_kout[h], orph);
 }
 
 __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
@@ -543,69 +602,76 @@ __device__ __forceinline__ uint32_t sort_block_scan(uint32_t x, uint32_t* wsum, 
 }
 
 // One stable pass of the LDS radix sort on key bits [sh, sh + 8): key[s] / ix[s] -> key[s ^ 1] /
-// ix[s ^ 1], in tiles of one element per thread ranked with wave ballots.
+// ix[s ^ 1]. Wave w ranks the consecutive chunk w of the elements, 64 at a time with ballots, in
+// its own digit counters; one scan over (digit, wave) then places every wave's run of each digit.
+constexpr int kSortIt = kSortCap / kSortThreads;  // elements per lane at most
 __device__ __forceinline__ void sort_pass(SortLds& L, int s, int sh, uint32_t n) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid < 256) L.dbase[tid] = 0;
+  uint16_t* wcf = &L.wc[0][0];
+  for (uint32_t k = tid; k < kSortWaves * 256; k += kSortThreads) wcf[k] = 0;
   __syncthreads();
-  for (uint32_t i = tid; i < n; i += kSortThreads) atomicAdd(&L.dbase[(L.key[s][i] >> sh) & 255], 1u);
-  __syncthreads();
-  if (wv == 0) {  // exclusive scan of the 256 digit counts, 4 per lane
-    uint32_t c[4], t = 0;
+  const uint32_t chunk = (n + kSortWaves * 64 - 1) / (kSortWaves * 64) * 64;  // per wave, whole sub-tiles
+  const uint32_t base = wv * chunk;
+  const uint64_t lt = (1ull << lane) - 1;
+  uint32_t kk[kSortIt], rr[kSortIt];
+  uint16_t xx[kSortIt];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      c[k] = L.dbase[lane * 4 + k];
-      t += c[k];
+  for (int it = 0; it < kSortIt; ++it) {
+    kk[it] = rr[it] = 0;
+    xx[it] = 0;
+    if ((uint32_t)it * 64 < chunk) {  // (uniform)
+      const uint32_t i = base + it * 64 + lane;
+      const bool valid = i < n;
+      const uint32_t key = valid ? L.key[s][i] : 0;
+      xx[it] = valid ? L.ix[s][i] : 0;
+      kk[it] = key;
+      const uint32_t d = (key >> sh) & 255;
+      uint64_t peers = __ballot(valid);  // the wave's valid lanes with this lane's digit
+#pragma unroll
+      for (int bit = 0; bit < 8; ++bit) {
+        const uint64_t bb = __ballot((d >> bit) & 1);
+        peers &= ((d >> bit) & 1) ? bb : ~bb;
+      }
+      const uint32_t below = (uint32_t)__popcll(peers & lt);
+      const uint32_t cur = L.wc[wv][d];  // (one wave's LDS accesses stay in order)
+      rr[it] = cur + below;
+      if (valid && below == 0) L.wc[wv][d] = (uint16_t)(cur + __popcll(peers));
     }
-    uint32_t inc = t;
+  }
+  __syncthreads();
+  // digit d: prefix over the waves, then the digits' totals scanned (wave totals in dbase[0..3])
+  uint32_t tot = 0, inc = 0;
+  if (tid < 256) {
+#pragma unroll
+    for (int w = 0; w < kSortWaves; ++w) {
+      const uint32_t c = L.wc[w][tid];
+      L.wc[w][tid] = (uint16_t)tot;
+      tot += c;
+    }
+    inc = tot;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = (uint32_t)__shfl_up((int)inc, d);
       if (lane >= (uint32_t)d) inc += y;
     }
-    uint32_t ex = inc - t;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      L.dbase[lane * 4 + k] = ex;
-      ex += c[k];
-    }
+    if (lane == 63) L.dbase[wv] = inc;
   }
-  const uint64_t lt = (1ull << lane) - 1;
-  for (uint32_t base = 0; base < n; base += kSortThreads) {  // (uniform)
-    uint16_t* wcf = &L.wc[0][0];
-    for (uint32_t k = tid; k < kSortWaves * 256; k += kSortThreads) wcf[k] = 0;
-    __syncthreads();
-    const uint32_t i = base + tid;
-    const bool valid = i < n;
-    const uint32_t key = valid ? L.key[s][i] : 0;
-    const uint16_t ix = valid ? L.ix[s][i] : 0;
-    const uint32_t d = (key >> sh) & 255;
-    uint64_t peers = __ballot(valid);  // the wave's valid lanes with this lane's digit
+  __syncthreads();
+  if (tid < 256) {
+    uint32_t dbase = inc - tot;
+    for (uint32_t k = 0; k < wv; ++k) dbase += L.dbase[k];
 #pragma unroll
-    for (int bit = 0; bit < 8; ++bit) {
-      const uint64_t bb = __ballot((d >> bit) & 1);
-      peers &= ((d >> bit) & 1) ? bb : ~bb;
-    }
-    const uint32_t rank = (uint32_t)__popcll(peers & lt);
-    if (valid && rank == 0) L.wc[wv][d] = (uint16_t)__popcll(peers);
-    __syncthreads();
-    uint32_t tot = 0;
-    if (tid < 256) {
+    for (int w = 0; w < kSortWaves; ++w) L.wc[w][tid] = (uint16_t)(L.wc[w][tid] + dbase);
+  }
+  __syncthreads();
 #pragma unroll
-      for (int w = 0; w < kSortWaves; ++w) {
-        const uint32_t c = L.wc[w][tid];
-        L.wc[w][tid] = (uint16_t)tot;
-        tot += c;
-      }
+  for (int it = 0; it < kSortIt; ++it) {
+    const uint32_t i = base + it * 64 + lane;
+    if ((uint32_t)it * 64 < chunk && i < n) {
+      const uint32_t dst = L.wc[wv][(kk[it] >> sh) & 255] + rr[it];
+      L.key[s ^ 1][dst] = kk[it];
+      L.ix[s ^ 1][dst] = xx[it];
     }
-    __syncthreads();
-    if (valid) {
-      const uint32_t dst = L.dbase[d] + L.wc[wv][d] + rank;
-      L.key[s ^ 1][dst] = key;
-      L.ix[s ^ 1][dst] = ix;
-    }
-    __syncthreads();
-    if (tid < 256) L.dbase[tid] += tot;
   }
   __syncthreads();
 }
@@ -636,16 +702,62 @@ __global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A
     L.misc[2] = n;    // first marker position after the sort
     L.misc[3] = L.misc[4] = 0;
   }
+  // the bucket's key table and run slices, in the sort's second buffers until the sort
+  HotKeyTab T;
+  uint64_t* tkh = (uint64_t*)&L.key[1][0];
+  T.kh = tkh;
+  T.kf = tkh + kCapK;
+  T.vm = tkh + 2 * kCapK;
+  T.tp = (const uint32_t*)(tkh + 3 * kCapK);
+  for (uint32_t o = tid; o < kout; o += kSortThreads) {
+    tkh[o] = H.hk_h[g0 + o];
+    tkh[kCapK + o] = H.hk_f[g0 + o];
+    tkh[2 * kCapK + o] = H.hk_vm[g0 + o];
+    ((uint32_t*)(tkh + 3 * kCapK))[o] = H.hk_tp[g0 + o];
+  }
+  uint32_t* sl = (uint32_t*)&L.ix[1][0];  // [family 0/1][run]: first row, then rows before the run
+  const uint32_t nr = H.runs ? H.V.nr : 0;
+  if (tid < 2 * nr) {
+    const uint32_t f = tid / nr, r = tid % nr;
+    const uint32_t* d = H.V.rdir[1 + f] + (uint64_t)r * H.V.nbp1 + b;
+    sl[f * 2 * kMaxRuns + r] = d[0];
+    sl[f * 2 * kMaxRuns + kMaxRuns + r] = d[1] - d[0];
+  }
+  __syncthreads();
+  if (tid < 2) {  // lengths -> exclusive prefix
+    uint32_t acc = 0;
+    for (uint32_t r = 0; r < nr; ++r) {
+      const uint32_t len = sl[tid * 2 * kMaxRuns + kMaxRuns + r];
+      sl[tid * 2 * kMaxRuns + kMaxRuns + r] = acc;
+      acc += len;
+    }
+  }
   __syncthreads();
   // 1. tags (rec[j] written as on the global path)
   uint32_t kand = ~0u, kor = 0;
-  for (uint32_t i = tid; i < n; i += kSortThreads) {
-    const uint64_t W = hot_tag_child(A, H, h, (uint64_t)c0 + i, orph);
+  auto row_of = [&](uint32_t i) -> uint32_t {
+    const bool isn = i < N;
+    if (!nr) return hot_row(A, H, b, i, N);
+    const uint32_t k = isn ? i : i - N, *fs = sl + (isn ? 0 : 2 * kMaxRuns);
+    uint32_t r = 0;
+    while (r + 1 < nr && fs[kMaxRuns + r + 1] <= k) ++r;
+    return fs[r] + (k - fs[kMaxRuns + r]);
+  };
+  auto tag = [&](uint32_t i, const HotFields& F) {
+    const uint64_t W = hot_tag_row(A, H, h, (uint64_t)c0 + i, i < N, F, T, kout, orph);
     const uint32_t k32 = (uint32_t)((W >> 6) - ((uint64_t)g0 << id_bits));
     L.key[0][i] = k32;
     L.ix[0][i] = (uint16_t)i;
     kand &= k32;
     kor |= k32;
+  };
+  for (uint32_t i = tid; i < n; i += 2 * kSortThreads) {  // two children per step, their loads first
+    const uint32_t i2 = i + kSortThreads;
+    const HotFields F1 = hot_fields(A, H, i < N, row_of(i));
+    HotFields F2;
+    if (i2 < n) F2 = hot_fields(A, H, i2 < N, row_of(i2));
+    tag(i, F1);
+    if (i2 < n) tag(i2, F2);
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -743,11 +855,11 @@ __global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A
   const uint32_t kb = A.kbase[b];
   uint32_t nn = 0, nm = 0;
   for (uint32_t o = tid; o < kout; o += kSortThreads) {
-    const uint32_t T = H.hk_tp[g0 + o] & 0xFF, kc = L.kcnt[o];
-    if (T == TAG_COUNTER) {
+    const uint32_t tk = H.hk_tp[g0 + o] & 0xFF, kc = L.kcnt[o];
+    if (tk == TAG_COUNTER) {
       A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_WIN] = L.ksum[o];
       nn += kc;
-    } else if (T == TAG_SET || T == TAG_DICT) {
+    } else if (tk == TAG_SET || tk == TAG_DICT) {
       nm += kc;
     }
     A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_CREF] = cref_pack(kc ? L.kcb[o] : 0, kc);
