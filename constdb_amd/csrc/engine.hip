@@ -678,7 +678,8 @@ namespace {
 // rows in the batch (the key table's index width in the sort tag and the child row indices).
 cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& wide_ids,
                      const std::vector<uint32_t>& hk_off, const std::vector<uint32_t>& c_off, uint64_t tk,
-                     uint64_t tc, uint64_t cmax, const RunView* rv, bool run_order, hipStream_t s) {
+                     uint64_t tc, uint64_t cmax, uint64_t kmax, const RunView* rv, bool run_order,
+                     hipStream_t s) {
   cdb_status st = CDB_OK;
   const uint32_t H = (uint32_t)wide_ids.size();
   // device: ids[H] | hk_off[H + 1] | c_off[H + 1] | hk_kout[H] | run count
@@ -756,6 +757,7 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   HA.emit_m = HA.emit_n + nc;
   uint32_t* rank_n = HA.emit_m + nc;
   uint32_t* rank_m = rank_n + nc;
+  uint32_t* run_list = rank_m + nc;
   HA.rank_n = rank_n;
   HA.rank_m = rank_m;
   HA.w = w;
@@ -770,7 +772,10 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
       HA.prof = nc >= 8 ? (unsigned long long*)w2 : nullptr;  // (the global sort's spare keys)
       if (HA.prof) CDB_HIP(hipMemsetAsync(HA.prof, 0, 64, s), "memset");
     }
-    hot_sortfold_kernel<<<H, kSortThreads, 0, s>>>(A, HA, id_bits);
+    if (cmax <= SortSmall::Cap && kmax <= SortSmall::KCap)
+      hot_sortfold_kernel<SortSmall><<<H, SortSmall::Threads, 0, s>>>(A, HA, id_bits);
+    else
+      hot_sortfold_kernel<SortBig><<<H, SortBig::Threads, 0, s>>>(A, HA, id_bits);
     CDB_TRY(launch_check(ctx, s, "hot_sortfold_kernel"));
     CDB_HIP(hipStreamSynchronize(s), "sync");  // the host vectors are copy sources
     if (prof && HA.prof) {
@@ -787,18 +792,16 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   }
   const uint32_t grid = (uint32_t)std::min<uint64_t>((tc + 255) / 256, 16384);
   if (tc) {
-    hot_tag_kernel<<<grid, 256, 0, s>>>(A, HA);
+    hot_tag_kernel<<<(uint32_t)((tc + kTagChunk - 1) / kTagChunk), 256, 0, s>>>(A, HA);
     CDB_TRY(launch_check(ctx, s, "hot_tag_kernel"));
     // (per-bucket bitonic sorts in LDS measured slower than this global radix sort: C3 9.98 vs
     // 8.90 ms, C5 25.9 vs 24.3 ms; profiles/r03/experiments_r3.txt)
     CDB_TRY(radix_sort_pairs(ctx, &HA.w, &HA.v, w2, v2, tc, lo, HA.g_shift + gbits, s));
-  }
-  if (tc) {
     // the sort's other buffers are free now: fold results per run start
     HA.fold_v = HA.w == w ? w2 : w;
     HA.fold_q = HA.v == v ? v2 : v;
     HA.run_count = d_runs;
-    HA.run_list = rank_m + nc;
+    HA.run_list = run_list;
     // run starts -> run list (ascending): flags in emit_n, their scan in rank_n
     hot_runflag_kernel<<<grid, 256, 0, s>>>(HA, HA.emit_n);
     CDB_TRY(launch_check(ctx, s, "hot_runflag_kernel"));
@@ -851,16 +854,16 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   std::vector<uint32_t> wide_ids, legacy;  // wide: the chip-wide child path
   std::vector<uint32_t> hk_off(1, 0), c_off(1, 0);
   std::vector<uint32_t> lk, ln, lm;
-  uint64_t tk = 0, tc = 0, cmax = 0, orphans = 0;
+  uint64_t tk = 0, tc = 0, cmax = 0, kmax = 0, orphans = 0;
   bool runs_batch = false;  // the batch being built reads its children from the runs
   auto flush = [&]() -> cdb_status {
     if (wide_ids.empty()) return CDB_OK;
     const cdb_status r =
-        chip_wide(ctx, A, wide_ids, hk_off, c_off, tk, tc, cmax, runs_batch ? rv : nullptr, rv != nullptr, s);
+        chip_wide(ctx, A, wide_ids, hk_off, c_off, tk, tc, cmax, kmax, runs_batch ? rv : nullptr, rv != nullptr, s);
     wide_ids.clear();
     hk_off.assign(1, 0);
     c_off.assign(1, 0);
-    tk = tc = cmax = 0;
+    tk = tc = cmax = kmax = 0;
     return r;
   };
   // the same rule as mat_count_kernel's: runs-mode buckets first, then the copied ones
@@ -868,18 +871,24 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
     return rv && runs_child_max && !legacy_all && cnt3[3 * i] <= (uint32_t)kCapK &&
            cnt3[3 * i + 1] + cnt3[3 * i + 2] <= runs_child_max;
   };
-  // Each kind in two size classes: the sort's id bits follow the batch's largest bucket and its
-  // key bits the batch's key count, so many small buckets and a few huge ones sorted together
-  // can take a pass more than either alone (C5: 20.1 -> 19.6 ms split).
-  // (On run order the small class is the LDS path's: at most kSortCap children.)
-  const uint32_t kBigBucket = rv ? kSortCap : 16384;
-  for (int pass = 0; pass < 4; ++pass) {
-    runs_batch = pass < 2;
-    const bool big = pass & 1;
+  // Each kind in size classes: the sort's id bits follow the batch's largest bucket and its key
+  // bits the batch's key count, so many small buckets and a few huge ones sorted together can take
+  // a pass more than either alone (C5: 20.1 -> 19.6 ms split). On run order the LDS path's two
+  // shapes are classes of their own (at most 2048 children and 256 keys; at most kSortCap
+  // children), the rest takes the global sort.
+  auto size_class = [&](uint32_t i) -> int {
+    const uint32_t K = cnt3[3 * i], C = cnt3[3 * i + 1] + cnt3[3 * i + 2];
+    if (!rv) return C > 16384 ? 2 : 1;
+    if (C <= SortSmall::Cap && K <= SortSmall::KCap) return 0;
+    return C <= kSortCap ? 1 : 2;
+  };
+  for (int pass = 0; pass < 6; ++pass) {
+    runs_batch = pass < 3;
+    const int cls = pass % 3;
     for (uint32_t i : order) {
       if (runs_mode(i) != runs_batch) continue;
       const uint32_t K = cnt3[3 * i], N = cnt3[3 * i + 1], M = cnt3[3 * i + 2];
-      if ((N + M > kBigBucket) != big) continue;
+      if (size_class(i) != cls) continue;
       if (K == 0) {  // no key rows: every child is an orphan and nothing is output (the bucket's
         orphans += N + M;  // counts were zeroed when it was listed); kept off the chip-wide path,
         continue;          // whose per-bucket marker needs a key row
@@ -896,6 +905,7 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
       tk += K;
       tc += N + M;
       cmax = std::max<uint64_t>(cmax, N + M);
+      kmax = std::max<uint64_t>(kmax, K);
       hk_off.push_back((uint32_t)tk);
       c_off.push_back((uint32_t)tc);
     }

@@ -239,19 +239,59 @@ __device__ __forceinline__ uint64_t hot_tag_child(const BucketArgs& A, const Hot
                      H.hk_kout[h], orph);
 }
 
+// One block per kTagChunk consecutive flat children: its first bucket is searched once, and the
+// run slices of that bucket and the next (a chunk of a big bucket spans at most two) come from LDS.
+constexpr uint32_t kTagChunk = 4096;
 __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
+  __shared__ uint32_t sl[2][4 * kMaxRuns];  // bucket h0 + slot: [family][run] first row, rows before
+  __shared__ uint32_t h_first;
   unsigned long long orph = 0;
-  const uint32_t lane = threadIdx.x & 63;
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < H.n_children;
-       j += (uint64_t)gridDim.x * blockDim.x) {
-    // the wave's children are consecutive: lane 0 (active whenever any lane is) searches the
-    // bucket of the first, the others step forward from it (buckets here hold hundreds of rows)
-    uint32_t h = lane == 0 ? hot_bucket_of(H, j) : 0;
-    h = (uint32_t)__shfl((int)h, 0);
+  const uint32_t tid = threadIdx.x;
+  const uint64_t j0 = (uint64_t)blockIdx.x * kTagChunk;
+  if (tid == 0) h_first = hot_bucket_of(H, j0);
+  __syncthreads();
+  const uint32_t h0 = h_first;
+  const uint32_t nr = H.runs ? H.V.nr : 0;
+  for (uint32_t t = tid; t < 4 * nr; t += blockDim.x) {
+    const uint32_t slot = t / (2 * nr), f = (t / nr) & 1, r = t % nr;
+    if (h0 + slot < H.H) {
+      const uint32_t* d = H.V.rdir[1 + f] + (uint64_t)r * H.V.nbp1 + H.ids[h0 + slot];
+      sl[slot][f * 2 * kMaxRuns + r] = d[0];
+      sl[slot][f * 2 * kMaxRuns + kMaxRuns + r] = d[1] - d[0];
+    }
+  }
+  __syncthreads();
+  if (tid < 4 && nr) {  // lengths -> exclusive prefix
+    uint32_t* len = &sl[tid >> 1][(tid & 1) * 2 * kMaxRuns + kMaxRuns];
+    uint32_t acc = 0;
+    for (uint32_t r = 0; r < nr; ++r) {
+      const uint32_t l = len[r];
+      len[r] = acc;
+      acc += l;
+    }
+  }
+  __syncthreads();
+  uint32_t h = h0;
+  for (uint32_t it = 0; it < kTagChunk / 256; ++it) {
+    const uint64_t j = j0 + it * 256 + tid;
+    if (j >= H.n_children) break;
     while (h + 1 < H.H && H.c_off[h + 1] <= j) ++h;
-    H.w[j] = hot_tag_child(A, H, h, j, orph);
+    const uint32_t b = H.ids[h];
+    const uint32_t i = (uint32_t)(j - H.c_off[h]), N = A.ncnt[b];
+    const bool isn = i < N;
+    uint32_t row;
+    if (nr && h - h0 < 2) {
+      const uint32_t k = isn ? i : i - N, *fs = &sl[h - h0][isn ? 0 : 2 * kMaxRuns];
+      uint32_t r = 0;
+      while (r + 1 < nr && fs[kMaxRuns + r + 1] <= k) ++r;
+      row = fs[r] + (k - fs[kMaxRuns + r]);
+    } else {
+      row = hot_row(A, H, b, i, N);
+    }
+    H.w[j] = hot_tag_row(A, H, h, j, isn, hot_fields(A, H, isn, row), hot_key_tab(H, H.hk_off[h]), H.hk_kout[h],
+                         orph);
     H.v[j] = (uint32_t)j;
-    H.c_h[j] = h | ((uint32_t)(j - H.c_off[h]) < A.ncnt[H.ids[h]] ? 0u : 0x80000000u);
+    H.c_h[j] = h | (isn ? 0u : 0x80000000u);
   }
   if (orph) atomicAdd(&stat_shard(A.stats)[ST_ORPHANS], orph);
 }
@@ -563,22 +603,34 @@ __global__ void __launch_bounds__(256) hot_finish_kernel(BucketArgs A, HotArgs H
 // the global path gives for the same id_bits. Runs are folded by hot_fold_run, ranked by a
 // workgroup scan, and the key rows finished from LDS accumulators.
 constexpr uint32_t kSortCap = 8192;
-constexpr int kSortThreads = 1024;
-constexpr int kSortWaves = kSortThreads / 64;
 constexpr int kSortIdBits = 22;
+// Two shapes: buckets of at most 8192 children (1024 threads, one workgroup per CU), and buckets
+// of at most 2048 children and 256 keys (256 threads, four workgroups per CU).
+template <uint32_t CAP, int THREADS, uint32_t KCAP>
+struct SortCfg {
+  static constexpr uint32_t Cap = CAP, KCap = KCAP;
+  static constexpr int Threads = THREADS, Waves = THREADS / 64, It = CAP / THREADS;
+};
+using SortBig = SortCfg<kSortCap, 1024, kCapK>;
+using SortSmall = SortCfg<2048, 256, 256>;
 
+template <class C>
 struct SortLds {
-  uint32_t key[2][kSortCap];        // key32 (ping-pong); after the sort: run list, then run offsets
-  uint16_t ix[2][kSortCap];         // flat index - c_off[h] (ping-pong); then outputs per run
-  uint16_t wc[kSortWaves][256];     // a tile's digit counts per wave, then their prefixes
-  uint32_t dbase[256];              // digit histogram, then the digits' next output slot
-  uint32_t kcnt[kCapK], kcb[kCapK];  // per output key: children out, first child slot
-  unsigned long long ksum[kCapK];   // per output key: counter sum
-  uint32_t wsum[kSortWaves];
+  uint32_t key[2][C::Cap];          // key32 (ping-pong); after the sort: run list, then run offsets
+  uint16_t ix[2][C::Cap];           // flat index - c_off[h] (ping-pong); then outputs per run
+  uint16_t wc[C::Waves][256];       // a tile's digit counts per wave, then their prefixes
+  uint32_t dbase[256];              // wave totals of the digit scan
+  uint32_t kcnt[C::KCap], kcb[C::KCap];  // per output key: children out, first child slot
+  unsigned long long ksum[C::KCap];      // per output key: counter sum
+  uint64_t tab[3 * C::KCap];        // the bucket's output keys: kh, kf, vm
+  uint32_t ttp[C::KCap];            // ... and tag / pos words
+  uint32_t sl[4 * kMaxRuns];        // [family][run]: first row, rows before the run
+  uint32_t wsum[C::Waves];
   uint32_t misc[8];                 // AND / OR of the keys, first marker position, totals
 };
 
 // Exclusive scan of one value per thread over the workgroup (total in *total).
+template <int WAVES>
 __device__ __forceinline__ uint32_t sort_block_scan(uint32_t x, uint32_t* wsum, uint32_t* total) {
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t inc = x;
@@ -591,7 +643,7 @@ __device__ __forceinline__ uint32_t sort_block_scan(uint32_t x, uint32_t* wsum, 
   __syncthreads();
   uint32_t pre = 0, tot = 0;
 #pragma unroll
-  for (int k = 0; k < kSortWaves; ++k) {
+  for (int k = 0; k < WAVES; ++k) {
     const uint32_t v = wsum[k];
     pre += (uint32_t)k < wv ? v : 0;
     tot += v;
@@ -604,19 +656,19 @@ __device__ __forceinline__ uint32_t sort_block_scan(uint32_t x, uint32_t* wsum, 
 // One stable pass of the LDS radix sort on key bits [sh, sh + 8): key[s] / ix[s] -> key[s ^ 1] /
 // ix[s ^ 1]. Wave w ranks the consecutive chunk w of the elements, 64 at a time with ballots, in
 // its own digit counters; one scan over (digit, wave) then places every wave's run of each digit.
-constexpr int kSortIt = kSortCap / kSortThreads;  // elements per lane at most
-__device__ __forceinline__ void sort_pass(SortLds& L, int s, int sh, uint32_t n) {
+template <class C>
+__device__ __forceinline__ void sort_pass(SortLds<C>& L, int s, int sh, uint32_t n) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   uint16_t* wcf = &L.wc[0][0];
-  for (uint32_t k = tid; k < kSortWaves * 256; k += kSortThreads) wcf[k] = 0;
+  for (uint32_t k = tid; k < C::Waves * 256; k += C::Threads) wcf[k] = 0;
   __syncthreads();
-  const uint32_t chunk = (n + kSortWaves * 64 - 1) / (kSortWaves * 64) * 64;  // per wave, whole sub-tiles
+  const uint32_t chunk = (n + C::Waves * 64 - 1) / (C::Waves * 64) * 64;  // per wave, whole sub-tiles
   const uint32_t base = wv * chunk;
   const uint64_t lt = (1ull << lane) - 1;
-  uint32_t kk[kSortIt], rr[kSortIt];
-  uint16_t xx[kSortIt];
+  uint32_t kk[C::It], rr[C::It];
+  uint16_t xx[C::It];
 #pragma unroll
-  for (int it = 0; it < kSortIt; ++it) {
+  for (int it = 0; it < C::It; ++it) {
     kk[it] = rr[it] = 0;
     xx[it] = 0;
     if ((uint32_t)it * 64 < chunk) {  // (uniform)
@@ -643,7 +695,7 @@ __device__ __forceinline__ void sort_pass(SortLds& L, int s, int sh, uint32_t n)
   uint32_t tot = 0, inc = 0;
   if (tid < 256) {
 #pragma unroll
-    for (int w = 0; w < kSortWaves; ++w) {
+    for (int w = 0; w < C::Waves; ++w) {
       const uint32_t c = L.wc[w][tid];
       L.wc[w][tid] = (uint16_t)tot;
       tot += c;
@@ -661,11 +713,11 @@ __device__ __forceinline__ void sort_pass(SortLds& L, int s, int sh, uint32_t n)
     uint32_t dbase = inc - tot;
     for (uint32_t k = 0; k < wv; ++k) dbase += L.dbase[k];
 #pragma unroll
-    for (int w = 0; w < kSortWaves; ++w) L.wc[w][tid] = (uint16_t)(L.wc[w][tid] + dbase);
+    for (int w = 0; w < C::Waves; ++w) L.wc[w][tid] = (uint16_t)(L.wc[w][tid] + dbase);
   }
   __syncthreads();
 #pragma unroll
-  for (int it = 0; it < kSortIt; ++it) {
+  for (int it = 0; it < C::It; ++it) {
     const uint32_t i = base + it * 64 + lane;
     if ((uint32_t)it * 64 < chunk && i < n) {
       const uint32_t dst = L.wc[wv][(kk[it] >> sh) & 255] + rr[it];
@@ -676,8 +728,9 @@ __device__ __forceinline__ void sort_pass(SortLds& L, int s, int sh, uint32_t n)
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A, HotArgs H, int id_bits) {
-  __shared__ SortLds L;
+template <class C>
+__global__ void __launch_bounds__(C::Threads) hot_sortfold_kernel(BucketArgs A, HotArgs H, int id_bits) {
+  __shared__ SortLds<C> L;
   const uint32_t h = blockIdx.x, b = H.ids[h], tid = threadIdx.x;
   const uint32_t c0 = H.c_off[h], n = H.c_off[h + 1] - c0, g0 = H.hk_off[h];
   const uint32_t K = H.hk_off[h + 1] - g0, kout = H.hk_kout[h], N = A.ncnt[b];
@@ -691,7 +744,7 @@ __global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A
       clk = now;
     }
   };
-  for (uint32_t o = tid; o < kout; o += kSortThreads) {
+  for (uint32_t o = tid; o < kout; o += C::Threads) {
     L.kcnt[o] = 0;
     L.kcb[o] = kNone;
     L.ksum[o] = H.hk_sum[g0 + o];
@@ -702,20 +755,19 @@ __global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A
     L.misc[2] = n;    // first marker position after the sort
     L.misc[3] = L.misc[4] = 0;
   }
-  // the bucket's key table and run slices, in the sort's second buffers until the sort
+  // the bucket's key table and run slices
   HotKeyTab T;
-  uint64_t* tkh = (uint64_t*)&L.key[1][0];
-  T.kh = tkh;
-  T.kf = tkh + kCapK;
-  T.vm = tkh + 2 * kCapK;
-  T.tp = (const uint32_t*)(tkh + 3 * kCapK);
-  for (uint32_t o = tid; o < kout; o += kSortThreads) {
-    tkh[o] = H.hk_h[g0 + o];
-    tkh[kCapK + o] = H.hk_f[g0 + o];
-    tkh[2 * kCapK + o] = H.hk_vm[g0 + o];
-    ((uint32_t*)(tkh + 3 * kCapK))[o] = H.hk_tp[g0 + o];
+  T.kh = L.tab;
+  T.kf = L.tab + C::KCap;
+  T.vm = L.tab + 2 * C::KCap;
+  T.tp = L.ttp;
+  for (uint32_t o = tid; o < kout; o += C::Threads) {
+    L.tab[o] = H.hk_h[g0 + o];
+    L.tab[C::KCap + o] = H.hk_f[g0 + o];
+    L.tab[2 * C::KCap + o] = H.hk_vm[g0 + o];
+    L.ttp[o] = H.hk_tp[g0 + o];
   }
-  uint32_t* sl = (uint32_t*)&L.ix[1][0];  // [family 0/1][run]: first row, then rows before the run
+  uint32_t* sl = L.sl;  // [family 0/1][run]: first row, then rows before the run
   const uint32_t nr = H.runs ? H.V.nr : 0;
   if (tid < 2 * nr) {
     const uint32_t f = tid / nr, r = tid % nr;
@@ -751,8 +803,8 @@ __global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A
     kand &= k32;
     kor |= k32;
   };
-  for (uint32_t i = tid; i < n; i += 2 * kSortThreads) {  // two children per step, their loads first
-    const uint32_t i2 = i + kSortThreads;
+  for (uint32_t i = tid; i < n; i += 2 * C::Threads) {  // two children per step, their loads first
+    const uint32_t i2 = i + C::Threads;
     const HotFields F1 = hot_fields(A, H, i < N, row_of(i));
     HotFields F2;
     if (i2 < n) F2 = hot_fields(A, H, i2 < N, row_of(i2));
@@ -775,7 +827,7 @@ __global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A
   int s = 0;
   for (int sh = 0; sh < 32; sh += 8) {
     if (((vary >> sh) & 255) == 0) continue;
-    sort_pass(L, s, sh, n);
+    sort_pass<C>(L, s, sh, n);
     s ^= 1;
   }
   phase(1);
@@ -784,7 +836,7 @@ __global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A
   // 3. runs (equal key32; markers, sorted last, start none): list in key[s ^ 1] as
   //    start | (G - g0) << 16, in chunks of consecutive positions per thread
   uint32_t* rl = L.key[s ^ 1];
-  const uint32_t per = (n + kSortThreads - 1) / kSortThreads;
+  const uint32_t per = (n + C::Threads - 1) / C::Threads;
   const uint32_t q0 = min(n, tid * per), q1 = min(n, q0 + per);
   uint32_t cnt = 0;
   for (uint32_t q = q0; q < q1; ++q) {
@@ -794,7 +846,7 @@ __global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A
     if (k == mk && !prev_same) L.misc[2] = q;
   }
   uint32_t nruns = 0;
-  uint32_t ex = sort_block_scan(cnt, L.wsum, &nruns);
+  uint32_t ex = sort_block_scan<C::Waves>(cnt, L.wsum, &nruns);
   for (uint32_t q = q0; q < q1; ++q) {
     const uint32_t k = sk[q];
     if (k != mk && !(q > 0 && sk[q - 1] == k)) rl[ex++] = q | ((k >> id_bits) << 16);
@@ -806,7 +858,7 @@ __global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A
   uint16_t* no = L.ix[s ^ 1];
   uint32_t* fq = H.fold_q + c0;
   uint64_t* fv = H.fold_v + c0;
-  for (uint32_t base = 0; base < nruns; base += kSortThreads) {  // (uniform)
+  for (uint32_t base = 0; base < nruns; base += C::Threads) {  // (uniform)
     const uint32_t r = base + tid;
     const bool act = r < nruns;
     const uint32_t e = act ? rl[r] : 0, q = e & 0xFFFF;
@@ -820,12 +872,12 @@ __global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A
   __syncthreads();
   // ranks: one scan of (member outputs << 16 | node outputs) over the runs, into key[s]
   uint32_t* ro = L.key[s];
-  const uint32_t pr = (nruns + kSortThreads - 1) / kSortThreads;
+  const uint32_t pr = (nruns + C::Threads - 1) / C::Threads;
   const uint32_t r0 = min(nruns, tid * pr), r1 = min(nruns, r0 + pr);
   uint32_t c = 0;
   for (uint32_t r = r0; r < r1; ++r) c += sx[rl[r] & 0xFFFF] < N ? (uint32_t)no[r] : (uint32_t)no[r] << 16;
   uint32_t tot = 0;
-  ex = sort_block_scan(c, L.wsum, &tot);
+  ex = sort_block_scan<C::Waves>(c, L.wsum, &tot);
   for (uint32_t r = r0; r < r1; ++r) {
     ro[r] = ex;
     ex += sx[rl[r] & 0xFFFF] < N ? (uint32_t)no[r] : (uint32_t)no[r] << 16;
@@ -833,7 +885,7 @@ __global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A
   __syncthreads();
   phase(3);
   // 5. fold, pass 1: outputs at their rank, their key rows' counts, first slots and sums in LDS
-  for (uint32_t base = 0; base < nruns; base += kSortThreads) {  // (uniform)
+  for (uint32_t base = 0; base < nruns; base += C::Threads) {  // (uniform)
     const uint32_t r = base + tid;
     const bool act = r < nruns;
     const uint32_t e = act ? rl[r] : 0, q = e & 0xFFFF, gr = e >> 16;
@@ -854,7 +906,7 @@ __global__ void __launch_bounds__(kSortThreads) hot_sortfold_kernel(BucketArgs A
   // 6. key rows (as hot_finish_kernel)
   const uint32_t kb = A.kbase[b];
   uint32_t nn = 0, nm = 0;
-  for (uint32_t o = tid; o < kout; o += kSortThreads) {
+  for (uint32_t o = tid; o < kout; o += C::Threads) {
     const uint32_t tk = H.hk_tp[g0 + o] & 0xFF, kc = L.kcnt[o];
     if (tk == TAG_COUNTER) {
       A.kos[(uint64_t)(kb + o) * kKeyOutCols + O_WIN] = L.ksum[o];
