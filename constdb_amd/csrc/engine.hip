@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <map>
 #include <cstdlib>
@@ -683,7 +684,7 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   cdb_status st = CDB_OK;
   const uint32_t H = (uint32_t)wide_ids.size();
   // device: ids[H] | hk_off[H + 1] | c_off[H + 1] | hk_kout[H] | run count
-  uint32_t* meta = (uint32_t*)ws_get(ctx, WS_HOTMETA, (5ull * H + 8) * sizeof(uint32_t), &st);
+  uint32_t* meta = (uint32_t*)ws_get(ctx, WS_HOTMETA, (6ull * H + 8) * sizeof(uint32_t), &st);
   if (!meta) return st;
   HotArgs HA;
   std::memset(&HA, 0, sizeof HA);
@@ -698,7 +699,8 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   HA.hk_off = d_hk_off;
   HA.c_off = d_c_off;
   HA.hk_kout = d_c_off + H + 1;
-  uint64_t* d_runs = (uint64_t*)(((uintptr_t)(HA.hk_kout + H) + 7) & ~(uintptr_t)7);
+  HA.first_run = HA.hk_kout + H;
+  uint64_t* d_runs = (uint64_t*)(((uintptr_t)(HA.first_run + H) + 7) & ~(uintptr_t)7);
   HA.H = H;
   HA.n_children = tc;
   // Tag layout W = G << g_shift | id hash bits << 6 | pos, sorted on bits [lo, g_shift + gbits) in
@@ -731,6 +733,10 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   }
   HA.g_shift = 6 + id_bits;
   HA.id_shift = 64 - id_bits;
+  if (std::getenv("CDB_HOT_PROF"))  // test hook
+    std::fprintf(stderr, "chip_wide: H %u tk %llu tc %llu cmax %llu kmax %llu gbits %d id_bits %d lds %d\n", H,
+                 (unsigned long long)tk, (unsigned long long)tc, (unsigned long long)cmax, (unsigned long long)kmax,
+                 gbits, id_bits, (int)lds);
   CDB_HIP(hipMemcpyAsync(d_ids, wide_ids.data(), H * 4, hipMemcpyHostToDevice, s), "h2d");
   CDB_HIP(hipMemcpyAsync(d_hk_off, hk_off.data(), (H + 1) * 4, hipMemcpyHostToDevice, s), "h2d");
   CDB_HIP(hipMemcpyAsync(d_c_off, c_off.data(), (H + 1) * 4, hipMemcpyHostToDevice, s), "h2d");
@@ -762,7 +768,10 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   HA.rank_m = rank_m;
   HA.w = w;
   HA.v = v;
-  hot_keys_kernel<<<H, kBktThreads, 0, s>>>(A, HA);
+  if (kmax <= 256)
+    hot_keys_kernel<256><<<H, kBktThreads, 0, s>>>(A, HA);
+  else
+    hot_keys_kernel<kCapK><<<H, kBktThreads, 0, s>>>(A, HA);
   CDB_TRY(launch_check(ctx, s, "hot_keys_kernel"));
   if (lds) {  // fold results per run go to the (unused) tag arrays
     HA.fold_v = w;
@@ -808,12 +817,18 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
     CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, HA.emit_n, tc, rank_n, (uint32_t*)nullptr, d_runs, s));
     hot_runlist_kernel<<<grid, 256, 0, s>>>(HA, HA.emit_n, rank_n);
     CDB_TRY(launch_check(ctx, s, "hot_runlist_kernel"));
-    CDB_HIP(hipMemsetAsync(HA.emit_n, 0, 2 * tc * sizeof(uint32_t), s), "memset");  // emit_n | emit_m
-    hot_fold_kernel<<<grid, 256, 0, s>>>(A, HA, 0);
+    hot_first_run_kernel<<<(H + 255) / 256, 256, 0, s>>>(HA);
+    CDB_TRY(launch_check(ctx, s, "hot_first_run_kernel"));
+    // the fold's counts, folds and ranks are per run: the scans run over the runs, not the rows
+    uint64_t nruns = 0;
+    CDB_HIP(hipMemcpyAsync(&nruns, d_runs, sizeof nruns, hipMemcpyDeviceToHost, s), "d2h");
+    CDB_HIP(hipStreamSynchronize(s), "sync");
+    const uint32_t fgrid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nruns + 255) / 256, 16384));
+    hot_fold_kernel<<<fgrid, 256, 0, s>>>(A, HA, 0);
     CDB_TRY(launch_check(ctx, s, "hot_fold_kernel"));
-    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, HA.emit_n, tc, rank_n, (uint32_t*)nullptr, nullptr, s));
-    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, HA.emit_m, tc, rank_m, (uint32_t*)nullptr, nullptr, s));
-    hot_fold_kernel<<<grid, 256, 0, s>>>(A, HA, 1);
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, HA.emit_n, nruns, rank_n, (uint32_t*)nullptr, nullptr, s));
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, HA.emit_m, nruns, rank_m, (uint32_t*)nullptr, nullptr, s));
+    hot_fold_kernel<<<fgrid, 256, 0, s>>>(A, HA, 1);
     CDB_TRY(launch_check(ctx, s, "hot_fold_kernel"));
   }
   hot_finish_kernel<<<H, 256, 0, s>>>(A, HA);
@@ -843,9 +858,22 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   CDB_HIP(hipMemcpyAsync(ids.data(), d_hot_list, hot * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipMemcpyAsync(cnt3.data(), d_cnt3, 3ull * hot * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");
   CDB_HIP(hipStreamSynchronize(s), "sync");
+  const bool hprof = std::getenv("CDB_HOT_PROF") != nullptr;  // test hook: host clock to stderr
+  const auto h0 = std::chrono::steady_clock::now();
+  // (bucket id, list slot) sorted by bucket id: two 16-bit counting passes (std::sort took 0.48 ms
+  // of host time on C5's 14.7K listed buckets)
+  std::vector<uint64_t> packed(hot), spare(hot);
+  for (uint32_t i = 0; i < hot; ++i) packed[i] = (uint64_t)ids[i] << 32 | i;
+  for (int sh = 32; sh < 64; sh += 16) {
+    std::vector<uint32_t> at(65537, 0);
+    for (uint64_t x : packed) ++at[((x >> sh) & 0xFFFF) + 1];
+    for (int d = 0; d < 65536; ++d) at[d + 1] += at[d];
+    for (uint64_t x : packed) spare[at[(x >> sh) & 0xFFFF]++] = x;
+    packed.swap(spare);
+  }
   std::vector<uint32_t> order(hot);
-  for (uint32_t i = 0; i < hot; ++i) order[i] = i;
-  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return ids[a] < ids[b]; });
+  for (uint32_t i = 0; i < hot; ++i) order[i] = (uint32_t)packed[i];
+  const double sort_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
   // test hook: a smaller batch cap runs the chip-wide path in many batches on small inputs
   uint64_t key_cap = kHotKeyCap;
   if (const char* e = std::getenv("CDB_HOT_KEY_CAP"))
@@ -858,6 +886,10 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
   bool runs_batch = false;  // the batch being built reads its children from the runs
   auto flush = [&]() -> cdb_status {
     if (wide_ids.empty()) return CDB_OK;
+    if (hprof)
+      std::fprintf(stderr, "over_capacity: hot %u, batch of %zu buckets after %.3f ms of host work (sort %.3f)\n",
+                   hot, wide_ids.size(),
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count(), sort_ms);
     const cdb_status r =
         chip_wide(ctx, A, wide_ids, hk_off, c_off, tk, tc, cmax, kmax, runs_batch ? rv : nullptr, rv != nullptr, s);
     wide_ids.clear();
@@ -882,13 +914,12 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
     if (C <= SortSmall::Cap && K <= SortSmall::KCap) return 0;
     return C <= kSortCap ? 1 : 2;
   };
+  std::vector<uint32_t> lists[6];  // (runs mode ? 0 : 3) + size class, each in bucket order
+  for (uint32_t i : order) lists[(runs_mode(i) ? 0 : 3) + size_class(i)].push_back(i);
   for (int pass = 0; pass < 6; ++pass) {
     runs_batch = pass < 3;
-    const int cls = pass % 3;
-    for (uint32_t i : order) {
-      if (runs_mode(i) != runs_batch) continue;
+    for (uint32_t i : lists[pass]) {
       const uint32_t K = cnt3[3 * i], N = cnt3[3 * i + 1], M = cnt3[3 * i + 2];
-      if (size_class(i) != cls) continue;
       if (K == 0) {  // no key rows: every child is an orphan and nothing is output (the bucket's
         orphans += N + M;  // counts were zeroed when it was listed); kept off the chip-wide path,
         continue;          // whose per-bucket marker needs a key row

@@ -53,8 +53,9 @@ struct HotArgs {
   uint32_t* v;               // flat child index (then sorted)
   ulonglong2* rec;           // flat child j's fold fields: rec[2j] = (id1, id2), rec[2j + 1] = (t, meta)
   uint32_t* c_h;             // bucket h of flat child j, bit 31 = member
-  uint32_t *emit_n, *emit_m; // per sorted position: outputs of the run starting there
+  uint32_t *emit_n, *emit_m; // per run (global sort): its node / member outputs
   const uint32_t *rank_n, *rank_m;  // exclusive scans of emit_n / emit_m
+  uint32_t* first_run;       // per bucket h: its first run (global sort)
   uint64_t n_children;
   int id_shift;              // W's id bits = id hash >> id_shift (64 + 6 - g_shift; larger in tests)
   int g_shift;               // W's key-id bits start here (kHotIdBits or less)
@@ -93,15 +94,27 @@ __device__ __forceinline__ uint64_t hot_marker(const HotArgs& H, uint32_t h) {
 }
 __device__ __forceinline__ bool hot_takes_part(uint64_t W) { return (W & 63) != 63; }
 
+// The key phase's LDS (bucket_keys touches no child arrays): sized for KC key rows, so that batches
+// of buckets of at most 256 keys run several workgroups per CU.
+template <uint32_t KC>
+struct KeyLds {
+  uint64_t kh[KC], kf[KC], meta[KC];
+  uint64_t okh[KC], okf[KC], ovm[KC], osum[KC];
+  uint32_t idx[KC], rk[KC], flag[KC], rank[KC];
+  uint32_t otp[KC], ocb[KC], occ[KC];
+  uint32_t cnt[(kDig > KC + 1 ? kDig : KC + 1) + 1];
+  unsigned long long st[ST_COUNT];
+  uint32_t misc[32];
+};
+
+template <uint32_t KC>
 __global__ void __launch_bounds__(kBktThreads) hot_keys_kernel(BucketArgs A, HotArgs H) {
-  __shared__ LdsPool L;
-  Scratch S;
+  __shared__ KeyLds<KC> L;
+  Scratch S = {};
   S.kh = L.kh; S.kf = L.kf; S.meta = L.meta;
   S.idx = L.idx; S.rk = L.rk; S.flag = L.flag; S.rank = L.rank; S.cnt = L.cnt;
   S.okh = L.okh; S.okf = L.okf; S.ovm = L.ovm; S.osum = L.osum;
   S.otp = L.otp; S.ocb = L.ocb; S.occ = L.occ;
-  S.c1 = L.c1; S.c2 = L.c2; S.cm = L.cm; S.rt = L.rt; S.rm = L.rm;
-  S.ck = L.ck; S.cidx = L.cidx; S.crk = L.crk; S.cflag = L.cflag; S.crank = L.crank;
   S.st = L.st; S.misc = L.misc;
   const uint32_t h = blockIdx.x, b = H.ids[h];
   const uint32_t kout = bucket_keys(A, b, S);
@@ -337,6 +350,19 @@ __global__ void __launch_bounds__(256) hot_runlist_kernel(HotArgs H, const uint3
        p += (uint64_t)gridDim.x * blockDim.x)
     if (flag[p]) H.run_list[idx[p]] = (uint32_t)p;
 }
+// The first run of every bucket: the first run start at or after the bucket's first position.
+__global__ void __launch_bounds__(256) hot_first_run_kernel(HotArgs H) {
+  const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H.H) return;
+  const uint32_t x = H.c_off[h];
+  uint32_t lo = 0, hi = (uint32_t)*H.run_count;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (H.run_list[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  H.first_run[h] = lo;
+}
 
 constexpr uint32_t kFoldFast = 8;  // runs up to this many rows: rows in registers, loads overlapped
 
@@ -499,7 +525,7 @@ __device__ __forceinline__ void hot_fold_run(const BucketArgs& A, const HotArgs&
 }
 
 // One thread per W-run of the global sort (a (key, child id) group, ~ one row per replica): pass
-// 0 counts (emit_n / emit_m at the run's first position), pass 1 writes at the run's rank in its
+// 0 counts (emit_n / emit_m at the run's index), pass 1 writes at the run's rank in its
 // bucket (after scans of the counts) and adds the run to its key row.
 __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, int pass) {
   unsigned long long gcm = 0, nslow = 0;
@@ -526,13 +552,19 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
       isn = (hc >> 31) == 0;
       b = H.ids[h];
       G = (uint32_t)(W >> H.g_shift);
-      if (pass == 1) obase = (isn ? H.rank_n[p] - H.rank_n[H.c_off[h]] : H.rank_m[p] - H.rank_m[H.c_off[h]]);
+      if (pass == 1) {
+        const uint32_t f = H.first_run[h];
+        obase = isn ? H.rank_n[i] - H.rank_n[f] : H.rank_m[i] - H.rank_m[f];
+      }
     }
-    const bool emitted = act && pass == 1 && (isn ? H.emit_n : H.emit_m)[p] != 0;
+    const bool emitted = act && pass == 1 && (isn ? H.emit_n : H.emit_m)[i] != 0;
     HotAcc acc;
     hot_fold_run(A, H, pass, act, isn, b, G, nrows, [&](uint32_t k) { return H.v[p + k]; }, obase, emitted,
-                 &H.fold_q[p], &H.fold_v[p], acc, gcm, nslow);
-    if (pass == 0 && act) (isn ? H.emit_n : H.emit_m)[p] = acc.nout;
+                 &H.fold_q[i], &H.fold_v[i], acc, gcm, nslow);
+    if (pass == 0 && act) {
+      H.emit_n[i] = isn ? acc.nout : 0;
+      H.emit_m[i] = isn ? 0 : acc.nout;
+    }
     if (pass == 1) {
       // runs are in sorted order, so the wave's active lanes hold non-decreasing keys G:
       // a segmented reduction per key, and the segment's last lane does the atomics (one per key
