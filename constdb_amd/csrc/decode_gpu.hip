@@ -1301,6 +1301,31 @@ __global__ void __launch_bounds__(kDecThreads) sort_off_kernel(const uint32_t* _
     moff[e] = mso[j];
   }
 }
+// After a stable sort on the top 32 key-hash bits: every run of equal top halves (a few entries --
+// a key's DATAS / EXPIRES / DELETES entries, or a 2^-32 coincidence) is insertion-sorted on the
+// whole hash by the thread at its first position, stably, so the pairs end in the order the full
+// 64-bit stable sort gives.
+__global__ void __launch_bounds__(kDecThreads) sort_low_fixup_kernel(uint64_t* __restrict__ k, uint32_t* __restrict__ v,
+                                                                     uint64_t n) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j + 1 < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t hi = k[j] >> 32;
+    if ((k[j + 1] >> 32) != hi || (j > 0 && (k[j - 1] >> 32) == hi)) continue;  // not a run's first
+    uint64_t e = j + 2;
+    while (e < n && (k[e] >> 32) == hi) ++e;
+    for (uint64_t a = j + 1; a < e; ++a) {
+      const uint64_t x = k[a];
+      const uint32_t y = v[a];
+      uint64_t b = a;
+      while (b > j && k[b - 1] > x) {
+        k[b] = k[b - 1];
+        v[b] = v[b - 1];
+        --b;
+      }
+      k[b] = x;
+      v[b] = y;
+    }
+  }
+}
 __global__ void __launch_bounds__(kDecThreads) iota32_kernel(uint32_t* __restrict__ v, uint64_t n) {
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x)
     v[j] = (uint32_t)j;
@@ -1308,8 +1333,9 @@ __global__ void __launch_bounds__(kDecThreads) iota32_kernel(uint32_t* __restric
 
 // The reference dumps its DB by iterating a HashMap (db.rs:122-136), so a peer running it sends
 // DATAS, EXPIRES and DELETES in no key order. Such a snapshot still becomes ONE sorted run: a stable
-// radix sort of (key hash, entry) pairs over all its entries (8 passes of 8 bits; equal hashes keep
-// stream order, so DATAS precede EXPIRES precede DELETES, as dest_kernel orders a hash-ordered
+// sort of (key hash, entry) pairs over all its entries (4 radix passes on the top 32 bits, then the
+// few runs of equal top halves insertion-sorted on the whole hash; equal hashes keep stream order,
+// so DATAS precede EXPIRES precede DELETES, as dest_kernel orders a hash-ordered
 // snapshot), then every entry's key row is its sorted position and its children are laid out in
 // that order (the count scans redone in sorted order). Entries left to the host tier keep the
 // snapshot in stream order (no run).
@@ -1333,8 +1359,11 @@ cdb_status GpuDecode::sort_to_run() {
   ck(hipGetLastError(), "iota32_kernel");
   uint64_t* kk = kh;
   uint32_t* vv = v;
-  if (st_ == CDB_OK) st_ = radix_sort_pairs(ctx_, &kk, &vv, k2, v2, n, 0, 64, s_);
+  // (4 passes on the top half, then the equal-top runs fixed up: the 8-pass sort's order)
+  if (st_ == CDB_OK) st_ = radix_sort_pairs(ctx_, &kk, &vv, k2, v2, n, 32, 64, s_);
   if (st_ != CDB_OK) return st_;
+  sort_low_fixup_kernel<<<g, kDecThreads, 0, s_>>>(kk, vv, n);
+  ck(hipGetLastError(), "sort_low_fixup_kernel");
   sort_perm_kernel<<<g, kDecThreads, 0, s_>>>(vv, n, A_.ncount, A_.mcount, dest, ns, ms);
   ck(hipGetLastError(), "sort_perm_kernel");
   if (st_ == CDB_OK) st_ = exclusive_scan_u32(ctx_, ns, n, nso, nullptr, s_);
