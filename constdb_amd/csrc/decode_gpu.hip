@@ -611,7 +611,19 @@ class GpuDecode {
   int dd_host(size_t* err_off);
   int status() const { return st_ != CDB_OK ? (int)st_ : rc_; }
   // everything after it (returns the index pass's status when the device part succeeds)
-  int prepare_device(size_t* err_off);
+  int prepare_device(size_t* err_off) {
+    const int rc = prepare_launch(err_off);
+    if (!prep_.pending) return rc;
+    ck(hipStreamSynchronize(s_), "sync(decode)");
+    return prepare_finish(err_off);
+  }
+  // ... in two halves, so that several snapshots' device work is queued before one
+  // synchronisation: prepare_launch queues the bytes, counts, scans and checksum and the small
+  // words' download (prepare_pending() then says prepare_finish must follow, after the context
+  // stream is synchronised); prepare_finish reads them and does the rest
+  int prepare_launch(size_t* err_off);
+  int prepare_finish(size_t* err_off);
+  bool prepare_pending() const { return prep_.pending; }
   cdb_status emit_host(DecodeTiming* tm);
   cdb_status emit_device(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t ks, uint32_t cs,
                          uint32_t pos, bool run,
@@ -619,12 +631,11 @@ class GpuDecode {
   // key-hash order (after prepare_device): queues the key-hash pass and the sections' order check
   // on the context's stream; the verdict reads after a synchronisation (read_order).
   cdb_status order_check();
-  bool read_order() const { return ordered_ && !order_flag_; }
+  bool read_order() const { return ordered_ && !(prep_.small && prep_.small[4]); }
   // a snapshot not in key-hash order (the reference's HashMap order) made ONE run anyway (after
   // read_order): its entries sorted by key hash on the device, children laid out in that order
   cdb_status sort_to_run();
   bool sorted() const { return sorted_; }
-  unsigned long long order_flag_ = 0;  // written by the D2H copy queued in order_check
   uint64_t keys() const { return n_; }
   uint64_t nodes() const { return nn_; }
   uint64_t members() const { return nm_; }
@@ -712,6 +723,17 @@ class GpuDecode {
   DecArgs A_;
   uint32_t grid_ = 0;
   EvPair ev_;
+  struct PrepState {  // prepare_launch -> prepare_finish
+    bool pending = false;
+    uint64_t dd = 0, n = 0;
+    uint64_t *d_off = nullptr, *d_noff = nullptr, *d_moff = nullptr;
+    uint32_t *d_ncnt = nullptr, *d_mcnt = nullptr;
+    uint64_t* small = nullptr;  // page-locked words (downloads stay asynchronous): crc | node rows |
+                                // member rows | host-tier flag | order flag
+    ~PrepState() {
+      if (small) (void)hipHostFree(small);
+    }
+  } prep_;
 };
 
 int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTiming* tm) {
@@ -948,7 +970,8 @@ int GpuDecode::finish_index(size_t* err_off) {
   return st_ != CDB_OK ? st_ : rc_;
 }
 
-int GpuDecode::prepare_device(size_t* err_off) {
+int GpuDecode::prepare_launch(size_t* err_off) {
+  prep_.pending = false;
   if (cursor_) {
     const int rc = finish_index(err_off);
     if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) return rc;
@@ -1021,10 +1044,32 @@ int GpuDecode::prepare_device(size_t* err_off) {
   ck(hipGetLastError(), "decode scans");
   if (dcrc_.pending && st_ == CDB_OK)  // the index pass left the stream checksum to the GPU
     st_ = crc64_device(ctx_, crc_base, pad + dcrc_.len, d_small, s);
-  uint64_t small[4] = {0, 0, 0, 0};
-  ck(hipMemcpyAsync(small, d_small, 32, hipMemcpyDeviceToHost, s), "d2h(decode)");
-  ck(hipStreamSynchronize(s), "sync(decode)");
+  if (!prep_.small && st_ == CDB_OK) ck(hipHostMalloc((void**)&prep_.small, 48, hipHostMallocDefault), "host alloc(decode)");
   if (st_ != CDB_OK) return st_;
+  ck(hipMemcpyAsync(prep_.small, d_small, 32, hipMemcpyDeviceToHost, s), "d2h(decode)");
+  if (st_ != CDB_OK) return st_;
+  prep_.pending = true;
+  prep_.dd = dd;
+  prep_.n = n;
+  prep_.d_off = d_off;
+  prep_.d_noff = d_noff;
+  prep_.d_moff = d_moff;
+  prep_.d_ncnt = d_ncnt;
+  prep_.d_mcnt = d_mcnt;
+  return rc_;
+}
+
+int GpuDecode::prepare_finish(size_t* err_off) {
+  prep_.pending = false;
+  if (st_ != CDB_OK) return st_;
+  const hipStream_t s = s_;
+  const uint64_t dd = prep_.dd, n = prep_.n;
+  uint64_t* const d_off = prep_.d_off;
+  uint64_t* const d_noff = prep_.d_noff;
+  uint64_t* const d_moff = prep_.d_moff;
+  uint32_t* const d_ncnt = prep_.d_ncnt;
+  uint32_t* const d_mcnt = prep_.d_mcnt;
+  const uint64_t* small = prep_.small;
   if (dcrc_.pending && small[0] != dcrc_.got) {
     rc_ = CDB_INVALID_SNAPSHOT_CHECKSUM;
     *err_off = dcrc_.err_off;
@@ -1243,7 +1288,9 @@ cdb_status GpuDecode::emit_host(DecodeTiming* tm) {
 
 cdb_status GpuDecode::order_check() {
   ordered_ = false;
-  order_flag_ = 0;
+  if (!prep_.small) ck(hipHostMalloc((void**)&prep_.small, 48, hipHostMallocDefault), "host alloc(decode)");
+  if (st_ != CDB_OK) return st_;
+  prep_.small[4] = 0;  // the order flag (written by the download queued below)
   const uint64_t n = n_;
   if (n == 0) {
     ordered_ = true;
@@ -1271,7 +1318,7 @@ cdb_status GpuDecode::order_check() {
   ck(hipGetLastError(), "key_hash_kernel");
   order_check_kernel<<<std::min<uint32_t>(grid_, 2048), kDecThreads, 0, s_>>>(kh, sec_, flag);
   ck(hipGetLastError(), "order_check_kernel");
-  ck(hipMemcpyAsync(&order_flag_, flag, 8, hipMemcpyDeviceToHost, s_), "d2h(decode order)");
+  ck(hipMemcpyAsync(prep_.small + 4, flag, 8, hipMemcpyDeviceToHost, s_), "d2h(decode order)");
   ordered_ = st_ == CDB_OK;
   return st_;
 }
@@ -1632,10 +1679,24 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     for (uint32_t i = 0; i < n; ++i) v.push_back(dec[i]->lt_[k]);
     clk.add(names[k], v);
   }
+  // every snapshot's device preparation queued, one synchronisation, then the halves that read
+  // back; statuses are taken in snapshot order (a launch failure stops the launches after it)
+  std::vector<int> prc(n, CDB_OK);
+  std::vector<size_t> peo(ieo);
+  bool any_pending = false;
   for (uint32_t i = 0; i < n; ++i) {
-    size_t eo = ieo[i];
     int rc = irc[i];
-    if (rc == CDB_OK || rc == CDB_INVALID_SNAPSHOT_CHECKSUM) rc = dec[i]->prepare_device(&eo);
+    if (rc == CDB_OK || rc == CDB_INVALID_SNAPSHOT_CHECKSUM) rc = dec[i]->prepare_launch(&peo[i]);
+    prc[i] = rc;
+    any_pending |= dec[i]->prepare_pending();
+    if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) break;
+  }
+  if (any_pending && hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync(decode)") != CDB_OK)
+    return CDB_DEVICE_ERROR;
+  for (uint32_t i = 0; i < n; ++i) {
+    size_t eo = peo[i];
+    int rc = prc[i];
+    if (dec[i]->prepare_pending()) rc = dec[i]->prepare_finish(&eo);
     if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) {
       *failed = i;
       *err_off = eo;
