@@ -621,7 +621,9 @@ class GpuDecode {
   // synchronisation: prepare_launch queues the bytes, counts, scans and checksum and the small
   // words' download (prepare_pending() then says prepare_finish must follow, after the context
   // stream is synchronised); prepare_finish reads them and does the rest
-  int prepare_launch(size_t* err_off);
+  // pin (may be null): page-locked room for side_bytes() bytes, untouched until the call's end
+  int prepare_launch(size_t* err_off, uint8_t* pin = nullptr, uint64_t pin_room = 0);
+  uint64_t side_bytes() const { return idx_.offset.size() * 9; }
   int prepare_finish(size_t* err_off);
   bool prepare_pending() const { return prep_.pending; }
   cdb_status emit_host(DecodeTiming* tm);
@@ -970,7 +972,7 @@ int GpuDecode::finish_index(size_t* err_off) {
   return st_ != CDB_OK ? st_ : rc_;
 }
 
-int GpuDecode::prepare_launch(size_t* err_off) {
+int GpuDecode::prepare_launch(size_t* err_off, uint8_t* pin, uint64_t pin_room) {
   prep_.pending = false;
   if (cursor_) {
     const int rc = finish_index(err_off);
@@ -1013,8 +1015,15 @@ int GpuDecode::prepare_launch(size_t* err_off) {
     ck(hipMemcpyAsync(d_off, di_.offs.p, dd * 8, hipMemcpyDeviceToDevice, s), "d2d(decode)");
     ck(hipMemsetAsync(d_kind, 0, dd, s), "memset(decode)");
   }
-  if (st_ == CDB_OK) st_ = staged_h2d(ctx_, d_off + dd, idx_.offset.data(), (n - dd) * 8, s);
-  ck(hipMemcpyAsync(d_kind + dd, idx_.kind.data(), n - dd, hipMemcpyHostToDevice, s), "h2d(decode)");
+  if (pin && (n - dd) * 9 <= pin_room) {  // page-locked room of the caller's: no staging-ring waits
+    std::memcpy(pin, idx_.offset.data(), (n - dd) * 8);
+    std::memcpy(pin + (n - dd) * 8, idx_.kind.data(), n - dd);
+    ck(hipMemcpyAsync(d_off + dd, pin, (n - dd) * 8, hipMemcpyHostToDevice, s), "h2d(decode)");
+    ck(hipMemcpyAsync(d_kind + dd, pin + (n - dd) * 8, n - dd, hipMemcpyHostToDevice, s), "h2d(decode)");
+  } else {
+    if (st_ == CDB_OK) st_ = staged_h2d(ctx_, d_off + dd, idx_.offset.data(), (n - dd) * 8, s);
+    ck(hipMemcpyAsync(d_kind + dd, idx_.kind.data(), n - dd, hipMemcpyHostToDevice, s), "h2d(decode)");
+  }
   if (st_ != CDB_OK) return st_;
   std::memset(&A_, 0, sizeof A_);
   A_.raw = raw_dev;
@@ -1043,7 +1052,7 @@ int GpuDecode::prepare_launch(size_t* err_off) {
                                                                                (uint64_t*)nullptr);
   ck(hipGetLastError(), "decode scans");
   if (dcrc_.pending && st_ == CDB_OK)  // the index pass left the stream checksum to the GPU
-    st_ = crc64_device(ctx_, crc_base, pad + dcrc_.len, d_small, s);
+    st_ = crc64_device_queued(ctx_, crc_base, pad + dcrc_.len, d_small, s);
   if (!prep_.small && st_ == CDB_OK) ck(hipHostMalloc((void**)&prep_.small, 48, hipHostMallocDefault), "host alloc(decode)");
   if (st_ != CDB_OK) return st_;
   ck(hipMemcpyAsync(prep_.small, d_small, 32, hipMemcpyDeviceToHost, s), "d2h(decode)");
@@ -1635,7 +1644,10 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     cdb_status st = CDB_OK;
     for (uint32_t i = 0; i < n && st == CDB_OK; ++i) {
       if ((irc[i] != CDB_OK && irc[i] != CDB_INVALID_SNAPSHOT_CHECKSUM) || !dec[i]->deferred()) continue;
-      st = hip_check(ctx, hipStreamCreateWithFlags(&ks[i], hipStreamNonBlocking), "stream(index)");
+      if (ctx->idx_streams.size() <= i) ctx->idx_streams.resize(i + 1, nullptr);
+      if (!ctx->idx_streams[i])
+        st = hip_check(ctx, hipStreamCreateWithFlags(&ctx->idx_streams[i], hipStreamNonBlocking), "stream(index)");
+      ks[i] = ctx->idx_streams[i];
       if (st == CDB_OK && dec[i]->dd_launch(ks[i]) < 0) {
         (void)dec[i]->dd_step(&ieo[i]);
         irc[i] = dec[i]->status();
@@ -1668,8 +1680,6 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
       work();
       for (auto& t : th) t.join();
     }
-    for (hipStream_t k : ks)
-      if (k) (void)hipStreamDestroy(k);
     if (st != CDB_OK) return st;
   }
   clk.mark("deferred_datas");
@@ -1684,9 +1694,22 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
   std::vector<int> prc(n, CDB_OK);
   std::vector<size_t> peo(ieo);
   bool any_pending = false;
+  // the side sections' offsets and kinds go up from one page-locked region (kept in the context)
+  std::vector<uint64_t> pin_at(n + 1, 0);
+  for (uint32_t i = 0; i < n; ++i) pin_at[i + 1] = pin_at[i] + ((dec[i]->side_bytes() + 63) & ~uint64_t(63));
+  if (pin_at[n] > ctx->dec_pin_bytes) {
+    if (ctx->dec_pin) (void)hipHostFree(ctx->dec_pin);
+    ctx->dec_pin = nullptr;
+    ctx->dec_pin_bytes = 0;
+    const size_t want = pin_at[n] + pin_at[n] / 4;
+    if (hipHostMalloc(&ctx->dec_pin, want, hipHostMallocDefault) == hipSuccess) ctx->dec_pin_bytes = want;
+    else ctx->dec_pin = nullptr;  // (the staging ring then)
+  }
   for (uint32_t i = 0; i < n; ++i) {
     int rc = irc[i];
-    if (rc == CDB_OK || rc == CDB_INVALID_SNAPSHOT_CHECKSUM) rc = dec[i]->prepare_launch(&peo[i]);
+    uint8_t* pin = ctx->dec_pin ? (uint8_t*)ctx->dec_pin + pin_at[i] : nullptr;
+    if (rc == CDB_OK || rc == CDB_INVALID_SNAPSHOT_CHECKSUM)
+      rc = dec[i]->prepare_launch(&peo[i], pin, pin ? pin_at[i + 1] - pin_at[i] : 0);
     prc[i] = rc;
     any_pending |= dec[i]->prepare_pending();
     if (rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) break;

@@ -1066,4 +1066,31 @@ cdb_status crc64_device(cdb_ctx* ctx, const uint8_t* dev, uint64_t padded, uint6
   return crc_device(ctx, dev, padded, nullptr, d_crc, s);
 }
 
+cdb_status crc64_device_queued(cdb_ctx* ctx, const uint8_t* dev, uint64_t padded, uint64_t* d_crc, hipStream_t s) {
+  struct CrcTables {
+    uint64_t t[8 * 256];
+    CrcTables() { crc_tables(t); }
+  };
+  static const CrcTables tab;
+  const uint64_t tiles = padded / kCrcTile;
+  const uint64_t run = std::max<uint64_t>(1, (tiles + kCrcThreads - 1) / kCrcThreads);
+  CrcConsts K;
+  for (int k = 0; k < 8; ++k) K.chunk_lvl[k] = x8n_mod((uint64_t)kCrcChunk << k);
+  K.tile = x8n_mod(kCrcTile);
+  for (int k = 0; k < 8; ++k) K.run_lvl[k] = x8n_mod((kCrcTile * run) << k);
+  cdb_status st = CDB_OK;
+  const bool fresh = ctx->ws[WS_CRCTAB].p == nullptr;
+  uint64_t* dt = (uint64_t*)ws_get(ctx, WS_CRCTAB, sizeof tab.t, &st);
+  if (!dt) return st;
+  if (fresh) {  // the tables go up once per context (a synchronous copy: the host table is static)
+    if ((st = hip_check(ctx, hipMemcpy(dt, tab.t, sizeof tab.t, hipMemcpyHostToDevice), "h2d(crc tables)")) != CDB_OK)
+      return st;
+  }
+  uint64_t* dtc = (uint64_t*)ws_get(ctx, WS_CRCPART, std::max<uint64_t>(tiles, 1) * 8, &st);
+  if (!dtc) return st;
+  if (tiles) crc_tile_kernel<<<tiles, kCrcThreads, 0, s>>>(dev, dt, K, dtc);
+  crc_final_kernel<<<1, kCrcThreads, 0, s>>>(dtc, tiles, run, run * kCrcThreads - tiles, K, d_crc, nullptr);
+  return launch_check(ctx, s, "crc");
+}
+
 }  // namespace cdb

@@ -30,6 +30,11 @@ struct cdb_ctx {
   uint64_t pin_next = 0;                              // next slot of the ring (continues across calls)
   uint64_t runs_host[3 * 65] = {};                    // sorted-run path: run starts staged for the device
   uint32_t runs_err = 0;                              // sorted-run path: run_mark_kernel's verdict
+  void* dec_pin = nullptr;                            // decode: page-locked side-section offsets and
+  size_t dec_pin_bytes = 0;                           // kinds of every snapshot (grown, kept)
+  std::vector<hipStream_t> idx_streams;               // decode: one stream per snapshot's entry index
+                                                      // (created on first use, kept: creating and
+                                                      // destroying 8 cost 13 ms per call)
   // multi-device context (cdb_ctx_create_multi): this context is device slot 0; shards[i - 1] is
   // the context of device slot i; node holds the RCCL communicators (shard.hip)
   std::vector<cdb_ctx*> shards;
@@ -59,6 +64,7 @@ enum WsSlot {
   WS_YK, WS_YN, WS_YM,                                  // sharded merge: this device's output rows
   WS_PK, WS_PN, WS_PM,                                  // sharded merge: owner-packed rows (inputs not in runs)
   WS_SPLIT,                                             // sharded merge: owner splits of the runs
+  WS_CRCTAB, WS_CRCPART,                                // decode: CRC tables, per-tile CRC partials
   WS_STATE,                                             // cdb_dev_state_rows: zero bases, error word
   WS_COUNT
 };
@@ -97,6 +103,9 @@ cdb_status staged_d2h(cdb_ctx* ctx, void* host, const void* dev, size_t bytes, h
 void advise_huge(void* p, size_t bytes);
 uint64_t crc_tile_bytes();
 cdb_status crc64_device(cdb_ctx* ctx, const uint8_t* dev, uint64_t padded, uint64_t* d_crc, hipStream_t s);
+// The same, queued only (no synchronisation): tables and partials in the context's workspace, so
+// calls on one stream may follow each other without waiting.
+cdb_status crc64_device_queued(cdb_ctx* ctx, const uint8_t* dev, uint64_t padded, uint64_t* d_crc, hipStream_t s);
 cdb_status stamp_pos(cdb_ctx* ctx, uint64_t* meta, uint64_t n, uint32_t pos, hipStream_t s);
 // Stable LSD radix sort of n (u64 key, u32 value) pairs on key bits [lo, bits) (radix.hip.h; workspace
 // slots WS_RADIX, WS_SCAN); *k / *v receive whichever buffers hold the result.

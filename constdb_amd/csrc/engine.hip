@@ -1442,6 +1442,9 @@ void cdb_ctx_destroy(cdb_ctx* ctx) {
   for (hipEvent_t e : ctx->pin_ev)
     if (e) hipEventDestroy(e);
   if (ctx->pin) hipHostFree(ctx->pin);
+  for (hipStream_t k : ctx->idx_streams)
+    if (k) hipStreamDestroy(k);
+  if (ctx->dec_pin) hipHostFree(ctx->dec_pin);
   if (ctx->side) hipStreamDestroy(ctx->side);
   if (ctx->side2) hipStreamDestroy(ctx->side2);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
