@@ -698,6 +698,7 @@ class GpuDecode {
   std::vector<HostEntry> hosted_;
   DevBuf d_raw_, d_meta_, d_crc_, d_rows_, d_ord_;
   uint64_t raw_front_ = 0;  // the deferred index uploaded the bytes to d_raw_ + raw_front_
+  bool early_up_ = false;   // the index pass queued that upload (from the caller's buffer)
   struct HostReg {  // the batch's bytes, page-locked for a direct upload (unlocked after every sync)
     void* p = nullptr;
     ~HostReg() {
@@ -740,13 +741,30 @@ class GpuDecode {
 
 int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTiming* tm) {
   const auto t0 = std::chrono::steady_clock::now();
+  // A large snapshot's bytes go up at once, from the caller's buffer (page-locked for the call),
+  // while this thread copies them into the batch and indexes them: the DMA no longer waits for
+  // the host index passes (the walk waits on di_.up.a; prepare_device finds them in d_raw_).
+  // CDB_H2D_STAGED=1: through the staging ring after the index pass instead.
+  static const bool staged = std::getenv("CDB_H2D_STAGED") != nullptr;
+  if (!staged && buf && len >= (size_t(64) << 20) && hipSetDevice(ctx_->device) == hipSuccess &&
+      hipHostRegister(const_cast<uint8_t*>(buf), len, hipHostRegisterDefault) == hipSuccess) {
+    reg_.p = const_cast<uint8_t*>(buf);
+    const uint64_t front = crc_tile_bytes();
+    if ((st_ = alloc(&d_raw_.p, front + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK)
+      return st_;
+    raw_front_ = front;
+    ck(hipMemcpyAsync((uint8_t*)d_raw_.p + front, buf, len, hipMemcpyHostToDevice, ctx_->stream), "h2d(index)");
+    ck(hipEventRecord(di_.up.a, ctx_->stream), "event(index)");
+    if (st_ != CDB_OK) return st_;
+    early_up_ = true;
+  }
   rc_ = index_snapshot(buf, len, flags_, out_, &idx_, err_off, &dcrc_, index_threads_, &defer_, &cursor_);
   if (rc_ == kIndexDeferred) rc_ = CDB_OK;  // the DATAS section is indexed in prepare_device
-  // a deferred section's snapshot goes up whole right after: page-lock the batch's bytes here, on
-  // this thread (the index passes of several snapshots run side by side, and so do the page-locks;
-  // one after another they cost as much as the uploads). CDB_H2D_STAGED=1: through the staging ring.
-  static const bool staged = std::getenv("CDB_H2D_STAGED") != nullptr;
-  if (!staged && cursor_ && out_->raw.size() >= (size_t(64) << 20) && hipSetDevice(ctx_->device) == hipSuccess &&
+  // otherwise a deferred section's snapshot goes up whole right after: page-lock the batch's bytes
+  // here, on this thread (the index passes of several snapshots run side by side, and so do the
+  // page-locks; one after another they cost as much as the uploads)
+  if (!early_up_ && !staged && cursor_ && out_->raw.size() >= (size_t(64) << 20) &&
+      hipSetDevice(ctx_->device) == hipSuccess &&
       hipHostRegister(out_->raw.data(), out_->raw.size(), hipHostRegisterDefault) == hipSuccess)
     reg_.p = out_->raw.data();
   if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -766,20 +784,24 @@ int GpuDecode::dd_launch(hipStream_t ks) {
   };
   // the bytes go to their final place: one CRC tile of room in front, so prepare_device zero-fills
   // the checksum's leading pad there instead of moving the stream
-  const uint64_t front = crc_tile_bytes();
-  if ((st_ = alloc(&d_raw_.p, front + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK) return -1;
-  raw_front_ = front;
-  uint8_t* const dst = (uint8_t*)d_raw_.p + front;
+  if (!early_up_) {  // (else the index pass started the upload)
+    const uint64_t front = crc_tile_bytes();
+    if ((st_ = alloc(&d_raw_.p, front + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK)
+      return -1;
+    raw_front_ = front;
+  }
+  uint8_t* const dst = (uint8_t*)d_raw_.p + raw_front_;
   lap(&lt_[0]);
   // bytes page-locked by the index pass go up directly (no second host copy through the staging
   // ring, and this thread does not wait for the upload)
-  if (reg_.p) {
+  if (early_up_) {
+  } else if (reg_.p) {
     ck(hipMemcpyAsync(dst, out_->raw.data(), len, hipMemcpyHostToDevice, s), "h2d(index)");
     if (st_ != CDB_OK) return -1;
   } else if ((st_ = staged_h2d(ctx_, dst, out_->raw.data(), len, s)) != CDB_OK) {
     return -1;
   }
-  ck(hipEventRecord(d.up.a, s), "event(index)");
+  if (!early_up_) ck(hipEventRecord(d.up.a, s), "event(index)");
   ck(hipStreamWaitEvent(ks, d.up.a, 0), "wait(index)");
   lap(&lt_[1]);
   const uint32_t T = d.T = (uint32_t)((len - S + kIdxChunk - 1) / kIdxChunk);
