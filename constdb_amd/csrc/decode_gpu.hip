@@ -628,8 +628,18 @@ class GpuDecode {
   bool prepare_pending() const { return prep_.pending; }
   cdb_status emit_host(DecodeTiming* tm);
   cdb_status emit_device(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t ks, uint32_t cs,
-                         uint32_t pos, bool run,
-                         DecodeTiming* tm);
+                         uint32_t pos, bool run, DecodeTiming* tm) {
+    if (emit_launch(k, nd, mb, ks, cs, pos, run) != CDB_OK) return st_;
+    if (!emit_pending_) return CDB_OK;
+    ck(hipStreamSynchronize(s_), "sync(decode)");
+    return emit_finish(tm);
+  }
+  // ... in two halves (several snapshots' emits queued before one synchronisation of the context
+  // stream, then emit_finish for each when emit_pending())
+  cdb_status emit_launch(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t ks, uint32_t cs,
+                         uint32_t pos, bool run);
+  cdb_status emit_finish(DecodeTiming* tm);
+  bool emit_pending() const { return emit_pending_; }
   // key-hash order (after prepare_device): queues the key-hash pass and the sections' order check
   // on the context's stream; the verdict reads after a synchronisation (read_order).
   cdb_status order_check();
@@ -699,6 +709,7 @@ class GpuDecode {
   DevBuf d_raw_, d_meta_, d_crc_, d_rows_, d_ord_;
   uint64_t raw_front_ = 0;  // the deferred index uploaded the bytes to d_raw_ + raw_front_
   bool early_up_ = false;   // the index pass queued that upload (from the caller's buffer)
+  bool emit_pending_ = false;  // emit_launch -> emit_finish
   struct HostReg {  // the batch's bytes, page-locked for a direct upload (unlocked after every sync)
     void* p = nullptr;
     ~HostReg() {
@@ -1478,8 +1489,9 @@ static void up_rows(std::vector<ColVec>& up, std::vector<HostSeg>& segs, uint64_
   segs.push_back({r.data(), dst[1] + at * s, n * s * 8});
 }
 
-cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t ks,
-                                  uint32_t cs, uint32_t pos, bool run, DecodeTiming* tm) {
+cdb_status GpuDecode::emit_launch(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb, uint32_t ks,
+                                  uint32_t cs, uint32_t pos, bool run) {
+  emit_pending_ = false;
   out_->rows_on_device = true;
   out_->dev_rows[0] = n_;
   out_->dev_rows[1] = nn_;
@@ -1539,8 +1551,15 @@ cdb_status GpuDecode::emit_device(uint64_t* const* k, uint64_t* const* nd, uint6
   }
   if (!segs.empty() && (st_ = staged_copy(ctx_, segs.data(), segs.size(), true, s)) != CDB_OK) return st_;
   ck(hipEventRecord(ev_.b, s), "event");
-  ck(hipStreamSynchronize(s), "sync(decode)");
   if (st_ != CDB_OK) return st_;
+  emit_pending_ = true;
+  return CDB_OK;
+}
+
+cdb_status GpuDecode::emit_finish(DecodeTiming* tm) {
+  emit_pending_ = false;
+  if (st_ != CDB_OK) return st_;
+  const uint64_t n = n_, nn = nn_, nm = nm_;
   if (tm) {
     float ms = 0;
     hipEventElapsedTime(&ms, ev_.a, ev_.b);
@@ -1798,10 +1817,11 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     for (int c = 0; c < kKeyCols; ++c) k[c] = din->keys.col[c] + o[0] * (c ? ks : 1);
     for (int c = 0; c < kNodeCols; ++c) nd[c] = din->nodes.col[c] + o[1] * (c ? cs : 1);
     for (int c = 0; c < kMemberCols; ++c) mb[c] = din->members.col[c] + o[2] * (c ? cs : 1);
-    DecodeTiming t1;
     if (runs)
       for (int f = 0; f < 3; ++f) din->run_start[f][i] = o[f];
-    if ((st = dec[i]->emit_device(k, nd, mb, (uint32_t)ks, (uint32_t)cs, i, runs, &t1)) != CDB_OK) {
+    // (every snapshot's emit queued, one synchronisation, then the halves that read back)
+    if ((st = dec[i]->emit_launch(k, nd, mb, (uint32_t)ks, (uint32_t)cs, i, runs)) != CDB_OK) {
+      (void)hipStreamSynchronize(ctx->stream);
       cdb_dev_rows_release(ctx, &din->keys);
       cdb_dev_rows_release(ctx, &din->nodes);
       cdb_dev_rows_release(ctx, &din->members);
@@ -1811,6 +1831,17 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     o[0] += dec[i]->keys();
     o[1] += dec[i]->nodes();
     o[2] += dec[i]->members();
+  }
+  st = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync(decode emit)");
+  for (uint32_t i = 0; i < n && st == CDB_OK; ++i) {
+    DecodeTiming t1;
+    if (dec[i]->emit_pending() && (st = dec[i]->emit_finish(&t1)) != CDB_OK) *failed = i;
+  }
+  if (st != CDB_OK) {
+    cdb_dev_rows_release(ctx, &din->keys);
+    cdb_dev_rows_release(ctx, &din->nodes);
+    cdb_dev_rows_release(ctx, &din->members);
+    return st;
   }
   din->n_pos = n;
   if (runs) {
