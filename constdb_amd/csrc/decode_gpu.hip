@@ -756,8 +756,12 @@ int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTimi
   // while this thread copies them into the batch and indexes them: the DMA no longer waits for
   // the host index passes (the walk waits on di_.up.a; prepare_device finds them in d_raw_).
   // CDB_H2D_STAGED=1: through the staging ring after the index pass instead.
+  // Up to 512 MB: page-locking the caller's buffer (small pages) costs little; beyond, locking
+  // 8 x 2 GB of it took 444 ms of host index time against 179 for the batch's huge-page copy
+  // (the C4 shard's decode leg: 935 vs 789 ms), so those take the batch copy after the pass.
   static const bool staged = std::getenv("CDB_H2D_STAGED") != nullptr;
-  if (!staged && buf && len >= (size_t(64) << 20) && hipSetDevice(ctx_->device) == hipSuccess &&
+  if (!staged && buf && len >= (size_t(64) << 20) && len <= (size_t(512) << 20) &&
+      hipSetDevice(ctx_->device) == hipSuccess &&
       hipHostRegister(const_cast<uint8_t*>(buf), len, hipHostRegisterDefault) == hipSuccess) {
     reg_.p = const_cast<uint8_t*>(buf);
     const uint64_t front = crc_tile_bytes();
