@@ -146,6 +146,7 @@ struct WaveArgs {
   uint32_t* big_list;   // buckets for the workgroup tier
   uint32_t* big_count;
   RunView V;            // sorted-run path only
+  uint32_t* wide_next;  // the wide tier's next group of 64 buckets (one counter per range)
 };
 
 // A bucket's directory entry (row counts and first row of each family).
@@ -747,14 +748,33 @@ __device__ __forceinline__ bool wide_bucket_candidate(const BucketArgs& A, uint3
   return K > WaveLds<1>::KC || C > WaveLds<1>::CC || A.force_tier == 3;
 }
 
-// Persistent: each wave scans the bucket directory 64 buckets at a time (no global list,
-// so no single-word atomic shared by every wave) and merges the candidates one by one.
+// The wide tier's next group of 64 buckets: one atomic per group on a counter of the range, so
+// that a second, wider launch queued behind the wave tier joins the one running beside it and
+// takes the groups left when the wave tier ends (C5's wide tier ran 0.7 ms past it at one wave
+// per SIMD).
+// A claim takes kWideClaim groups (one atomic per 512 buckets: claiming single groups cost C4's
+// 105K-group wide tier ~0.4 ms of contention).
+constexpr uint32_t kWideClaim = 8;
+__device__ __forceinline__ uint32_t wide_group(const WaveArgs& W, int lane, uint32_t& next, uint32_t& end) {
+  if (next < end) return next++;  // (wave-uniform)
+  uint32_t c = 0;
+  if (lane == 0) c = atomicAdd(W.wide_next, 1u);
+  c = (uint32_t)__shfl((int)c, 0);
+  next = c * kWideClaim + 1;
+  end = (c + 1) * kWideClaim;
+  return c * kWideClaim;
+}
+
+// Persistent: each wave takes the bucket directory 64 buckets at a time and merges the
+// candidates one by one.
 __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_kernel(WaveArgs W) {
   __shared__ WaveLds<2> lds_all[kWavesPerWG];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t groups = (W.bhi - W.blo + 63) / 64;
   unsigned long long found = 0;
-  for (uint32_t g = blockIdx.x * kWavesPerWG + wv; g < groups; g += gridDim.x * kWavesPerWG) {
+  (void)wv;
+  uint32_t nx = 0, en = 0;
+  for (uint32_t g = wide_group(W, lane, nx, en); g < groups; g = wide_group(W, lane, nx, en)) {
     const uint32_t b = W.blo + g * 64 + lane;
     uint64_t m = __ballot(b < W.bhi && wide_bucket_candidate(W.A, b));
     found += __popcll(m);

@@ -65,6 +65,7 @@ enum WsSlot {
   WS_PK, WS_PN, WS_PM,                                  // sharded merge: owner-packed rows (inputs not in runs)
   WS_SPLIT,                                             // sharded merge: owner splits of the runs
   WS_CRCTAB, WS_CRCPART,                                // decode: CRC tables, per-tile CRC partials
+  WS_WIDE,                                              // wide tier: group counters per range
   WS_STATE,                                             // cdb_dev_state_rows: zero bases, error word
   WS_COUNT
 };

@@ -1137,6 +1137,9 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   WA.big_list = d_big_list;
   WA.big_count = d_big_count;
   WA.V = RV;
+  uint32_t* d_wide = (uint32_t*)ws_get(ctx, WS_WIDE, 64 * sizeof(uint32_t), &st);
+  if (!d_wide) return st;
+  CDB_HIP(hipMemsetAsync(d_wide, 0, 64 * sizeof(uint32_t), s), "memset wide");
   CDB_HIP(hipEventRecord(ctx->ev_fork, s), "event");  // inputs of both bucket tiers are ready
   // The wave and wide tiers run over P consecutive bucket ranges. Range p is scanned and compacted
   // into the dense outputs on stream cs while range p + 1 merges: the tiers are VALU-bound and
@@ -1160,7 +1163,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     CDB_HIP(hipStreamSynchronize(s), "sync");
     pipe_auto = over == 0;
   }
-  const uint32_t P = pipe_opt ? (uint32_t)std::min<uint64_t>(pipe_opt, std::max<uint64_t>(nb, 1))
+  const uint32_t P = pipe_opt ? (uint32_t)std::min<uint64_t>({pipe_opt, std::max<uint64_t>(nb, 1), 64})
                      : pipe_auto ? kPipeRanges : 1;
   const bool pipelined = P > 1;
   CompactArgs C;
@@ -1203,17 +1206,25 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     // the wide tier strides over its buckets beside the wave tier: 256 workgroups (one per CU)
     // measured ~1 ms faster per C4 step than 1024, which crowd the wave tier's workgroups out
     const uint32_t gw = (uint32_t)std::min<uint64_t>((nr_b + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 256);
+    // behind the wave tier, a wider launch of the same kernel takes the wide groups still left
+    // (they share the range's counter; with none left its workgroups exit at once)
+    const uint32_t gt = (uint32_t)std::min<uint64_t>((nr_b + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024);
+    WA.wide_next = d_wide + p;  // (P <= 64: the counters were zeroed before the fork)
     if (use_runs) {
       bucket_wave_runs_kernel<<<(nr_b + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, 0, s>>>(WA);
       CDB_TRY(launch_check(ctx, s, "bucket_wave_runs_kernel"));
       // the wide tier's buckets are disjoint from the wave tier's: beside it on a side stream
       bucket_wide_runs_kernel<<<gw, kWavesPerWG * 64, 0, ws>>>(WA);
       CDB_TRY(launch_check(ctx, ws, "bucket_wide_runs_kernel"));
+      bucket_wide_runs_kernel<<<gt, kWavesPerWG * 64, 0, s>>>(WA);
+      CDB_TRY(launch_check(ctx, s, "bucket_wide_runs_kernel"));
     } else {
       bucket_wave_kernel<<<(nr_b + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, 0, s>>>(WA);
       CDB_TRY(launch_check(ctx, s, "bucket_wave_kernel"));
       bucket_wide_kernel<<<gw, kWavesPerWG * 64, 0, ws>>>(WA);
       CDB_TRY(launch_check(ctx, ws, "bucket_wide_kernel"));
+      bucket_wide_kernel<<<gt, kWavesPerWG * 64, 0, s>>>(WA);
+      CDB_TRY(launch_check(ctx, s, "bucket_wide_kernel"));
     }
     if (pipelined) {  // range p: scans and compaction on cs once both tiers are through it
       CDB_HIP(hipEventRecord(ctx->ev_cs, s), "event");

@@ -331,7 +331,8 @@ __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_runs_kernel(Wave
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t groups = (W.bhi - W.blo + 63) / 64;
   unsigned long long found = 0;
-  for (uint32_t g = blockIdx.x * kWavesPerWG + wv; g < groups; g += gridDim.x * kWavesPerWG) {
+  uint32_t nx = 0, en = 0;
+  for (uint32_t g = wide_group(W, lane, nx, en); g < groups; g = wide_group(W, lane, nx, en)) {
     const uint32_t b = W.blo + g * 64 + lane;
     uint64_t m = __ballot(b < W.bhi && wide_bucket_candidate(W.A, b));
     found += __popcll(m);
