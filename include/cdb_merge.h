@@ -113,7 +113,10 @@ cdb_status cdb_decode_snapshot_gpu(cdb_ctx* ctx, const uint8_t* buf, size_t len,
  * partition path; the same result). Errors: *failed
  * is the snapshot, *err_offset the byte offset in it, and nothing is allocated; a checksum
  * mismatch (CDB_INVALID_SNAPSHOT_CHECKSUM) still returns every batch and the rows, as the
- * reference merges a snapshot's entries before it reaches the checksum. */
+ * reference merges a snapshot's entries before it reaches the checksum. A snapshot of 64 MB to
+ * 512 MB is uploaded straight from bufs[i], which the call page-locks (hipHostRegister) for its
+ * duration; where that fails, from the batch's copy. The buffers must not be freed or written
+ * during the call. */
 struct cdb_dev_input; /* below, with cdb_merge_device */
 cdb_status cdb_decode_snapshots_device(cdb_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, uint32_t n,
                                        uint32_t flags, cdb_batch** batches, struct cdb_dev_input* out,
