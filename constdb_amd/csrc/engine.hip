@@ -801,6 +801,7 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   }
   const uint32_t grid = (uint32_t)std::min<uint64_t>((tc + 255) / 256, 16384);
   if (tc) {
+    HA.small_keys = kmax <= kTagKeys ? 1 : 0;
     hot_tag_kernel<<<(uint32_t)((tc + kTagChunk - 1) / kTagChunk), 256, 0, s>>>(A, HA);
     CDB_TRY(launch_check(ctx, s, "hot_tag_kernel"));
     // (per-bucket bitonic sorts in LDS measured slower than this global radix sort: C3 9.98 vs

@@ -69,6 +69,8 @@ struct HotArgs {
   int runs;
   RunView V;
   unsigned long long* prof;  // test hook (CDB_HOT_PROF): hot_sortfold_kernel's phase clocks, or null
+  int small_keys;            // every bucket of the batch has at most kTagKeys output keys: the tag
+                             // kernel searches its buckets' key tables in LDS
 };
 
 // A child's columns: its copied AoS row, or (runs mode) the runs' SoA columns.
@@ -255,8 +257,11 @@ __device__ __forceinline__ uint64_t hot_tag_child(const BucketArgs& A, const Hot
 // One block per kTagChunk consecutive flat children: its first bucket is searched once, and the
 // run slices of that bucket and the next (a chunk of a big bucket spans at most two) come from LDS.
 constexpr uint32_t kTagChunk = 4096;
+constexpr uint32_t kTagKeys = 256;
 __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
   __shared__ uint32_t sl[2][4 * kMaxRuns];  // bucket h0 + slot: [family][run] first row, rows before
+  __shared__ uint64_t tk[2][3][kTagKeys];   // (small_keys) bucket h0 + slot's keys: kh, kf, vm
+  __shared__ uint32_t ttp[2][kTagKeys];     // ... and tag / pos words
   __shared__ uint32_t h_first;
   unsigned long long orph = 0;
   const uint32_t tid = threadIdx.x;
@@ -265,6 +270,17 @@ __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
   __syncthreads();
   const uint32_t h0 = h_first;
   const uint32_t nr = H.runs ? H.V.nr : 0;
+  if (H.small_keys) {
+    for (uint32_t slot = 0; slot < 2 && h0 + slot < H.H; ++slot) {
+      const uint32_t g0 = H.hk_off[h0 + slot], ko = H.hk_kout[h0 + slot];
+      for (uint32_t o = tid; o < ko; o += blockDim.x) {
+        tk[slot][0][o] = H.hk_h[g0 + o];
+        tk[slot][1][o] = H.hk_f[g0 + o];
+        tk[slot][2][o] = H.hk_vm[g0 + o];
+        ttp[slot][o] = H.hk_tp[g0 + o];
+      }
+    }
+  }
   for (uint32_t t = tid; t < 4 * nr; t += blockDim.x) {
     const uint32_t slot = t / (2 * nr), f = (t / nr) & 1, r = t % nr;
     if (h0 + slot < H.H) {
@@ -301,8 +317,17 @@ __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
     } else {
       row = hot_row(A, H, b, i, N);
     }
-    H.w[j] = hot_tag_row(A, H, h, j, isn, hot_fields(A, H, isn, row), hot_key_tab(H, H.hk_off[h]), H.hk_kout[h],
-                         orph);
+    HotKeyTab T;
+    if (H.small_keys && h - h0 < 2) {
+      const uint32_t slot = h - h0;
+      T.kh = tk[slot][0];
+      T.kf = tk[slot][1];
+      T.vm = tk[slot][2];
+      T.tp = ttp[slot];
+    } else {
+      T = hot_key_tab(H, H.hk_off[h]);
+    }
+    H.w[j] = hot_tag_row(A, H, h, j, isn, hot_fields(A, H, isn, row), T, H.hk_kout[h], orph);
     H.v[j] = (uint32_t)j;
     H.c_h[j] = h | (isn ? 0u : 0x80000000u);
   }
