@@ -2,14 +2,20 @@
 """Benchmark: ConstDB snapshot merge on MI355X (BASELINE.json metric:
 "merged CRDT entries/sec + achieved HBM GB/s, snapshot merge at 1/2/4/8 GPUs").
 
-One step = one full merge of R replica states already resident in HBM as columnar rows:
-bucket partition -> fused bucket merge -> dense compaction, i.e. everything
-DB::merge_entry / Object::merge / DB::delete / DB::expire_at (and DB::gc for C3) would do for
-those entries. Configs (constdb_amd/configs.py):
+One step = one full merge of R replica states already resident in HBM (cdb_merge_device): the
+run directories of the key-hash-ordered runs, the fused bucket merge into the bucket layout (the
+result every consumer reads; --output dense adds the compaction into dense columns), i.e.
+everything DB::merge_entry / Object::merge / DB::delete / DB::expire_at (and DB::gc for C3) would
+do for those entries. Configs (constdb_amd/configs.py):
   c4 (default)  8-replica anti-entropy. Weak scaling: every GPU owns a 62.5M-key universe; at
                 N=8 the job is exactly C4 (500M keys x 8 replicas). For N>1 replica r lives on
-                GPU r*N/8 and rows go to the GPU owning their key hash by an RCCL all-to-all
-                (torch.distributed "nccl") inside the timed step.
+                GPU r*N/8 and rows go to the GPU owning their key hash inside the timed step:
+                by default in ONE process over a multi-device context (cdb_merge_sharded: owner
+                splits, RCCL point-to-point inside the library, per-device merges -- the C-ABI
+                path INTEGRATION.md §5 gives the reference's one server process); under a
+                launcher (torch.distributed.run, WORLD_SIZE=N) rank 0 drives every GPU that way
+                and the other ranks only join the barriers. --dist: one process per GPU instead
+                (constdb_amd/dist.py, torch.distributed "nccl" point-to-point).
   c1            2-node MEET, 1M Bytes + 1M counters per node, 50 % overlap (C1/C2).
   c3            4 replicas built by replaying 10M sadd/srem/hset/hdel each, merge + DB::gc.
   c5            Zipf hot keys: 10M keys, 80M node/member rows over 8 replicas.
@@ -53,8 +59,12 @@ def parse():
                     help="use the multi-GPU (RCCL all-to-all) path even when WORLD_SIZE == 1")
     ap.add_argument("--c3-ops", type=int, default=10_000_000, help="ops per replica of config c3")
     ap.add_argument("--single-process", action="store_true",
-                    help="one process drives every GPU: a multi-device context (cdb_ctx_create_multi) and "
-                         "cdb_merge_sharded, rows exchanged by RCCL inside the library")
+                    help="one process drives every device slot: a multi-device context (cdb_ctx_create_multi) and "
+                         "cdb_merge_sharded, rows exchanged by RCCL inside the library (the default for --gpus N > 1; "
+                         "this flag also takes it at N = 1, e.g. with --devices 0,0)")
+    ap.add_argument("--dist", action="store_true",
+                    help="N > 1: one process per GPU (torch.distributed, constdb_amd/dist.py) instead of the "
+                         "single-process cdb_merge_sharded path")
     ap.add_argument("--devices", default=None,
                     help="--single-process: device slots, e.g. 0,1,2,3 (default 0..gpus-1); a device listed twice "
                          "gives two shards on one GPU (rows then move by device copies)")
@@ -381,6 +391,8 @@ def run_single_process(cdb, args):
     from constdb_amd import configs
     from constdb_amd.runs import sort_into_runs
     devs = [int(x) for x in args.devices.split(",")] if args.devices else list(range(args.gpus))
+    if len(devs) > 8:
+        raise SystemExit("at most 8 device slots (cdb_ctx_create_multi)")
     N = len(devs)
     L = cdb.lib()
     ctx = cdb.Context(devices=devs)
@@ -455,10 +467,33 @@ def spawn_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
+def launcher_barrier(world, rank):
+    """Under a launcher with the single-process path: a gloo group (no GPU) whose barriers bracket
+    rank 0's run, so every rank starts and ends together. Returns a callable barrier."""
+    import torch.distributed as tdist
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    return tdist
+
+
 def main():
     args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.single_process:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and not args.dist:
+        args.single_process = True
+    if args.gpus > 1 and world == 1 and args.dist:
         raise SystemExit(spawn_ranks(args))
+    tdist = None
+    if args.single_process and world > 1:
+        if world != args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+        tdist = launcher_barrier(world, rank)
+        tdist.barrier()
+        if rank != 0:  # rank 0 drives every GPU; this rank touches none
+            tdist.barrier()
+            tdist.destroy_process_group()
+            return
     # RCCL and the HIP runtime may print banners on the C-level stdout: keep fd 1 for the
     # single JSON line and send everything else to stderr.
     json_fd = os.dup(1)
@@ -467,11 +502,13 @@ def main():
     import constdb_amd as cdb
     from constdb_amd import build as b
     b.build()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.single_process:
-        res = run_single_process(cdb, args)
+        try:
+            res = run_single_process(cdb, args)
+        finally:
+            if tdist is not None:
+                tdist.barrier()
+                tdist.destroy_process_group()
         sample = None
     elif world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
@@ -487,6 +524,8 @@ def main():
     if rank != 0:
         os.close(json_fd)
         return
+    if tdist is not None:
+        res["config"]["launcher"] = f"{world} ranks: rank 0 drives every GPU, the others join its barriers"
     if not args.no_cpu_baseline and sample is not None:
         snaps, desc = sample()
         res["cpu_baseline"] = cpu_baseline(cdb, args, snaps, desc)

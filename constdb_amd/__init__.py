@@ -477,11 +477,13 @@ def decode_snapshots_device(ctx: "Context", snaps, reference_checksum: bool = Fa
     device columns (release each family with cdb_dev_rows_release), each batch holding the
     host side (bytes, references, header). Errors are raised for the failing snapshot. records: the rows
     in the records layout (cdb_dev_rows.stride) instead of columns; keep_bytes: the snapshot bytes
-    stay in HBM with the batches (cdb_encode_device)."""
+    stay in HBM with the batches (cdb_encode_device). A snapshot may also be a CPU uint8 tensor
+    (for instance page-locked memory): its bytes are passed in place."""
     n = len(snaps)
-    datas = [bytes(x) for x in snaps]
-    bufs = (ctypes.c_char_p * max(n, 1))(*datas)
-    lens = (ctypes.c_size_t * max(n, 1))(*[len(x) for x in datas])
+    datas = [x if hasattr(x, "data_ptr") else bytes(x) for x in snaps]
+    bufs = (ctypes.c_char_p * max(n, 1))(*[ctypes.cast(x.data_ptr(), ctypes.c_char_p) if hasattr(x, "data_ptr")
+                                           else x for x in datas])
+    lens = (ctypes.c_size_t * max(n, 1))(*[x.numel() if hasattr(x, "data_ptr") else len(x) for x in datas])
     hs = (ctypes.c_void_p * max(n, 1))()
     din = DevInput()
     failed = ctypes.c_uint32()

@@ -137,6 +137,8 @@ struct RunView {
   const uint64_t* nin[kNodeCols];
   const uint64_t* min[kMemberCols];
   uint32_t ks, ns, ms;        // record strides of the families (1: plain columns; common.h row_field)
+  uint32_t rs_sum[3];         // per family, the sum of the runs' first rows (mod 2^32): a bucket's
+                              // dense base is the sum of its slices' first rows minus this
 };
 
 struct WaveArgs {
@@ -147,6 +149,7 @@ struct WaveArgs {
   uint32_t* big_count;
   RunView V;            // sorted-run path only
   uint32_t* wide_next;  // the wide tier's next group of 64 buckets (one counter per range)
+  uint32_t* pipe_next;  // the persistent wave tier's next chunk, one counter per XCD slab (8)
 };
 
 // A bucket's directory entry (row counts and first row of each family).
@@ -236,34 +239,44 @@ __device__ __forceinline__ void load_cols(const BucketArgs& A, const WaveDir& d,
   }
 }
 
+// A bucket is merged in two halves. The first (phases 0-3) consumes the bucket's input registers:
+// keys ranked and folded, children found, ranked and staged in LDS. The second (phases 4-5) folds
+// the children and writes every output from LDS and the key state below. Between them the input
+// registers are dead, which is where a streaming kernel issues the next bucket's loads (one
+// program point: wave_bucket's `next()`).
+template <int KE>
+struct WaveMid {
+  uint32_t K, N, M, kb, nb0, mb0, kout, nlive;  // (wave-uniform)
+  uint64_t kh[KE], kf[KE], o_ct[KE], o_ut[KE], o_dt[KE], o_meta[KE], o_win[KE];
+  uint32_t o_T[KE], orank[KE], fam[KE];
+  bool emit[KE];
+  uint32_t st_conf, st_dict, st_gcd, orph;
+};
+enum { WAVE_GO = 0, WAVE_DONE = 1, WAVE_PUSH = 2 };  // first half: second half / nothing more / exact tier
+
+// Hands bucket b to the workgroup tier (no outputs until that tier's: a pipelined compaction may
+// read them first).
+__device__ __forceinline__ void wave_push(const WaveArgs& W, uint32_t b, int lane) {
+  if (lane == 0) {
+    W.A.kout[b] = W.A.nout[b] = W.A.mout[b] = 0;
+    W.big_list[atomicAdd(W.big_count, 1u)] = b;
+  }
+}
+
 // One bucket on one wave, up to 64*KE key rows and 128*KE child rows, from the columns in
 // `in`. KE = 1 leaves buckets over that capacity to bucket_wide_kernel and lists those over
-// ITS capacity (and forced tiers) for the workgroup tier. `next()` runs exactly once, as
-// soon as `in` is dead (after the children are staged in LDS): the streaming kernel issues
-// the next bucket's loads there, so they are in flight while this bucket's children fold.
-template <int KE, int CE, typename Next>
-__device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, uint32_t b, int lane,
-                                            const WaveIn<KE, CE>& in, Next&& next) {
+// ITS capacity (and forced tiers) for the workgroup tier (WAVE_PUSH).
+template <int KE, int CE>
+__device__ __forceinline__ int wave_phase_a(const WaveArgs& W, WaveLds<KE>& L, uint32_t b, int lane,
+                                            const WaveIn<KE, CE>& in, WaveMid<KE>& mid) {
   static_assert(CE <= 2 * KE, "child slots per lane");
   constexpr uint32_t KC = WaveLds<KE>::KC, CC = WaveLds<KE>::CC;
   const BucketArgs& A = W.A;
   const uint32_t K = in.d.K, N = in.d.N, M = in.d.M;
-  auto push = [&](uint32_t* list, uint32_t* count) {
-    if (lane == 0) {  // no outputs until the workgroup tier's (a pipelined compaction may read them first)
-      A.kout[b] = A.nout[b] = A.mout[b] = 0;
-      list[atomicAdd(count, 1u)] = b;
-    }
-  };
   if (KE == 1) {  // the wide kernel finds its buckets itself (wide_bucket_candidate)
-    if (A.force_tier == 1 || A.force_tier == 2 || A.force_tier == 4 || N + M > WaveLds<2>::CC || K > WaveLds<2>::KC) {
-      next();
-      push(W.big_list, W.big_count);
-      return;
-    }
-    if (K > KC || N + M > CC || A.force_tier == 3) {
-      next();
-      return;
-    }
+    if (A.force_tier == 1 || A.force_tier == 2 || A.force_tier == 4 || N + M > WaveLds<2>::CC || K > WaveLds<2>::KC)
+      return WAVE_PUSH;
+    if (K > KC || N + M > CC || A.force_tier == 3) return WAVE_DONE;
   }
   const uint32_t kb = in.d.kb, nb0 = in.d.nb0, mb0 = in.d.mb0;
   const uint32_t C = N + M;
@@ -297,7 +310,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
       A.kout[b] = A.nout[b] = A.mout[b] = 0;
       atomicAdd(&stat_shard(A.stats)[kStatStride - 1], sk);
     }
-    return;
+    return WAVE_DONE;
   }
   // ------------------------------------------------------------ 1. keys: rank + scatter
   // word = rel << 20 | family << 18 | pos << 12 | slot   (pos < 64, slot < 4096), where rel is
@@ -355,11 +368,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     coll |= same_key && (pkh != kh[e] || pkf != kf[e] || (pw >> 12) == (w[e] >> 12));
     Hk[e] = __ballot(kin[e] && (s == 0 || (pw >> 18) != (w[e] >> 18)));
   }
-  if (__ballot(coll)) {
-    next();
-    push(W.big_list, W.big_count);
-    return;
-  }
+  if (__ballot(coll)) return WAVE_PUSH;
 
   if (CDB_WAVE_STOP <= 1) {
     const unsigned long long sk = wave_sum_u64((unsigned long long)(w[0] ^ kh[0] ^ (uint64_t)Hk[0]));
@@ -367,7 +376,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
       A.kout[b] = A.nout[b] = A.mout[b] = 0;
       atomicAdd(&stat_shard(A.stats)[kStatStride - 1], sk);
     }
-    return;
+    return WAVE_DONE;
   }
   // ------------------------------------------------------------ 2. key folds (tail slots)
   const uint64_t last_bad = (A.flags & F_GC_DELETES) ? *A.last_bad : 0;
@@ -473,11 +482,11 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
       A.kout[b] = A.nout[b] = A.mout[b] = 0;
       atomicAdd(&stat_shard(A.stats)[kStatStride - 1], sk);
     }
-    return;
+    return WAVE_DONE;
   }
   // ------------------------------------------------------------ 3. children: key lookup
   // word = key rank << 56 | id hash[41:0] << 14 | pos << 8 | slot   (rank < 128, slot < 256)
-  uint32_t orph = 0, gcm = 0;
+  uint32_t orph = 0;
   uint32_t ckey[CE];
   bool clive[CE];
 #pragma unroll
@@ -560,10 +569,57 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     }
   }
   wave_sync();
-  next();  // this bucket's input registers are dead from here on
+  // this bucket's input registers are dead from here on
+  mid.K = K;
+  mid.N = N;
+  mid.M = M;
+  mid.kb = kb;
+  mid.nb0 = nb0;
+  mid.mb0 = mb0;
+  mid.kout = kout;
+  mid.nlive = nlive;
+#pragma unroll
+  for (int e = 0; e < KE; ++e) {
+    mid.kh[e] = kh[e];
+    mid.kf[e] = kf[e];
+    mid.o_ct[e] = o_ct[e];
+    mid.o_ut[e] = o_ut[e];
+    mid.o_dt[e] = o_dt[e];
+    mid.o_meta[e] = o_meta[e];
+    mid.o_win[e] = o_win[e];
+    mid.o_T[e] = o_T[e];
+    mid.orank[e] = orank[e];
+    mid.fam[e] = fam[e];
+    mid.emit[e] = emit[e];
+  }
+  mid.st_conf = st_conf;
+  mid.st_dict = st_dict;
+  mid.st_gcd = st_gcd;
+  mid.orph = orph;
+  return WAVE_GO;
+}
 
+template <int KE, int CE>
+__device__ __forceinline__ void wave_phase_b(const WaveArgs& W, WaveLds<KE>& L, uint32_t b, int lane,
+                                             const WaveMid<KE>& mid) {
+  constexpr uint32_t KC = WaveLds<KE>::KC;
+  const BucketArgs& A = W.A;
+  const uint32_t kb = mid.kb, nb0 = mid.nb0, mb0 = mid.mb0, kout = mid.kout, nlive = mid.nlive;
+  const uint32_t st_conf = mid.st_conf, st_dict = mid.st_dict, st_gcd = mid.st_gcd, orph = mid.orph;
+  const auto& kh = mid.kh;
+  const auto& kf = mid.kf;
+  const auto& o_ct = mid.o_ct;
+  const auto& o_ut = mid.o_ut;
+  const auto& o_dt = mid.o_dt;
+  const auto& o_meta = mid.o_meta;
+  const auto& o_win = mid.o_win;
+  const auto& o_T = mid.o_T;
+  const auto& orank = mid.orank;
+  const auto& fam = mid.fam;
+  const auto& emit = mid.emit;
+  uint32_t gcm = 0;
   if (CDB_WAVE_STOP <= 3) {
-    const unsigned long long sk = wave_sum_u64((unsigned long long)((uint64_t)nlive ^ cw[0] ^ orph));
+    const unsigned long long sk = wave_sum_u64((unsigned long long)((uint64_t)nlive ^ orph));
     if (lane == 0) {
       A.kout[b] = A.nout[b] = A.mout[b] = 0;
       atomicAdd(&stat_shard(A.stats)[kStatStride - 1], sk);
@@ -590,7 +646,7 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
     Lv[e] = __ballot(live[e]);
   }
   if (__ballot(coll2)) {  // id-hash collision or duplicate: exact tier (nothing written yet)
-    push(W.big_list, W.big_count);
+    wave_push(W, b, lane);
     return;
   }
   uint64_t En[CE], Em[CE], c_v[CE], c_t[CE], c_m[CE];
@@ -712,6 +768,19 @@ __device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, u
   }
 }
 
+
+// The whole bucket: first half, `next()` (exactly once per bucket, at this one point), second half.
+template <int KE, int CE, typename Next>
+__device__ __forceinline__ void wave_bucket(const WaveArgs& W, WaveLds<KE>& L, uint32_t b, int lane,
+                                            const WaveIn<KE, CE>& in, Next&& next) {
+  WaveMid<KE> mid;
+  const int act = wave_phase_a<KE, CE>(W, L, b, lane, in, mid);
+  next();
+  if (act == WAVE_PUSH)
+    wave_push(W, b, lane);
+  else if (act == WAVE_GO)
+    wave_phase_b<KE, CE>(W, L, b, lane, mid);
+}
 
 constexpr uint32_t kXcds = 8;
 

@@ -597,7 +597,9 @@ class GpuDecode {
     const int rc = index(buf, len, err_off, tm);
     return rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM ? rc : prepare_device(err_off);
   }
-  // the host index pass alone (no HIP call: several snapshots are indexed on parallel threads)
+  // the host index pass (several snapshots are indexed on parallel threads). Its HIP calls -- the
+  // early upload of a large snapshot and the page-lock of its bytes -- record their failures in
+  // this object (st_); fail() serialises the context's last_error
   int index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTiming* tm);
   // the device index of a deferred DATAS section in steps, so that the sections of several
   // snapshots are indexed side by side (decode_snapshots_gpu_device):
@@ -663,6 +665,11 @@ class GpuDecode {
   void ck(hipError_t e, const char* what) {
     if (e != hipSuccess && st_ == CDB_OK) st_ = hip_check(ctx_, e, what);
   }
+  static bool host_register(void* p, size_t bytes) {  // false: not locked, and no pending HIP error
+    if (hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess) return true;
+    (void)hipGetLastError();
+    return false;
+  }
   cdb_status alloc(void** p, size_t bytes, const char* what) {  // reported, no pending HIP error
     if (hipMalloc(p, bytes) == hipSuccess) return CDB_OK;
     (void)hipGetLastError();
@@ -712,8 +719,14 @@ class GpuDecode {
   bool emit_pending_ = false;  // emit_launch -> emit_finish
   struct HostReg {  // the batch's bytes, page-locked for a direct upload (unlocked after every sync)
     void* p = nullptr;
+    hipStream_t s = nullptr;  // the stream an upload from p was queued on
     ~HostReg() {
-      if (p) (void)hipHostUnregister(p);
+      if (!p) return;
+      // an upload may still read p when the call ends early (an index pass failed after it was
+      // queued): wait for it before the pages are unlocked
+      if (s) (void)hipStreamSynchronize(s);
+      (void)hipHostUnregister(p);
+      (void)hipGetLastError();
     }
   } reg_;
   uint64_t raw_pad_ = 0;  // d_raw_ + raw_pad_ = byte 0 of the snapshot
@@ -760,10 +773,13 @@ int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTimi
   // 8 x 2 GB of it took 444 ms of host index time against 179 for the batch's huge-page copy
   // (the C4 shard's decode leg: 935 vs 789 ms), so those take the batch copy after the pass.
   static const bool staged = std::getenv("CDB_H2D_STAGED") != nullptr;
+  // (a failed page-lock -- a buffer the caller already locked, a read-only mapping, the same bytes
+  // passed twice -- falls back silently: its error is cleared so that no later check reports it)
   if (!staged && buf && len >= (size_t(64) << 20) && len <= (size_t(512) << 20) &&
       hipSetDevice(ctx_->device) == hipSuccess &&
-      hipHostRegister(const_cast<uint8_t*>(buf), len, hipHostRegisterDefault) == hipSuccess) {
+      host_register(const_cast<uint8_t*>(buf), len)) {
     reg_.p = const_cast<uint8_t*>(buf);
+    reg_.s = ctx_->stream;
     const uint64_t front = crc_tile_bytes();
     if ((st_ = alloc(&d_raw_.p, front + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK)
       return st_;
@@ -779,9 +795,10 @@ int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTimi
   // here, on this thread (the index passes of several snapshots run side by side, and so do the
   // page-locks; one after another they cost as much as the uploads)
   if (!early_up_ && !staged && cursor_ && out_->raw.size() >= (size_t(64) << 20) &&
-      hipSetDevice(ctx_->device) == hipSuccess &&
-      hipHostRegister(out_->raw.data(), out_->raw.size(), hipHostRegisterDefault) == hipSuccess)
+      hipSetDevice(ctx_->device) == hipSuccess && host_register(out_->raw.data(), out_->raw.size())) {
     reg_.p = out_->raw.data();
+    reg_.s = ctx_->stream;
+  }
   if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return rc_;
 }

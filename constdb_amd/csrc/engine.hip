@@ -1,6 +1,7 @@
 // HIP driver of the merge pipeline (gfx950): partition -> fused bucket merge ->
 // over-capacity buckets -> dense compaction. Also the device-level C-ABI entry points.
 #include <hip/hip_runtime.h>
+#include <mutex>
 
 #include <algorithm>
 #include <chrono>
@@ -21,7 +22,12 @@
 namespace cdb {
 
 cdb_status fail(cdb_ctx* ctx, cdb_status st, const std::string& msg) {
-  if (ctx) ctx->last_error = msg;
+  // (the decoder's index threads may fail side by side: the message string is written under a lock)
+  static std::mutex mu;
+  if (ctx) {
+    std::lock_guard<std::mutex> g(mu);
+    ctx->last_error = msg;
+  }
   return st;
 }
 
@@ -38,6 +44,32 @@ cdb_status launch_check(cdb_ctx* ctx, hipStream_t s, const char* what) {
   cdb_status st = hip_check(ctx, hipGetLastError(), what);
   if (st == CDB_OK && sync) st = hip_check(ctx, hipStreamSynchronize(s), what);
   return st;
+}
+
+// The persistent wave tier (bucket_wave_pipe_kernel) on runs of at most 8 per family;
+// CDB_WAVE_PIPE=0 runs the one-bucket-per-wave kernel instead (A/B and test hook).
+bool pipe_wave_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("CDB_WAVE_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// Its grid: every workgroup slot of the device (resident workgroups per CU x CUs).
+uint32_t pipe_wave_grid(cdb_ctx* ctx) {
+  static uint32_t grid[64] = {0};
+  const int dev = ctx->device;
+  if (dev >= 0 && dev < 64 && grid[dev]) return grid[dev];
+  int cus = 0, per_cu = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bucket_wave_pipe_kernel<true>, kWavesPerWG * 64, 0) !=
+          hipSuccess ||
+      per_cu <= 0)
+    per_cu = 4;
+  (void)hipGetLastError();
+  const uint32_t g = (uint32_t)(cus * per_cu);
+  if (dev >= 0 && dev < 64) grid[dev] = g;
+  return g;
 }
 
 void* ws_get(cdb_ctx* ctx, int slot, size_t bytes, cdb_status* st) {
@@ -622,6 +654,7 @@ cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, const InLayout&
     const uint64_t blocks = std::min<uint64_t>((nb + 255) / 256, 8192);
     uint64_t rs_sum = 0;
     for (uint32_t r = 0; r < nr; ++r) rs_sum += ctx->runs_host[f * (kMaxRuns + 1) + r];
+    V->rs_sum[f] = (uint32_t)rs_sum;
     run_reduce_kernel<<<(uint32_t)blocks, 256, 0, s>>>(V->rdir[f], nr, nb, rs_sum, dirs[f].base, dirs[f].hist);
     CDB_TRY(launch_check(ctx, s, "run_reduce_kernel"));
   }
@@ -1138,9 +1171,13 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   WA.big_list = d_big_list;
   WA.big_count = d_big_count;
   WA.V = RV;
-  uint32_t* d_wide = (uint32_t*)ws_get(ctx, WS_WIDE, 64 * sizeof(uint32_t), &st);
+  // counters: the wide tier's per range [0, 64), the persistent wave tier's per (range, XCD slab)
+  uint32_t* d_wide = (uint32_t*)ws_get(ctx, WS_WIDE, (64 + 64 * kXcds) * sizeof(uint32_t), &st);
   if (!d_wide) return st;
-  CDB_HIP(hipMemsetAsync(d_wide, 0, 64 * sizeof(uint32_t), s), "memset wide");
+  CDB_HIP(hipMemsetAsync(d_wide, 0, (64 + 64 * kXcds) * sizeof(uint32_t), s), "memset wide");
+  // the persistent wave tier (runs of at most 8 per family): one resident grid
+  const bool wave_pipe = use_runs && RV.nr <= 8 && pipe_wave_enabled();
+  const uint32_t pipe_grid = wave_pipe ? pipe_wave_grid(ctx) : 0;
   CDB_HIP(hipEventRecord(ctx->ev_fork, s), "event");  // inputs of both bucket tiers are ready
   // The wave and wide tiers run over P consecutive bucket ranges. Range p is scanned and compacted
   // into the dense outputs on stream cs while range p + 1 merges: the tiers are VALU-bound and
@@ -1211,7 +1248,20 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     // (they share the range's counter; with none left its workgroups exit at once)
     const uint32_t gt = (uint32_t)std::min<uint64_t>((nr_b + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024);
     WA.wide_next = d_wide + p;  // (P <= 64: the counters were zeroed before the fork)
-    if (use_runs) {
+    WA.pipe_next = d_wide + 64 + kXcds * p;
+    if (wave_pipe) {
+      const uint32_t g = (uint32_t)std::min<uint64_t>(pipe_grid, (nr_b + kPipeChunk - 1) / kPipeChunk * kXcds);
+      const bool rec = RV.ks == kKeyCols - 1 && RV.ns == kNodeCols - 1 && RV.ms == kMemberCols - 1;
+      if (rec)
+        bucket_wave_pipe_kernel<true><<<std::max<uint32_t>(g, 1), kWavesPerWG * 64, 0, s>>>(WA);
+      else
+        bucket_wave_pipe_kernel<false><<<std::max<uint32_t>(g, 1), kWavesPerWG * 64, 0, s>>>(WA);
+      CDB_TRY(launch_check(ctx, s, "bucket_wave_pipe_kernel"));
+      bucket_wide_runs_kernel<<<gw, kWavesPerWG * 64, 0, ws>>>(WA);
+      CDB_TRY(launch_check(ctx, ws, "bucket_wide_runs_kernel"));
+      bucket_wide_runs_kernel<<<gt, kWavesPerWG * 64, 0, s>>>(WA);
+      CDB_TRY(launch_check(ctx, s, "bucket_wide_runs_kernel"));
+    } else if (use_runs) {
       bucket_wave_runs_kernel<<<(nr_b + kWavesPerWG - 1) / kWavesPerWG, kWavesPerWG * 64, 0, s>>>(WA);
       CDB_TRY(launch_check(ctx, s, "bucket_wave_runs_kernel"));
       // the wide tier's buckets are disjoint from the wave tier's: beside it on a side stream

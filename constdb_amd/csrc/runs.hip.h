@@ -232,8 +232,63 @@ __device__ __forceinline__ uint64_t run_row(const RunMap& q, uint32_t c) {
   return shfl_u64(q.off, lane_slice(q.incl, q.L, c)) + c;
 }
 
-// The columns of bucket b (KE key rows and CE child rows per lane) from the runs, field by field
-// (either input layout: a lane reads its row's fields with one 8-B load each).
+// Key row `row` of the runs into key slot e (either input layout: a lane reads its row's fields
+// with one 8-B load each, or the record as 16-B pieces).
+// (REC: the records layout is known at compile time -- the column pointers stay out of registers)
+template <bool REC = false, int KE, int CE>
+__device__ __forceinline__ void load_key_row(const RunView& V, uint64_t row, int e, WaveIn<KE, CE>& in) {
+  in.kh[e] = V.kin[K_KH][row];
+  // aux (a counter's load-time total) is read only by a counter key no other replica holds:
+  // the fold fetches it then, by the row index kept in its place (wave_bucket, RunView)
+  in.kaux[e] = row;
+  if (REC || V.ks == kKeyCols - 1) {  // (uniform) records: kf ct | ut dt as two 16-B pieces, then meta
+    const uint64_t* rec = V.kin[1] + row * (kKeyCols - 1);
+    const u64x2 q0 = reinterpret_cast<const u64x2*>(rec)[0], q1 = reinterpret_cast<const u64x2*>(rec)[1];
+    in.kf[e] = q0.x;
+    in.kct[e] = q0.y;
+    in.kut[e] = q1.x;
+    in.kdt[e] = q1.y;
+    in.kmeta[e] = rec[K_META - 1];
+  } else {
+    in.kf[e] = V.kin[K_KF][row];
+    in.kct[e] = V.kin[K_CT][row];
+    in.kut[e] = V.kin[K_UT][row];
+    in.kdt[e] = V.kin[K_DT][row];
+    in.kmeta[e] = V.kin[K_META][row];
+  }
+}
+// Child row `row` (a node row when isn, else a member row) into child slot e.
+template <bool REC = false, int KE, int CE>
+__device__ __forceinline__ void load_child_row(const RunView& V, bool isn, uint64_t row, int e, WaveIn<KE, CE>& in) {
+  const uint64_t* const* col = isn ? V.nin : V.min;
+  const uint32_t s = isn ? V.ns : V.ms;
+  in.cpkh[e] = col[C_PKH][row];
+  if (REC || s == kNodeCols - 1) {  // records: the 40-B record as two 16-B pieces and a word (8-B aligned)
+    const uint64_t* rec = col[1] + row * (kNodeCols - 1);
+    const u64x2 q0 = reinterpret_cast<const u64x2*>(rec)[0], q1 = reinterpret_cast<const u64x2*>(rec + 2)[0];
+    in.cpkf[e] = q0.x;
+    in.cid1[e] = q0.y;
+    in.cid2[e] = q1.x;
+    in.ct[e] = q1.y;
+    in.cm[e] = rec[4];
+  } else {
+    in.cpkf[e] = col[C_PKF][row];
+    in.cid1[e] = col[C_ID1][row];
+    in.cid2[e] = col[C_ID2][row];
+    in.ct[e] = col[C_T][row];
+    in.cm[e] = col[C_META][row];
+  }
+}
+template <int KE, int CE>
+__device__ __forceinline__ void zero_key_slot(int e, WaveIn<KE, CE>& in) {
+  in.kh[e] = in.kf[e] = in.kct[e] = in.kut[e] = in.kdt[e] = in.kaux[e] = in.kmeta[e] = 0;
+}
+template <int KE, int CE>
+__device__ __forceinline__ void zero_child_slot(int e, WaveIn<KE, CE>& in) {
+  in.cpkh[e] = in.cpkf[e] = in.cid1[e] = in.cid2[e] = in.ct[e] = in.cm[e] = 0;
+}
+
+// The rows of bucket b (KE key rows and CE child rows per lane) from the runs.
 template <int KE, int CE = 2 * KE>
 __device__ __forceinline__ void load_runs(const WaveArgs& W, const WaveDir& d, const RunMap& qk, const RunMap& qc,
                                           int lane, WaveIn<KE, CE>& in) {
@@ -243,57 +298,17 @@ __device__ __forceinline__ void load_runs(const WaveArgs& W, const WaveDir& d, c
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
     const uint32_t c = lane + 64 * e;
-    in.kh[e] = in.kf[e] = in.kct[e] = in.kut[e] = in.kdt[e] = in.kaux[e] = in.kmeta[e] = 0;
+    zero_key_slot(e, in);
     const uint64_t row = run_row(qk, c);
-    if (c < d.K) {
-      in.kh[e] = V.kin[K_KH][row];
-      // aux (a counter's load-time total) is read only by a counter key no other replica holds:
-      // the fold fetches it then, by the row index kept in its place (wave_bucket, RunView)
-      in.kaux[e] = row;
-      if (V.ks == kKeyCols - 1) {  // (uniform) records: kf ct | ut dt as two 16-B pieces, then meta
-        const uint64_t* rec = V.kin[1] + row * (kKeyCols - 1);
-        const u64x2 q0 = reinterpret_cast<const u64x2*>(rec)[0], q1 = reinterpret_cast<const u64x2*>(rec)[1];
-        in.kf[e] = q0.x;
-        in.kct[e] = q0.y;
-        in.kut[e] = q1.x;
-        in.kdt[e] = q1.y;
-        in.kmeta[e] = rec[K_META - 1];
-      } else {
-        in.kf[e] = V.kin[K_KF][row];
-        in.kct[e] = V.kin[K_CT][row];
-        in.kut[e] = V.kin[K_UT][row];
-        in.kdt[e] = V.kin[K_DT][row];
-        in.kmeta[e] = V.kin[K_META][row];
-      }
-    }
+    if (c < d.K) load_key_row(V, row, e, in);
   }
 #pragma unroll
   for (int e = 0; e < CE; ++e) {
     const uint32_t c = lane + 64 * e;
-    in.cpkh[e] = in.cpkf[e] = in.cid1[e] = in.cid2[e] = in.ct[e] = in.cm[e] = 0;
+    zero_child_slot(e, in);
     if (__ballot(c < C) == 0) continue;  // (uniform) no child in this slot group
     const uint64_t row = run_row(qc, c);
-    if (c < C) {
-      const bool isn = c < d.N;
-      const uint64_t* const* col = isn ? V.nin : V.min;
-      const uint32_t s = isn ? V.ns : V.ms;
-      in.cpkh[e] = col[C_PKH][row];
-      if (s == kNodeCols - 1) {  // records: the 40-B record as two 16-B pieces and a word (8-B aligned)
-        const uint64_t* rec = col[1] + row * (kNodeCols - 1);
-        const u64x2 q0 = reinterpret_cast<const u64x2*>(rec)[0], q1 = reinterpret_cast<const u64x2*>(rec + 2)[0];
-        in.cpkf[e] = q0.x;
-        in.cid1[e] = q0.y;
-        in.cid2[e] = q1.x;
-        in.ct[e] = q1.y;
-        in.cm[e] = rec[4];
-      } else {
-        in.cpkf[e] = col[C_PKF][row];
-        in.cid1[e] = col[C_ID1][row];
-        in.cid2[e] = col[C_ID2][row];
-        in.ct[e] = col[C_T][row];
-        in.cm[e] = col[C_META][row];
-      }
-    }
+    if (c < C) load_child_row(V, c < d.N, row, e, in);
   }
 }
 
@@ -322,6 +337,205 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, 5) bucket_wave_runs_kernel(W
     WaveIn<1> in;
     load_runs<1>(W, d, qk, qc, lane, in);
     wave_bucket<1>(W, lds_all[wv], b, lane, in, []() {});
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The persistent, software-pipelined wave tier (runs of at most 8 per family, C4's shape).
+//
+// bucket_wave_runs_kernel spends most of a bucket waiting: the run-directory pairs, then (after a
+// chain of lane shuffles) the rows, then the fold. Here each wave streams through consecutive
+// buckets and keeps the next ones' memory in flight while it folds the current one:
+//   * bucket b + 2's run-directory pairs are loaded while bucket b folds (one 8-B load per lane:
+//     lanes 0..nr-1 the key runs, lanes 16..16+2nr-1 the node then member runs);
+//   * bucket b + 1's run map comes from those pairs by one DPP row scan (keys in DPP row 0, the
+//     children in row 1), which also yields its row counts and dense bases -- no directory load;
+//   * bucket b + 1's rows are loaded into the input registers as soon as bucket b's inputs are
+//     dead (wave_bucket's `next()`, after its children are staged in LDS).
+// Work: the bucket range is cut into 8 XCD slabs; waves of XCD x claim chunks of kPipeChunk
+// consecutive buckets of slab x from its counter (the next claim is issued when a chunk starts)
+// and then help the other slabs. Results are those of bucket_wave_runs_kernel bucket for bucket.
+#ifndef CDB_PIPE_CHUNK
+#define CDB_PIPE_CHUNK 32
+#endif
+constexpr uint32_t kPipeChunk = CDB_PIPE_CHUNK;
+constexpr uint32_t kPipeDone = 0xFFFFFFFFu;
+
+__device__ __forceinline__ u32x2 pipe_pairs(const RunView& V, uint32_t b, int lane, bool valid) {
+  const uint32_t nr = V.nr;
+  const bool keys = (uint32_t)lane < nr;
+  const bool kids = lane >= 16 && (uint32_t)(lane - 16) < 2 * nr;
+  u32x2 se = {0u, 0u};
+  if (valid && (keys || kids)) {  // the families' directories are one allocation: family f's run r is row f * nr + r
+    const uint32_t j = keys ? (uint32_t)lane : nr + (uint32_t)(lane - 16);
+    se = *reinterpret_cast<const u32x2*>(V.rdir[0] + (uint64_t)j * V.nbp1 + b);
+  }
+  return se;
+}
+
+struct PipeMap {
+  uint32_t incl, off;  // inclusive prefix of the slice lengths in the lane's DPP row; row of slot c = off + c
+};
+__device__ __forceinline__ uint32_t dpp_row_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  return x;
+}
+__device__ __forceinline__ PipeMap pipe_map(const RunView& V, u32x2 se, WaveDir& d) {
+  const uint32_t n = se.y - se.x;
+  PipeMap q;
+  q.incl = dpp_row_scan(n);
+  q.off = se.x - (q.incl - n);
+  const uint32_t ss = dpp_row_scan(se.x);
+  const int nr = (int)V.nr;
+  d.K = (uint32_t)__builtin_amdgcn_readlane((int)q.incl, nr - 1);
+  const uint32_t cn = (uint32_t)__builtin_amdgcn_readlane((int)q.incl, 16 + nr - 1);
+  const uint32_t cc = (uint32_t)__builtin_amdgcn_readlane((int)q.incl, 16 + 2 * nr - 1);
+  d.N = cn;
+  d.M = cc - cn;
+  const uint32_t sk = (uint32_t)__builtin_amdgcn_readlane((int)ss, nr - 1);
+  const uint32_t sn = (uint32_t)__builtin_amdgcn_readlane((int)ss, 16 + nr - 1);
+  const uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)ss, 16 + 2 * nr - 1);
+  d.kb = sk - V.rs_sum[0];
+  d.nb0 = sn - V.rs_sum[1];
+  d.mb0 = sc - sn - V.rs_sum[2];
+  return q;
+}
+// Row of slot c among the L slices held by lanes base .. base + L - 1.
+__device__ __forceinline__ uint32_t pipe_row(const PipeMap& q, int base, uint32_t L, uint32_t c) {
+  uint32_t r = 0, k = 1;
+  while (2 * k <= L) k <<= 1;
+  for (; k; k >>= 1) {
+    const uint32_t v = (uint32_t)__shfl((int)q.incl, base + (int)min(r + k - 1, L - 1), 64);
+    if (r + k <= L && v <= c) r += k;
+  }
+  r = min(r, L - 1);
+  return (uint32_t)__shfl((int)q.off, base + (int)r, 64) + c;
+}
+// (REC: the records layout, known at compile time; else the layout is read from V)
+template <bool REC, int CE>
+__device__ __forceinline__ void pipe_load_child(const RunView& V, const WaveDir& d, const PipeMap& q, int lane, int e,
+                                                WaveIn<1, CE>& in) {
+  const uint32_t c = lane + 64 * e;
+  zero_child_slot(e, in);
+  const uint32_t row = pipe_row(q, 16, 2 * V.nr, c);
+  if (c < d.N + d.M) load_child_row<REC>(V, c < d.N, row, e, in);
+}
+template <bool REC>
+__device__ __forceinline__ void pipe_load(const RunView& V, const WaveDir& d, const PipeMap& q, int lane,
+                                          WaveIn<1, 1>& in) {
+  in.d = d;
+  zero_key_slot(0, in);
+  const uint32_t krow = pipe_row(q, 0, V.nr, (uint32_t)lane);
+  if ((uint32_t)lane < d.K) load_key_row<REC>(V, krow, 0, in);
+  pipe_load_child<REC>(V, d, q, lane, 0, in);
+}
+
+// REC: every family in the records layout (the host checks the strides)
+template <bool REC>
+__global__ void __launch_bounds__(kWavesPerWG * 64, 4) bucket_wave_pipe_kernel(WaveArgs W) {
+  __shared__ WaveLds<1> lds_all[kWavesPerWG];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  WaveLds<1>& L = lds_all[wv];
+  const RunView& V = W.V;
+  const uint32_t x0 = blockIdx.x % kXcds;  // (workgroups are dispatched round-robin over the XCDs)
+  const uint64_t span = W.bhi - W.blo;
+  auto slab_lo = [&](uint32_t x) { return W.blo + (uint32_t)(span * x / kXcds); };
+  auto claim = [&](uint32_t x) {
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(W.pipe_next + x, 1u);
+    return v;  // (lane 0's; read once the chunk is needed)
+  };
+  // the bucket stream (wave-uniform): chunk [sc, se) of slab xs, the next chunk's claim in flight
+  uint32_t xs = x0, sc = 0, se = 0, pend = claim(x0);
+  bool done = false;
+  auto produce = [&]() -> uint32_t {
+    if (done) return kPipeDone;
+    if (sc >= se) {
+      uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)pend, 0);
+      for (;;) {
+        const uint32_t lo = slab_lo(xs), hi = slab_lo(xs + 1);
+        const uint64_t st = (uint64_t)lo + (uint64_t)c * kPipeChunk;
+        if (st < hi) {
+          sc = (uint32_t)st;
+          se = (uint32_t)min((uint64_t)hi, st + kPipeChunk);
+          break;
+        }
+        xs = (xs + 1) % kXcds;  // slab drained: help the next one
+        if (xs == x0) {
+          done = true;
+          return kPipeDone;
+        }
+        c = (uint32_t)__builtin_amdgcn_readlane((int)claim(xs), 0);
+      }
+      pend = claim(xs);
+    }
+    return sc++;
+  };
+
+  uint32_t b = produce();
+  if (b == kPipeDone) return;
+  WaveIn<1, 1> in;
+  PipeMap qc;
+  {
+    WaveDir d;
+    qc = pipe_map(V, pipe_pairs(V, b, lane, true), d);
+    pipe_load<REC>(V, d, qc, lane, in);
+  }
+  uint32_t b1 = produce();
+  u32x2 pr = pipe_pairs(V, b1, lane, b1 != kPipeDone);  // (no bucket: zero pairs, an empty map)
+  while (b != kPipeDone) {
+    const uint32_t b2 = b1 != kPipeDone ? produce() : kPipeDone;
+    const WaveDir d = in.d;
+    const uint32_t C = d.N + d.M;
+    // 65..128 children: a second child slot per lane, loaded now (9 % of C4's buckets)
+    const bool two = C > 64 && C <= WaveLds<1>::CC && d.K <= WaveLds<1>::KC;
+    WaveMid<1> mid;
+    int act;
+    if (!two) {
+      act = wave_phase_a<1, 1>(W, L, b, lane, in, mid);
+    } else {
+      WaveIn<1, 2> in2;
+      in2.d = d;
+      in2.kh[0] = in.kh[0];
+      in2.kf[0] = in.kf[0];
+      in2.kct[0] = in.kct[0];
+      in2.kut[0] = in.kut[0];
+      in2.kdt[0] = in.kdt[0];
+      in2.kaux[0] = in.kaux[0];
+      in2.kmeta[0] = in.kmeta[0];
+      in2.cpkh[0] = in.cpkh[0];
+      in2.cpkf[0] = in.cpkf[0];
+      in2.cid1[0] = in.cid1[0];
+      in2.cid2[0] = in.cid2[0];
+      in2.ct[0] = in.ct[0];
+      in2.cm[0] = in.cm[0];
+      pipe_load_child<REC>(V, d, qc, lane, 1, in2);
+      act = wave_phase_a<1, 2>(W, L, b, lane, in2, mid);
+    }
+    // bucket b's input registers are dead: bucket b + 1's rows into them and b + 2's pairs, in
+    // flight while b's children fold and its outputs are written. (One program point for every
+    // path, and unconditional -- past the last bucket the pairs are zero and the map empty -- so
+    // the loads land in the registers the next iteration reads: no copy that waits for them.)
+    {
+      WaveDir dn;
+      qc = pipe_map(V, pr, dn);
+      pipe_load<REC>(V, dn, qc, lane, in);
+      pr = pipe_pairs(V, b2, lane, b2 != kPipeDone);
+    }
+    if (act == WAVE_PUSH) {
+      wave_push(W, b, lane);
+    } else if (act == WAVE_GO) {
+      if (!two)
+        wave_phase_b<1, 1>(W, L, b, lane, mid);
+      else
+        wave_phase_b<1, 2>(W, L, b, lane, mid);
+    }
+    wave_sync();  // (the next bucket reuses this one's LDS)
+    b = b1;
+    b1 = b2;
   }
 }
 

@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -280,15 +281,28 @@ cdb_status cdb_ctx_create_multi(cdb_ctx** out, int device_count, const int* devi
     for (int j = 0; j < i; ++j) distinct = distinct && devices[i] != devices[j];
   root->node = new Node();
   if (device_count > 1 && distinct) {
-    if ((st = load_rccl(root, root->node)) == CDB_OK) {
+    // RCCL point-to-point between the GPUs. Where RCCL cannot be loaded or its communicators not
+    // created (or CDB_SHARD_TRANSPORT=peer), the rows move by HIP peer copies over the same links
+    // instead (transport 2 in cdb_exchange_stats): the merge is the same either way.
+    const char* tr = std::getenv("CDB_SHARD_TRANSPORT");
+    const bool want_rccl = !(tr && std::strcmp(tr, "peer") == 0);
+    if (want_rccl && load_rccl(root, root->node) == CDB_OK) {
       root->node->comms.assign(device_count, nullptr);
-      st = nccl_check(root, root->node, root->node->init_all(root->node->comms.data(), device_count, devices),
-                      "ncclCommInitAll");
-      root->node->rccl = st == CDB_OK;
+      root->node->rccl = nccl_check(root, root->node, root->node->init_all(root->node->comms.data(), device_count,
+                                                                          devices),
+                                    "ncclCommInitAll") == CDB_OK;
     }
-    if (st != CDB_OK) {
-      cdb_ctx_destroy(root);
-      return st;
+    if (!root->node->rccl) {
+      for (int i = 0; i < device_count; ++i) {  // direct peer access where the links allow it
+        hipSetDevice(devices[i]);
+        for (int j = 0; j < device_count; ++j) {
+          int ok = 0;
+          if (i != j && hipDeviceCanAccessPeer(&ok, devices[i], devices[j]) == hipSuccess && ok)
+            (void)hipDeviceEnablePeerAccess(devices[j], 0);
+        }
+      }
+      (void)hipGetLastError();
+      hipSetDevice(devices[0]);
     }
   }
   *out = root;

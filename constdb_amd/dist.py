@@ -168,7 +168,18 @@ def exchange_runs(fams, plan: Plan, recv_bufs, max_piece_bytes: int = MAX_PIECE_
                     for x, y in _pieces(0, dst.numel(), piece):
                         ops.append(dist.P2POp(dist.irecv, dst[x:y], peer))
     if ops:
-        for w in dist.batch_isend_irecv(ops):
+        works = dist.batch_isend_irecv(ops)
+        # RCCL: the same deadline as the library's exchange (shard.hip: 60 s + 1 ms per MB moved): a
+        # peer that never posts its half ends the step with an error instead of a hang (gloo's
+        # transfers progress inside wait(), under the process group's own timeout)
+        moved = sum(op.tensor.numel() * op.tensor.element_size() for op in ops)
+        deadline = time.monotonic() + 60.0 + moved / 1e9
+        while dist.get_backend() == "nccl" and not all(w.is_completed() for w in works):
+            if time.monotonic() > deadline:
+                raise TimeoutError(f"rank {me}: row exchange not complete after {60.0 + moved / 1e9:.0f} s "
+                                   f"({len(ops)} point-to-point operations, {moved} bytes)")
+            time.sleep(1e-4)
+        for w in works:
             w.wait()
     return len(ops)
 

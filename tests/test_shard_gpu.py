@@ -224,6 +224,61 @@ def test_sharded_vs_oracle(ctx):
         mctx.close()
 
 
+def test_sharded_8_slots_records_vs_oracle(ctx):
+    """The north star's node shape (server.rs:95,128-130 with 8 GPUs): 8 slots, 3 owner bits, one replica
+    per slot, C4's shape at 1M keys in the records layout. Each slot's replica is decoded on the host,
+    uploaded to its slot with its fold position, laid out as one run; cdb_merge_sharded splits every run
+    into 8 owner slices, moves 56 of them between slots and merges each shard; the concatenated result's
+    canonical dump equals the oracle's sequential fold of the 8 snapshots."""
+    from constdb_amd.runs import to_records
+    R = N = 8
+    cfg = configs.c4(cdb, 1_000_000)
+    snaps = [cdb.gen_snapshot(cfg, r) for r in range(R)]
+    batches = [cdb.decode_snapshot(s) for s in snaps]
+    rc, want, ost = cdb_oracle.fold(snaps)
+    assert rc == 0
+    mctx = cdb.Context(devices=[0] * N)
+    try:
+        ins = []
+        for i in range(N):
+            c = mctx.shard(i)
+            d = cdb.DevInput()
+            arr = (ctypes.c_void_p * 1)(batches[i].handle)
+            c.check(cdb.lib().cdb_upload_batches(c.handle, arr, 1, ctypes.byref(d)))
+            for name, nc in KCOLS:
+                rows = getattr(d, name)
+                if rows.n:
+                    wrap(rows.col[nc - 1], rows.n).add_(i << 48)
+            to_records(cdb, c, d)
+            assert d.keys.stride == 6 and d.nodes.stride == 5
+            d.n_pos = R
+            sort_into_runs(d, R)
+            ins.append(d)
+        outs, sts, xs = cdb.merge_sharded(mctx, ins)
+        assert xs.n_devices == N and xs.transport == 2
+        assert all(s.sorted_runs == 1 for s in sts)
+        assert sum(s.type_conflicts for s in sts) == ost.type_conflicts
+        moved = [[xs.link_bytes[i][j] for j in range(N)] for i in range(N)]
+        assert all(moved[i][j] > 0 for i in range(N) for j in range(N) if i != j)  # every pair exchanged rows
+        got = _concat(outs)
+        for i in range(N):
+            _release(mctx.shard(i), ins[i])
+        _owner_ok(got[0], N)
+        keep = [t.contiguous() for t in got]
+        dout = cdb.DevOutput()
+        for f, (name, nc) in enumerate(OCOLS):
+            r = cdb.DevRows()
+            for c in range(nc):
+                r.col[c] = keep[f][c].data_ptr()
+            r.n = keep[f].shape[1]
+            setattr(dout, name, r)
+        dout.compact = 1
+        m = cdb.merged_from_device(ctx, dout, batches)
+        assert m.canonical_dump() == want
+    finally:
+        mctx.close()
+
+
 @pytest.mark.parametrize("slots", [1, 2])
 def test_sharded_output_passed_back_is_rejected(ctx, slots):
     """A previous call's outputs live in the library's workspace, which the next call may regrow:
