@@ -238,6 +238,11 @@ ABI_FUNCTIONS = (
 _lib = None
 
 
+def _take(addr: int, n: int) -> bytes:
+    """n bytes at addr as a bytes object (ctypes.string_at takes a C int size: at most 2 GiB)."""
+    return bytes((ctypes.c_char * n).from_address(addr)) if n else b""
+
+
 def lib_path() -> str:
     return _LIB_PATH
 
@@ -535,7 +540,7 @@ def _encode_header(node_id, alias, addr, last_uuid, replicas, keep, rep=None):
 
 def _take_bytes(out, n):
     try:
-        return ctypes.string_at(out.value, n.value)
+        return _take(out.value, n.value)
     finally:
         lib().cdb_free(out)
 
@@ -652,7 +657,7 @@ class Merged:
         self._ctx.check(lib().cdb_merged_canonical_dump(self._ctx.handle, self._h, ctypes.byref(out),
                                                         ctypes.byref(n)))
         try:
-            return ctypes.string_at(out.value, n.value) if n.value else b""
+            return _take(out.value, n.value) if n.value else b""
         finally:
             lib().cdb_free(out)
 
@@ -820,7 +825,7 @@ def gen_ops(cfg: GenConfig, n_ops: int, uuid_he_sent: int = 0, zipf_milli: int =
     if st != OK:
         _raise(st)
     try:
-        return ctypes.string_at(out.value, n.value)
+        return _take(out.value, n.value)
     finally:
         lib().cdb_free(out)
 
@@ -832,6 +837,6 @@ def gen_snapshot(cfg: GenConfig, replica: int) -> bytes:
     if st != OK:
         _raise(st)
     try:
-        return ctypes.string_at(out.value, n.value)
+        return _take(out.value, n.value)
     finally:
         lib().cdb_free(out)

@@ -1249,7 +1249,18 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     const uint32_t gt = (uint32_t)std::min<uint64_t>((nr_b + 64 * kWavesPerWG - 1) / (64 * kWavesPerWG), 1024);
     WA.wide_next = d_wide + p;  // (P <= 64: the counters were zeroed before the fork)
     WA.pipe_next = d_wide + 64 + kXcds * p;
-    if (wave_pipe) {
+    static const bool wide_first = std::getenv("CDB_WIDE_FIRST") != nullptr;  // A/B hook
+    if (wave_pipe && wide_first) {
+      bucket_wide_runs_kernel<<<gt, kWavesPerWG * 64, 0, s>>>(WA);
+      CDB_TRY(launch_check(ctx, s, "bucket_wide_runs_kernel"));
+      const uint32_t g = (uint32_t)std::min<uint64_t>(pipe_grid, (nr_b + kPipeChunk - 1) / kPipeChunk * kXcds);
+      const bool rec = RV.ks == kKeyCols - 1 && RV.ns == kNodeCols - 1 && RV.ms == kMemberCols - 1;
+      if (rec)
+        bucket_wave_pipe_kernel<true><<<std::max<uint32_t>(g, 1), kWavesPerWG * 64, 0, s>>>(WA);
+      else
+        bucket_wave_pipe_kernel<false><<<std::max<uint32_t>(g, 1), kWavesPerWG * 64, 0, s>>>(WA);
+      CDB_TRY(launch_check(ctx, s, "bucket_wave_pipe_kernel"));
+    } else if (wave_pipe) {
       const uint32_t g = (uint32_t)std::min<uint64_t>(pipe_grid, (nr_b + kPipeChunk - 1) / kPipeChunk * kXcds);
       const bool rec = RV.ks == kKeyCols - 1 && RV.ns == kNodeCols - 1 && RV.ms == kMemberCols - 1;
       if (rec)

@@ -60,7 +60,7 @@ def fold(snaps, flags=0, gc_watermark=0):
                      ctypes.byref(st))
     dump = b""
     if rc == 0:
-        dump = ctypes.string_at(out.value, out_len.value) if out_len.value else b""
+        dump = bytes((ctypes.c_char * out_len.value).from_address(out.value)) if out_len.value else b""  # (> 2 GiB too)
         L.cdbo_free(out)
     return rc, dump, st
 
