@@ -715,19 +715,31 @@ class GpuDecode {
   std::vector<HostEntry> hosted_;
   DevBuf d_raw_, d_meta_, d_crc_, d_rows_, d_ord_;
   uint64_t raw_front_ = 0;  // the deferred index uploaded the bytes to d_raw_ + raw_front_
-  bool early_up_ = false;   // the index pass queued that upload (from the caller's buffer)
+  bool early_up_ = false;   // the index pass queued that upload (from the caller's buffer, or chunked)
+ public:
+  hipStream_t up_s_ = nullptr;  // (several snapshots) this snapshot's own stream: the chunked upload
+ private:
+  // A snapshot over 512 MB: copied into the batch's huge pages in chunks, each chunk page-locked
+  // and uploaded on up_s_ as soon as it is copied, so PCIe works while the host copies. False:
+  // nothing queued (the call then takes the batch-copy path).
+  bool chunked_upload(const uint8_t* buf, size_t len);
   bool emit_pending_ = false;  // emit_launch -> emit_finish
-  struct HostReg {  // the batch's bytes, page-locked for a direct upload (unlocked after every sync)
+  struct HostReg {  // page-locked ranges of the snapshot's bytes (unlocked at the end of the call)
     void* p = nullptr;
-    hipStream_t s = nullptr;  // the stream an upload from p was queued on
-    ~HostReg() {
-      if (!p) return;
-      // an upload may still read p when the call ends early (an index pass failed after it was
-      // queued): wait for it before the pages are unlocked
+    std::vector<void*> more;   // the chunks of a chunked upload
+    hipStream_t s = nullptr;   // the stream an upload from them was queued on
+    void release() {
+      if (!p && more.empty()) return;
+      // an upload may still read them when the call ends early (an index pass failed after it
+      // was queued): wait for it before the pages are unlocked
       if (s) (void)hipStreamSynchronize(s);
-      (void)hipHostUnregister(p);
+      if (p) (void)hipHostUnregister(p);
+      for (void* q : more) (void)hipHostUnregister(q);
       (void)hipGetLastError();
+      p = nullptr;
+      more.clear();
     }
+    ~HostReg() { release(); }
   } reg_;
   uint64_t raw_pad_ = 0;  // d_raw_ + raw_pad_ = byte 0 of the snapshot
  public:
@@ -789,7 +801,12 @@ int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTimi
     if (st_ != CDB_OK) return st_;
     early_up_ = true;
   }
-  rc_ = index_snapshot(buf, len, flags_, out_, &idx_, err_off, &dcrc_, index_threads_, &defer_, &cursor_);
+  const bool chunked = !early_up_ && !staged && buf && len > (size_t(512) << 20) && up_s_ &&
+                       hipSetDevice(ctx_->device) == hipSuccess && chunked_upload(buf, len);
+  if (st_ != CDB_OK) return st_;
+  // (chunked: the bytes are in the batch already)
+  rc_ = index_snapshot(chunked ? nullptr : buf, len, flags_, out_, &idx_, err_off, &dcrc_, index_threads_, &defer_,
+                       &cursor_);
   if (rc_ == kIndexDeferred) rc_ = CDB_OK;  // the DATAS section is indexed in prepare_device
   // otherwise a deferred section's snapshot goes up whole right after: page-lock the batch's bytes
   // here, on this thread (the index passes of several snapshots run side by side, and so do the
@@ -801,6 +818,44 @@ int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTimi
   }
   if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return rc_;
+}
+
+bool GpuDecode::chunked_upload(const uint8_t* buf, size_t len) {
+  Batch* b = out_;
+  b->raw.resize(len);  // default-initialised
+  advise_huge(b->raw.data(), len);
+  const uint64_t front = crc_tile_bytes();
+  if ((st_ = alloc(&d_raw_.p, front + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK)
+    return false;
+  uint8_t* const raw = b->raw.data();
+  uint8_t* const dst = (uint8_t*)d_raw_.p + front;
+  // chunk boundaries at 64 MB-aligned addresses: no two page-locked ranges share a page
+  constexpr uintptr_t kChunk = uintptr_t(64) << 20;
+  const uintptr_t base = (uintptr_t)raw;
+  reg_.s = up_s_;
+  bool ok = true;
+  for (size_t a = 0; a < len;) {
+    const size_t e = std::min<size_t>(len, ((base + a + kChunk) & ~(kChunk - 1)) - base);
+    std::memcpy(raw + a, buf + a, e - a);
+    if (ok && host_register(raw + a, e - a)) {
+      reg_.more.push_back(raw + a);
+      ok = hipMemcpyAsync(dst + a, raw + a, e - a, hipMemcpyHostToDevice, up_s_) == hipSuccess;
+      if (!ok) (void)hipGetLastError();
+    } else {
+      ok = false;  // (the rest is only copied)
+    }
+    a = e;
+  }
+  if (!ok) {  // a chunk could not be locked or queued: nothing of it is used
+    reg_.release();
+    (void)hipFree(d_raw_.p);
+    d_raw_.p = nullptr;
+    return true;  // (the bytes are in the batch)
+  }
+  raw_front_ = front;
+  ck(hipEventRecord(di_.up.a, up_s_), "event(index)");
+  early_up_ = st_ == CDB_OK;
+  return true;
 }
 
 int GpuDecode::dd_launch(hipStream_t ks) {
@@ -998,6 +1053,7 @@ int GpuDecode::dd_done(int dv, uint64_t end, size_t* err_off) {
   } else if (dv > 0) {
     if (d.offs.p) (void)hipFree(d.offs.p);
     d.offs.p = nullptr;  // the host index pass over the whole stream: its statuses and offsets
+    if (up_s_) (void)hipStreamSynchronize(up_s_);  // (a chunked upload may still write d_raw_)
     if (d_raw_.p) (void)hipFree(d_raw_.p);
     d_raw_.p = nullptr;
     raw_front_ = 0;
@@ -1037,6 +1093,7 @@ int GpuDecode::prepare_launch(size_t* err_off, uint8_t* pin, uint64_t pin_room) 
   if (n == 0) return rc_;
   if (hipSetDevice(ctx_->device) != hipSuccess) return CDB_DEVICE_ERROR;
   hipStream_t s = s_ = ctx_->stream;
+  if (early_up_) ck(hipStreamWaitEvent(s, di_.up.a, 0), "wait(decode)");  // (an upload on another stream)
   // the raw stream sits after `pad` zero bytes, so the checksummed prefix ends on a CRC tile
   const uint64_t tile = crc_tile_bytes();
   const uint64_t pad = dcrc_.pending ? (tile - dcrc_.len % tile) % tile : 0;
@@ -1675,11 +1732,21 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
   // 16 at once); their statuses are then taken in snapshot order, as one pass after another would
   std::vector<int> irc(n, CDB_OK);
   std::vector<size_t> ieo(n, 0);
+  // every snapshot's own stream (kept in the context): its chunked upload, then its walks
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, CDB_DEVICE_ERROR, "hipSetDevice");
+  if (ctx->idx_streams.size() < n) ctx->idx_streams.resize(n, nullptr);
+  for (uint32_t i = 0; i < n; ++i)
+    if (!ctx->idx_streams[i]) {
+      const cdb_status st = hip_check(ctx, hipStreamCreateWithFlags(&ctx->idx_streams[i], hipStreamNonBlocking),
+                                      "stream(index)");
+      if (st != CDB_OK) return st;
+    }
   for (uint32_t i = 0; i < n; ++i) {
     dec.emplace_back(new GpuDecode(ctx, outs[i], flags));
     // several snapshots are indexed side by side: a few split their DATAS sections over their
     // share of the threads; 8 snapshots measured faster unsplit (271 vs 311 ms in all)
     dec.back()->index_threads_ = n <= 4 ? std::max(1u, host_index_threads() / std::max(1u, n)) : 1u;
+    dec.back()->up_s_ = ctx->idx_streams[i];
   }
   {
     const uint32_t nt = std::min<uint32_t>(n, 16);

@@ -783,7 +783,8 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   HA.hk_tp = (uint32_t*)(HA.hk_sum + nk);
   HA.hk_cnt = HA.hk_tp + nk;
   HA.hk_cb = HA.hk_cnt + nk;
-  uint8_t* ct = (uint8_t*)ws_get(ctx, WS_HOTCH, nc * (32 + 2 * 8 + 2 * 4 + 6 * 4) + 64, &st);
+  // (+ 40 B per child: the global fold's per-run stash, fold_rec / fold_hg)
+  uint8_t* ct = (uint8_t*)ws_get(ctx, WS_HOTCH, nc * (32 + 2 * 8 + 2 * 4 + 6 * 4 + 40) + 64, &st);
   if (!ct) return st;
   HA.rec = (ulonglong2*)ct;  // (the workspace is 256-B aligned)
   ct += nc * 32;
@@ -797,6 +798,8 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   uint32_t* rank_n = HA.emit_m + nc;
   uint32_t* rank_m = rank_n + nc;
   uint32_t* run_list = rank_m + nc;
+  HA.fold_rec = (ulonglong2*)(((uintptr_t)(run_list + nc) + 15) & ~(uintptr_t)15);
+  HA.fold_hg = (uint2*)(HA.fold_rec + 2 * nc);
   HA.rank_n = rank_n;
   HA.rank_m = rank_m;
   HA.w = w;

@@ -64,6 +64,11 @@ struct HotArgs {
   uint32_t* fold_q;          // per run: the row of the run (k from its start) that is the output
                              // (members: the winner; nodes: the head), kNone: selection path
   uint64_t* fold_v;          // per run: a counter node's folded value
+  // the global sort's fold, per run folded by pass 0 (fold_q != kNone): its output row's fields
+  // (fold_rec[2 i] = (id1, id2 | a node's value), [2 i + 1] = (t, meta)) and (c_h of its rows, key
+  // G) in fold_hg[i], so that pass 1 writes it without re-reading the run's rows (null: re-read)
+  ulonglong2* fold_rec;
+  uint2* fold_hg;
   // runs mode (sorted-run input, buckets of at most MatArgs::runs_child_max children): the
   // tag pass reads the children from the runs' columns (the absolute run row), not from copies
   int runs;
@@ -413,7 +418,7 @@ struct HotAcc {
 template <class JAt>
 __device__ __forceinline__ void hot_fold_run(const BucketArgs& A, const HotArgs& H, int pass, bool act, bool isn,
                                              uint32_t b, uint32_t G, uint32_t nrows, JAt jat, uint64_t obase,
-                                             bool emitted, uint32_t* fq, uint64_t* fv, HotAcc& acc,
+                                             bool emitted, uint32_t* fq, uint64_t* fv, ulonglong2* fs, HotAcc& acc,
                                              unsigned long long& gcm, unsigned long long& nslow) {
   auto put = [&](uint64_t id1, uint64_t id2, uint64_t t, uint64_t meta, uint64_t v) {
     const uint32_t o = (uint32_t)(obase + acc.nout);
@@ -485,7 +490,18 @@ __device__ __forceinline__ void hot_fold_run(const BucketArgs& A, const HotArgs&
       hd.j = 0;
       emit_id(hd, v, tw, wm);
       *fq = isn ? 0u : qw;
-      *fv = v;
+      if (fs) {  // the output row's fields (nodes: the head row, the folded value; members: the winner)
+        uint64_t i2 = xi2[0], i1 = xi1[0];
+#pragma unroll
+        for (uint32_t k = 1; k < kFoldFast; ++k) {
+          i1 = (k == qw) ? xi1[k] : i1;
+          i2 = (k == qw) ? xi2[k] : i2;
+        }
+        fs[0] = make_ulonglong2(isn ? xi1[0] : i1, isn ? v : i2);
+        fs[1] = make_ulonglong2(isn ? xt[0] : tw, isn ? xm[0] : wm);
+      } else {
+        *fv = v;
+      }
       slow = false;
     } else if (act) {
       *fq = kNone;
@@ -494,7 +510,10 @@ __device__ __forceinline__ void hot_fold_run(const BucketArgs& A, const HotArgs&
     const uint32_t q = *fq;
     if (q != kNone) {
       slow = false;
-      if (emitted) {
+      if (emitted && fs) {
+        const ulonglong2 a = fs[0], c = fs[1];
+        put(a.x, a.y, c.x, c.y, a.y);
+      } else if (emitted) {
         const HotChild x = hot_child(H, jat(q));
         put(x.id1, x.id2, x.t, x.meta, *fv);
       }
@@ -560,23 +579,33 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < nruns; base += stride) {  // wave-uniform
     const uint64_t i = base + threadIdx.x;
     const bool act = i < nruns;
-    const uint64_t p = act ? H.run_list[i] : 0;
-    const uint64_t W = H.w[p];
-    uint32_t nrows = 0;
-    if (act) {
+    // pass 1: a run pass 0 folded (fold_q != kNone) is written from the stash alone; the others
+    // (the selection path) find their rows again
+    const bool kept = act && pass == 1 && H.fold_q[i] != kNone;
+    const bool rows = act && !kept;
+    const uint64_t p = rows ? H.run_list[i] : 0;
+    uint64_t W = 0;
+    uint32_t nrows = 0, hc = 0, G = 0;
+    if (rows) {
+      W = H.w[p];
       uint64_t e = p + 1;
       while (e < H.n_children && (H.w[e] >> 6) == (W >> 6) && hot_takes_part(H.w[e])) ++e;
       nrows = (uint32_t)(e - p);
+      hc = H.c_h[H.v[p]];
+      G = (uint32_t)(W >> H.g_shift);
+    } else if (kept) {
+      const uint2 hg = H.fold_hg[i];
+      hc = hg.x;
+      G = hg.y;
     }
-    uint32_t hc = 0, h = 0, b = 0, G = 0;
+    uint32_t h = 0, b = 0;
     bool isn = false;
     uint64_t obase = 0;
     if (act) {
-      hc = H.c_h[H.v[p]];
       h = hc & 0x7FFFFFFFu;
       isn = (hc >> 31) == 0;
       b = H.ids[h];
-      G = (uint32_t)(W >> H.g_shift);
+      if (pass == 0) H.fold_hg[i] = make_uint2(hc, G);
       if (pass == 1) {
         const uint32_t f = H.first_run[h];
         obase = isn ? H.rank_n[i] - H.rank_n[f] : H.rank_m[i] - H.rank_m[f];
@@ -585,7 +614,7 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
     const bool emitted = act && pass == 1 && (isn ? H.emit_n : H.emit_m)[i] != 0;
     HotAcc acc;
     hot_fold_run(A, H, pass, act, isn, b, G, nrows, [&](uint32_t k) { return H.v[p + k]; }, obase, emitted,
-                 &H.fold_q[i], &H.fold_v[i], acc, gcm, nslow);
+                 &H.fold_q[i], &H.fold_v[i], H.fold_rec + 2 * i, acc, gcm, nslow);
     if (pass == 0 && act) {
       H.emit_n[i] = isn ? acc.nout : 0;
       H.emit_m[i] = isn ? 0 : acc.nout;
@@ -923,7 +952,7 @@ __global__ void __launch_bounds__(C::Threads) hot_sortfold_kernel(BucketArgs A, 
     const bool isn = act && sx[q] < N;
     HotAcc acc;
     hot_fold_run(A, H, 0, act, isn, b, g0 + (e >> 16), nrows, [&](uint32_t k) { return c0 + sx[q + k]; }, 0,
-                 false, fq + r, fv + r, acc, gcm, nslow);
+                 false, fq + r, fv + r, nullptr, acc, gcm, nslow);
     if (act) no[r] = (uint16_t)acc.nout;
   }
   __syncthreads();
@@ -951,7 +980,7 @@ __global__ void __launch_bounds__(C::Threads) hot_sortfold_kernel(BucketArgs A, 
     const uint32_t off = act ? ro[r] : 0;
     HotAcc acc;
     hot_fold_run(A, H, 1, act, isn, b, g0 + gr, nrows, [&](uint32_t k) { return c0 + sx[q + k]; },
-                 isn ? (off & 0xFFFF) : (off >> 16), act && no[r] != 0, fq + r, fv + r, acc, gcm, nslow);
+                 isn ? (off & 0xFFFF) : (off >> 16), act && no[r] != 0, fq + r, fv + r, nullptr, acc, gcm, nslow);
     if (act && acc.k_cnt) {
       atomicAdd(&L.kcnt[gr], acc.k_cnt);
       atomicMin(&L.kcb[gr], acc.k_cb);

@@ -2,7 +2,7 @@
 # One parameterised GPU recipe (replaces the per-experiment gpu_r3*/gpu_r4* scripts).
 # Every step is optional and bounded by its own timeout; the first failure ends the call.
 #   TAG      name prefix of every output under gpurun_out/
-#   TESTS    pytest arguments (e.g. "tests/test_runs_oracle_gpu.py -k c4")
+#   TESTS    pytest arguments (e.g. "tests/test_runs_oracle_gpu.py"); KEXPR: a -k expression
 #   BENCHES  ";"-separated "name|ENV=v ENV2=w|bench.py arguments"
 #   PROF     "name|ENV=v|bench.py arguments": rocprofv3 --kernel-trace --stats of that command
 #   PMC      ";"-separated "name|ENV=v|bench.py arguments|COUNTERS": one rocprofv3 --pmc pass per
@@ -15,7 +15,7 @@ O=gpurun_out
 mkdir -p $O
 T=${TAG:-exp}
 if [ -n "$TESTS" ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest -x -q --timeout ${TEST_CASE_TIMEOUT:-300} --timeout-method thread $TESTS > $O/pytest_$T.log 2>&1
+  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest -x -q --timeout ${TEST_CASE_TIMEOUT:-300} --timeout-method thread $TESTS ${KEXPR:+-k "$KEXPR"} > $O/pytest_$T.log 2>&1
   rc=$?
   tail -3 $O/pytest_$T.log
   [ $rc -eq 0 ] || { echo "pytest failed rc=$rc"; grep -E "^(FAILED|ERROR)|Error|assert" $O/pytest_$T.log | head -20; exit 1; }
