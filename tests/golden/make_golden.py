@@ -8,8 +8,10 @@ Each case is a directory holding snap_<i>.bin (the snapshots in fold order, writ
 server.rs:183-215), merged.txt (the oracle's canonical dump of the fold, after DB::gc when the case
 has a watermark) and case.json (watermark, the fold's type-conflict and Dict-merge counts, and where
 the case comes from). Cases: every merge KAT of tests/test_oracle_kat.py (each cites
-the reference lines it is derived from), the bin/test.rs:85-106 MEET scenario, and two 2000-key
-random replica sets from the seeded generator (one with DB::gc).
+the reference lines it is derived from), the bin/test.rs:85-116 MEET scenarios (k1-k4, and k5 over
+three replicas), and two 2000-key random replica sets from the seeded generator (one with DB::gc).
+case.json's "pinning" says which cases the reference's own assertions pin (REFERENCE_ASSERTED), which
+restate a cited rule, and which are oracle-only regression fixtures.
 """
 import json
 import os
@@ -108,6 +110,13 @@ def kat_cases():
                            snap({b"k1": counter({1: (1, 1 * t)}), b"k2": counter({2: (2, 3 * t)}),
                                  b"k3": counter({1: (1, 8 * t), 2: (1, 9 * t)}), b"k4": counter({2: (4, 7 * t)})},
                                 node_id=2)], None),
+        # bin/test.rs:110-116: r3, r1 and r2 each INCR k5 once (after r3 MEETs r2, every node's
+        # increment reaches the others); GET k5 == 3 on every replica. As snapshots: each replica
+        # holds its own node's increment, and the merged counter sums to 3
+        "meet_k5_three_replicas": ("bin/test.rs:110-116",
+                                   [snap({b"k5": counter({3: (1, 20 * t)})}, node_id=3),
+                                    snap({b"k5": counter({1: (1, 21 * t)})}, node_id=1),
+                                    snap({b"k5": counter({2: (1, 22 * t)})}, node_id=2)], None),
         "canonical_sorted": ("canonical dump order", [snap({b"b": bytes_(1, b"\x00"),
                                                              b"a": set_({b"z": 1, b"y": 2}, {b"q": 3})},
                                                             deletes={b"d": 4}, expires={b"e": 5})], None),
@@ -124,6 +133,24 @@ def random_cases():
     wm = (configs.T0_MS + (1 << 30)) << 22
     return {"random_2k": ("seeded generator, 2000 keys x 3 replicas", snaps, None),
             "random_2k_gc": ("the same with DB::gc after every time", snaps, wm)}
+
+
+# What pins each case to the reference (case.json "pinning"): the values the reference's own test
+# asserts (bin/test.rs GET results, checked in the frozen dump by tests/test_golden.py), a merge rule
+# restated from the cited lines (the expected dump is the oracle's), or nothing but the oracle
+# (a regression fixture: its parity with the reference is unpinned).
+REFERENCE_ASSERTED = {
+    "meet_bin_test": {"k1": 1, "k2": 2, "k3": 2, "k4": 4},  # bin/test.rs:97-98, 104, 108-109
+    "meet_k5_three_replicas": {"k5": 3},                    # bin/test.rs:116
+}
+
+
+def pinning(name, src):
+    if name in REFERENCE_ASSERTED:
+        return {"kind": "reference-asserted", "counter_sums": REFERENCE_ASSERTED[name]}
+    if name.startswith("random_"):
+        return {"kind": "oracle-only regression fixture (parity unpinned)"}
+    return {"kind": "rule restated from " + src}
 
 
 def fold(snaps, wm):
@@ -148,7 +175,8 @@ def main():
             f.write(o.canonical_dump(db))
         with open(os.path.join(d, "case.json"), "w") as f:
             json.dump({"source": src, "snapshots": len(snaps), "gc_watermark": wm,
-                       "type_conflicts": db.type_conflicts, "dict_merges": db.dict_merges}, f, indent=1)
+                       "type_conflicts": db.type_conflicts, "dict_merges": db.dict_merges,
+                       "pinning": pinning(name, src)}, f, indent=1)
             f.write("\n")
     print(f"{len(cases)} cases written under {HERE}")
 

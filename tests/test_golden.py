@@ -1,7 +1,10 @@
 """The frozen golden fixtures (tests/golden/, written by tests/golden/make_golden.py from the Python
 oracle): both oracles and the GPU path must reproduce every frozen merge result byte for byte, so a
 regression in any of them -- including the oracles the other parity tests compare against -- fails
-here. Cases: the §8a-T merge KATs, the bin/test.rs:85-106 MEET scenario, 2000-key random sets."""
+here. Cases: the §8a-T merge KATs, the bin/test.rs:85-116 MEET scenarios, 2000-key random sets. What pins
+each case to the reference is declared in its case.json ("pinning"): the values bin/test.rs asserts
+(checked below in the frozen dumps), a rule restated from cited lines, or only the oracle (the random
+sets: regression fixtures whose parity with the reference is unpinned)."""
 import ctypes
 import json
 import os
@@ -23,9 +26,35 @@ def load(name):
     return snaps, want, meta
 
 
+def _counter_sums(dump):
+    """Counter sums by key in a canonical dump: a key line `K <hex key> ...` followed by ` S <sum>`."""
+    sums, key = {}, None
+    for line in dump.split(b"\n"):
+        if line.startswith(b"K "):
+            key = bytes.fromhex(line.split()[1].decode()).decode()
+        elif line.startswith(b" S ") and key is not None:
+            sums[key] = int(line.split()[1])
+    return sums
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_pinning_declared_and_reference_assertions_hold(name):
+    """Every case says what pins it (case.json "pinning"). The reference-asserted ones (the bin/test.rs
+    MEET scenarios: GET k1..k5 after the merges) hold those values in the frozen dump; the KATs restate
+    a cited rule; the random sets are oracle-only regression fixtures (parity unpinned)."""
+    snaps, want, meta = load(name)
+    kind = meta["pinning"]["kind"]
+    assert kind == "reference-asserted" or kind.startswith("rule restated from ") or "oracle-only" in kind
+    if kind == "reference-asserted":
+        sums = _counter_sums(want)
+        for k, v in meta["pinning"]["counter_sums"].items():
+            assert sums[k] == v, (k, sums.get(k), v)
+
+
 def test_fixture_set_complete():
     assert len(CASES) >= 17
-    for c in ("meet_bin_test", "gc_lifo", "random_2k", "counter_order_a", "set_ties_remote_dels"):
+    for c in ("meet_bin_test", "meet_k5_three_replicas", "gc_lifo", "random_2k", "counter_order_a",
+              "set_ties_remote_dels"):
         assert c in CASES
 
 
