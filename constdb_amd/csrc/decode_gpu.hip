@@ -17,6 +17,9 @@
 //   Entries whose children exceed the per-thread dedup limits (a key with thousands of
 //   members) are decoded on the host by decode.cpp's own functions into their reserved slots.
 #include <hip/hip_runtime.h>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 
 #include <algorithm>
 #include <atomic>
@@ -642,6 +645,14 @@ class GpuDecode {
                          uint32_t pos, bool run);
   cdb_status emit_finish(DecodeTiming* tm);
   bool emit_pending() const { return emit_pending_; }
+  // (several snapshots, records layout) the rows emitted into rows of the snapshot's own, right
+  // after its preparation and sort, while later snapshots still cross PCIe (emit_own queues the
+  // emit; emit_finish follows a later synchronisation); once every snapshot is counted, move_rows
+  // copies them into the caller's columns at the snapshot's offsets (device copies on the context's
+  // stream)
+  cdb_status emit_own(uint32_t pos);
+  bool emitted_own() const { return own_; }
+  cdb_status move_rows(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb);
   // key-hash order (after prepare_device): queues the key-hash pass and the sections' order check
   // on the context's stream; the verdict reads after a synchronisation (read_order).
   cdb_status order_check();
@@ -724,6 +735,11 @@ class GpuDecode {
   // nothing queued (the call then takes the batch-copy path).
   bool chunked_upload(const uint8_t* buf, size_t len);
   bool emit_pending_ = false;  // emit_launch -> emit_finish
+  bool own_ = false;           // emit_own: the rows are in own_rows_ (records: hash column + records)
+  DevBuf own_rows_;
+  uint64_t* own_k_[kKeyCols] = {};
+  uint64_t* own_n_[kNodeCols] = {};
+  uint64_t* own_m_[kMemberCols] = {};
   struct HostReg {  // page-locked ranges of the snapshot's bytes (unlocked at the end of the call)
     void* p = nullptr;
     std::vector<void*> more;   // the chunks of a chunked upload
@@ -836,7 +852,7 @@ bool GpuDecode::chunked_upload(const uint8_t* buf, size_t len) {
   bool ok = true;
   for (size_t a = 0; a < len;) {
     const size_t e = std::min<size_t>(len, ((base + a + kChunk) & ~(kChunk - 1)) - base);
-    std::memcpy(raw + a, buf + a, e - a);
+    parallel_copy(raw + a, buf + a, e - a);
     if (ok && host_register(raw + a, e - a)) {
       reg_.more.push_back(raw + a);
       ok = hipMemcpyAsync(dst + a, raw + a, e - a, hipMemcpyHostToDevice, up_s_) == hipSuccess;
@@ -1043,8 +1059,8 @@ int GpuDecode::dd_host(size_t* err_off) {
 int GpuDecode::dd_done(int dv, uint64_t end, size_t* err_off) {
   DevIndex& d = di_;
   d.active = false;
-  if (d.work.p) (void)hipFree(d.work.p);
-  d.work.p = nullptr;
+  // (the walk's scratch is freed with this object, at the end of the call: a hipFree waits for the
+  // device, and while later snapshots upload and walk that wait stalls every thread's HIP calls)
   if (dv == 0) {  // the section's offsets on the device, the side sections' on the host after them
     idx_.offset.clear();
     idx_.kind.clear();
@@ -1194,9 +1210,7 @@ int GpuDecode::prepare_finish(size_t* err_off) {
     rc_ = CDB_INVALID_SNAPSHOT_CHECKSUM;
     *err_off = dcrc_.err_off;
   }
-  if (di_.offs.p) (void)hipFree(di_.offs.p);
-  di_.offs.p = nullptr;
-  if (!small[3]) {  // every entry's children were counted on the device
+  if (!small[3]) {  // every entry's children were counted on the device (offs: freed with the object)
     nn_ = small[1];
     nm_ = small[2];
     return rc_;
@@ -1634,6 +1648,42 @@ cdb_status GpuDecode::emit_launch(uint64_t* const* k, uint64_t* const* nd, uint6
   return CDB_OK;
 }
 
+cdb_status GpuDecode::emit_own(uint32_t pos) {
+  const uint64_t n = n_, nn = nn_, nm = nm_;
+  auto words = [](uint64_t rows, int nc) { return ((rows + 2 + 1) & ~1ull) + (((rows * (nc - 1)) + 2 + 1) & ~1ull); };
+  const uint64_t w = words(n, kKeyCols) + words(nn, kNodeCols) + words(nm, kMemberCols);
+  if ((st_ = alloc(&own_rows_.p, w * 8 + 64, "decode: the snapshot's own device rows")) != CDB_OK) return st_;
+  uint64_t* q = (uint64_t*)(((uintptr_t)own_rows_.p + 15) & ~(uintptr_t)15);
+  auto lay = [&](uint64_t** col, uint64_t rows, int nc) {  // the records layout of cdb_dev_rows
+    col[0] = q;
+    q += (rows + 2 + 1) & ~1ull;
+    for (int c = 1; c < nc; ++c) col[c] = q + (c - 1);
+    q += ((rows * (nc - 1)) + 2 + 1) & ~1ull;
+  };
+  lay(own_k_, n, kKeyCols);
+  lay(own_n_, nn, kNodeCols);
+  lay(own_m_, nm, kMemberCols);
+  // (the snapshot alone decides its row order: a run if it is one; the merge takes the rows of
+  // every snapshot in any order when not all of them are runs)
+  if (emit_launch(own_k_, own_n_, own_m_, kKeyCols - 1, kNodeCols - 1, pos, sorted_ || read_order()) != CDB_OK)
+    return st_;
+  own_ = st_ == CDB_OK;  // (emit_finish after the caller's next synchronisation of the stream)
+  return st_;
+}
+
+cdb_status GpuDecode::move_rows(uint64_t* const* k, uint64_t* const* nd, uint64_t* const* mb) {
+  const hipStream_t s = s_ ? s_ : ctx_->stream;
+  auto mv = [&](uint64_t* const* dst, uint64_t* const* src, uint64_t rows, int nc) {
+    if (!rows) return;
+    ck(hipMemcpyAsync(dst[0], src[0], rows * 8, hipMemcpyDeviceToDevice, s), "d2d(decode rows)");
+    ck(hipMemcpyAsync(dst[1], src[1], rows * (nc - 1) * 8, hipMemcpyDeviceToDevice, s), "d2d(decode rows)");
+  };
+  mv(k, own_k_, n_, kKeyCols);
+  mv(nd, own_n_, nn_, kNodeCols);
+  mv(mb, own_m_, nm_, kMemberCols);
+  return st_;
+}
+
 cdb_status GpuDecode::emit_finish(DecodeTiming* tm) {
   emit_pending_ = false;
   if (st_ != CDB_OK) return st_;
@@ -1748,42 +1798,150 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     dec.back()->index_threads_ = n <= 4 ? std::max(1u, host_index_threads() / std::max(1u, n)) : 1u;
     dec.back()->up_s_ = ctx->idx_streams[i];
   }
+  // the deferred DATAS sections: every snapshot's bytes go up with its speculative walk queued
+  // behind them on its own stream; the stitch rounds then run per snapshot (below, or on the
+  // after-walk thread)
+  std::vector<hipStream_t> ks(n, nullptr);
+  std::vector<uint32_t> live;
+  // launch(i): snapshot i's walk, after its index pass. True: its stitch rounds remain (dd_step)
+  auto launch = [&](uint32_t i) {
+    if ((irc[i] != CDB_OK && irc[i] != CDB_INVALID_SNAPSHOT_CHECKSUM) || !dec[i]->deferred()) return false;
+    ks[i] = ctx->idx_streams[i];
+    if (dec[i]->dd_launch(ks[i]) < 0) {
+      (void)dec[i]->dd_step(&ieo[i]);
+      irc[i] = dec[i]->status();
+      return false;
+    }
+    return true;
+  };
+  // Snapshots over 512 MB, one after another: copied into their batches by every host thread and
+  // uploaded chunk by chunk on their own streams (GpuDecode::chunked_upload), indexed, and their
+  // walks launched at once, so the walk of snapshot i runs while snapshot i + 1 crosses PCIe (side
+  // by side, every upload ended near the last one and the walks queued behind them). What follows
+  // a walk -- the stitch rounds, the host pass resumed after the section, the device preparation
+  // (counts, checksum), the order check and the key-hash sort -- runs for such a snapshot on the
+  // after-walk thread, in snapshot order, while later snapshots still cross PCIe; it alone uses the
+  // context's stream until it is joined. The other snapshots are indexed side by side, one thread
+  // each, and take the steps below.
+  static const bool staged = std::getenv("CDB_H2D_STAGED") != nullptr;
+  std::vector<char> seq(n, 0);
+  std::vector<int> prc(n, CDB_OK), erc(n, CDB_OK);
+  std::vector<size_t> peo(n, 0);
   {
-    const uint32_t nt = std::min<uint32_t>(n, 16);
+    // two stages, each a thread taking snapshots in order from its queue: the walk stage (stitch
+    // rounds on the snapshot's stream, the host pass resumed after the section) hands each snapshot
+    // to the device stage (preparation, order check, sort, emit on the context's stream), so one
+    // snapshot's host pass overlaps the previous one's device work
+    struct Queue {
+      std::mutex mu;
+      std::condition_variable cv;
+      std::deque<uint32_t> q;
+      bool closed = false;
+      void push(uint32_t i) {
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          q.push_back(i);
+        }
+        cv.notify_one();
+      }
+      void close() {
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          closed = true;
+        }
+        cv.notify_one();
+      }
+      bool pop(uint32_t* i) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return closed || !q.empty(); });
+        if (q.empty()) return false;
+        *i = q.front();
+        q.pop_front();
+        return true;
+      }
+    } walked, launched_q;
+    // the host pass resumed after a walked section runs on a thread of its own per snapshot (they
+    // take 15-20 ms each on C4's snapshots: in line they held back the next snapshot's stitch)
+    std::vector<std::thread> resume(n);
+    auto walk_stage = [&]() {
+      (void)hipSetDevice(ctx->device);
+      for (uint32_t i; launched_q.pop(&i);) {
+        GpuDecode& d = *dec[i];
+        if (d.deferred()) {
+          int r;
+          while ((r = d.dd_step(&ieo[i])) == 1) {
+          }
+          if (r == 2) {
+            resume[i] = std::thread([&, i] {
+              (void)hipSetDevice(ctx->device);
+              dec[i]->dd_host(&ieo[i]);
+              irc[i] = dec[i]->status();
+            });
+          } else {
+            irc[i] = d.status();
+          }
+        }
+        walked.push(i);
+      }
+      walked.close();
+    };
+    auto device_stage = [&]() {
+      (void)hipSetDevice(ctx->device);
+      for (uint32_t i; walked.pop(&i);) {
+        if (resume[i].joinable()) resume[i].join();
+        GpuDecode& d = *dec[i];
+        peo[i] = ieo[i];
+        int rc = irc[i];
+        if (rc == CDB_OK || rc == CDB_INVALID_SNAPSHOT_CHECKSUM) rc = d.prepare_launch(&peo[i]);
+        // the order check is queued behind the preparation: one synchronisation reads both
+        const bool ordered = d.prepare_pending() && n <= CDB_MAX_RUNS && d.order_check() == CDB_OK;
+        if (d.prepare_pending()) {
+          if (hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync(decode)") != CDB_OK) rc = CDB_DEVICE_ERROR;
+          else rc = d.prepare_finish(&peo[i]);
+        }
+        prc[i] = rc;
+        if ((rc != CDB_OK && rc != CDB_INVALID_SNAPSHOT_CHECKSUM) || !ordered)
+          continue;  // (the order and the sort are taken again below, where an error is reported)
+        if (!d.read_order() && !(flags & CDB_DECODE_STREAM_ORDER) && d.sort_to_run() != CDB_OK) continue;
+        // the emit is queued, not waited for: its finish runs after the call's last synchronisation
+        if (flags & CDB_DECODE_ROWS_RECORDS) erc[i] = d.emit_own(i);
+      }
+    };
+    std::thread walk_th(walk_stage), device_th(device_stage);
+    for (uint32_t i = 0; i < n; ++i) {
+      if (staged || lens[i] <= (size_t(512) << 20)) continue;
+      irc[i] = dec[i]->index(bufs[i], lens[i], &ieo[i], nullptr);
+      launch(i);
+      seq[i] = 1;
+      launched_q.push(i);
+    }
+    std::vector<uint32_t> par;
+    for (uint32_t i = 0; i < n; ++i)
+      if (!seq[i]) par.push_back(i);
+    const uint32_t nt = std::min<uint32_t>((uint32_t)par.size(), 16);
     std::atomic<uint32_t> next{0};
     auto work = [&]() {
-      for (uint32_t i; (i = next.fetch_add(1)) < n;) irc[i] = dec[i]->index(bufs[i], lens[i], &ieo[i], nullptr);
+      for (uint32_t j; (j = next.fetch_add(1)) < par.size();) {
+        const uint32_t i = par[j];
+        irc[i] = dec[i]->index(bufs[i], lens[i], &ieo[i], nullptr);
+      }
     };
     std::vector<std::thread> th;
     for (uint32_t t = 1; t < nt; ++t) th.emplace_back(work);
-    work();
+    if (nt) work();
     for (auto& t : th) t.join();
+    launched_q.close();
+    walk_th.join();
+    device_th.join();
   }
   if (tm) tm->index_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
   // CDB_DECODE_TRACE=<file>: one JSON line of phase times (host clock, ms) appended per call
   PhaseClock clk(t_start);
   clk.mark("index");
   {
-    // the deferred DATAS sections, side by side: every snapshot's bytes go up (one after another
-    // through the staging ring) with its speculative walk queued behind them on its own stream,
-    // then the stitch rounds of all of them interleave, so one snapshot's walks run while the next
-    // one's bytes cross PCIe
-    std::vector<hipStream_t> ks(n, nullptr);
-    std::vector<uint32_t> live;
     cdb_status st = CDB_OK;
-    for (uint32_t i = 0; i < n && st == CDB_OK; ++i) {
-      if ((irc[i] != CDB_OK && irc[i] != CDB_INVALID_SNAPSHOT_CHECKSUM) || !dec[i]->deferred()) continue;
-      if (ctx->idx_streams.size() <= i) ctx->idx_streams.resize(i + 1, nullptr);
-      if (!ctx->idx_streams[i])
-        st = hip_check(ctx, hipStreamCreateWithFlags(&ctx->idx_streams[i], hipStreamNonBlocking), "stream(index)");
-      ks[i] = ctx->idx_streams[i];
-      if (st == CDB_OK && dec[i]->dd_launch(ks[i]) < 0) {
-        (void)dec[i]->dd_step(&ieo[i]);
-        irc[i] = dec[i]->status();
-        continue;
-      }
-      live.push_back(i);
-    }
+    for (uint32_t i = 0; i < n; ++i)
+      if (!seq[i] && launch(i)) live.push_back(i);
     std::vector<uint32_t> host;  // sections whose host part (the pass resumed after them) remains
     while (!live.empty()) {
       std::vector<uint32_t> next;
@@ -1820,12 +1978,13 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
   }
   // every snapshot's device preparation queued, one synchronisation, then the halves that read
   // back; statuses are taken in snapshot order (a launch failure stops the launches after it)
-  std::vector<int> prc(n, CDB_OK);
-  std::vector<size_t> peo(ieo);
+  for (uint32_t i = 0; i < n; ++i)
+    if (!seq[i]) peo[i] = ieo[i];
   bool any_pending = false;
   // the side sections' offsets and kinds go up from one page-locked region (kept in the context)
   std::vector<uint64_t> pin_at(n + 1, 0);
-  for (uint32_t i = 0; i < n; ++i) pin_at[i + 1] = pin_at[i] + ((dec[i]->side_bytes() + 63) & ~uint64_t(63));
+  for (uint32_t i = 0; i < n; ++i)
+    pin_at[i + 1] = pin_at[i] + (seq[i] ? 0 : ((dec[i]->side_bytes() + 63) & ~uint64_t(63)));
   if (pin_at[n] > ctx->dec_pin_bytes) {
     if (ctx->dec_pin) (void)hipHostFree(ctx->dec_pin);
     ctx->dec_pin = nullptr;
@@ -1835,6 +1994,10 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     else ctx->dec_pin = nullptr;  // (the staging ring then)
   }
   for (uint32_t i = 0; i < n; ++i) {
+    if (seq[i]) {  // (prepared on the after-walk thread)
+      if (prc[i] != CDB_OK && prc[i] != CDB_INVALID_SNAPSHOT_CHECKSUM) break;
+      continue;
+    }
     int rc = irc[i];
     uint8_t* pin = ctx->dec_pin ? (uint8_t*)ctx->dec_pin + pin_at[i] : nullptr;
     if (rc == CDB_OK || rc == CDB_INVALID_SNAPSHOT_CHECKSUM)
@@ -1869,11 +2032,12 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
   cdb_status st;
   // one run per snapshot when every snapshot is in key-hash order (written from a merge result)
   bool runs = n <= CDB_MAX_RUNS;
-  for (uint32_t i = 0; i < n && runs; ++i)
-    if ((st = dec[i]->order_check()) != CDB_OK) return st;
+  for (uint32_t i = 0; i < n && runs; ++i)  // (a snapshot the after-walk thread sorted is checked again)
+    if ((!seq[i] || !dec[i]->sorted()) && (st = dec[i]->order_check()) != CDB_OK) return st;
   if (runs) {
     if ((st = hip_check(ctx, hipStreamSynchronize(ctx->stream), "sync(decode order)")) != CDB_OK) return st;
     for (uint32_t i = 0; i < n && runs; ++i) {
+      if (seq[i] && dec[i]->sorted()) continue;
       if (dec[i]->read_order()) continue;
       // the reference's HashMap order: sorted into a run unless the caller keeps stream order
       if (!(flags & CDB_DECODE_STREAM_ORDER) && (st = dec[i]->sort_to_run()) != CDB_OK) return st;
@@ -1907,8 +2071,12 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     for (int c = 0; c < kMemberCols; ++c) mb[c] = din->members.col[c] + o[2] * (c ? cs : 1);
     if (runs)
       for (int f = 0; f < 3; ++f) din->run_start[f][i] = o[f];
-    // (every snapshot's emit queued, one synchronisation, then the halves that read back)
-    if ((st = dec[i]->emit_launch(k, nd, mb, (uint32_t)ks, (uint32_t)cs, i, runs)) != CDB_OK) {
+    // (every snapshot's emit queued, one synchronisation, then the halves that read back; a snapshot
+    // the after-walk thread emitted into rows of its own is copied into place)
+    if (erc[i] != CDB_OK || (dec[i]->emitted_own() ? (st = dec[i]->move_rows(k, nd, mb))
+                                                   : (st = dec[i]->emit_launch(k, nd, mb, (uint32_t)ks,
+                                                                               (uint32_t)cs, i, runs))) != CDB_OK) {
+      if (erc[i] != CDB_OK) st = (cdb_status)erc[i];
       (void)hipStreamSynchronize(ctx->stream);
       cdb_dev_rows_release(ctx, &din->keys);
       cdb_dev_rows_release(ctx, &din->nodes);
