@@ -44,6 +44,21 @@ constexpr int kWavesPerWG = 4;
 #endif
 constexpr uint64_t kM44 = (1ull << 44) - 1, kM42 = (1ull << 42) - 1;
 
+// Output rows are written once and not read again by this kernel: streaming (non-temporal)
+// stores keep them from displacing the input lines neighbouring buckets still read from L2.
+#ifndef CDB_NT_OUT
+#define CDB_NT_OUT 1
+#endif
+typedef unsigned long long u64x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_row16(ulonglong2* p, unsigned long long x, unsigned long long y) {
+  if (CDB_NT_OUT) {
+    u64x2v v = {x, y};
+    __builtin_nontemporal_store(v, reinterpret_cast<u64x2v*>(p));
+  } else {
+    *p = make_ulonglong2(x, y);
+  }
+}
+
 
 // Per-wave LDS. KE = key rows per lane (1 or 2); child rows per lane CE = 2 KE.
 template <int KE>
@@ -139,6 +154,7 @@ struct RunView {
   uint32_t ks, ns, ms;        // record strides of the families (1: plain columns; common.h row_field)
   uint32_t rs_sum[3];         // per family, the sum of the runs' first rows (mod 2^32): a bucket's
                               // dense base is the sum of its slices' first rows minus this
+  const uint32_t* bdir;       // at most 8 runs: the bucket-major directory (run_reduce3_kernel), else null
 };
 
 struct WaveArgs {
@@ -708,9 +724,9 @@ __device__ __forceinline__ void wave_phase_b(const WaveArgs& W, WaveLds<KE>& L, 
       const uint64_t id2 = knode[e] ? c_v[e] : sid2[e];
       {  // one whole 48-B AoS row
         ulonglong2* row = (ulonglong2*)((knode[e] ? A.nos : A.mos) + ((knode[e] ? xn : xm) + crank) * kChildStride);
-        row[0] = make_ulonglong2(L.okh[k], L.okf[k]);
-        row[1] = make_ulonglong2(sid1[e], id2);
-        row[2] = make_ulonglong2(c_t[e], c_m[e]);
+        st_row16(row + 0, L.okh[k], L.okf[k]);
+        st_row16(row + 1, sid1[e], id2);
+        st_row16(row + 2, c_t[e], c_m[e]);
       }
       if (knode[e] && (L.ovm[k] & kVmaskMerged))
         atomicAdd((unsigned long long*)&L.osum[k], (unsigned long long)c_v[e]);
@@ -732,10 +748,10 @@ __device__ __forceinline__ void wave_phase_b(const WaveArgs& W, WaveLds<KE>& L, 
       const uint64_t cref = cref_pack(L.ocnt[r] ? L.ocb[r] : 0, L.ocnt[r]);
       {  // one whole 64-B AoS row
         ulonglong2* row = (ulonglong2*)(A.kos + (xk + r) * kKeyOutCols);
-        row[0] = make_ulonglong2(kh[e], kf[e]);
-        row[1] = make_ulonglong2(o_ct[e], o_ut[e]);
-        row[2] = make_ulonglong2(o_dt[e], o_meta[e]);
-        row[3] = make_ulonglong2(win, cref);
+        st_row16(row + 0, kh[e], kf[e]);
+        st_row16(row + 1, o_ct[e], o_ut[e]);
+        st_row16(row + 2, o_dt[e], o_meta[e]);
+        st_row16(row + 3, win, cref);
       }
     }
   }

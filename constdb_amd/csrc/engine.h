@@ -67,6 +67,7 @@ enum WsSlot {
   WS_CRCTAB, WS_CRCPART,                                // decode: CRC tables, per-tile CRC partials
   WS_WIDE,                                              // wide tier: group counters per range
   WS_STATE,                                             // cdb_dev_state_rows: zero bases, error word
+  WS_RUNBDIR,                                           // sorted-run path: bucket-major run directory
   WS_COUNT
 };
 static_assert(WS_COUNT <= 48, "cdb_ctx::ws has 48 slots");

@@ -651,12 +651,34 @@ cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, const InLayout&
   CDB_HIP(hipStreamSynchronize(s), "sync");
   if (ctx->runs_err) return CDB_OK;  // a run is not ordered (or the gap list overflowed)
   for (int f = 0; f < 3; ++f) {
-    const uint64_t blocks = std::min<uint64_t>((nb + 255) / 256, 8192);
     uint64_t rs_sum = 0;
     for (uint32_t r = 0; r < nr; ++r) rs_sum += ctx->runs_host[f * (kMaxRuns + 1) + r];
     V->rs_sum[f] = (uint32_t)rs_sum;
-    run_reduce_kernel<<<(uint32_t)blocks, 256, 0, s>>>(V->rdir[f], nr, nb, rs_sum, dirs[f].base, dirs[f].hist);
-    CDB_TRY(launch_check(ctx, s, "run_reduce_kernel"));
+  }
+  V->bdir = nullptr;
+  if (nr <= 8 && pipe_wave_enabled()) {
+    // the persistent wave tier's bucket-major directory, built with the three bucket directories
+    uint32_t* bdir = (uint32_t*)ws_get(ctx, WS_RUNBDIR, row * kBdirRow * sizeof(uint32_t), &st);
+    if (!bdir) return st;
+    Reduce3Args a;
+    a.rdir = rdir;
+    a.nr = nr;
+    a.nb = nb;
+    for (int f = 0; f < 3; ++f) {
+      a.rs_sum[f] = V->rs_sum[f];
+      a.base[f] = dirs[f].base;
+      a.cnt[f] = dirs[f].hist;
+    }
+    a.bdir = bdir;
+    run_reduce3_kernel<<<(uint32_t)std::min<uint64_t>((row + 255) / 256, 8192), 256, 0, s>>>(a);
+    CDB_TRY(launch_check(ctx, s, "run_reduce3_kernel"));
+    V->bdir = bdir;
+  } else {
+    for (int f = 0; f < 3; ++f) {
+      const uint64_t blocks = std::min<uint64_t>((nb + 255) / 256, 8192);
+      run_reduce_kernel<<<(uint32_t)blocks, 256, 0, s>>>(V->rdir[f], nr, nb, V->rs_sum[f], dirs[f].base, dirs[f].hist);
+      CDB_TRY(launch_check(ctx, s, "run_reduce_kernel"));
+    }
   }
   V->rbase = d_rbase;
   V->nr = nr;
@@ -1179,7 +1201,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   if (!d_wide) return st;
   CDB_HIP(hipMemsetAsync(d_wide, 0, (64 + 64 * kXcds) * sizeof(uint32_t), s), "memset wide");
   // the persistent wave tier (runs of at most 8 per family): one resident grid
-  const bool wave_pipe = use_runs && RV.nr <= 8 && pipe_wave_enabled();
+  const bool wave_pipe = use_runs && RV.bdir != nullptr;
   const uint32_t pipe_grid = wave_pipe ? pipe_wave_grid(ctx) : 0;
   CDB_HIP(hipEventRecord(ctx->ev_fork, s), "event");  // inputs of both bucket tiers are ready
   // The wave and wide tiers run over P consecutive bucket ranges. Range p is scanned and compacted

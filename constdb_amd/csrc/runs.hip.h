@@ -170,6 +170,52 @@ __global__ void __launch_bounds__(256) run_reduce_kernel(const uint32_t* __restr
   }
 }
 
+// At most 8 runs per family: the three families' bucket directories in one pass, plus the
+// bucket-major copy of the run directories that the persistent wave tier reads -- row b of bdir is
+// 32 u32 (one 128-B line): key run r at slot r, node run r at 16 + r, member run r at 24 + r, the
+// other slots 0. A wave streaming through consecutive buckets then reads one line per bucket
+// instead of 3 nr lines of the run-major directories, lines that L2 no longer holds by the time
+// the same wave reaches the neighbouring bucket (PMC: 68 GB fetched per C4 launch, not 28).
+constexpr int kBdirRow = 32;
+struct Reduce3Args {
+  const uint32_t* rdir;  // the three families' run-major directories, one allocation
+  uint32_t nr;
+  uint64_t nb;
+  uint32_t rs_sum[3];
+  uint32_t* base[3];
+  uint32_t* cnt[3];
+  uint32_t* bdir;        // (nb + 1) x kBdirRow
+};
+__global__ void __launch_bounds__(256) run_reduce3_kernel(Reduce3Args a) {
+  const uint64_t row = a.nb + 1, per_fam = (uint64_t)a.nr * row;
+  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b <= a.nb; b += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t v[kBdirRow];
+#pragma unroll
+    for (int j = 0; j < kBdirRow; ++j) v[j] = 0;
+#pragma unroll
+    for (int f = 0; f < 3; ++f) {
+      uint32_t s0 = 0, s1 = 0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        if ((uint32_t)r < a.nr) {
+          const uint32_t* d = a.rdir + f * per_fam + (uint64_t)r * row + b;
+          const uint32_t x = d[0];
+          v[f == 0 ? r : 8 + 8 * f + r] = x;
+          s0 += x;
+          if (b < a.nb) s1 += d[1];
+        }
+      }
+      if (b < a.nb) {
+        a.base[f][b] = s0 - a.rs_sum[f];
+        a.cnt[f][b] = s1 - s0;
+      }
+    }
+    uint4* o = reinterpret_cast<uint4*>(a.bdir + b * kBdirRow);
+#pragma unroll
+    for (int q = 0; q < kBdirRow / 4; ++q) o[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  }
+}
+
 // A bucket's slices of the runs, one per lane: lane j < L holds slice j of the family group --
 // keys: the nr key runs; children: the nr node runs, then the nr member runs (child slots are
 // node rows first, then member rows). incl = inclusive prefix of the slice lengths over lanes;
@@ -346,8 +392,9 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, 5) bucket_wave_runs_kernel(W
 // bucket_wave_runs_kernel spends most of a bucket waiting: the run-directory pairs, then (after a
 // chain of lane shuffles) the rows, then the fold. Here each wave streams through consecutive
 // buckets and keeps the next ones' memory in flight while it folds the current one:
-//   * bucket b + 2's run-directory pairs are loaded while bucket b folds (one 8-B load per lane:
-//     lanes 0..nr-1 the key runs, lanes 16..16+2nr-1 the node then member runs);
+//   * bucket b + 2's run-directory pairs are loaded while bucket b folds (rows b + 2 and b + 3 of
+//     the bucket-major directory bdir, one 256-B load: lanes 0..7 the key runs, 16..23 the node
+//     runs, 24..31 the member runs);
 //   * bucket b + 1's run map comes from those pairs by one DPP row scan (keys in DPP row 0, the
 //     children in row 1), which also yields its row counts and dense bases -- no directory load;
 //   * bucket b + 1's rows are loaded into the input registers as soon as bucket b's inputs are
@@ -361,15 +408,14 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, 5) bucket_wave_runs_kernel(W
 constexpr uint32_t kPipeChunk = CDB_PIPE_CHUNK;
 constexpr uint32_t kPipeDone = 0xFFFFFFFFu;
 
+// Bucket b's slices from its bdir row (lanes 0..31) and bucket b + 1's (lanes 32..63): one
+// 256-B load, then lane j < 32 holds slice j's (first row, end row).
 __device__ __forceinline__ u32x2 pipe_pairs(const RunView& V, uint32_t b, int lane, bool valid) {
-  const uint32_t nr = V.nr;
-  const bool keys = (uint32_t)lane < nr;
-  const bool kids = lane >= 16 && (uint32_t)(lane - 16) < 2 * nr;
-  u32x2 se = {0u, 0u};
-  if (valid && (keys || kids)) {  // the families' directories are one allocation: family f's run r is row f * nr + r
-    const uint32_t j = keys ? (uint32_t)lane : nr + (uint32_t)(lane - 16);
-    se = *reinterpret_cast<const u32x2*>(V.rdir[0] + (uint64_t)j * V.nbp1 + b);
-  }
+  uint32_t v = 0;
+  if (valid) v = V.bdir[(uint64_t)b * kBdirRow + (uint32_t)lane];
+  const uint32_t e = (uint32_t)__shfl((int)v, (lane + 32) & 63, 64);
+  u32x2 se = {v, e};
+  if (lane >= 32) se = {0u, 0u};
   return se;
 }
 
@@ -389,15 +435,15 @@ __device__ __forceinline__ PipeMap pipe_map(const RunView& V, u32x2 se, WaveDir&
   q.incl = dpp_row_scan(n);
   q.off = se.x - (q.incl - n);
   const uint32_t ss = dpp_row_scan(se.x);
-  const int nr = (int)V.nr;
-  d.K = (uint32_t)__builtin_amdgcn_readlane((int)q.incl, nr - 1);
-  const uint32_t cn = (uint32_t)__builtin_amdgcn_readlane((int)q.incl, 16 + nr - 1);
-  const uint32_t cc = (uint32_t)__builtin_amdgcn_readlane((int)q.incl, 16 + 2 * nr - 1);
+  // (bdir slots: key runs 0..7, node runs 16..23, member runs 24..31; unused slots are empty)
+  d.K = (uint32_t)__builtin_amdgcn_readlane((int)q.incl, 7);
+  const uint32_t cn = (uint32_t)__builtin_amdgcn_readlane((int)q.incl, 23);
+  const uint32_t cc = (uint32_t)__builtin_amdgcn_readlane((int)q.incl, 31);
   d.N = cn;
   d.M = cc - cn;
-  const uint32_t sk = (uint32_t)__builtin_amdgcn_readlane((int)ss, nr - 1);
-  const uint32_t sn = (uint32_t)__builtin_amdgcn_readlane((int)ss, 16 + nr - 1);
-  const uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)ss, 16 + 2 * nr - 1);
+  const uint32_t sk = (uint32_t)__builtin_amdgcn_readlane((int)ss, 7);
+  const uint32_t sn = (uint32_t)__builtin_amdgcn_readlane((int)ss, 23);
+  const uint32_t sc = (uint32_t)__builtin_amdgcn_readlane((int)ss, 31);
   d.kb = sk - V.rs_sum[0];
   d.nb0 = sn - V.rs_sum[1];
   d.mb0 = sc - sn - V.rs_sum[2];
@@ -420,7 +466,7 @@ __device__ __forceinline__ void pipe_load_child(const RunView& V, const WaveDir&
                                                 WaveIn<1, CE>& in) {
   const uint32_t c = lane + 64 * e;
   zero_child_slot(e, in);
-  const uint32_t row = pipe_row(q, 16, 2 * V.nr, c);
+  const uint32_t row = pipe_row(q, 16, 16, c);
   if (c < d.N + d.M) load_child_row<REC>(V, c < d.N, row, e, in);
 }
 template <bool REC>
@@ -428,7 +474,7 @@ __device__ __forceinline__ void pipe_load(const RunView& V, const WaveDir& d, co
                                           WaveIn<1, 1>& in) {
   in.d = d;
   zero_key_slot(0, in);
-  const uint32_t krow = pipe_row(q, 0, V.nr, (uint32_t)lane);
+  const uint32_t krow = pipe_row(q, 0, 8, (uint32_t)lane);
   if ((uint32_t)lane < d.K) load_key_row<REC>(V, krow, 0, in);
   pipe_load_child<REC>(V, d, q, lane, 0, in);
 }

@@ -18,12 +18,12 @@ cat $O/bench_${C}_$T.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_${C}_$T -o run -- python bench.py --config $C --steps 5 --warmup 2 --no-cpu-baseline --no-general > $O/prof_${C}_$T.log 2>&1 || { echo "prof failed"; exit 3; }
 if [ -z "$NO_PMC" ]; then
   for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -s KILL 200 rocprofv3 --pmc $c --kernel-include-regex "$KRE" --output-format csv -d $O/pmc_${C}_${T}_$c -o run -- python bench.py --config $C --steps 1 --warmup 0 --no-cpu-baseline --no-general > $O/pmc_${C}_${T}_$c.log 2>&1 || { echo "pmc $c failed"; exit 4; }
+    timeout -s KILL 200 rocprofv3 --pmc $c --kernel-include-regex "$KRE" --output-format csv -d $O/pmc_${C}_${T}_$c -o run -- python bench.py --config $C --steps 1 --warmup 0 --no-cpu-baseline --no-general --no-decode-leg > $O/pmc_${C}_${T}_$c.log 2>&1 || { echo "pmc $c failed"; exit 4; }
   done
   python3 scripts/pmc_traffic.py $O/pmc_${C}_${T}_FETCH_SIZE $O/pmc_${C}_${T}_WRITE_SIZE $O/pmc_traffic_${C}_$T.json || exit 5
   if [ -n "$GENERAL_PMC" ]; then
     for c in FETCH_SIZE WRITE_SIZE; do
-      timeout -s KILL 200 rocprofv3 --pmc $c --kernel-include-regex "$KRE" --output-format csv -d $O/pmcg_${C}_${T}_$c -o run -- python bench.py --config $C --steps 1 --warmup 0 --no-cpu-baseline --input-order hash-random > $O/pmcg_${C}_${T}_$c.log 2>&1 || { echo "pmc general $c failed"; exit 6; }
+      timeout -s KILL 200 rocprofv3 --pmc $c --kernel-include-regex "$KRE" --output-format csv -d $O/pmcg_${C}_${T}_$c -o run -- python bench.py --config $C --steps 1 --warmup 0 --no-cpu-baseline --no-decode-leg --input-order hash-random > $O/pmcg_${C}_${T}_$c.log 2>&1 || { echo "pmc general $c failed"; exit 6; }
     done
     python3 scripts/pmc_traffic.py $O/pmcg_${C}_${T}_FETCH_SIZE $O/pmcg_${C}_${T}_WRITE_SIZE $O/pmc_traffic_${C}_general_$T.json || exit 7
   fi
