@@ -281,11 +281,20 @@ def run_single(cdb, args):
                    "traffic_over_alg": gtr["total"] / gB if gtr else None,
                    "traffic_source": gtr["source"] if gtr else None}
     if args.input_order == "sorted":
-        from constdb_amd.runs import sort_into_runs
-        sort_into_runs(din)
-        info["workload"] += ("; input: one key-hash-ordered run per replica (a merge result kept as position 0, "
-                             "or a snapshot this engine encoded, decoded by cdb_decode_snapshots_device): "
-                             "the sorted-run path")
+        from constdb_amd.runs import sort_into_runs, state_runs
+        if args.config in ("c1", "c4", "c5") and args.layout == "records":
+            # each replica's rows as this engine keeps a replica state: merged alone, read back as
+            # position-0 rows, moved to the replica's position (setup, untimed)
+            log("replica states: each replica merged alone and kept as state rows")
+            state_runs(cdb, ctx, din)
+            info["workload"] += ("; input: one key-hash-ordered run per replica, each the replica's own merge "
+                                 "result kept in HBM as state rows (cdb_dev_state_rows, cdb_dev_input_append): "
+                                 "the sorted-run path")
+        else:
+            sort_into_runs(din)
+            info["workload"] += ("; input: one key-hash-ordered run per replica (a merge result kept as position 0, "
+                                 "or a snapshot this engine encoded, decoded by cdb_decode_snapshots_device): "
+                                 "the sorted-run path")
     else:
         info["workload"] += "; input: rows in generator order, random in key hash: the partition path"
     ms, per, st = timed_merges(cdb, ctx, din, opts, args, args.steps)
@@ -329,7 +338,8 @@ def run_single(cdb, args):
         "stats": {"type_conflicts": st.type_conflicts, "dict_merges": st.dict_merges,
                   "deletes_gced": st.deletes_gced, "hot_buckets": st.hot_buckets,
                   "wide_buckets": st.wide_buckets, "mid_buckets": st.mid_buckets,
-                  "orphans": st.orphan_children, "hot_slow_runs": st.hot_slow_runs},
+                  "orphans": st.orphan_children, "hot_slow_runs": st.hot_slow_runs,
+                  "hot_merged_children": st.hot_merged_children},
     }
     if tr:
         res["roofline"]["traffic_per_kernel"] = tr["per_kernel"]

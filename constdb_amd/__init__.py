@@ -129,7 +129,8 @@ class MergeStats(ctypes.Structure):
         "type_conflicts", "dict_merges", "deletes_gced", "members_gced", "duplicate_rows", "orphan_children",
         "hot_buckets", "wide_buckets", "mid_buckets")] + [(n, ctypes.c_double) for n in (
         "device_ms", "partition_ms", "bucket_ms", "finish_ms")] + [("sorted_runs", ctypes.c_uint64),
-                                                                  ("hot_slow_runs", ctypes.c_uint64)]
+                                                                  ("hot_slow_runs", ctypes.c_uint64),
+                                                                  ("hot_merged_children", ctypes.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

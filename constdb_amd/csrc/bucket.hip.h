@@ -35,7 +35,7 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 enum Stat {
   ST_TYPE_CONFLICTS = 0, ST_DICT_MERGES, ST_DELETES_GCED, ST_MEMBERS_GCED, ST_DUP_ROWS,
-  ST_ORPHANS, ST_HOT, ST_WIDE, ST_HOT_SLOW, ST_COUNT
+  ST_ORPHANS, ST_HOT, ST_WIDE, ST_HOT_SLOW, ST_HOT_MERGED, ST_COUNT
 };
 // Statistics are counted into kStatShards shards of kStatStride u64 (one 128-B line each):
 // millions of waves adding to ONE word serialise at its memory-side atomic unit.
@@ -158,7 +158,7 @@ struct ChildLess {
     if (a == kNone) return false;
     if (b == kNone) return true;
     if (S.ck[a] != S.ck[b]) return S.ck[a] < S.ck[b];
-    if (S.c1[a] != S.c1[b]) return S.c1[a] < S.c1[b];
+    if (S.c1[a] != S.c1[b]) return child_order(S.c1[a]) < child_order(S.c1[b]);
     if (S.c2[a] != S.c2[b]) return S.c2[a] < S.c2[b];
     return meta_order(S.cm[a]) < meta_order(S.cm[b]);
   }

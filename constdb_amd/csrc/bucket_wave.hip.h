@@ -501,7 +501,7 @@ __device__ __forceinline__ int wave_phase_a(const WaveArgs& W, WaveLds<KE>& L, u
     return WAVE_DONE;
   }
   // ------------------------------------------------------------ 3. children: key lookup
-  // word = key rank << 56 | id hash[41:0] << 14 | pos << 8 | slot   (rank < 128, slot < 256)
+  // word = key rank << 56 | child_order(id1)[63:22] << 14 | pos << 8 | slot   (rank < 128, slot < 256)
   uint32_t orph = 0;
   uint32_t ckey[CE];
   bool clive[CE];
@@ -552,9 +552,9 @@ __device__ __forceinline__ int wave_phase_a(const WaveArgs& W, WaveLds<KE>& L, u
     const bool isn = c < N;
     cw[e] = ~0ull;
     if (clive[e]) {
-      // a node is ranked by its raw id, a member by its hash (ids that share the low 42 bits
-      // are caught below and go to the exact tier)
-      cw[e] = ((uint64_t)ckey[e] << 56) | ((cid1[e] & kM42) << 14) | ((uint64_t)meta_pos(cm[e]) << 8) | c;
+      // ranked by the leading 42 bits of child_order(id1) (ids that share them are caught below
+      // and go to the exact tier)
+      cw[e] = ((uint64_t)ckey[e] << 56) | ((child_order(cid1[e]) >> 22) << 14) | ((uint64_t)meta_pos(cm[e]) << 8) | c;
     }
     const uint64_t Lm = __ballot(clive[e]);
     if (clive[e]) L.sw[nlive + lane_rank(Lm)] = cw[e];

@@ -69,6 +69,20 @@ CDB_HD uint64_t row_field(const uint64_t* const* col, uint32_t s, int c, uint64_
 
 // ---------------------------------------------------------------- hashing
 // splitmix64 finalizer: full-avalanche 64-bit mix.
+// A child's order key inside its key (every merge tier writes a key's children in ascending
+// child_order(id1), then id2): the id's bits reversed, so that the leading bits that the chip-wide
+// tiers sort on are the id's low bits -- distinct for small counter node ids as for member hashes.
+// A merge result's children are then sorted by every prefix of it, which is what lets the chip-wide
+// path merge the runs of such inputs instead of sorting them (hot.hip.h).
+CDB_HD uint64_t child_order(uint64_t id1) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_bitreverse64(id1);
+#else
+  uint64_t r = 0;
+  for (int i = 0; i < 64; ++i) r |= ((id1 >> i) & 1) << (63 - i);
+  return r;
+#endif
+}
 CDB_HD uint64_t mix64(uint64_t x) {
   x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
   x ^= x >> 27; x *= 0x94D049BB133111EBull;

@@ -68,6 +68,7 @@ enum WsSlot {
   WS_WIDE,                                              // wide tier: group counters per range
   WS_STATE,                                             // cdb_dev_state_rows: zero bases, error word
   WS_RUNBDIR,                                           // sorted-run path: bucket-major run directory
+  WS_HOTMERGE,                                          // chip-wide path: list bounds, merge tiles
   WS_COUNT
 };
 static_assert(WS_COUNT <= 48, "cdb_ctx::ws has 48 slots");

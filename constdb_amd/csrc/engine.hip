@@ -734,9 +734,10 @@ namespace {
 // rows in the batch (the key table's index width in the sort tag and the child row indices).
 cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& wide_ids,
                      const std::vector<uint32_t>& hk_off, const std::vector<uint32_t>& c_off, uint64_t tk,
-                     uint64_t tc, uint64_t cmax, uint64_t kmax, const RunView* rv, bool run_order,
+                     uint64_t tc, uint64_t cmax, uint64_t kmax, const RunView* rv, const RunView* orv,
                      hipStream_t s) {
   cdb_status st = CDB_OK;
+  const bool run_order = orv != nullptr;  // sorted-run input (rv: and this batch reads its children from the runs)
   const uint32_t H = (uint32_t)wide_ids.size();
   // device: ids[H] | hk_off[H + 1] | c_off[H + 1] | hk_kout[H] | run count
   uint32_t* meta = (uint32_t*)ws_get(ctx, WS_HOTMETA, (6ull * H + 8) * sizeof(uint32_t), &st);
@@ -860,11 +861,78 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   const uint32_t grid = (uint32_t)std::min<uint64_t>((tc + 255) / 256, 16384);
   if (tc) {
     HA.small_keys = kmax <= kTagKeys ? 1 : 0;
-    hot_tag_kernel<<<(uint32_t)((tc + kTagChunk - 1) / kTagChunk), 256, 0, s>>>(A, HA);
-    CDB_TRY(launch_check(ctx, s, "hot_tag_kernel"));
-    // (per-bucket bitonic sorts in LDS measured slower than this global radix sort: C3 9.98 vs
-    // 8.90 ms, C5 25.9 vs 24.3 ms; profiles/r03/experiments_r3.txt)
-    CDB_TRY(radix_sort_pairs(ctx, &HA.w, &HA.v, w2, v2, tc, lo, HA.g_shift + gbits, s));
+    // Children read from the runs: their lists are merged when they arrive sorted (a merge
+    // result's child order, hot.hip.h), else radix-sorted (test hook CDB_HOT_MERGE=0: always sorted)
+    const char* merge_env = std::getenv("CDB_HOT_MERGE");
+    bool merged = false;
+    if (run_order && orv->nr >= 2 && tc < (1ull << 31) && !(merge_env && merge_env[0] == '0')) {
+      // (a batch of copied rows keeps each bucket's run slices in run order: the same lists)
+      if (!HA.runs) HA.V = *orv;
+      uint32_t L = 2;
+      while (L < 2 * HA.V.nr) L <<= 1;
+      const uint64_t jobs0 = (uint64_t)H * (L / 2);
+      uint8_t* mw = (uint8_t*)ws_get(ctx, WS_HOTMERGE, ((uint64_t)H * (L + 1) + 2 * jobs0) * 4 + 64, &st);
+      if (!mw) return st;
+      uint64_t* d_ntiles = (uint64_t*)mw;
+      uint32_t* d_unsorted = (uint32_t*)(mw + 8);
+      uint32_t* bounds = (uint32_t*)(mw + 64);
+      uint32_t* tcnt = bounds + (uint64_t)H * (L + 1);
+      uint32_t* toff = tcnt + jobs0;
+      CDB_HIP(hipMemsetAsync(d_unsorted, 0, 4, s), "memset");
+      HA.inline_markers = 1;
+      hot_tag_kernel<<<(uint32_t)((tc + kTagChunk - 1) / kTagChunk), 256, 0, s>>>(A, HA);
+      CDB_TRY(launch_check(ctx, s, "hot_tag_kernel"));
+      hot_lists_kernel<<<(H + 255) / 256, 256, 0, s>>>(HA, L, bounds);
+      CDB_TRY(launch_check(ctx, s, "hot_lists_kernel"));
+      uint64_t *wa = w, *wb = w2;
+      uint32_t *va = v, *vb = v2;
+      for (uint32_t span = 1; span < L; span <<= 1) {
+        MergeArgs M;
+        M.bounds = bounds;
+        M.L = L;
+        M.span = span;
+        M.n_jobs = (uint32_t)((uint64_t)H * (L / (2 * span)));
+        M.tiles = toff;
+        M.n_tiles = d_ntiles;
+        M.wi = wa;
+        M.vi = va;
+        M.wo = wb;
+        M.vo = vb;
+        M.unsorted = d_unsorted;
+        M.check = span == 1;
+        MergeArgs Mc = M;
+        Mc.tiles = tcnt;
+        hot_merge_count_kernel<<<(M.n_jobs + 255) / 256, 256, 0, s>>>(Mc);
+        CDB_TRY(launch_check(ctx, s, "hot_merge_count_kernel"));
+        CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, tcnt, M.n_jobs, toff, (uint32_t*)nullptr, d_ntiles, s));
+        const uint64_t tiles_max = tc / kMergeTile + M.n_jobs;
+        hot_merge_kernel<<<(uint32_t)std::min<uint64_t>(tiles_max, 8192), 256, 0, s>>>(M);
+        CDB_TRY(launch_check(ctx, s, "hot_merge_kernel"));
+        std::swap(wa, wb);
+        std::swap(va, vb);
+      }
+      uint32_t unsorted = 0;
+      CDB_HIP(hipMemcpyAsync(&unsorted, d_unsorted, 4, hipMemcpyDeviceToHost, s), "d2h");
+      CDB_HIP(hipStreamSynchronize(s), "sync");
+      HA.inline_markers = 0;
+      if (std::getenv("CDB_HOT_PROF"))  // test hook
+        std::fprintf(stderr, "chip_wide: list merge of %u buckets x %u lists: %s\n", H, L,
+                     unsorted ? "a list is not sorted (radix sort)" : "merged");
+      if (!unsorted) {
+        HA.w = wa;
+        HA.v = va;
+        merged = true;
+        add_stat_kernel<<<1, 1, 0, s>>>(A.stats, ST_HOT_MERGED, tc);
+        CDB_TRY(launch_check(ctx, s, "add_stat_kernel"));
+      }
+    }
+    if (!merged) {
+      hot_tag_kernel<<<(uint32_t)((tc + kTagChunk - 1) / kTagChunk), 256, 0, s>>>(A, HA);
+      CDB_TRY(launch_check(ctx, s, "hot_tag_kernel"));
+      // (per-bucket bitonic sorts in LDS measured slower than this global radix sort: C3 9.98 vs
+      // 8.90 ms, C5 25.9 vs 24.3 ms; profiles/r03/experiments_r3.txt)
+      CDB_TRY(radix_sort_pairs(ctx, &HA.w, &HA.v, w2, v2, tc, lo, HA.g_shift + gbits, s));
+    }
     // the sort's other buffers are free now: fold results per run start
     HA.fold_v = HA.w == w ? w2 : w;
     HA.fold_q = HA.v == v ? v2 : v;
@@ -950,7 +1018,7 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
                    hot, wide_ids.size(),
                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count(), sort_ms);
     const cdb_status r =
-        chip_wide(ctx, A, wide_ids, hk_off, c_off, tk, tc, cmax, kmax, runs_batch ? rv : nullptr, rv != nullptr, s);
+        chip_wide(ctx, A, wide_ids, hk_off, c_off, tk, tc, cmax, kmax, runs_batch ? rv : nullptr, rv, s);
     wide_ids.clear();
     hk_off.assign(1, 0);
     c_off.assign(1, 0);
@@ -1401,7 +1469,9 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     CDB_HIP(hipStreamSynchronize(s), "sync");
   }
   const uint32_t hot = mid_wide ? 0 : counts[0];
-  if (hot) CDB_TRY(over_capacity(ctx, A, d_hot_list, hot, s));
+  // (sorted-run input: the forwarded buckets' rows were copied in run order -- their child lists
+  // can be merged, and the small ones take the per-bucket LDS path)
+  if (hot) CDB_TRY(over_capacity(ctx, A, d_hot_list, hot, s, use_runs ? &RV : nullptr, 0));
 
   // ---- 5. dense compaction into the caller's output columns (already done range by range when
   //         the bucket phase was pipelined and no workgroup tier added outputs)
@@ -1484,6 +1554,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     stats->finish_ms = ms;
     stats->sorted_runs = use_runs ? 1 : 0;
     stats->hot_slow_runs = hs[ST_HOT_SLOW];
+    stats->hot_merged_children = hs[ST_HOT_MERGED];
   }
   if ((flags & CDB_MERGE_STRICT_DICT_PANIC) && hs[ST_DICT_MERGES])
     return fail(ctx, CDB_DICT_MERGE_UNIMPLEMENTED, "Dict::merge reached (lwwhash.rs:180 unimplemented!())");

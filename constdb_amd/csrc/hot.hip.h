@@ -9,12 +9,14 @@
 //                     bucket's table), copies the fields the fold reads into a 32-B record,
 //                     decides whether it takes part (head type, element type, remote dels
 //                     ignored, exactly as the wave tier) and tags it with
-//                     W = G << g_shift | id-hash top (g_shift - 6) bits << 6 | pos (g_shift:
+//                     W = G << g_shift | child_order(id1) top (g_shift - 6) bits << 6 | pos (g_shift:
 //                     40, or less where that saves a sort pass -- see chip_wide); a child that
 //                     takes no part gets its bucket's marker (every W bit of the bucket's last key
 //                     set: pos 63, which no row has, and an id field no child gets), so it sorts
 //                     to the end of its bucket's children and every bucket's children keep their
 //                     flat range;
+//   the sort: a merge of the buckets' sorted child lists when they arrive sorted (a merge result's
+//                     child order: hot_merge_kernel below), else
 //   radix sort of (W, child) pairs (radix.hip.h) on W's bits above pos, stable, so equal W >> 6
 //                     keep (bucket, row) order: run order, which is fold order on the sorted-run
 //                     path unless two ids share the hash bits;
@@ -35,7 +37,7 @@
 
 namespace cdb {
 
-constexpr int kHotIdBits = 40;     // largest g_shift: W = G << 40 | (child-id hash >> 30) << 6 | pos
+constexpr int kHotIdBits = 40;     // largest g_shift: W = G << 40 | (child_order(id1) >> 30) << 6 | pos
 constexpr int kHotMinIdBits = 20;  // fewest id-hash bits chosen to save a sort pass
 
 struct HotArgs {
@@ -76,6 +78,9 @@ struct HotArgs {
   unsigned long long* prof;  // test hook (CDB_HOT_PROF): hot_sortfold_kernel's phase clocks, or null
   int small_keys;            // every bucket of the batch has at most kTagKeys output keys: the tag
                              // kernel searches its buckets' key tables in LDS
+  int inline_markers;        // tag: a child that takes no part keeps the W it would have (its list
+                             // stays sorted for the merge) and is flagged in v (kInlineMarker)
+                             // instead of getting the bucket's marker
 };
 
 // A child's columns: its copied AoS row, or (runs mode) the runs' SoA columns.
@@ -100,6 +105,10 @@ __device__ __forceinline__ uint64_t hot_marker(const HotArgs& H, uint32_t h) {
   return ((uint64_t)H.hk_off[h + 1] << H.g_shift) - 1;
 }
 __device__ __forceinline__ bool hot_takes_part(uint64_t W) { return (W & 63) != 63; }
+// v's top bit: a child that takes no part, tagged with its own W (HotArgs::inline_markers); the low
+// 31 bits are the flat index.
+constexpr uint32_t kInlineMarker = 0x80000000u;
+__device__ __forceinline__ bool hot_row_part(uint64_t W, uint32_t v) { return hot_takes_part(W) && !(v & kInlineMarker); }
 
 // The key phase's LDS (bucket_keys touches no child arrays): sized for KC key rows, so that batches
 // of buckets of at most 256 keys run several workgroups per CU.
@@ -211,11 +220,12 @@ __device__ __forceinline__ HotFields hot_fields(const BucketArgs& A, const HotAr
 }
 
 // Flat child j of hot bucket h (fields F, a node when isn): its fold fields into rec[j] and its tag
-// W (the bucket's marker when it takes no part; orph counts children whose key is not in the
-// bucket). T: the bucket's kout output keys.
+// W (when it takes no part: the bucket's marker; with inline_markers, when its key is in the bucket,
+// the W it would have, and *inline_marker is set -- the tag kernel flags it in v's top bit; orph
+// counts children whose key is not in the bucket). T: the bucket's kout output keys.
 __device__ __forceinline__ uint64_t hot_tag_row(const BucketArgs& A, const HotArgs& H, uint32_t h, uint64_t j,
                                                 bool isn, const HotFields& F, const HotKeyTab& T, uint32_t kout,
-                                                unsigned long long& orph) {
+                                                unsigned long long& orph, bool* inline_marker = nullptr) {
   const int ks = A.key_shift;
   const uint64_t pkh = F.pkh, pkf = F.pkf, id1 = F.id1, id2 = F.id2, t = F.t, m = F.m;
   // lower bound over the bucket's sorted output keys on (kh << shift, kh, kf)
@@ -230,19 +240,28 @@ __device__ __forceinline__ uint64_t hot_tag_row(const BucketArgs& A, const HotAr
     hi = less ? hi : mid;
   }
   uint64_t w = hot_marker(H, h);
-  if (lo < kout && T.kh[lo] == pkh && T.kf[lo] == pkf && (T.tp[lo] & 0xFF) <= TAG_SET) {
+  const bool found = lo < kout && T.kh[lo] == pkh && T.kf[lo] == pkf;
+  // (the id field stops one below all ones: the bucket's marker is above every W of the bucket in
+  // the sorted bits, which leave out the pos bits)
+  const uint64_t ih = child_order(id1), top = (1ull << (H.g_shift - 6)) - 2;
+  const uint64_t wk = ((uint64_t)(g0 + lo) << H.g_shift) | (min(ih >> H.id_shift, top) << 6);
+  if (found && (T.tp[lo] & 0xFF) <= TAG_SET) {
     const uint32_t TT = T.tp[lo] & 0xFF, hp = T.tp[lo] >> 8, p = meta_pos(m);
     const bool type_ok = isn ? TT == TAG_COUNTER : (TT == TAG_SET || TT == TAG_DICT);
     const bool elem_ok = (T.vm[lo] >> p) & 1;
     const bool cand = isn || meta_tag(m) == KIND_ADD || p == hp;  // remote dels ignored
     if (type_ok && elem_ok && cand) {
-      // (the id field stops one below all ones: the marker is above every W of the bucket in
-      // the sorted bits, which leave out the pos bits)
-      const uint64_t ih = isn ? mix64(id1) : id1, top = (1ull << (H.g_shift - 6)) - 2;
-      w = ((uint64_t)(g0 + lo) << H.g_shift) | (min(ih >> H.id_shift, top) << 6) | p;
+      w = wk | p;
+    } else if (H.inline_markers) {
+      w = wk | p;
+      *inline_marker = true;
     }
   } else {
     ++orph;
+    if (found && H.inline_markers) {
+      w = wk | meta_pos(m);
+      *inline_marker = true;
+    }
   }
   // the fold reads a child's four fields as one 32-B record (flat order: written in sequence)
   H.rec[2 * j] = make_ulonglong2(id1, id2);
@@ -332,8 +351,9 @@ __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
     } else {
       T = hot_key_tab(H, H.hk_off[h]);
     }
-    H.w[j] = hot_tag_row(A, H, h, j, isn, hot_fields(A, H, isn, row), T, H.hk_kout[h], orph);
-    H.v[j] = (uint32_t)j;
+    bool mk = false;
+    H.w[j] = hot_tag_row(A, H, h, j, isn, hot_fields(A, H, isn, row), T, H.hk_kout[h], orph, &mk);
+    H.v[j] = (uint32_t)j | (mk ? kInlineMarker : 0u);
     H.c_h[j] = h | (isn ? 0u : 0x80000000u);
   }
   if (orph) atomicAdd(&stat_shard(A.stats)[ST_ORPHANS], orph);
@@ -357,7 +377,7 @@ __device__ __forceinline__ HotChild hot_child(const HotArgs& H, uint32_t j) {
 // Total order of a run's rows: exact id (nodes: the node id alone), fold position (pos, src),
 // flat index. The fold visits the rows in this order.
 __device__ __forceinline__ bool hot_before(const HotChild& a, const HotChild& b, bool isn) {
-  if (a.id1 != b.id1) return a.id1 < b.id1;
+  if (a.id1 != b.id1) return child_order(a.id1) < child_order(b.id1);
   if (!isn && a.id2 != b.id2) return a.id2 < b.id2;
   const uint64_t oa = meta_order(a.meta), ob = meta_order(b.meta);
   if (oa != ob) return oa < ob;
@@ -369,9 +389,17 @@ __global__ void __launch_bounds__(256) hot_runflag_kernel(HotArgs H, uint32_t* _
   for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < H.n_children;
        p += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t W = H.w[p];
-    // a run: equal W but the pos bits (a marker never starts one; one before W belongs to an
-    // earlier bucket, so it never hides a start either)
-    flag[p] = hot_takes_part(W) && !(p > 0 && (H.w[p - 1] >> 6) == (W >> 6));
+    // a run: equal W but the pos bits, from its first row that takes part (a bucket's marker never
+    // starts one; one before W belongs to an earlier bucket, so it never hides a start either;
+    // inline markers sit inside runs)
+    bool start = hot_row_part(W, H.v[p]);
+    for (uint64_t q = p; start && q > 0;) {
+      --q;
+      const uint64_t X = H.w[q];
+      if ((X >> 6) != (W >> 6)) break;
+      if (hot_row_part(X, H.v[q])) start = false;
+    }
+    flag[p] = start;
   }
 }
 __global__ void __launch_bounds__(256) hot_runlist_kernel(HotArgs H, const uint32_t* __restrict__ flag,
@@ -394,6 +422,142 @@ __global__ void __launch_bounds__(256) hot_first_run_kernel(HotArgs H) {
   H.first_run[h] = lo;
 }
 
+// ---- The chip-wide sort as a merge of sorted lists. Every merge tier writes a key's children in
+// child_order (common.h), so in a merge result -- and so in a position-0 state, or a snapshot this
+// engine encoded from one and decoded again -- bucket h's flat children are 2 nr lists (the node
+// runs, then the member runs: hot_row's order) that are each non-decreasing in W: the key id G
+// follows the run's key-hash order and the id bits are a prefix of child_order(id1). A child that
+// takes no part keeps the W it would have (inline_markers) and is flagged in v instead, so it stays
+// in place in its sorted list; after the merge it sits inside its W-run, where run detection and
+// the fold skip it. The sort is then log2(L) rounds of stable pairwise merges of
+// neighbouring lists (L = 2 nr rounded up to a power of two; on equal W the lower list first,
+// i.e. flat order -- what the stable radix sort keeps), each one read and one write of the
+// (W, child) pairs instead of the radix sort's six passes and their histograms. Round 0 verifies
+// that every list is sorted; an input that is not (a reference snapshot's HashMap order, or a
+// producer that is not a merge) sets *unsorted and the caller re-tags and radix-sorts.
+constexpr uint32_t kMergeItems = 8;
+constexpr uint32_t kMergeTile = 256 * kMergeItems;  // outputs per workgroup tile
+
+// List bounds of every bucket: bounds[h * (L + 1) + l] = flat start of list l (l < 2 nr: family
+// l / nr, run l % nr), padding lists empty, bounds[h * (L + 1) + L] = the bucket's end.
+__global__ void __launch_bounds__(256) hot_lists_kernel(HotArgs H, uint32_t L, uint32_t* __restrict__ bounds) {
+  const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H.H) return;
+  const uint32_t b = H.ids[h], nr = H.V.nr;
+  uint32_t* o = bounds + (uint64_t)h * (L + 1);
+  uint32_t x = H.c_off[h];
+  for (uint32_t f = 0; f < 2; ++f)
+    for (uint32_t r = 0; r < nr; ++r) {
+      o[f * nr + r] = x;
+      const uint32_t* d = H.V.rdir[1 + f] + (uint64_t)r * H.V.nbp1 + b;
+      x += d[1] - d[0];
+    }
+  for (uint32_t l = 2 * nr; l <= L; ++l) o[l] = x;
+}
+
+struct MergeArgs {
+  const uint32_t* bounds;    // hot_lists_kernel
+  uint32_t L, span;          // this round merges list groups [2 span m, 2 span m + span) and [.. + span, 2 span (m + 1))
+  uint32_t n_jobs;           // H * L / (2 span): job J = bucket J / (L / 2 span), pair J % (L / 2 span)
+  uint32_t* tiles;           // per job: its tiles, then (scanned) its first tile
+  const uint64_t* n_tiles;   // total tiles (device)
+  const uint64_t* wi;
+  const uint32_t* vi;
+  uint64_t* wo;
+  uint32_t* vo;
+  uint32_t* unsorted;        // check: a list decreases somewhere
+  int check;
+};
+__device__ __forceinline__ void merge_job(const MergeArgs& M, uint32_t J, uint32_t& a0, uint32_t& a1, uint32_t& b1) {
+  const uint32_t per = M.L / (2 * M.span), h = J / per, m = J % per;
+  const uint32_t* o = M.bounds + (uint64_t)h * (M.L + 1) + 2 * M.span * m;
+  a0 = o[0];
+  a1 = o[M.span];
+  b1 = o[2 * M.span];
+}
+__global__ void __launch_bounds__(256) hot_merge_count_kernel(MergeArgs M) {
+  const uint32_t J = blockIdx.x * blockDim.x + threadIdx.x;
+  if (J >= M.n_jobs) return;
+  uint32_t a0, a1, b1;
+  merge_job(M, J, a0, a1, b1);
+  M.tiles[J] = (b1 - a0 + kMergeTile - 1) / kMergeTile;
+}
+// A's elements before output position d of the stable merge of A[0, na) and B[0, nb) (A first on
+// equal keys).
+template <class KA, class KB>
+__device__ __forceinline__ uint32_t merge_path(KA a, uint32_t na, KB bk, uint32_t nb, uint32_t d) {
+  uint32_t lo = d > nb ? d - nb : 0, hi = min(d, na);
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a(mid) <= bk(d - 1 - mid)) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+// One tile of kMergeTile outputs of one job per iteration: the tile's two input slices are found
+// by merge path (two threads), staged in LDS with coalesced loads, and each thread merges
+// kMergeItems outputs from LDS.
+__global__ void __launch_bounds__(256) hot_merge_kernel(MergeArgs M) {
+  __shared__ uint64_t sw[kMergeTile];
+  __shared__ uint32_t sv[kMergeTile];
+  __shared__ uint32_t split[2];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t nt = *M.n_tiles;
+  for (uint64_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    uint32_t lo = 0, hi = M.n_jobs;  // the last job whose first tile is at or before t
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (M.tiles[mid] <= t) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t J = lo;
+    uint32_t a0, a1, b1;
+    merge_job(M, J, a0, a1, b1);
+    const uint32_t na = a1 - a0, nb = b1 - a1;
+    const uint32_t d0 = (uint32_t)(t - M.tiles[J]) * kMergeTile, d1 = min(d0 + kMergeTile, na + nb);
+    const uint64_t* A = M.wi + a0;
+    const uint64_t* B = M.wi + a1;
+    if (tid < 2)
+      split[tid] = merge_path([&](uint32_t i) { return A[i]; }, na, [&](uint32_t i) { return B[i]; }, nb,
+                              tid ? d1 : d0);
+    __syncthreads();
+    const uint32_t ia0 = split[0], ia1 = split[1], ib0 = d0 - ia0, ib1 = d1 - ia1;
+    const uint32_t la = ia1 - ia0, lb = ib1 - ib0;
+    for (uint32_t x = tid; x < la + lb; x += blockDim.x) {
+      const uint32_t src = x < la ? a0 + ia0 + x : a1 + ib0 + (x - la);
+      sw[x] = M.wi[src];
+      sv[x] = M.vi[src];
+    }
+    __syncthreads();
+    if (M.check) {  // every element against its list predecessor (the first one's from global memory)
+      bool bad = false;
+      for (uint32_t x = tid; x < la + lb; x += blockDim.x) {
+        const bool ina = x < la;
+        const uint32_t k = ina ? ia0 + x : ib0 + (x - la);  // index inside its list
+        if (k == 0) continue;
+        const uint64_t prev = (x != 0 && x != la) ? sw[x - 1] : (ina ? A[k - 1] : B[k - 1]);
+        bad |= sw[x] < prev;
+      }
+      if (__ballot(bad) && (tid & 63) == 0) atomicOr(M.unsorted, 1u);
+    }
+    const uint32_t d = tid * kMergeItems;
+    if (d < la + lb) {
+      uint32_t i = merge_path([&](uint32_t k) { return sw[k]; }, la, [&](uint32_t k) { return sw[la + k]; }, lb, d);
+      uint32_t j = d - i;
+      const uint32_t e = min(d + kMergeItems, la + lb);
+      for (uint32_t q = d; q < e; ++q) {
+        const bool takea = j >= lb || (i < la && sw[i] <= sw[la + j]);
+        const uint32_t x = takea ? i : la + j;
+        M.wo[a0 + d0 + q] = sw[x];
+        M.vo[a0 + d0 + q] = sv[x];
+        i += takea ? 1 : 0;
+        j += takea ? 0 : 1;
+      }
+    }
+    __syncthreads();  // (the next tile reuses the LDS)
+  }
+}
+
 constexpr uint32_t kFoldFast = 8;  // runs up to this many rows: rows in registers, loads overlapped
 
 // One run's contribution to its key's row: outputs, first output slot, counter sum.
@@ -414,10 +578,11 @@ struct HotAcc {
 // the sort left them in. Every lane of the wave calls this (act false for idle lanes): loops have
 // wave-uniform trip counts with per-lane predicates -- a loop-carried row must not be a live-out
 // of a loop with divergent exits (gfx950 compilers have produced the first candidate instead of
-// the smallest there).
-template <class JAt>
+// the smallest there). Rows k with !part(k) take no part (inline markers, after the run's first
+// row): they are skipped.
+template <class JAt, class Part>
 __device__ __forceinline__ void hot_fold_run(const BucketArgs& A, const HotArgs& H, int pass, bool act, bool isn,
-                                             uint32_t b, uint32_t G, uint32_t nrows, JAt jat, uint64_t obase,
+                                             uint32_t b, uint32_t G, uint32_t nrows, JAt jat, Part part, uint64_t obase,
                                              bool emitted, uint32_t* fq, uint64_t* fv, ulonglong2* fs, HotAcc& acc,
                                              unsigned long long& gcm, unsigned long long& nslow) {
   auto put = [&](uint64_t id1, uint64_t id2, uint64_t t, uint64_t meta, uint64_t v) {
@@ -447,12 +612,16 @@ __device__ __forceinline__ void hot_fold_run(const BucketArgs& A, const HotArgs&
     // fast path: up to kFoldFast rows, their loads issued together
     const bool fast = act && nrows <= kFoldFast;
     uint32_t rj[kFoldFast];
+    bool pk[kFoldFast];
 #pragma unroll
-    for (uint32_t k = 0; k < kFoldFast; ++k) rj[k] = (fast && k < nrows) ? jat(k) : 0;
+    for (uint32_t k = 0; k < kFoldFast; ++k) {
+      pk[k] = fast && k < nrows && (k == 0 || part(k));
+      rj[k] = pk[k] ? jat(k) : 0;
+    }
     uint64_t xi1[kFoldFast], xi2[kFoldFast], xt[kFoldFast], xm[kFoldFast];
 #pragma unroll
     for (uint32_t k = 0; k < kFoldFast; ++k) {
-      if (fast && k < nrows) {
+      if (pk[k]) {
         const ulonglong2 a = H.rec[2 * (uint64_t)rj[k]], c = H.rec[2 * (uint64_t)rj[k] + 1];
         xi1[k] = a.x;
         xi2[k] = a.y;
@@ -464,12 +633,13 @@ __device__ __forceinline__ void hot_fold_run(const BucketArgs& A, const HotArgs&
     }
     bool simple = fast;
     uint64_t v = xi2[0], tw = xt[0];
+    uint64_t last_order = meta_order(xm[0]);
     uint32_t qw = 0;  // winner (members)
 #pragma unroll
     for (uint32_t k = 1; k < kFoldFast; ++k) {
-      if (k < nrows) {
-        simple = simple && xi1[k] == xi1[0] && (isn || xi2[k] == xi2[0]) &&
-                 meta_order(xm[k]) > meta_order(xm[k - 1]);
+      if (pk[k]) {
+        simple = simple && xi1[k] == xi1[0] && (isn || xi2[k] == xi2[0]) && meta_order(xm[k]) > last_order;
+        last_order = meta_order(xm[k]);
         if (isn) {  // Counter::merge (type_counter.rs:60-84): the head's t is kept
           v = xt[k] > xt[0] ? xi2[k] : (xt[k] == xt[0] ? imax64(v, xi2[k]) : v);
         } else if (!(tw > xt[k])) {  // LWWHash::set (lwwhash.rs:87-107): later wins ties
@@ -533,7 +703,7 @@ __device__ __forceinline__ void hot_fold_run(const BucketArgs& A, const HotArgs&
     HotChild c = last;
     bool have = false;
     for (uint32_t k = 0; k < kslow; ++k) {
-      if (slow && k < nrows && step < nrows) {
+      if (slow && k < nrows && step < nrows && (k == 0 || part(k))) {
         const HotChild x = hot_child(H, jat(k));
         const bool after = step == 0 || hot_before(last, x, isn);
         const bool take = after && (!have || hot_before(x, c, isn));
@@ -588,10 +758,10 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
     uint32_t nrows = 0, hc = 0, G = 0;
     if (rows) {
       W = H.w[p];
-      uint64_t e = p + 1;
+      uint64_t e = p + 1;  // (inline markers inside the run are rows of it; the fold skips them)
       while (e < H.n_children && (H.w[e] >> 6) == (W >> 6) && hot_takes_part(H.w[e])) ++e;
       nrows = (uint32_t)(e - p);
-      hc = H.c_h[H.v[p]];
+      hc = H.c_h[H.v[p] & ~kInlineMarker];
       G = (uint32_t)(W >> H.g_shift);
     } else if (kept) {
       const uint2 hg = H.fold_hg[i];
@@ -613,7 +783,8 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
     }
     const bool emitted = act && pass == 1 && (isn ? H.emit_n : H.emit_m)[i] != 0;
     HotAcc acc;
-    hot_fold_run(A, H, pass, act, isn, b, G, nrows, [&](uint32_t k) { return H.v[p + k]; }, obase, emitted,
+    hot_fold_run(A, H, pass, act, isn, b, G, nrows, [&](uint32_t k) { return H.v[p + k] & ~kInlineMarker; },
+                 [&](uint32_t k) { return !(H.v[p + k] & kInlineMarker); }, obase, emitted,
                  &H.fold_q[i], &H.fold_v[i], H.fold_rec + 2 * i, acc, gcm, nslow);
     if (pass == 0 && act) {
       H.emit_n[i] = isn ? acc.nout : 0;
@@ -951,7 +1122,8 @@ __global__ void __launch_bounds__(C::Threads) hot_sortfold_kernel(BucketArgs A, 
     const uint32_t nrows = act ? (r + 1 < nruns ? (rl[r + 1] & 0xFFFF) : m) - q : 0;
     const bool isn = act && sx[q] < N;
     HotAcc acc;
-    hot_fold_run(A, H, 0, act, isn, b, g0 + (e >> 16), nrows, [&](uint32_t k) { return c0 + sx[q + k]; }, 0,
+    hot_fold_run(A, H, 0, act, isn, b, g0 + (e >> 16), nrows, [&](uint32_t k) { return c0 + sx[q + k]; },
+                 [](uint32_t) { return true; }, 0,
                  false, fq + r, fv + r, nullptr, acc, gcm, nslow);
     if (act) no[r] = (uint16_t)acc.nout;
   }
@@ -980,6 +1152,7 @@ __global__ void __launch_bounds__(C::Threads) hot_sortfold_kernel(BucketArgs A, 
     const uint32_t off = act ? ro[r] : 0;
     HotAcc acc;
     hot_fold_run(A, H, 1, act, isn, b, g0 + gr, nrows, [&](uint32_t k) { return c0 + sx[q + k]; },
+                 [](uint32_t) { return true; },
                  isn ? (off & 0xFFFF) : (off >> 16), act && no[r] != 0, fq + r, fv + r, nullptr, acc, gcm, nslow);
     if (act && acc.k_cnt) {
       atomicAdd(&L.kcnt[gr], acc.k_cnt);

@@ -406,6 +406,9 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, 5) bucket_wave_runs_kernel(W
 #define CDB_PIPE_CHUNK 32
 #endif
 constexpr uint32_t kPipeChunk = CDB_PIPE_CHUNK;
+#ifndef CDB_PIPE_MINB  // workgroups per CU the register budget is sized for
+#define CDB_PIPE_MINB 4
+#endif
 constexpr uint32_t kPipeDone = 0xFFFFFFFFu;
 
 // Bucket b's slices from its bdir row (lanes 0..31) and bucket b + 1's (lanes 32..63): one
@@ -481,7 +484,7 @@ __device__ __forceinline__ void pipe_load(const RunView& V, const WaveDir& d, co
 
 // REC: every family in the records layout (the host checks the strides)
 template <bool REC>
-__global__ void __launch_bounds__(kWavesPerWG * 64, 4) bucket_wave_pipe_kernel(WaveArgs W) {
+__global__ void __launch_bounds__(kWavesPerWG * 64, CDB_PIPE_MINB) bucket_wave_pipe_kernel(WaveArgs W) {
   __shared__ WaveLds<1> lds_all[kWavesPerWG];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   WaveLds<1>& L = lds_all[wv];

@@ -112,3 +112,70 @@ def to_records(cdb, ctx, din) -> None:
             torch.cuda.synchronize()
         L.cdb_dev_rows_release(ctx.handle, ctypes.byref(rows))
         setattr(din, name, rec)
+
+
+def _run_view(cdb, rows, a: int, n: int):
+    """cdb_dev_rows of rows [a, a + n) of `rows` (plain columns or the records layout)."""
+    v = cdb.DevRows()
+    v.n, v.stride, v.stride0 = n, rows.stride, rows.stride0
+    for c in range(8):
+        if rows.col[c]:
+            step = (rows.stride0 if c == 0 else rows.stride) or 1
+            v.col[c] = rows.col[c] + 8 * a * step
+    return v
+
+
+def state_runs(cdb, ctx, din, opts=None) -> None:
+    """Setup helper: replaces every replica's rows by that replica's state as this engine keeps it --
+    its rows merged alone (cdb_merge_device, bucket layout) and read back as position-0 rows
+    (cdb_dev_state_rows), moved to the replica's fold position (cdb_dev_input_append). That is what
+    a node holding merge results has: one key-hash-ordered run per replica whose children follow
+    every merge tier's child order (common.h child_order), so the chip-wide path merges those runs
+    instead of sorting them. The replicas' content is unchanged (a single-replica merge folds
+    nothing). din must be in the records layout; its rows are released and replaced."""
+    import ctypes
+    L = cdb.lib()
+    names = ("keys", "nodes", "members")
+    sort_into_runs(din)
+    R = din.n_runs
+    mopts = opts if opts is not None else cdb.MergeOpts()
+    dst = cdb.DevInput()
+    for name, ncol in zip(names, FAMILY_COLS):
+        r = cdb.DevRows()
+        ctx.check(L.cdb_dev_rows_alloc_records(ctx.handle, ctypes.byref(r), max(getattr(din, name).n, 1), ncol))
+        r.n = 0
+        setattr(dst, name, r)
+    for rep in range(R):
+        one = cdb.DevInput()
+        for f, name in enumerate(names):
+            a, b = din.run_start[f][rep], din.run_start[f][rep + 1]
+            setattr(one, name, _run_view(cdb, getattr(din, name), a, b - a))
+            one.run_start[f][0], one.run_start[f][1] = 0, b - a
+        one.n_pos, one.n_runs = rep + 1, 1
+        out = cdb.DevOutput()
+        out.compact = 0
+        st = cdb.MergeStats()
+        ctx.check(L.cdb_merge_device(ctx.handle, ctypes.byref(one), ctypes.byref(mopts), ctypes.byref(out),
+                                     ctypes.byref(st), None))
+        sdin = cdb.DevInput()
+        for name, ncol in zip(names, FAMILY_COLS):
+            r = cdb.DevRows()
+            ctx.check(L.cdb_dev_rows_alloc_records(ctx.handle, ctypes.byref(r), max(getattr(out, name).n, 1), ncol))
+            setattr(sdin, name, r)
+        ctx.check(L.cdb_dev_state_rows(ctx.handle, ctypes.byref(out), ctypes.byref(sdin.keys),
+                                       ctypes.byref(sdin.nodes), ctypes.byref(sdin.members), None))
+        sdin.n_pos, sdin.n_runs = 1, 1
+        for f, name in enumerate(names):
+            sdin.run_start[f][0], sdin.run_start[f][1] = 0, getattr(sdin, name).n
+        if rep == 0:
+            dst.n_runs = 0  # (the first append sets the runs: dst has no rows yet)
+        ctx.check(L.cdb_dev_input_append(ctx.handle, ctypes.byref(dst), ctypes.byref(sdin), rep, None))
+        if rep == 0:  # an empty dst is not "in runs": the first state becomes run 0 explicitly
+            dst.n_runs = 1
+            for f, name in enumerate(names):
+                dst.run_start[f][0], dst.run_start[f][1] = 0, getattr(dst, name).n
+        for name in names:
+            L.cdb_dev_rows_release(ctx.handle, ctypes.byref(getattr(sdin, name)))
+    for name in names:
+        L.cdb_dev_rows_release(ctx.handle, ctypes.byref(getattr(din, name)))
+    ctypes.memmove(ctypes.byref(din), ctypes.byref(dst), ctypes.sizeof(din))

@@ -190,6 +190,8 @@ typedef struct cdb_merge_stats {
   uint64_t sorted_runs;      /* 1 when the sorted-run path ran (partition_ms = its run directories) */
   uint64_t hot_slow_runs;    /* chip-wide path: (key, id-bits) runs folded by successor selection
                                 (ids sharing the sort tag's id bits, or runs of > 8 rows) */
+  uint64_t hot_merged_children; /* chip-wide path: children whose runs arrived in child order
+                                (a merge result's) and were merged instead of radix-sorted */
 } cdb_merge_stats;
 
 cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n,

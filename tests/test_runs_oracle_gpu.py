@@ -137,7 +137,7 @@ def test_chip_wide_in_batches_vs_oracle(ctx, monkeypatch):
     check_runs(ctx, [cdb.gen_snapshot(cfg, r) for r in range(4)], force_tier=2)
 
 
-@pytest.mark.parametrize("lds,id_bits", [("1", None), ("0", None), ("1", "6"), ("1", "12")])
+@pytest.mark.parametrize("lds,id_bits", [("1", None), ("0", None), ("1", "4"), ("1", "12")])
 def test_chip_wide_lds_and_global_sort_vs_oracle(ctx, monkeypatch, lds, id_bits):
     """Run-order batches of buckets of at most 8192 children take the per-bucket LDS sort and fold
     (hot_sortfold_kernel); CDB_HOT_LDS=0 sends them through the global tag sort instead. Both equal
@@ -153,7 +153,7 @@ def test_chip_wide_lds_and_global_sort_vs_oracle(ctx, monkeypatch, lds, id_bits)
     wm = (configs.T0_MS + (1 << 19)) << 22
     m = check_runs(ctx, snaps, force_tier=2, gc=wm, gc_members=True)
     assert m.stats.hot_buckets > 0
-    if id_bits == "6":
+    if id_bits == "4":  # (16 member ids per key over 16 id-bit values: runs of several ids)
         assert m.stats.hot_slow_runs > 0
 
 
