@@ -871,13 +871,16 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
       uint32_t L = 2;
       while (L < 2 * HA.V.nr) L <<= 1;
       const uint64_t jobs0 = (uint64_t)H * (L / 2);
-      uint8_t* mw = (uint8_t*)ws_get(ctx, WS_HOTMERGE, ((uint64_t)H * (L + 1) + 2 * jobs0) * 4 + 64, &st);
+      const uint64_t tiles_cap = tc / kMergeTile + jobs0 + 1;  // (a round's tiles: at most this many)
+      uint8_t* mw = (uint8_t*)ws_get(ctx, WS_HOTMERGE, ((uint64_t)H * (L + 1) + 2 * jobs0) * 4 + tiles_cap * 8 + 128,
+                                     &st);
       if (!mw) return st;
       uint64_t* d_ntiles = (uint64_t*)mw;
       uint32_t* d_unsorted = (uint32_t*)(mw + 8);
       uint32_t* bounds = (uint32_t*)(mw + 64);
       uint32_t* tcnt = bounds + (uint64_t)H * (L + 1);
       uint32_t* toff = tcnt + jobs0;
+      uint2* splits = (uint2*)(((uintptr_t)(toff + jobs0) + 15) & ~(uintptr_t)15);
       CDB_HIP(hipMemsetAsync(d_unsorted, 0, 4, s), "memset");
       HA.inline_markers = 1;
       hot_tag_kernel<<<(uint32_t)((tc + kTagChunk - 1) / kTagChunk), 256, 0, s>>>(A, HA);
@@ -906,7 +909,9 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
         CDB_TRY(launch_check(ctx, s, "hot_merge_count_kernel"));
         CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, tcnt, M.n_jobs, toff, (uint32_t*)nullptr, d_ntiles, s));
         const uint64_t tiles_max = tc / kMergeTile + M.n_jobs;
-        hot_merge_kernel<<<(uint32_t)std::min<uint64_t>(tiles_max, 8192), 256, 0, s>>>(M);
+        hot_merge_split_kernel<<<(uint32_t)((tiles_max + 255) / 256), 256, 0, s>>>(M, splits);
+        CDB_TRY(launch_check(ctx, s, "hot_merge_split_kernel"));
+        hot_merge_kernel<<<(uint32_t)tiles_max, 256, 0, s>>>(M, splits);
         CDB_TRY(launch_check(ctx, s, "hot_merge_kernel"));
         std::swap(wa, wb);
         std::swap(va, vb);

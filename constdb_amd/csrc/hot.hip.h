@@ -494,67 +494,101 @@ __device__ __forceinline__ uint32_t merge_path(KA a, uint32_t na, KB bk, uint32_
   }
   return lo;
 }
-// One tile of kMergeTile outputs of one job per iteration: the tile's two input slices are found
-// by merge path (two threads), staged in LDS with coalesced loads, and each thread merges
-// kMergeItems outputs from LDS.
-__global__ void __launch_bounds__(256) hot_merge_kernel(MergeArgs M) {
+// Each tile's job and its first A element (merge path at the tile's first output), one thread per
+// tile, so that the merge's workgroups start with their split in hand instead of a chain of global
+// loads.
+__global__ void __launch_bounds__(256) hot_merge_split_kernel(MergeArgs M, uint2* __restrict__ split) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= *M.n_tiles) return;
+  uint32_t lo = 0, hi = M.n_jobs;  // the last job whose first tile is at or before t
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (M.tiles[mid] <= t) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t J = lo;
+  uint32_t a0, a1, b1;
+  merge_job(M, J, a0, a1, b1);
+  const uint64_t* A = M.wi + a0;
+  const uint64_t* B = M.wi + a1;
+  const uint32_t d0 = (uint32_t)(t - M.tiles[J]) * kMergeTile;
+  split[t] = make_uint2(merge_path([&](uint32_t i) { return A[i]; }, a1 - a0, [&](uint32_t i) { return B[i]; },
+                                   b1 - a1, d0), J);
+}
+// One tile of kMergeTile outputs per workgroup: the tile's two input slices (from its split and
+// the next tile's) are staged in LDS with coalesced loads, and each thread merges kMergeItems
+// outputs from LDS.
+__global__ void __launch_bounds__(256) hot_merge_kernel(MergeArgs M, const uint2* __restrict__ split) {
   __shared__ uint64_t sw[kMergeTile];
   __shared__ uint32_t sv[kMergeTile];
-  __shared__ uint32_t split[2];
   const uint32_t tid = threadIdx.x;
   const uint64_t nt = *M.n_tiles;
-  for (uint64_t t = blockIdx.x; t < nt; t += gridDim.x) {
-    uint32_t lo = 0, hi = M.n_jobs;  // the last job whose first tile is at or before t
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (M.tiles[mid] <= t) lo = mid;
-      else hi = mid;
-    }
-    const uint32_t J = lo;
-    uint32_t a0, a1, b1;
-    merge_job(M, J, a0, a1, b1);
-    const uint32_t na = a1 - a0, nb = b1 - a1;
-    const uint32_t d0 = (uint32_t)(t - M.tiles[J]) * kMergeTile, d1 = min(d0 + kMergeTile, na + nb);
-    const uint64_t* A = M.wi + a0;
-    const uint64_t* B = M.wi + a1;
-    if (tid < 2)
-      split[tid] = merge_path([&](uint32_t i) { return A[i]; }, na, [&](uint32_t i) { return B[i]; }, nb,
-                              tid ? d1 : d0);
-    __syncthreads();
-    const uint32_t ia0 = split[0], ia1 = split[1], ib0 = d0 - ia0, ib1 = d1 - ia1;
-    const uint32_t la = ia1 - ia0, lb = ib1 - ib0;
+  const uint64_t t = blockIdx.x;
+  if (t >= nt) return;
+  const uint2 sp = split[t];
+  const uint32_t J = sp.y;
+  uint32_t a0, a1, b1;
+  merge_job(M, J, a0, a1, b1);
+  const uint32_t na = a1 - a0, nb = b1 - a1;
+  const uint32_t d0 = (uint32_t)(t - M.tiles[J]) * kMergeTile, d1 = min(d0 + kMergeTile, na + nb);
+  uint32_t ia1 = na;  // (the job's last tile ends at the job's end)
+  if (t + 1 < nt) {
+    const uint2 nx = split[t + 1];
+    if (nx.y == J) ia1 = nx.x;
+  }
+  const uint32_t ia0 = sp.x, ib0 = d0 - ia0, ib1 = d1 - ia1;
+  const uint32_t la = ia1 - ia0, lb = ib1 - ib0;
+  const uint64_t* A = M.wi + a0;
+  const uint64_t* B = M.wi + a1;
+  for (uint32_t x = tid; x < la + lb; x += blockDim.x) {
+    const uint32_t src = x < la ? a0 + ia0 + x : a1 + ib0 + (x - la);
+    sw[x] = M.wi[src];
+    sv[x] = M.vi[src];
+  }
+  __syncthreads();
+  if (M.check) {  // every element against its list predecessor (the first one's from global memory)
+    bool bad = false;
     for (uint32_t x = tid; x < la + lb; x += blockDim.x) {
-      const uint32_t src = x < la ? a0 + ia0 + x : a1 + ib0 + (x - la);
-      sw[x] = M.wi[src];
-      sv[x] = M.vi[src];
+      const bool ina = x < la;
+      const uint32_t k = ina ? ia0 + x : ib0 + (x - la);  // index inside its list
+      if (k == 0) continue;
+      const uint64_t prev = (x != 0 && x != la) ? sw[x - 1] : (ina ? A[k - 1] : B[k - 1]);
+      bad |= sw[x] < prev;
     }
-    __syncthreads();
-    if (M.check) {  // every element against its list predecessor (the first one's from global memory)
-      bool bad = false;
-      for (uint32_t x = tid; x < la + lb; x += blockDim.x) {
-        const bool ina = x < la;
-        const uint32_t k = ina ? ia0 + x : ib0 + (x - la);  // index inside its list
-        if (k == 0) continue;
-        const uint64_t prev = (x != 0 && x != la) ? sw[x - 1] : (ina ? A[k - 1] : B[k - 1]);
-        bad |= sw[x] < prev;
+    if (__ballot(bad) && (tid & 63) == 0) atomicOr(M.unsorted, 1u);
+  }
+  // each thread merges its kMergeItems outputs into registers, then they go back through LDS so
+  // that the global stores are coalesced
+  const uint32_t d = tid * kMergeItems, n = la + lb;
+  uint64_t ow[kMergeItems];
+  uint32_t ov[kMergeItems];
+  if (d < n) {
+    uint32_t i = merge_path([&](uint32_t k) { return sw[k]; }, la, [&](uint32_t k) { return sw[la + k]; }, lb, d);
+    uint32_t j = d - i;
+#pragma unroll
+    for (uint32_t q = 0; q < kMergeItems; ++q) {
+      const bool takea = j >= lb || (i < la && sw[i] <= sw[la + j]);
+      const uint32_t x = takea ? i : la + j;
+      ow[q] = sw[x];
+      ov[q] = sv[x];
+      i += takea ? 1 : 0;
+      j += takea ? 0 : 1;
+    }
+  }
+  __syncthreads();
+  if (d < n) {
+#pragma unroll
+    for (uint32_t q = 0; q < kMergeItems; ++q) {
+      if (d + q < n) {
+        sw[d + q] = ow[q];
+        sv[d + q] = ov[q];
       }
-      if (__ballot(bad) && (tid & 63) == 0) atomicOr(M.unsorted, 1u);
     }
-    const uint32_t d = tid * kMergeItems;
-    if (d < la + lb) {
-      uint32_t i = merge_path([&](uint32_t k) { return sw[k]; }, la, [&](uint32_t k) { return sw[la + k]; }, lb, d);
-      uint32_t j = d - i;
-      const uint32_t e = min(d + kMergeItems, la + lb);
-      for (uint32_t q = d; q < e; ++q) {
-        const bool takea = j >= lb || (i < la && sw[i] <= sw[la + j]);
-        const uint32_t x = takea ? i : la + j;
-        M.wo[a0 + d0 + q] = sw[x];
-        M.vo[a0 + d0 + q] = sv[x];
-        i += takea ? 1 : 0;
-        j += takea ? 0 : 1;
-      }
-    }
-    __syncthreads();  // (the next tile reuses the LDS)
+  }
+  __syncthreads();
+  for (uint32_t x = tid; x < n; x += blockDim.x) {
+    M.wo[a0 + d0 + x] = sw[x];
+    M.vo[a0 + d0 + x] = sv[x];
   }
 }
 
