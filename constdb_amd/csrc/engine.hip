@@ -926,6 +926,7 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
       if (!unsorted) {
         HA.w = wa;
         HA.v = va;
+        HA.flagged = 1;
         merged = true;
         add_stat_kernel<<<1, 1, 0, s>>>(A.stats, ST_HOT_MERGED, tc);
         CDB_TRY(launch_check(ctx, s, "add_stat_kernel"));

@@ -78,6 +78,7 @@ struct HotArgs {
   unsigned long long* prof;  // test hook (CDB_HOT_PROF): hot_sortfold_kernel's phase clocks, or null
   int small_keys;            // every bucket of the batch has at most kTagKeys output keys: the tag
                              // kernel searches its buckets' key tables in LDS
+  int flagged;               // the sorted tags may hold inline markers (v's kInlineMarker bit)
   int inline_markers;        // tag: a child that takes no part keeps the W it would have (its list
                              // stays sorted for the merge) and is flagged in v (kInlineMarker)
                              // instead of getting the bucket's marker
@@ -392,8 +393,9 @@ __global__ void __launch_bounds__(256) hot_runflag_kernel(HotArgs H, uint32_t* _
     // a run: equal W but the pos bits, from its first row that takes part (a bucket's marker never
     // starts one; one before W belongs to an earlier bucket, so it never hides a start either;
     // inline markers sit inside runs)
-    bool start = hot_row_part(W, H.v[p]);
-    for (uint64_t q = p; start && q > 0;) {
+    bool start = H.flagged ? hot_row_part(W, H.v[p]) : hot_takes_part(W);
+    if (!H.flagged) start = start && !(p > 0 && (H.w[p - 1] >> 6) == (W >> 6));
+    for (uint64_t q = p; H.flagged && start && q > 0;) {
       --q;
       const uint64_t X = H.w[q];
       if ((X >> 6) != (W >> 6)) break;
@@ -621,14 +623,12 @@ __device__ __forceinline__ void hot_fold_run(const BucketArgs& A, const HotArgs&
                                              unsigned long long& gcm, unsigned long long& nslow) {
   auto put = [&](uint64_t id1, uint64_t id2, uint64_t t, uint64_t meta, uint64_t v) {
     const uint32_t o = (uint32_t)(obase + acc.nout);
-    uint64_t* row = (isn ? A.nos + (uint64_t)(A.nbase[b] + o) * kChildStride
-                         : A.mos + (uint64_t)(A.mbase[b] + o) * kChildStride);
-    row[C_PKH] = H.hk_h[G];
-    row[C_PKF] = H.hk_f[G];
-    row[C_ID1] = id1;
-    row[C_ID2] = isn ? v : id2;
-    row[C_T] = t;
-    row[C_META] = isn ? meta_pack(0, meta_pos(meta), meta_src(meta)) : meta;
+    // (one whole 48-B row as three 16-B stores: pkh pkf | id1 id2 | t meta)
+    ulonglong2* row = (ulonglong2*)(isn ? A.nos + (uint64_t)(A.nbase[b] + o) * kChildStride
+                                        : A.mos + (uint64_t)(A.mbase[b] + o) * kChildStride);
+    row[0] = make_ulonglong2(H.hk_h[G], H.hk_f[G]);
+    row[1] = make_ulonglong2(id1, isn ? v : id2);
+    row[2] = make_ulonglong2(t, isn ? meta_pack(0, meta_pos(meta), meta_src(meta)) : meta);
     acc.k_cb = min(acc.k_cb, o);
     ++acc.k_cnt;
     acc.k_sum += isn ? v : 0;
