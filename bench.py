@@ -35,7 +35,7 @@ sys.path.insert(0, ROOT)
 # SURVEY.md §8d algorithmic row widths (bytes): compulsory read + write per row
 W_KEY, W_NODE, W_SET, W_DICT = 50, 33, 34, 42
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
 # the merge pipeline's kernels (everything cdb_merge_device launches; not the generator)
 MERGE_KERNEL_PREFIXES = ("part_", "bucket_", "compact", "scan_", "stats_reduce", "gc_lastbad", "set_dir",
                          "stamp_pos", "iota", "hot_", "sorted_", "seg_", "run_", "mat_", "radix_hist",

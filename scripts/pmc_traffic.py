@@ -15,30 +15,32 @@ def _name(r):
 
 
 def load(d, counter):
-    """Per kernel, the counter's bytes of every dispatch between a merge_begin_marker and the next
-    merge_end_marker (the engine brackets each merge with them), so that a bench's setup kernels
-    (generator, op apply, the input sort) are not counted. Without markers: every dispatch."""
+    """Per kernel, the counter's bytes of every dispatch of the LAST merge of each process: between
+    its last merge_begin_marker and the merge_end_marker after it (the engine brackets each merge
+    with them), so that a bench's setup (generator, op apply, the input sort, the per-replica state
+    merges of runs.state_runs) is not counted. Without markers: every dispatch."""
     rows = []
     for f in glob.glob(f"{d}/**/run_counter_collection.csv", recursive=True):
         rows += [r for r in csv.DictReader(open(f)) if r["Counter_Name"].startswith(counter) or "marker" in r["Kernel_Name"]]
     rows.sort(key=lambda r: (r["Process_Id"], int(r["Dispatch_Id"])))
-    marked = any("merge_begin_marker" in r["Kernel_Name"] for r in rows)
     per = collections.defaultdict(list)
-    inside = not marked
     seen = set()
+    by_pid = collections.defaultdict(list)
     for r in rows:
-        n = _name(r)
-        if n == "merge_begin_marker":
-            inside = True
-            continue
-        if n == "merge_end_marker":
-            inside = False
-            continue
-        key = (r["Process_Id"], r["Dispatch_Id"], r["Counter_Name"])
-        if not inside or not r["Counter_Name"].startswith(counter) or key in seen:
-            continue
-        seen.add(key)
-        per[n].append(float(r["Counter_Value"]) * 1024.0)
+        by_pid[r["Process_Id"]].append(r)
+    for prow in by_pid.values():
+        begins = [i for i, r in enumerate(prow) if _name(r) == "merge_begin_marker"]
+        if begins:
+            i0 = begins[-1]
+            i1 = next((i for i in range(i0, len(prow)) if _name(prow[i]) == "merge_end_marker"), len(prow))
+            prow = prow[i0 + 1:i1]
+        for r in prow:
+            n = _name(r)
+            key = (r["Process_Id"], r["Dispatch_Id"], r["Counter_Name"])
+            if "marker" in n or not r["Counter_Name"].startswith(counter) or key in seen:
+                continue
+            seen.add(key)
+            per[n].append(float(r["Counter_Value"]) * 1024.0)
     return per
 
 
