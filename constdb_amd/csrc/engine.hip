@@ -48,6 +48,10 @@ cdb_status launch_check(cdb_ctx* ctx, hipStream_t s, const char* what) {
 
 // The persistent wave tier (bucket_wave_pipe_kernel) on runs of at most 8 per family;
 // CDB_WAVE_PIPE=0 runs the one-bucket-per-wave kernel instead (A/B and test hook).
+// The persistent wave tier pays off from this many buckets on: below it, its resident grid is mostly
+// claiming and the wide tier's buckets wait behind it (C1's 100K buckets: 0.33 -> 0.70 ms of bucket
+// phase with it; C3's few thousand large buckets likewise).
+constexpr uint64_t kPipeMinBuckets = 1ull << 19;
 bool pipe_wave_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("CDB_WAVE_PIPE");
@@ -656,7 +660,7 @@ cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, const InLayout&
     V->rs_sum[f] = (uint32_t)rs_sum;
   }
   V->bdir = nullptr;
-  if (nr <= 8 && pipe_wave_enabled()) {
+  if (nr <= 8 && nb >= kPipeMinBuckets && pipe_wave_enabled()) {
     // the persistent wave tier's bucket-major directory, built with the three bucket directories
     uint32_t* bdir = (uint32_t*)ws_get(ctx, WS_RUNBDIR, row * kBdirRow * sizeof(uint32_t), &st);
     if (!bdir) return st;
@@ -883,54 +887,61 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
       uint2* splits = (uint2*)(((uintptr_t)(toff + jobs0) + 15) & ~(uintptr_t)15);
       CDB_HIP(hipMemsetAsync(d_unsorted, 0, 4, s), "memset");
       HA.inline_markers = 1;
-      hot_tag_kernel<<<(uint32_t)((tc + kTagChunk - 1) / kTagChunk), 256, 0, s>>>(A, HA);
-      CDB_TRY(launch_check(ctx, s, "hot_tag_kernel"));
       hot_lists_kernel<<<(H + 255) / 256, 256, 0, s>>>(HA, L, bounds);
       CDB_TRY(launch_check(ctx, s, "hot_lists_kernel"));
-      uint64_t *wa = w, *wb = w2;
-      uint32_t *va = v, *vb = v2;
-      for (uint32_t span = 1; span < L; span <<= 1) {
-        MergeArgs M;
-        M.bounds = bounds;
-        M.L = L;
-        M.span = span;
-        M.n_jobs = (uint32_t)((uint64_t)H * (L / (2 * span)));
-        M.tiles = toff;
-        M.n_tiles = d_ntiles;
-        M.wi = wa;
-        M.vi = va;
-        M.wo = wb;
-        M.vo = vb;
-        M.unsorted = d_unsorted;
-        M.check = span == 1;
-        MergeArgs Mc = M;
-        Mc.tiles = tcnt;
-        hot_merge_count_kernel<<<(M.n_jobs + 255) / 256, 256, 0, s>>>(Mc);
-        CDB_TRY(launch_check(ctx, s, "hot_merge_count_kernel"));
-        CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, tcnt, M.n_jobs, toff, (uint32_t*)nullptr, d_ntiles, s));
-        const uint64_t tiles_max = tc / kMergeTile + M.n_jobs;
-        hot_merge_split_kernel<<<(uint32_t)((tiles_max + 255) / 256), 256, 0, s>>>(M, splits);
-        CDB_TRY(launch_check(ctx, s, "hot_merge_split_kernel"));
-        hot_merge_kernel<<<(uint32_t)tiles_max, 256, 0, s>>>(M, splits);
-        CDB_TRY(launch_check(ctx, s, "hot_merge_kernel"));
-        std::swap(wa, wb);
-        std::swap(va, vb);
-      }
+      // sampled pairs first: an input out of child order skips the tag for the merge at once
+      hot_sample_kernel<<<1, 256, 0, s>>>(A, HA, L, bounds, d_unsorted);
+      CDB_TRY(launch_check(ctx, s, "hot_sample_kernel"));
       uint32_t unsorted = 0;
       CDB_HIP(hipMemcpyAsync(&unsorted, d_unsorted, 4, hipMemcpyDeviceToHost, s), "d2h");
       CDB_HIP(hipStreamSynchronize(s), "sync");
+      if (!unsorted) {
+        hot_tag_kernel<<<(uint32_t)((tc + kTagChunk - 1) / kTagChunk), 256, 0, s>>>(A, HA);
+        CDB_TRY(launch_check(ctx, s, "hot_tag_kernel"));
+        uint64_t *wa = w, *wb = w2;
+        uint32_t *va = v, *vb = v2;
+        for (uint32_t span = 1; span < L; span <<= 1) {
+          MergeArgs M;
+          M.bounds = bounds;
+          M.L = L;
+          M.span = span;
+          M.n_jobs = (uint32_t)((uint64_t)H * (L / (2 * span)));
+          M.tiles = toff;
+          M.n_tiles = d_ntiles;
+          M.wi = wa;
+          M.vi = va;
+          M.wo = wb;
+          M.vo = vb;
+          M.unsorted = d_unsorted;
+          M.check = span == 1;
+          MergeArgs Mc = M;
+          Mc.tiles = tcnt;
+          hot_merge_count_kernel<<<(M.n_jobs + 255) / 256, 256, 0, s>>>(Mc);
+          CDB_TRY(launch_check(ctx, s, "hot_merge_count_kernel"));
+          CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, tcnt, M.n_jobs, toff, (uint32_t*)nullptr, d_ntiles, s));
+          const uint64_t tiles_max = tc / kMergeTile + M.n_jobs;
+          hot_merge_split_kernel<<<(uint32_t)((tiles_max + 255) / 256), 256, 0, s>>>(M, splits);
+          CDB_TRY(launch_check(ctx, s, "hot_merge_split_kernel"));
+          hot_merge_kernel<<<(uint32_t)tiles_max, 256, 0, s>>>(M, splits);
+          CDB_TRY(launch_check(ctx, s, "hot_merge_kernel"));
+          std::swap(wa, wb);
+          std::swap(va, vb);
+        }
+        CDB_HIP(hipMemcpyAsync(&unsorted, d_unsorted, 4, hipMemcpyDeviceToHost, s), "d2h");
+        CDB_HIP(hipStreamSynchronize(s), "sync");
+        if (!unsorted) {
+          HA.w = wa;
+          HA.v = va;
+          HA.flagged = 1;
+          merged = true;
+          add_stat_kernel<<<1, 1, 0, s>>>(A.stats, ST_HOT_MERGED, tc);
+          CDB_TRY(launch_check(ctx, s, "add_stat_kernel"));
+        }
+      }
       HA.inline_markers = 0;
       if (std::getenv("CDB_HOT_PROF"))  // test hook
         std::fprintf(stderr, "chip_wide: list merge of %u buckets x %u lists: %s\n", H, L,
-                     unsorted ? "a list is not sorted (radix sort)" : "merged");
-      if (!unsorted) {
-        HA.w = wa;
-        HA.v = va;
-        HA.flagged = 1;
-        merged = true;
-        add_stat_kernel<<<1, 1, 0, s>>>(A.stats, ST_HOT_MERGED, tc);
-        CDB_TRY(launch_check(ctx, s, "add_stat_kernel"));
-      }
+                     merged ? "merged" : "a list is not sorted (radix sort)");
     }
     if (!merged) {
       hot_tag_kernel<<<(uint32_t)((tc + kTagChunk - 1) / kTagChunk), 256, 0, s>>>(A, HA);

@@ -457,6 +457,34 @@ __global__ void __launch_bounds__(256) hot_lists_kernel(HotArgs H, uint32_t L, u
   for (uint32_t l = 2 * nr; l <= L; ++l) o[l] = x;
 }
 
+// A cheap early look at whether the lists are sorted, before anything is tagged: 256 sampled pairs
+// of neighbouring children of one list, tagged here (the tag kernel rewrites the same records) and
+// compared. An input whose children are not in child order (a reference snapshot's HashMap order)
+// fails here at once and goes straight to the radix sort; a pass is no proof -- the merge's round
+// 0 checks every element.
+__global__ void __launch_bounds__(256) hot_sample_kernel(BucketArgs A, HotArgs H, uint32_t L,
+                                                         const uint32_t* __restrict__ bounds, uint32_t* unsorted) {
+  if (H.n_children < 2) return;
+  const uint64_t j = 1 + mix64(0x51ED27A3C4B1F00Dull + threadIdx.x) % (H.n_children - 1);
+  const uint32_t h = hot_bucket_of(H, j);
+  const uint32_t* o = bounds + (uint64_t)h * (L + 1);
+  bool first = false;  // j opens its list: no pair
+  for (uint32_t l = 0; l <= L; ++l) first |= o[l] == j;
+  if (first || j <= H.c_off[h]) return;
+  unsigned long long orph = 0;
+  const uint32_t b = H.ids[h], N = A.ncnt[b];
+  uint64_t w[2];
+  for (int k = 0; k < 2; ++k) {
+    const uint64_t x = j - 1 + k;
+    const uint32_t i = (uint32_t)(x - H.c_off[h]);
+    const bool isn = i < N;
+    bool mk = false;
+    w[k] = hot_tag_row(A, H, h, x, isn, hot_fields(A, H, isn, hot_row(A, H, b, i, N)), hot_key_tab(H, H.hk_off[h]),
+                       H.hk_kout[h], orph, &mk);
+  }
+  if (w[1] < w[0]) atomicOr(unsorted, 1u);
+}
+
 struct MergeArgs {
   const uint32_t* bounds;    // hot_lists_kernel
   uint32_t L, span;          // this round merges list groups [2 span m, 2 span m + span) and [.. + span, 2 span (m + 1))
