@@ -728,6 +728,17 @@ class GpuDecode {
   uint64_t raw_front_ = 0;  // the deferred index uploaded the bytes to d_raw_ + raw_front_
   bool early_up_ = false;   // the index pass queued that upload (from the caller's buffer, or chunked)
  public:
+  // The early uploads of a call's snapshots, one after another across their streams (each waits on
+  // the one issued before it), so that the first snapshots land -- and their walks run -- while
+  // the later ones still cross PCIe.
+  struct UpChain {
+    std::mutex mu;
+    hipEvent_t last = nullptr;
+  };
+  UpChain* chain_ = nullptr;
+  bool early_upload() const { return early_up_; }
+ private:
+ public:
   hipStream_t up_s_ = nullptr;  // (several snapshots) this snapshot's own stream: the chunked upload
  private:
   // A snapshot over 512 MB: copied into the batch's huge pages in chunks, each chunk page-locked
@@ -807,13 +818,22 @@ int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTimi
       hipSetDevice(ctx_->device) == hipSuccess &&
       host_register(const_cast<uint8_t*>(buf), len)) {
     reg_.p = const_cast<uint8_t*>(buf);
-    reg_.s = ctx_->stream;
+    hipStream_t us = up_s_ ? up_s_ : ctx_->stream;  // (its walk queues behind it on the same stream)
+    reg_.s = us;
     const uint64_t front = crc_tile_bytes();
     if ((st_ = alloc(&d_raw_.p, front + len + 16, "decode: device buffer for the snapshot bytes")) != CDB_OK)
       return st_;
     raw_front_ = front;
-    ck(hipMemcpyAsync((uint8_t*)d_raw_.p + front, buf, len, hipMemcpyHostToDevice, ctx_->stream), "h2d(index)");
-    ck(hipEventRecord(di_.up.a, ctx_->stream), "event(index)");
+    {
+      std::unique_lock<std::mutex> lk;
+      if (chain_) {
+        lk = std::unique_lock<std::mutex>(chain_->mu);
+        if (chain_->last) ck(hipStreamWaitEvent(us, chain_->last, 0), "wait(upload chain)");
+      }
+      ck(hipMemcpyAsync((uint8_t*)d_raw_.p + front, buf, len, hipMemcpyHostToDevice, us), "h2d(index)");
+      ck(hipEventRecord(di_.up.a, us), "event(index)");
+      if (chain_) chain_->last = di_.up.a;
+    }
     if (st_ != CDB_OK) return st_;
     early_up_ = true;
   }
@@ -1775,6 +1795,7 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
                                 uint32_t flags, Batch* const* outs, cdb_dev_input* din, uint32_t* failed,
                                 size_t* err_off, DecodeTiming* tm) {
   const auto t_start = std::chrono::steady_clock::now();
+  GpuDecode::UpChain up_chain;  // (outlives the decoders that point at it)
   std::vector<std::unique_ptr<GpuDecode>> dec;
   int rc_all = CDB_OK;
   uint64_t tot[3] = {0, 0, 0};
@@ -1797,6 +1818,7 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     // share of the threads; 8 snapshots measured faster unsplit (271 vs 311 ms in all)
     dec.back()->index_threads_ = n <= 4 ? std::max(1u, host_index_threads() / std::max(1u, n)) : 1u;
     dec.back()->up_s_ = ctx->idx_streams[i];
+    dec.back()->chain_ = &up_chain;
   }
   // the deferred DATAS sections: every snapshot's bytes go up with its speculative walk queued
   // behind them on its own stream; the stitch rounds then run per snapshot (below, or on the
@@ -1920,10 +1942,18 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
       if (!seq[i]) par.push_back(i);
     const uint32_t nt = std::min<uint32_t>((uint32_t)par.size(), 16);
     std::atomic<uint32_t> next{0};
+    // (a snapshot whose bytes went up from the index pass -- 64 to 512 MB -- joins the two stages
+    // as soon as it is indexed: its walk runs while later snapshots still upload)
     auto work = [&]() {
+      (void)hipSetDevice(ctx->device);
       for (uint32_t j; (j = next.fetch_add(1)) < par.size();) {
         const uint32_t i = par[j];
         irc[i] = dec[i]->index(bufs[i], lens[i], &ieo[i], nullptr);
+        if (!staged && dec[i]->early_upload()) {
+          launch(i);
+          seq[i] = 1;
+          launched_q.push(i);
+        }
       }
     };
     std::vector<std::thread> th;
