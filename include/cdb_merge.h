@@ -399,6 +399,9 @@ typedef struct cdb_dev_buckets {
 /* Merge outputs.
  *   compact = 1: dense plain columns in caller-allocated keys / nodes / members (at least the
  *     input row counts), keys in key-hash order, cref = (absolute child row, count);
+ *   either layout: a key's children follow in ascending bit-reversed child id (id1), then id2, so
+ *     a result kept as the next merge's input brings its hot keys' children as sorted lists (the
+ *     chip-wide path merges those instead of sorting them; stats.hot_merged_children);
  *   compact = 0: the engine's bucket layout, no compaction pass: the merge points keys / nodes /
  *     members at its own row slots (whole AoS rows: stride0 = stride = 8 words per key row, 6 per
  *     child row; library-owned, valid until the next merge on the ctx) and fills `buckets`. Every row
