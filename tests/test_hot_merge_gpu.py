@@ -157,3 +157,34 @@ def test_c5_bench_size_state_runs_merged(ctx, monkeypatch):
     bench times, merged with the list merge, equal the radix sort's result and the generator rows'."""
     st = _check(ctx, monkeypatch, configs.c5(cdb), _opts())
     assert st.hot_merged_children > 40_000_000
+
+
+def test_one_list_out_of_order_falls_back(ctx, monkeypatch):
+    """State runs with ONE pair of neighbouring children of the hottest key swapped in run 0: the
+    sampled pairs almost surely miss it, round 0 of the merge finds it, and the batch is re-tagged
+    and radix-sorted -- the result equals CDB_HOT_MERGE=0's on the same rows, and nothing counts
+    as merged."""
+    cfg = configs.c5(cdb, universe=300_000, events=3_000_000)
+    state = _gen(ctx, cfg)
+    try:
+        state_runs(cdb, ctx, state)
+        rows = state.members
+        n0 = state.run_start[2][1]  # run 0's member rows
+        kh = wrap(rows.col[0], rows.n)[:n0]
+        rec = wrap(rows.col[1], rows.n * rows.stride).view(rows.n, rows.stride)[:n0]
+        _, inv, counts = torch.unique_consecutive(kh, return_inverse=True, return_counts=True)
+        hot = int(torch.argmax(counts))
+        first = int(torch.nonzero(inv == hot)[0])
+        assert int(counts[hot]) > 1000 and int(rec[first, 1]) != int(rec[first + 1, 1])
+        a, b = rec[first].clone(), rec[first + 1].clone()
+        rec[first].copy_(b)
+        rec[first + 1].copy_(a)
+        torch.cuda.synchronize()
+        got, st = _merge_cols(ctx, state, _opts())
+        assert st.sorted_runs == 1 and st.hot_merged_children == 0
+        monkeypatch.setenv("CDB_HOT_MERGE", "0")
+        want, _ = _merge_cols(ctx, state, _opts())
+    finally:
+        _release(ctx, state)
+    for fam, (x, y) in enumerate(zip(got, want)):
+        assert x.shape == y.shape and torch.equal(x, y), fam
