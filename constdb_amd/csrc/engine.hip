@@ -739,7 +739,7 @@ namespace {
 cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& wide_ids,
                      const std::vector<uint32_t>& hk_off, const std::vector<uint32_t>& c_off, uint64_t tk,
                      uint64_t tc, uint64_t cmax, uint64_t kmax, const RunView* rv, const RunView* orv,
-                     hipStream_t s) {
+                     uint64_t child_rows, hipStream_t s) {
   cdb_status st = CDB_OK;
   const bool run_order = orv != nullptr;  // sorted-run input (rv: and this batch reads its children from the runs)
   const uint32_t H = (uint32_t)wide_ids.size();
@@ -801,7 +801,7 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   CDB_HIP(hipMemcpyAsync(d_hk_off, hk_off.data(), (H + 1) * 4, hipMemcpyHostToDevice, s), "h2d");
   CDB_HIP(hipMemcpyAsync(d_c_off, c_off.data(), (H + 1) * 4, hipMemcpyHostToDevice, s), "h2d");
   const uint64_t nk = std::max<uint64_t>(tk, 1), nc = std::max<uint64_t>(tc, 1);
-  uint8_t* kt = (uint8_t*)ws_get(ctx, WS_HOTK, nk * (4 * 8 + 3 * 4) + 64, &st);
+  uint8_t* kt = (uint8_t*)ws_get(ctx, WS_HOTK, nk * (4 * 8 + 4 * 4) + 64, &st);
   if (!kt) return st;
   HA.hk_h = (uint64_t*)kt;
   HA.hk_f = HA.hk_h + nk;
@@ -810,6 +810,7 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   HA.hk_tp = (uint32_t*)(HA.hk_sum + nk);
   HA.hk_cnt = HA.hk_tp + nk;
   HA.hk_cb = HA.hk_cnt + nk;
+  HA.hk_bkt = HA.hk_cb + nk;
   // (+ 40 B per child: the global fold's per-run stash, fold_rec / fold_hg)
   uint8_t* ct = (uint8_t*)ws_get(ctx, WS_HOTCH, nc * (32 + 2 * 8 + 2 * 4 + 6 * 4 + 40) + 64, &st);
   if (!ct) return st;
@@ -865,6 +866,10 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   const uint32_t grid = (uint32_t)std::min<uint64_t>((tc + 255) / 256, 16384);
   if (tc) {
     HA.small_keys = kmax <= kTagKeys ? 1 : 0;
+    // the global path's fold reads each child's row itself (v = the row): the tag writes no 32-B
+    // records (test hook CDB_HOT_DIRECT=0: the records)
+    const char* direct_env = std::getenv("CDB_HOT_DIRECT");
+    HA.direct = child_rows < (1ull << 30) && !(direct_env && direct_env[0] == '0');
     // Children read from the runs: their lists are merged when they arrive sorted (a merge
     // result's child order, hot.hip.h), else radix-sorted (test hook CDB_HOT_MERGE=0: always sorted)
     const char* merge_env = std::getenv("CDB_HOT_MERGE");
@@ -992,7 +997,7 @@ constexpr uint64_t kHotKeyCap = 1ull << 23;
 // most kCapK keys) had only their keys copied (MatArgs): those take the chip-wide path in runs
 // mode, in batches of their own.
 cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list, uint32_t hot, hipStream_t s,
-                         const RunView* rv = nullptr, uint32_t runs_child_max = 0) {
+                         const RunView* rv = nullptr, uint32_t runs_child_max = 0, uint64_t child_rows = ~0ull) {
   cdb_status st = CDB_OK;
   uint32_t* d_cnt3 = (uint32_t*)ws_get(ctx, WS_HOTC3, 4ull * hot * sizeof(uint32_t), &st);
   if (!d_cnt3) return st;
@@ -1035,7 +1040,7 @@ cdb_status over_capacity(cdb_ctx* ctx, BucketArgs& A, const uint32_t* d_hot_list
                    hot, wide_ids.size(),
                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count(), sort_ms);
     const cdb_status r =
-        chip_wide(ctx, A, wide_ids, hk_off, c_off, tk, tc, cmax, kmax, runs_batch ? rv : nullptr, rv, s);
+        chip_wide(ctx, A, wide_ids, hk_off, c_off, tk, tc, cmax, kmax, runs_batch ? rv : nullptr, rv, child_rows, s);
     wide_ids.clear();
     hk_off.assign(1, 0);
     c_off.assign(1, 0);
@@ -1475,7 +1480,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     CDB_TRY(launch_check(ctx, s, "mat_copy_kernel"));
   }
   if (mid_wide) {
-    CDB_TRY(over_capacity(ctx, A, d_big_list, counts[1], s, use_runs ? &RV : nullptr, runs_child_max));
+    CDB_TRY(over_capacity(ctx, A, d_big_list, counts[1], s, use_runs ? &RV : nullptr, runs_child_max, std::max(N, M)));
   } else {
     bucket_mid_kernel<<<std::min<uint64_t>(nb, 2048), kBktThreads, 0, s>>>(A, d_big_list, d_big_count);
     CDB_TRY(launch_check(ctx, s, "bucket_mid_kernel"));
@@ -1488,7 +1493,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   const uint32_t hot = mid_wide ? 0 : counts[0];
   // (sorted-run input: the forwarded buckets' rows were copied in run order -- their child lists
   // can be merged, and the small ones take the per-bucket LDS path)
-  if (hot) CDB_TRY(over_capacity(ctx, A, d_hot_list, hot, s, use_runs ? &RV : nullptr, 0));
+  if (hot) CDB_TRY(over_capacity(ctx, A, d_hot_list, hot, s, use_runs ? &RV : nullptr, 0, std::max(N, M)));
 
   // ---- 5. dense compaction into the caller's output columns (already done range by range when
   //         the bucket phase was pipelined and no workgroup tier added outputs)

@@ -79,6 +79,10 @@ struct HotArgs {
   int small_keys;            // every bucket of the batch has at most kTagKeys output keys: the tag
                              // kernel searches its buckets' key tables in LDS
   int flagged;               // the sorted tags may hold inline markers (v's kInlineMarker bit)
+  int direct;                // global path: v = the child's row (| kMemberBit for a member row),
+                             // the fold reads the row itself; no rec records, no c_h; a key's
+                             // bucket from hk_bkt
+  uint32_t* hk_bkt;          // per key G: its bucket h
   int inline_markers;        // tag: a child that takes no part keeps the W it would have (its list
                              // stays sorted for the merge) and is flagged in v (kInlineMarker)
                              // instead of getting the bucket's marker
@@ -109,6 +113,7 @@ __device__ __forceinline__ bool hot_takes_part(uint64_t W) { return (W & 63) != 
 // v's top bit: a child that takes no part, tagged with its own W (HotArgs::inline_markers); the low
 // 31 bits are the flat index.
 constexpr uint32_t kInlineMarker = 0x80000000u;
+constexpr uint32_t kMemberBit = 0x40000000u;  // (direct mode: v's family bit; rows below 2^30)
 __device__ __forceinline__ bool hot_row_part(uint64_t W, uint32_t v) { return hot_takes_part(W) && !(v & kInlineMarker); }
 
 // The key phase's LDS (bucket_keys touches no child arrays): sized for KC key rows, so that batches
@@ -144,6 +149,7 @@ __global__ void __launch_bounds__(kBktThreads) hot_keys_kernel(BucketArgs A, Hot
     H.hk_tp[g0 + o] = S.otp[o];
     H.hk_cnt[g0 + o] = 0;
     H.hk_cb[g0 + o] = kNone;
+    H.hk_bkt[g0 + o] = h;
   }
   if (threadIdx.x == 0) H.hk_kout[h] = kout;
   __syncthreads();
@@ -265,8 +271,10 @@ __device__ __forceinline__ uint64_t hot_tag_row(const BucketArgs& A, const HotAr
     }
   }
   // the fold reads a child's four fields as one 32-B record (flat order: written in sequence)
-  H.rec[2 * j] = make_ulonglong2(id1, id2);
-  H.rec[2 * j + 1] = make_ulonglong2(t, m);
+  if (!H.direct) {
+    H.rec[2 * j] = make_ulonglong2(id1, id2);
+    H.rec[2 * j + 1] = make_ulonglong2(t, m);
+  }
   return w;
 }
 
@@ -354,8 +362,12 @@ __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
     }
     bool mk = false;
     H.w[j] = hot_tag_row(A, H, h, j, isn, hot_fields(A, H, isn, row), T, H.hk_kout[h], orph, &mk);
-    H.v[j] = (uint32_t)j | (mk ? kInlineMarker : 0u);
-    H.c_h[j] = h | (isn ? 0u : 0x80000000u);
+    if (H.direct) {
+      H.v[j] = row | (isn ? 0u : kMemberBit) | (mk ? kInlineMarker : 0u);
+    } else {
+      H.v[j] = (uint32_t)j | (mk ? kInlineMarker : 0u);
+      H.c_h[j] = h | (isn ? 0u : 0x80000000u);
+    }
   }
   if (orph) atomicAdd(&stat_shard(A.stats)[ST_ORPHANS], orph);
 }
@@ -365,8 +377,36 @@ struct HotChild {
   uint64_t id1, id2, t, meta;
   uint32_t j;
 };
-__device__ __forceinline__ HotChild hot_child(const HotArgs& H, uint32_t j) {
-  const ulonglong2 a = H.rec[2 * (uint64_t)j], b = H.rec[2 * (uint64_t)j + 1];
+// A child's fold fields (id1, id2) and (t, meta): its 32-B record, or (direct) its row.
+__device__ __forceinline__ void hot_rec(const BucketArgs& A, const HotArgs& H, uint32_t j, ulonglong2& a,
+                                        ulonglong2& c) {
+  if (!H.direct) {
+    a = H.rec[2 * (uint64_t)j];
+    c = H.rec[2 * (uint64_t)j + 1];
+    return;
+  }
+  const bool isn = !(j & kMemberBit);
+  const uint32_t row = j & (kMemberBit - 1);
+  if (H.runs) {
+    const uint64_t* const* col = isn ? H.V.nin : H.V.min;
+    const uint32_t st = isn ? H.V.ns : H.V.ms;
+    if (st > 1) {  // records: pkf id1 id2 t meta
+      const uint64_t* r = col[1] + (uint64_t)row * st;
+      a = make_ulonglong2(r[1], r[2]);
+      c = make_ulonglong2(r[3], r[4]);
+    } else {
+      a = make_ulonglong2(col[C_ID1][row], col[C_ID2][row]);
+      c = make_ulonglong2(col[C_T][row], col[C_META][row]);
+    }
+  } else {
+    const ulonglong2* r = (const ulonglong2*)((isn ? A.nr : A.mr) + (uint64_t)row * kChildStride);
+    a = r[1];
+    c = r[2];
+  }
+}
+__device__ __forceinline__ HotChild hot_child(const BucketArgs& A, const HotArgs& H, uint32_t j) {
+  ulonglong2 a, b;
+  hot_rec(A, H, j, a, b);
   HotChild c;
   c.id1 = a.x;
   c.id2 = a.y;
@@ -684,7 +724,8 @@ __device__ __forceinline__ void hot_fold_run(const BucketArgs& A, const HotArgs&
 #pragma unroll
     for (uint32_t k = 0; k < kFoldFast; ++k) {
       if (pk[k]) {
-        const ulonglong2 a = H.rec[2 * (uint64_t)rj[k]], c = H.rec[2 * (uint64_t)rj[k] + 1];
+        ulonglong2 a, c;
+        hot_rec(A, H, rj[k], a, c);
         xi1[k] = a.x;
         xi2[k] = a.y;
         xt[k] = c.x;
@@ -746,7 +787,7 @@ __device__ __forceinline__ void hot_fold_run(const BucketArgs& A, const HotArgs&
         const ulonglong2 a = fs[0], c = fs[1];
         put(a.x, a.y, c.x, c.y, a.y);
       } else if (emitted) {
-        const HotChild x = hot_child(H, jat(q));
+        const HotChild x = hot_child(A, H, jat(q));
         put(x.id1, x.id2, x.t, x.meta, *fv);
       }
     }
@@ -766,7 +807,7 @@ __device__ __forceinline__ void hot_fold_run(const BucketArgs& A, const HotArgs&
     bool have = false;
     for (uint32_t k = 0; k < kslow; ++k) {
       if (slow && k < nrows && step < nrows && (k == 0 || part(k))) {
-        const HotChild x = hot_child(H, jat(k));
+        const HotChild x = hot_child(A, H, jat(k));
         const bool after = step == 0 || hot_before(last, x, isn);
         const bool take = after && (!have || hot_before(x, c, isn));
         c.id1 = take ? x.id1 : c.id1;
@@ -823,8 +864,11 @@ __global__ void __launch_bounds__(256) hot_fold_kernel(BucketArgs A, HotArgs H, 
       uint64_t e = p + 1;  // (inline markers inside the run are rows of it; the fold skips them)
       while (e < H.n_children && (H.w[e] >> 6) == (W >> 6) && hot_takes_part(H.w[e])) ++e;
       nrows = (uint32_t)(e - p);
-      hc = H.c_h[H.v[p] & ~kInlineMarker];
       G = (uint32_t)(W >> H.g_shift);
+      if (H.direct)
+        hc = H.hk_bkt[G] | ((H.v[p] & kMemberBit) ? 0x80000000u : 0u);
+      else
+        hc = H.c_h[H.v[p] & ~kInlineMarker];
     } else if (kept) {
       const uint2 hg = H.fold_hg[i];
       hc = hg.x;
