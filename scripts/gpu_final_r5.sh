@@ -1,14 +1,26 @@
 #!/bin/bash
-# Round-5 final records: the GPU suite and smoke, then every config's bench line, kernel trace and
-# FETCH/WRITE passes (scripts/gpu_round.sh), the decode figures. Output under gpurun_out/.
+# Round-5 final records: smoke, the GPU suite with the first config's round, then every config's
+# bench line, kernel trace and FETCH/WRITE passes (scripts/gpu_round.sh), the decode figures.
+#   CONFIGS  configs in order (default "c4 c5 c1 c3"); the first one also runs the GPU suite
+#   DECODE   non-empty: scripts/bench_decode.py --device-snapshots 8 at the end
+#   TAG      output name suffix (default r5z)
+# Output under gpurun_out/. (The records: TAG=r5z with the default configs and DECODE=1, then
+# TAG=r5y CONFIGS="c5 c3" after the chip-wide direct-row fold.)
 set -o pipefail
 export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out
+T=${TAG:-r5z}
 mkdir -p $O
-timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_r5z.log 2>&1 || { echo "smoke failed"; tail -5 $O/smoke_r5z.log; exit 1; }
-tail -1 $O/smoke_r5z.log
-TAG=r5z CONFIG=c4 GENERAL_PMC=1 bash scripts/gpu_round.sh || exit 2
-for c in c5 c1 c3; do NO_TESTS=1 TAG=r5z CONFIG=$c GENERAL_PMC=1 bash scripts/gpu_round.sh || exit 3; done
-timeout -k 10 400 python scripts/bench_decode.py --device-snapshots 8 > $O/bench_decode_r5z.json 2> $O/bench_decode_r5z.err || exit 4
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_$T.log 2>&1 || { echo "smoke failed"; tail -5 $O/smoke_$T.log; exit 1; }
+tail -1 $O/smoke_$T.log
+first=1
+for c in ${CONFIGS:-c4 c5 c1 c3}; do
+  if [ $first = 1 ]; then TAG=$T CONFIG=$c GENERAL_PMC=1 bash scripts/gpu_round.sh || exit 2
+  else NO_TESTS=1 TAG=$T CONFIG=$c GENERAL_PMC=1 bash scripts/gpu_round.sh || exit 3; fi
+  first=0
+done
+if [ -n "$DECODE" ]; then
+  timeout -k 10 400 python scripts/bench_decode.py --device-snapshots 8 > $O/bench_decode_$T.json 2> $O/bench_decode_$T.err || exit 4
+fi
 echo "final ok"
