@@ -603,10 +603,32 @@ __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_runs_kernel(Wave
       const int i = __builtin_ctzll(m);
       m &= m - 1;
       const uint32_t bb = W.blo + g * 64 + i;
-      const WaveDir d = load_dir(W.A, bb);
-      const RunMap qk = run_map(W.V, bb, lane, false), qc = run_map(W.V, bb, lane, true);
       WaveIn<2> in;
-      load_runs<2>(W, d, qk, qc, lane, in);
+      if (W.V.bdir) {  // (wave-uniform) the bucket-major directory: one load, no directory entry
+        WaveDir d;
+        const PipeMap q = pipe_map(W.V, pipe_pairs(W.V, bb, lane, true), d);
+        in.d = d;
+        const uint32_t C = d.N + d.M;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const uint32_t c = lane + 64 * e;
+          zero_key_slot(e, in);
+          const uint32_t row = pipe_row(q, 0, 8, c);
+          if (c < d.K) load_key_row(W.V, row, e, in);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t c = lane + 64 * e;
+          zero_child_slot(e, in);
+          if (__ballot(c < C) == 0) continue;  // (uniform) no child in this slot group
+          const uint32_t row = pipe_row(q, 16, 16, c);
+          if (c < C) load_child_row(W.V, c < d.N, row, e, in);
+        }
+      } else {
+        const WaveDir d = load_dir(W.A, bb);
+        const RunMap qk = run_map(W.V, bb, lane, false), qc = run_map(W.V, bb, lane, true);
+        load_runs<2>(W, d, qk, qc, lane, in);
+      }
       wave_bucket<2>(W, lds_all[wv], bb, lane, in, []() {});
       wave_sync();  // (the next bucket reuses this one's LDS)
     }
