@@ -745,6 +745,15 @@ class GpuDecode {
   // and uploaded on up_s_ as soon as it is copied, so PCIe works while the host copies. False:
   // nothing queued (the call then takes the batch-copy path).
   bool chunked_upload(const uint8_t* buf, size_t len);
+  bool pre_chunked_ = false;  // pre_upload() did the chunked upload: index() goes straight to its pass
+ public:
+  // A snapshot over 512 MB: its chunked copy and upload ahead of (and on another thread than) its
+  // host index pass, so that pass overlaps the next snapshot's copy and upload.
+  void pre_upload(const uint8_t* buf, size_t len) {
+    if (buf && len > (size_t(512) << 20) && up_s_ && hipSetDevice(ctx_->device) == hipSuccess)
+      pre_chunked_ = chunked_upload(buf, len);
+  }
+ private:
   bool emit_pending_ = false;  // emit_launch -> emit_finish
   bool own_ = false;           // emit_own: the rows are in own_rows_ (records: hash column + records)
   DevBuf own_rows_;
@@ -837,8 +846,8 @@ int GpuDecode::index(const uint8_t* buf, size_t len, size_t* err_off, DecodeTimi
     if (st_ != CDB_OK) return st_;
     early_up_ = true;
   }
-  const bool chunked = !early_up_ && !staged && buf && len > (size_t(512) << 20) && up_s_ &&
-                       hipSetDevice(ctx_->device) == hipSuccess && chunked_upload(buf, len);
+  const bool chunked = pre_chunked_ || (!early_up_ && !staged && buf && len > (size_t(512) << 20) && up_s_ &&
+                                        hipSetDevice(ctx_->device) == hipSuccess && chunked_upload(buf, len));
   if (st_ != CDB_OK) return st_;
   // (chunked: the bytes are in the batch already)
   rc_ = index_snapshot(chunked ? nullptr : buf, len, flags_, out_, &idx_, err_off, &dcrc_, index_threads_, &defer_,
@@ -1930,13 +1939,25 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
       }
     };
     std::thread walk_th(walk_stage), device_th(device_stage);
+    // snapshots over 512 MB: this thread copies and uploads them one after another; a thread of
+    // their own runs each one's host index pass (and launches its walk) as soon as its bytes are
+    // in the batch, while the next one copies and uploads
+    Queue uploaded;
+    std::thread index_th([&]() {
+      (void)hipSetDevice(ctx->device);
+      for (uint32_t i; uploaded.pop(&i);) {
+        irc[i] = dec[i]->index(bufs[i], lens[i], &ieo[i], nullptr);
+        launch(i);
+        launched_q.push(i);
+      }
+    });
     for (uint32_t i = 0; i < n; ++i) {
       if (staged || lens[i] <= (size_t(512) << 20)) continue;
-      irc[i] = dec[i]->index(bufs[i], lens[i], &ieo[i], nullptr);
-      launch(i);
       seq[i] = 1;
-      launched_q.push(i);
+      dec[i]->pre_upload(bufs[i], lens[i]);
+      uploaded.push(i);
     }
+    uploaded.close();
     std::vector<uint32_t> par;
     for (uint32_t i = 0; i < n; ++i)
       if (!seq[i]) par.push_back(i);
@@ -1960,6 +1981,7 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
     for (uint32_t t = 1; t < nt; ++t) th.emplace_back(work);
     if (nt) work();
     for (auto& t : th) t.join();
+    index_th.join();
     launched_q.close();
     walk_th.join();
     device_th.join();
