@@ -3,7 +3,7 @@
 # bench line, kernel trace and FETCH/WRITE passes (scripts/gpu_round.sh), the decode figures.
 #   CONFIGS  configs in order (default "c4 c5 c1 c3"); the first one also runs the GPU suite
 #   DECODE   non-empty: scripts/bench_decode.py --device-snapshots 8 at the end
-#   TAG      output name suffix (default r5z)
+#   TAG      output name suffix (default r5z); NO_TESTS: no GPU suite
 # Output under gpurun_out/. (The records: TAG=r5z with the default configs and DECODE=1, then
 # TAG=r5y CONFIGS="c5 c3" after the chip-wide direct-row fold.)
 set -o pipefail
@@ -16,7 +16,7 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke_
 tail -1 $O/smoke_$T.log
 first=1
 for c in ${CONFIGS:-c4 c5 c1 c3}; do
-  if [ $first = 1 ]; then TAG=$T CONFIG=$c GENERAL_PMC=1 bash scripts/gpu_round.sh || exit 2
+  if [ $first = 1 ] && [ -z "$NO_TESTS" ]; then TAG=$T CONFIG=$c GENERAL_PMC=1 bash scripts/gpu_round.sh || exit 2
   else NO_TESTS=1 TAG=$T CONFIG=$c GENERAL_PMC=1 bash scripts/gpu_round.sh || exit 3; fi
   first=0
 done
