@@ -960,11 +960,12 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
     HA.fold_q = HA.v == v ? v2 : v;
     HA.run_count = d_runs;
     HA.run_list = run_list;
-    // run starts -> run list (ascending): flags in emit_n, their scan in rank_n
-    hot_runflag_kernel<<<grid, 256, 0, s>>>(HA, HA.emit_n);
-    CDB_TRY(launch_check(ctx, s, "hot_runflag_kernel"));
-    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, HA.emit_n, tc, rank_n, (uint32_t*)nullptr, d_runs, s));
-    hot_runlist_kernel<<<grid, 256, 0, s>>>(HA, HA.emit_n, rank_n);
+    // run starts -> run list (ascending): per-tile counts in emit_n, their scan in rank_n
+    const uint32_t ntile = (uint32_t)((tc + kRunTile - 1) / kRunTile);
+    hot_runcount_kernel<<<ntile, 256, 0, s>>>(HA, HA.emit_n);
+    CDB_TRY(launch_check(ctx, s, "hot_runcount_kernel"));
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, HA.emit_n, ntile, rank_n, (uint32_t*)nullptr, d_runs, s));
+    hot_runlist_kernel<<<ntile, 256, 0, s>>>(HA, rank_n);
     CDB_TRY(launch_check(ctx, s, "hot_runlist_kernel"));
     hot_first_run_kernel<<<(H + 255) / 256, 256, 0, s>>>(HA);
     CDB_TRY(launch_check(ctx, s, "hot_first_run_kernel"));

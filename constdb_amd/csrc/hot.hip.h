@@ -425,23 +425,76 @@ __device__ __forceinline__ bool hot_before(const HotChild& a, const HotChild& b,
   return a.j < b.j;
 }
 
-// Run starts: flag per sorted position (then an exclusive scan gives each run its index).
-__global__ void __launch_bounds__(256) hot_runflag_kernel(HotArgs H, uint32_t* __restrict__ flag) {
-  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < H.n_children;
-       p += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t W = H.w[p];
-    // a run: equal W but the pos bits, from its first row that takes part (a bucket's marker never
-    // starts one; one before W belongs to an earlier bucket, so it never hides a start either;
-    // inline markers sit inside runs)
-    bool start = H.flagged ? hot_row_part(W, H.v[p]) : hot_takes_part(W);
-    if (!H.flagged) start = start && !(p > 0 && (H.w[p - 1] >> 6) == (W >> 6));
-    for (uint64_t q = p; H.flagged && start && q > 0;) {
-      --q;
-      const uint64_t X = H.w[q];
-      if ((X >> 6) != (W >> 6)) break;
-      if (hot_row_part(X, H.v[q])) start = false;
+// Does sorted position p start a run?
+__device__ __forceinline__ bool hot_run_start(const HotArgs& H, uint64_t p) {
+  const uint64_t W = H.w[p];
+  // a run: equal W but the pos bits, from its first row that takes part (a bucket's marker never
+  // starts one; one before W belongs to an earlier bucket, so it never hides a start either;
+  // inline markers sit inside runs)
+  bool start = H.flagged ? hot_row_part(W, H.v[p]) : hot_takes_part(W);
+  if (!H.flagged) start = start && !(p > 0 && (H.w[p - 1] >> 6) == (W >> 6));
+  for (uint64_t q = p; H.flagged && start && q > 0;) {
+    --q;
+    const uint64_t X = H.w[q];
+    if ((X >> 6) != (W >> 6)) break;
+    if (hot_row_part(X, H.v[q])) start = false;
+  }
+  return start;
+}
+// hot_run_start for the wave's 64 consecutive positions p (lane order; inb: p is a position): in
+// flagged mode the nearest earlier row that takes part, when the wave holds one, decides by its key
+// alone (sorted W: an equal key means p is not the first, a smaller one that it is); only a wave's
+// first such row scans back through memory.
+__device__ __forceinline__ bool hot_run_start_wave(const HotArgs& H, uint64_t p, bool inb, int lane) {
+  if (!H.flagged) return inb && hot_run_start(H, p);
+  const uint64_t W = inb ? H.w[p] : 0;
+  const bool part = inb && hot_row_part(W, H.v[p]);
+  const uint64_t below = __ballot(part) & ((1ull << lane) - 1);
+  const int src = below ? 63 - __builtin_clzll(below) : lane;
+  const uint32_t klo = (uint32_t)__shfl((int)(uint32_t)(W >> 6), src, 64);
+  const uint32_t khi = (uint32_t)__shfl((int)(uint32_t)(W >> 38), src, 64);
+  if (!part) return false;
+  if (below) return (((uint64_t)khi << 32) | klo) != (W >> 6);
+  return hot_run_start(H, p);
+}
+// Run starts -> run list, in two passes over tiles of kRunTile sorted positions (one workgroup of
+// 256 each): count each tile's starts, scan the counts, then write each tile's starts at its
+// offset in position order. (Replaces a flag per position and a scan over all of them: 24 B per
+// child read instead of 36 B read and written.)
+constexpr uint32_t kRunTile = 4096;
+__global__ void __launch_bounds__(256) hot_runcount_kernel(HotArgs H, uint32_t* __restrict__ tile_n) {
+  __shared__ uint32_t tot;
+  if (threadIdx.x == 0) tot = 0;
+  __syncthreads();
+  const uint64_t p0 = (uint64_t)blockIdx.x * kRunTile;
+  const uint64_t p1 = min<uint64_t>(p0 + kRunTile, H.n_children);
+  uint32_t n = 0;  // (wave-uniform)
+  for (uint64_t p = p0 + threadIdx.x; p - threadIdx.x < p1; p += 256)
+    n += (uint32_t)__popcll(__ballot(hot_run_start_wave(H, p, p < p1, (int)(threadIdx.x & 63))));
+  if ((threadIdx.x & 63) == 0) atomicAdd(&tot, n);
+  __syncthreads();
+  if (threadIdx.x == 0) tile_n[blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(256) hot_runlist_kernel(HotArgs H, const uint32_t* __restrict__ tile_off) {
+  __shared__ uint32_t wn[2][4];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t p0 = (uint64_t)blockIdx.x * kRunTile;
+  const uint64_t p1 = min<uint64_t>(p0 + kRunTile, H.n_children);
+  uint32_t base = tile_off[blockIdx.x];
+  int par = 0;
+  for (uint64_t p = p0 + threadIdx.x; p - threadIdx.x < p1; p += 256, par ^= 1) {
+    const bool s = hot_run_start_wave(H, p, p < p1, lane);
+    const uint64_t m = __ballot(s);
+    if (lane == 0) wn[par][wv] = (uint32_t)__popcll(m);
+    __syncthreads();  // (two count buffers: the next round writes the other one)
+    uint32_t before = 0, all = 0;
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t c = wn[par][k];
+      before += k < wv ? c : 0u;
+      all += c;
     }
-    flag[p] = start;
+    if (s) H.run_list[base + before + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint32_t)p;
+    base += all;
   }
 }
 __global__ void __launch_bounds__(256) hot_runlist_kernel(HotArgs H, const uint32_t* __restrict__ flag,
