@@ -429,6 +429,8 @@ def run_single_process(cdb, args):
         acc["exchange"] += xs.exchange_ms
         acc["merge"] += xs.merge_ms
     t1 = time.perf_counter()
+    if len(set(devs)) > 1 and xs.transport != 1 and os.environ.get("CDB_SHARD_TRANSPORT") != "peer":
+        raise SystemExit(f"distinct devices {devs} exchanged rows by transport {xs.transport}, not RCCL")
     ms = (t1 - t0) * 1e3 / args.steps
     per = {k: v / args.steps for k, v in acc.items()}
     entries = sum(s.key_rows_in for s in sts)

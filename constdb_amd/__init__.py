@@ -130,7 +130,8 @@ class MergeStats(ctypes.Structure):
         "hot_buckets", "wide_buckets", "mid_buckets")] + [(n, ctypes.c_double) for n in (
         "device_ms", "partition_ms", "bucket_ms", "finish_ms")] + [("sorted_runs", ctypes.c_uint64),
                                                                   ("hot_slow_runs", ctypes.c_uint64),
-                                                                  ("hot_merged_children", ctypes.c_uint64)]
+                                                                  ("hot_merged_children", ctypes.c_uint64),
+                                                                  ("wave_pipe_buckets", ctypes.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -357,7 +358,8 @@ class Context:
             st = lib().cdb_ctx_create_multi(ctypes.byref(self._ctx), len(devices), arr)
             self.device = devices[0]
         if st != OK:
-            _raise(st, "no HIP device" if st == NO_DEVICE else "cdb_ctx_create failed")
+            why = lib().cdb_last_error(None).decode(errors="replace") if devices is not None else ""
+            _raise(st, why or ("no HIP device" if st == NO_DEVICE else "cdb_ctx_create failed"))
 
     @property
     def n_devices(self) -> int:
@@ -486,6 +488,10 @@ def decode_snapshots_device(ctx: "Context", snaps, reference_checksum: bool = Fa
     stay in HBM with the batches (cdb_encode_device). A snapshot may also be a CPU uint8 tensor
     (for instance page-locked memory): its bytes are passed in place."""
     n = len(snaps)
+    for x in snaps:
+        if hasattr(x, "data_ptr") and not (getattr(x, "device", None) is not None and x.device.type == "cpu"
+                                           and str(x.dtype) == "torch.uint8" and x.is_contiguous()):
+            raise TypeError("a snapshot tensor must be a contiguous CPU uint8 tensor (its bytes are read on the host)")
     datas = [x if hasattr(x, "data_ptr") else bytes(x) for x in snaps]
     bufs = (ctypes.c_char_p * max(n, 1))(*[ctypes.cast(x.data_ptr(), ctypes.c_char_p) if hasattr(x, "data_ptr")
                                            else x for x in datas])

@@ -12,6 +12,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -137,6 +138,9 @@ cdb_status staged_d2h(cdb_ctx* ctx, void* host, const void* dev, size_t bytes, h
 
 cdb_status staged_copy(cdb_ctx* ctx, const HostSeg* segs, size_t nseg, bool h2d, hipStream_t stream) {
   cdb_status st;
+  // one ring per context: the decoder's stage threads may stage side by side (decode_gpu.hip), so
+  // a call holds the ring -- its lazy allocation, slot cursor and slot events -- until it is done
+  std::lock_guard<std::mutex> ring(ctx->pin_mu);
   if (!ctx->pin) {
     if ((st = hip_check(ctx, hipHostMalloc(&ctx->pin, kStageSlots * kStageChunk, hipHostMallocDefault),
                         "hipHostMalloc(staging)")) != CDB_OK) {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -22,6 +23,7 @@ struct cdb_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;    // (timing disabled)
   hipEvent_t ev_pfork = nullptr, ev_pn = nullptr, ev_pm = nullptr;
   hipEvent_t ev_cs = nullptr, ev_cw = nullptr, ev_cdone = nullptr;  // pipelined compaction (side2)
+  std::mutex pin_mu;  // staged_copy's pinned ring (pin, pin_next, pin_ev): the decoder's threads share it
   std::string last_error;
   struct Buf { void* p = nullptr; size_t bytes = 0; };
   Buf ws[48];  // named workspace slots, grown on demand, reused across calls
@@ -81,6 +83,8 @@ int decode_snapshots_gpu_device(cdb_ctx* ctx, const uint8_t* const* bufs, const 
                                 uint32_t flags, Batch* const* outs, cdb_dev_input* din, uint32_t* failed,
                                 size_t* err_off, DecodeTiming* tm);
 cdb_status fail(cdb_ctx* ctx, cdb_status st, const std::string& msg);
+// Records why a context could not be created (cdb_last_error(NULL)); returns st.
+cdb_status set_create_error(cdb_status st, const std::string& msg);
 // The device merge pipeline (engine.hip) on stream s of ctx's device.
 cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_merge_opts* opts, cdb_dev_output* out,
                              cdb_merge_stats* stats, hipStream_t s);

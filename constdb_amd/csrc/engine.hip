@@ -31,6 +31,15 @@ cdb_status fail(cdb_ctx* ctx, cdb_status st, const std::string& msg) {
   return st;
 }
 
+// The last failed context creation's message (cdb_last_error(NULL)): no context exists to hold it.
+std::mutex g_create_mu;
+std::string g_create_error;
+cdb_status set_create_error(cdb_status st, const std::string& msg) {
+  std::lock_guard<std::mutex> g(g_create_mu);
+  g_create_error = msg;
+  return st;
+}
+
 cdb_status hip_check(cdb_ctx* ctx, hipError_t e, const char* what) {
   if (e == hipSuccess) return CDB_OK;
   return fail(ctx, e == hipErrorOutOfMemory ? CDB_OUT_OF_MEMORY : CDB_DEVICE_ERROR,
@@ -46,18 +55,18 @@ cdb_status launch_check(cdb_ctx* ctx, hipStream_t s, const char* what) {
   return st;
 }
 
-// The persistent wave tier (bucket_wave_pipe_kernel) on runs of at most 8 per family;
-// CDB_WAVE_PIPE=0 runs the one-bucket-per-wave kernel instead (A/B and test hook).
-// The persistent wave tier pays off from this many buckets on: below it, its resident grid is mostly
-// claiming and the wide tier's buckets wait behind it (C1's 100K buckets: 0.33 -> 0.70 ms of bucket
-// phase with it; C3's few thousand large buckets likewise).
+// The persistent wave tier (bucket_wave_pipe_kernel) on runs of at most 8 per family. It pays off
+// from kPipeMinBuckets buckets on: below it, its resident grid is mostly claiming and the wide tier's
+// buckets wait behind it (C1's 100K buckets: 0.33 -> 0.70 ms of bucket phase with it; C3's few
+// thousand large buckets likewise). Test and A/B hook, read per merge: CDB_WAVE_PIPE=0 runs the
+// one-bucket-per-wave kernel instead, CDB_WAVE_PIPE=force runs the persistent kernel at any bucket
+// count (the parity tests pin it against the oracle at sizes the oracle folds in seconds).
 constexpr uint64_t kPipeMinBuckets = 1ull << 19;
-bool pipe_wave_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("CDB_WAVE_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+bool pipe_wave_wanted(uint64_t nb) {
+  const char* e = std::getenv("CDB_WAVE_PIPE");
+  if (e && e[0] == '0') return false;
+  if (e && std::strcmp(e, "force") == 0) return true;
+  return nb >= kPipeMinBuckets;
 }
 // Its grid: every workgroup slot of the device (resident workgroups per CU x CUs).
 uint32_t pipe_wave_grid(cdb_ctx* ctx) {
@@ -660,7 +669,7 @@ cdb_status runs_directory(cdb_ctx* ctx, const cdb_dev_input* in, const InLayout&
     V->rs_sum[f] = (uint32_t)rs_sum;
   }
   V->bdir = nullptr;
-  if (nr <= 8 && nb >= kPipeMinBuckets && pipe_wave_enabled()) {
+  if (nr <= 8 && pipe_wave_wanted(nb)) {
     // the persistent wave tier's bucket-major directory, built with the three bucket directories
     uint32_t* bdir = (uint32_t*)ws_get(ctx, WS_RUNBDIR, row * kBdirRow * sizeof(uint32_t), &st);
     if (!bdir) return st;
@@ -840,6 +849,12 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
   if (lds) {  // fold results per run go to the (unused) tag arrays
     HA.fold_v = w;
     HA.fold_q = v;
+    // The fold reads each child's 32-B record, which the tag pass writes. CDB_HOT_DIRECT=1 (A/B and
+    // test hook): it reads the child's row in the runs instead -- no record writes (C3: 0.95 GB less
+    // written per step), but the rows' unaligned 32-B field reads cost more than the records: C3
+    // 3.37-3.42 vs 3.22-3.29 ms per step.
+    const char* direct_env = std::getenv("CDB_HOT_DIRECT");
+    HA.direct = child_rows < (1ull << 30) && direct_env && direct_env[0] == '1';
     const bool prof = std::getenv("CDB_HOT_PROF") != nullptr;  // test hook: phase clocks to stderr
     if (prof) {
       HA.prof = nc >= 8 ? (unsigned long long*)w2 : nullptr;  // (the global sort's spare keys)
@@ -892,7 +907,7 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
       uint2* splits = (uint2*)(((uintptr_t)(toff + jobs0) + 15) & ~(uintptr_t)15);
       CDB_HIP(hipMemsetAsync(d_unsorted, 0, 4, s), "memset");
       HA.inline_markers = 1;
-      hot_lists_kernel<<<(H + 255) / 256, 256, 0, s>>>(HA, L, bounds);
+      hot_lists_kernel<<<(H + 255) / 256, 256, 0, s>>>(HA, L, bounds, d_unsorted);
       CDB_TRY(launch_check(ctx, s, "hot_lists_kernel"));
       // sampled pairs first: an input out of child order skips the tag for the merge at once
       hot_sample_kernel<<<1, 256, 0, s>>>(A, HA, L, bounds, d_unsorted);
@@ -903,6 +918,7 @@ cdb_status chip_wide(cdb_ctx* ctx, BucketArgs& A, const std::vector<uint32_t>& w
       if (!unsorted) {
         hot_tag_kernel<<<(uint32_t)((tc + kTagChunk - 1) / kTagChunk), 256, 0, s>>>(A, HA);
         CDB_TRY(launch_check(ctx, s, "hot_tag_kernel"));
+        HA.orphans_counted = 1;  // (a fallback re-tag below must not count them twice)
         uint64_t *wa = w, *wb = w2;
         uint32_t *va = v, *vb = v2;
         for (uint32_t span = 1; span < L; span <<= 1) {
@@ -1578,6 +1594,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     stats->sorted_runs = use_runs ? 1 : 0;
     stats->hot_slow_runs = hs[ST_HOT_SLOW];
     stats->hot_merged_children = hs[ST_HOT_MERGED];
+    stats->wave_pipe_buckets = hs[ST_PIPE];
   }
   if ((flags & CDB_MERGE_STRICT_DICT_PANIC) && hs[ST_DICT_MERGES])
     return fail(ctx, CDB_DICT_MERGE_UNIMPLEMENTED, "Dict::merge reached (lwwhash.rs:180 unimplemented!())");
@@ -1643,7 +1660,11 @@ void cdb_ctx_destroy(cdb_ctx* ctx) {
   delete ctx;
 }
 
-const char* cdb_last_error(const cdb_ctx* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+const char* cdb_last_error(const cdb_ctx* ctx) {
+  if (ctx) return ctx->last_error.c_str();
+  std::lock_guard<std::mutex> g(g_create_mu);
+  return g_create_error.c_str();
+}
 
 cdb_status cdb_dev_rows_alloc(cdb_ctx* ctx, cdb_dev_rows* r, uint64_t rows, int ncols) {
   std::memset(r, 0, sizeof *r);

@@ -86,6 +86,8 @@ struct HotArgs {
   int inline_markers;        // tag: a child that takes no part keeps the W it would have (its list
                              // stays sorted for the merge) and is flagged in v (kInlineMarker)
                              // instead of getting the bucket's marker
+  int orphans_counted;       // tag: a previous tag pass of this batch already counted its orphan
+                             // children (the list merge's, before a fallback re-tag): not again
 };
 
 // A child's columns: its copied AoS row, or (runs mode) the runs' SoA columns.
@@ -369,7 +371,7 @@ __global__ void __launch_bounds__(256) hot_tag_kernel(BucketArgs A, HotArgs H) {
       H.c_h[j] = h | (isn ? 0u : 0x80000000u);
     }
   }
-  if (orph) atomicAdd(&stat_shard(A.stats)[ST_ORPHANS], orph);
+  if (orph && !H.orphans_counted) atomicAdd(&stat_shard(A.stats)[ST_ORPHANS], orph);
 }
 
 // One child of a W-run, by flat index j (the last tie-break).
@@ -534,8 +536,11 @@ constexpr uint32_t kMergeItems = 8;
 constexpr uint32_t kMergeTile = 256 * kMergeItems;  // outputs per workgroup tile
 
 // List bounds of every bucket: bounds[h * (L + 1) + l] = flat start of list l (l < 2 nr: family
-// l / nr, run l % nr), padding lists empty, bounds[h * (L + 1) + L] = the bucket's end.
-__global__ void __launch_bounds__(256) hot_lists_kernel(HotArgs H, uint32_t L, uint32_t* __restrict__ bounds) {
+// l / nr, run l % nr), padding lists empty, bounds[h * (L + 1) + L] = the bucket's end. Lists that
+// do not tile the bucket's flat children exactly (its copied rows laid out otherwise than the run
+// directory says) set *unsorted: the batch takes the radix sort, which needs no lists.
+__global__ void __launch_bounds__(256) hot_lists_kernel(HotArgs H, uint32_t L, uint32_t* __restrict__ bounds,
+                                                        uint32_t* __restrict__ unsorted) {
   const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= H.H) return;
   const uint32_t b = H.ids[h], nr = H.V.nr;
@@ -548,6 +553,7 @@ __global__ void __launch_bounds__(256) hot_lists_kernel(HotArgs H, uint32_t L, u
       x += d[1] - d[0];
     }
   for (uint32_t l = 2 * nr; l <= L; ++l) o[l] = x;
+  if (x != H.c_off[h + 1]) atomicOr(unsorted, 1u);
 }
 
 // A cheap early look at whether the lists are sorted, before anything is tagged: 256 sampled pairs
@@ -1270,6 +1276,12 @@ __global__ void __launch_bounds__(C::Threads) hot_sortfold_kernel(BucketArgs A, 
   __syncthreads();
   const uint32_t m = L.misc[2];  // rows taking part
   phase(2);
+  // the fold reads a child by its flat index (its 32-B record from the tag pass) or, direct, by its
+  // row in the runs / the copied rows (no records written: the rows were just read by the tag pass)
+  auto jat_of = [&](uint32_t i) -> uint32_t {
+    if (!H.direct) return c0 + i;
+    return row_of(i) | (i < N ? 0u : kMemberBit);
+  };
   // 4. fold, pass 0: outputs per run into ix[s ^ 1]
   uint16_t* no = L.ix[s ^ 1];
   uint32_t* fq = H.fold_q + c0;
@@ -1281,7 +1293,7 @@ __global__ void __launch_bounds__(C::Threads) hot_sortfold_kernel(BucketArgs A, 
     const uint32_t nrows = act ? (r + 1 < nruns ? (rl[r + 1] & 0xFFFF) : m) - q : 0;
     const bool isn = act && sx[q] < N;
     HotAcc acc;
-    hot_fold_run(A, H, 0, act, isn, b, g0 + (e >> 16), nrows, [&](uint32_t k) { return c0 + sx[q + k]; },
+    hot_fold_run(A, H, 0, act, isn, b, g0 + (e >> 16), nrows, [&](uint32_t k) { return jat_of(sx[q + k]); },
                  [](uint32_t) { return true; }, 0,
                  false, fq + r, fv + r, nullptr, acc, gcm, nslow);
     if (act) no[r] = (uint16_t)acc.nout;
@@ -1310,7 +1322,7 @@ __global__ void __launch_bounds__(C::Threads) hot_sortfold_kernel(BucketArgs A, 
     const bool isn = act && sx[q] < N;
     const uint32_t off = act ? ro[r] : 0;
     HotAcc acc;
-    hot_fold_run(A, H, 1, act, isn, b, g0 + gr, nrows, [&](uint32_t k) { return c0 + sx[q + k]; },
+    hot_fold_run(A, H, 1, act, isn, b, g0 + gr, nrows, [&](uint32_t k) { return jat_of(sx[q + k]); },
                  [](uint32_t) { return true; },
                  isn ? (off & 0xFFFF) : (off >> 16), act && no[r] != 0, fq + r, fv + r, nullptr, acc, gcm, nslow);
     if (act && acc.k_cnt) {

@@ -535,6 +535,7 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, CDB_PIPE_MINB) bucket_wave_p
   }
   uint32_t b1 = produce();
   u32x2 pr = pipe_pairs(V, b1, lane, b1 != kPipeDone);  // (no bucket: zero pairs, an empty map)
+  uint32_t folded = 0;  // (wave-uniform) buckets this wave folded: stats.wave_pipe_buckets
   while (b != kPipeDone) {
     const uint32_t b2 = b1 != kPipeDone ? produce() : kPipeDone;
     const WaveDir d = in.d;
@@ -581,11 +582,13 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, CDB_PIPE_MINB) bucket_wave_p
         wave_phase_b<1, 1>(W, L, b, lane, mid);
       else
         wave_phase_b<1, 2>(W, L, b, lane, mid);
+      ++folded;
     }
     wave_sync();  // (the next bucket reuses this one's LDS)
     b = b1;
     b1 = b2;
   }
+  if (lane == 0 && folded) atomicAdd(&stat_shard(W.A.stats)[ST_PIPE], (unsigned long long)folded);
 }
 
 // The wide tier (65..128 key rows or 129..256 child rows) on the runs: as bucket_wide_kernel.

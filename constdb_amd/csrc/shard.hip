@@ -75,10 +75,20 @@ cdb_ctx* slot_ctx(cdb_ctx* ctx, int i) { return i == 0 ? ctx : ctx->shards[i - 1
 
 int slot_count(const cdb_ctx* ctx) { return 1 + (int)ctx->shards.size(); }
 
-cdb_status load_rccl(cdb_ctx* ctx, Node* n) {
-  n->lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-  if (!n->lib) n->lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-  if (!n->lib) return fail(ctx, CDB_DEVICE_ERROR, std::string("cannot load RCCL: ") + dlerror());
+// RCCL's library: CDB_RCCL_LIB names it (tests point it at a missing file), else the soname, else
+// ROCm's copy. Returns an empty string, or what failed.
+std::string load_rccl(Node* n) {
+  const char* path = std::getenv("CDB_RCCL_LIB");
+  if (path && path[0]) {
+    n->lib = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  } else {
+    n->lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!n->lib) n->lib = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  }
+  if (!n->lib) {
+    const char* e = dlerror();
+    return std::string("cannot load RCCL: ") + (e ? e : "dlopen failed");
+  }
   auto sym = [&](const char* name) { return dlsym(n->lib, name); };
   n->init_all = (decltype(n->init_all))sym("ncclCommInitAll");
   n->destroy = (decltype(n->destroy))sym("ncclCommDestroy");
@@ -88,8 +98,8 @@ cdb_status load_rccl(cdb_ctx* ctx, Node* n) {
   n->group_end = (decltype(n->group_end))sym("ncclGroupEnd");
   n->error_string = (decltype(n->error_string))sym("ncclGetErrorString");
   if (!n->init_all || !n->destroy || !n->send || !n->recv || !n->group_start || !n->group_end)
-    return fail(ctx, CDB_DEVICE_ERROR, "RCCL lacks the point-to-point API");
-  return CDB_OK;
+    return "RCCL lacks the point-to-point API";
+  return std::string();
 }
 
 cdb_status nccl_check(cdb_ctx* ctx, const Node* n, ncclResult_t r, const char* what) {
@@ -265,45 +275,59 @@ cdb_status cdb_ctx_create_multi(cdb_ctx** out, int device_count, const int* devi
   if (!out) return CDB_BAD_ARGUMENT;
   *out = nullptr;
   if (!devices || device_count < 1 || device_count > 8 || (device_count & (device_count - 1))) return CDB_BAD_ARGUMENT;
+  bool distinct = true;
+  for (int i = 0; i < device_count; ++i)
+    for (int j = 0; j < i; ++j) distinct = distinct && devices[i] != devices[j];
+  // Distinct GPUs exchange rows over RCCL point-to-point. A context whose RCCL cannot be loaded or
+  // whose communicators cannot be created is refused (CDB_DEVICE_ERROR, the reason in
+  // cdb_last_error(NULL)): a node would otherwise merge over another transport than the one asked
+  // for. CDB_SHARD_TRANSPORT=peer selects HIP peer copies over the same links explicitly
+  // (transport 2 in cdb_exchange_stats). RCCL is loaded before any device is touched.
+  const char* tr = std::getenv("CDB_SHARD_TRANSPORT");
+  const bool want_rccl = device_count > 1 && distinct && !(tr && std::strcmp(tr, "peer") == 0);
+  Node* node = new Node();
+  if (want_rccl) {
+    const std::string why = load_rccl(node);
+    if (!why.empty()) {
+      node_destroy(node);
+      return set_create_error(CDB_DEVICE_ERROR, why + " (CDB_SHARD_TRANSPORT=peer selects HIP peer copies)");
+    }
+  }
   cdb_ctx* root = nullptr;
   cdb_status st = cdb_ctx_create(&root, devices[0]);
-  if (st != CDB_OK) return st;
+  if (st != CDB_OK) {
+    node_destroy(node);
+    return set_create_error(st, "device " + std::to_string(devices[0]) + " unavailable");
+  }
+  root->node = node;
   for (int i = 1; i < device_count; ++i) {
     cdb_ctx* c = nullptr;
     if ((st = cdb_ctx_create(&c, devices[i])) != CDB_OK) {
       cdb_ctx_destroy(root);
-      return st;
+      return set_create_error(st, "device " + std::to_string(devices[i]) + " unavailable");
     }
     root->shards.push_back(c);
   }
-  bool distinct = true;
-  for (int i = 0; i < device_count; ++i)
-    for (int j = 0; j < i; ++j) distinct = distinct && devices[i] != devices[j];
-  root->node = new Node();
-  if (device_count > 1 && distinct) {
-    // RCCL point-to-point between the GPUs. Where RCCL cannot be loaded or its communicators not
-    // created (or CDB_SHARD_TRANSPORT=peer), the rows move by HIP peer copies over the same links
-    // instead (transport 2 in cdb_exchange_stats): the merge is the same either way.
-    const char* tr = std::getenv("CDB_SHARD_TRANSPORT");
-    const bool want_rccl = !(tr && std::strcmp(tr, "peer") == 0);
-    if (want_rccl && load_rccl(root, root->node) == CDB_OK) {
-      root->node->comms.assign(device_count, nullptr);
-      root->node->rccl = nccl_check(root, root->node, root->node->init_all(root->node->comms.data(), device_count,
-                                                                          devices),
-                                    "ncclCommInitAll") == CDB_OK;
+  if (want_rccl) {
+    node->comms.assign(device_count, nullptr);
+    if (nccl_check(root, node, node->init_all(node->comms.data(), device_count, devices), "ncclCommInitAll") !=
+        CDB_OK) {
+      const std::string why = cdb_last_error(root);
+      cdb_ctx_destroy(root);
+      return set_create_error(CDB_DEVICE_ERROR, why + " (CDB_SHARD_TRANSPORT=peer selects HIP peer copies)");
     }
-    if (!root->node->rccl) {
-      for (int i = 0; i < device_count; ++i) {  // direct peer access where the links allow it
-        hipSetDevice(devices[i]);
-        for (int j = 0; j < device_count; ++j) {
-          int ok = 0;
-          if (i != j && hipDeviceCanAccessPeer(&ok, devices[i], devices[j]) == hipSuccess && ok)
-            (void)hipDeviceEnablePeerAccess(devices[j], 0);
-        }
+    node->rccl = true;
+  } else if (device_count > 1 && distinct) {
+    for (int i = 0; i < device_count; ++i) {  // peer copies, asked for: direct peer access where the links allow it
+      hipSetDevice(devices[i]);
+      for (int j = 0; j < device_count; ++j) {
+        int ok = 0;
+        if (i != j && hipDeviceCanAccessPeer(&ok, devices[i], devices[j]) == hipSuccess && ok)
+          (void)hipDeviceEnablePeerAccess(devices[j], 0);
       }
-      (void)hipGetLastError();
-      hipSetDevice(devices[0]);
     }
+    (void)hipGetLastError();
+    hipSetDevice(devices[0]);
   }
   *out = root;
   return CDB_OK;

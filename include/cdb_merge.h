@@ -54,7 +54,8 @@ typedef struct cdb_merged cdb_merged; /* a merge result (device-resident, host-r
 /* Creates a context on HIP device `device`. Fails with CDB_NO_DEVICE when no device. */
 cdb_status cdb_ctx_create(cdb_ctx** out, int device);
 void cdb_ctx_destroy(cdb_ctx* ctx);
-/* Human-readable last error of this context (static storage, valid until the next call). */
+/* Human-readable last error of this context (static storage, valid until the next call). With
+ * ctx == NULL: why the last cdb_ctx_create_multi of the process failed (no context exists then). */
 const char* cdb_last_error(const cdb_ctx* ctx);
 
 /* ------------------------------------------------------------------ decode
@@ -192,6 +193,7 @@ typedef struct cdb_merge_stats {
                                 (ids sharing the sort tag's id bits, or runs of > 8 rows) */
   uint64_t hot_merged_children; /* chip-wide path: children whose runs arrived in child order
                                 (a merge result's) and were merged instead of radix-sorted */
+  uint64_t wave_pipe_buckets;   /* buckets folded by the persistent wave tier (bucket_wave_pipe_kernel) */
 } cdb_merge_stats;
 
 cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n,
@@ -496,7 +498,12 @@ cdb_status cdb_merge_device(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_mer
  * parent key), so every §8a rule stays local to one device: no collective beyond the row exchange.
  * Device slot i may name any visible device; a device listed twice gives two shards on one GPU
  * (testing), whose rows then move by device copies instead of RCCL. device_count must be a power
- * of two, at most 8. The single-device functions take a multi-device context as its slot 0. */
+ * of two, at most 8. The single-device functions take a multi-device context as its slot 0.
+ * Distinct devices whose RCCL cannot be loaded (CDB_RCCL_LIB names the library, default
+ * librccl.so.1) or whose communicators cannot be created are refused with CDB_DEVICE_ERROR and
+ * the reason in cdb_last_error(NULL) -- never a silent change of transport; the environment
+ * variable CDB_SHARD_TRANSPORT=peer asks for HIP peer copies instead (cdb_exchange_stats.transport
+ * 2). */
 cdb_status cdb_ctx_create_multi(cdb_ctx** out, int device_count, const int* devices);
 int cdb_ctx_device_count(const cdb_ctx* ctx);
 /* The context of device slot i (slot 0: ctx itself), for per-device calls (cdb_gen_device,

@@ -221,3 +221,36 @@ def test_library_plan_cpu(world):
     st = (ctypes.c_uint64 * 6)()
     tot = (ctypes.c_uint64 * 3)()
     assert L.cdb_shard_recv_plan(1, nr, cnt, 1, ctypes.byref(k), a, b, st, tot) == cdb.BAD_ARGUMENT and k.value == 2
+
+
+def test_multi_context_refuses_missing_rccl(monkeypatch):
+    """cdb_ctx_create_multi over distinct devices never falls back silently to another transport:
+    with RCCL unloadable (CDB_RCCL_LIB naming a missing file) it returns CDB_DEVICE_ERROR with the
+    reason in cdb_last_error(NULL), before touching any device (so this runs without a GPU).
+    CDB_SHARD_TRANSPORT=peer asks for HIP peer copies explicitly and passes that check (here it then
+    finds no device). A device listed twice (slots sharing a GPU) never needs RCCL."""
+    import ctypes
+    from constdb_amd import build
+    build.build()
+    L = cdb.lib()
+    devs = (ctypes.c_int * 2)(0, 1)
+    h = ctypes.c_void_p()
+    monkeypatch.setenv("CDB_RCCL_LIB", "/nonexistent/librccl.so.1")
+    monkeypatch.delenv("CDB_SHARD_TRANSPORT", raising=False)
+    assert L.cdb_ctx_create_multi(ctypes.byref(h), 2, devs) == cdb.DEVICE_ERROR and not h.value
+    assert b"cannot load RCCL" in L.cdb_last_error(None)
+    with pytest.raises(Exception, match="cannot load RCCL"):
+        cdb.Context(devices=[0, 1])
+    monkeypatch.setenv("CDB_SHARD_TRANSPORT", "peer")
+    st = L.cdb_ctx_create_multi(ctypes.byref(h), 2, devs)
+    if st == cdb.OK:  # (a GPU box: a context over peer copies)
+        L.cdb_ctx_destroy(h)
+    else:
+        assert st == cdb.NO_DEVICE
+    monkeypatch.delenv("CDB_SHARD_TRANSPORT")
+    same = (ctypes.c_int * 2)(0, 0)
+    st = L.cdb_ctx_create_multi(ctypes.byref(h), 2, same)
+    if st == cdb.OK:
+        L.cdb_ctx_destroy(h)
+    else:
+        assert st == cdb.NO_DEVICE

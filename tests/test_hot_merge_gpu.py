@@ -188,3 +188,35 @@ def test_one_list_out_of_order_falls_back(ctx, monkeypatch):
         _release(ctx, state)
     for fam, (x, y) in enumerate(zip(got, want)):
         assert x.shape == y.shape and torch.equal(x, y), fam
+
+
+def test_orphans_in_sorted_lists_fall_back_counted_once(ctx, monkeypatch):
+    """State runs where three children of the hottest key in run 0 name a key that does not exist
+    (their pkf changed, pkh kept, so the runs stay in hash order): an orphan takes the bucket's marker
+    W, which breaks its list's order, so round 0 of the list merge finds it and the batch is re-tagged
+    and radix-sorted. The orphans are counted once (the list merge's tag pass counted them already),
+    and the result equals CDB_HOT_MERGE=0's bit for bit."""
+    cfg = configs.c5(cdb, universe=300_000, events=3_000_000)
+    state = _gen(ctx, cfg)
+    try:
+        state_runs(cdb, ctx, state)
+        rows = state.members
+        n0 = state.run_start[2][1]
+        kh = wrap(rows.col[0], rows.n)[:n0]
+        rec = wrap(rows.col[1], rows.n * rows.stride).view(rows.n, rows.stride)[:n0]
+        _, inv, counts = torch.unique_consecutive(kh, return_inverse=True, return_counts=True)
+        hot = int(torch.argmax(counts))
+        first = int(torch.nonzero(inv == hot)[0])
+        assert int(counts[hot]) > 1000
+        for k in (10, 200, 700):  # (records: pkf is word 0)
+            rec[first + k, 0] ^= 0x5A5A5A5A
+        torch.cuda.synchronize()
+        got, st = _merge_cols(ctx, state, _opts())
+        assert st.sorted_runs == 1 and st.hot_merged_children == 0
+        monkeypatch.setenv("CDB_HOT_MERGE", "0")
+        want, st0 = _merge_cols(ctx, state, _opts())
+    finally:
+        _release(ctx, state)
+    assert st.orphan_children == st0.orphan_children == 3
+    for fam, (x, y) in enumerate(zip(got, want)):
+        assert x.shape == y.shape and torch.equal(x, y), fam

@@ -137,16 +137,22 @@ def test_chip_wide_in_batches_vs_oracle(ctx, monkeypatch):
     check_runs(ctx, [cdb.gen_snapshot(cfg, r) for r in range(4)], force_tier=2)
 
 
-@pytest.mark.parametrize("lds,id_bits", [("1", None), ("0", None), ("1", "4"), ("1", "12")])
-def test_chip_wide_lds_and_global_sort_vs_oracle(ctx, monkeypatch, lds, id_bits):
+@pytest.mark.parametrize("lds,id_bits,direct", [("1", None, None), ("0", None, None), ("1", "4", None),
+                                                ("1", "12", None), ("1", None, "1"), ("1", "4", "1"),
+                                                ("0", None, "0")])
+def test_chip_wide_lds_and_global_sort_vs_oracle(ctx, monkeypatch, lds, id_bits, direct):
     """Run-order batches of buckets of at most 8192 children take the per-bucket LDS sort and fold
     (hot_sortfold_kernel); CDB_HOT_LDS=0 sends them through the global tag sort instead. Both equal
     the oracle on every bucket forced through the chip-wide path (force_tier 2), with counters,
     sets and dicts, GC of member deletes, and -- with few id-hash bits (CDB_HOT_ID_BITS) -- runs
-    holding several exact ids, folded by successor selection."""
+    holding several exact ids, folded by successor selection. The LDS path's folds read the 32-B
+    records the tag pass writes (default) or, with CDB_HOT_DIRECT=1, each child's row in the runs;
+    the global path reads the rows (default) or, with CDB_HOT_DIRECT=0, the records."""
     monkeypatch.setenv("CDB_HOT_LDS", lds)
     if id_bits:
         monkeypatch.setenv("CDB_HOT_ID_BITS", id_bits)
+    if direct:
+        monkeypatch.setenv("CDB_HOT_DIRECT", direct)
     cfg = _small(91, 40000, 5, mix_set=25, mix_dict=25, mean_members=20, side_permille=150, conflict_ppm=10000,
                  tie_permille=100, del_permille=300)
     snaps = [cdb.gen_snapshot(cfg, r) for r in range(5)]
