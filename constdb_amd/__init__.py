@@ -235,7 +235,7 @@ ABI_FUNCTIONS = (
     "cdb_decode_ops_gpu", "cdb_ops_column", "cdb_snapshot_index_selftest", "cdb_merge_into",
     "cdb_merged_from_device", "cdb_dev_state_rows", "cdb_ctx_create_multi", "cdb_ctx_device_count",
     "cdb_ctx_shard", "cdb_merge_sharded", "cdb_dev_rows_alloc_records", "cdb_dev_output_compact",
-    "cdb_dev_input_append", "cdb_shard_splits", "cdb_shard_recv_plan")
+    "cdb_dev_input_append", "cdb_shard_splits", "cdb_shard_recv_plan", "cdb_merged_gc", "cdb_merged_garbage_count")
 
 _lib = None
 
@@ -282,6 +282,8 @@ def lib():
         "cdb_merged_canonical_dump": (c_st, [vp, vp, P(vp), P(ctypes.c_size_t)]),
         "cdb_merge_into": (c_st, [vp, vp, P(vp), ctypes.c_uint32, P(MergeOpts), P(vp), P(MergeStats)]),
         "cdb_merged_from_device": (c_st, [vp, vp, P(vp), ctypes.c_uint32, P(DevOutput), P(vp)]),
+        "cdb_merged_gc": (c_st, [vp, vp, ctypes.c_uint64, P(ctypes.c_uint64)]),
+        "cdb_merged_garbage_count": (ctypes.c_uint64, [vp]),
         "cdb_dev_state_rows": (c_st, [vp, P(DevOutput), P(DevRows), P(DevRows), P(DevRows), vp]),
         "cdb_merged_replicas": (c_st, [vp, P(P(ReplicaEntry)), P(ctypes.c_size_t)]),
         "cdb_merged_free": (None, [vp]),
@@ -706,6 +708,17 @@ class Merged:
         self._ctx.check(lib().cdb_encode_snapshot(self._ctx.handle, self._h, ctypes.byref(hdr), ctypes.byref(out),
                                                   ctypes.byref(n), ctypes.byref(st)))
         return _take_bytes(out, n), st
+
+    def gc(self, tombstone: int) -> int:
+        """cdb_merged_gc: DB::gc(tombstone) (db.rs:82-119) on this result, in place, over the garbage
+        list it keeps (DB::garbages across merge_into chains). Returns the Deletes rows removed."""
+        removed = ctypes.c_uint64()
+        self._ctx.check(lib().cdb_merged_gc(self._ctx.handle, self._h, tombstone, ctypes.byref(removed)))
+        return removed.value
+
+    @property
+    def garbage_count(self) -> int:
+        return lib().cdb_merged_garbage_count(self._h)
 
     def apply_ops(self, ops: "Ops") -> "Merged":
         """cdb_apply_ops: the op stream applied on the device on top of this result (SURVEY

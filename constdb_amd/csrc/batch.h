@@ -155,6 +155,15 @@ bool decode_entry_children(const Batch& b, uint64_t off, uint64_t kh, uint64_t k
 struct cdb_merged {
   std::vector<std::shared_ptr<cdb::Batch>> inputs;  // pos -> decoded batch (byte arenas)
   cdb::ColVec k[cdb::kKeyOutCols], nd[cdb::kNodeCols], mb[cdb::kMemberCols];
+  // DB::garbages (db.rs:14, LinkedList<(key, field, uuid)>): every Deletes entry applied to this
+  // state (DB::delete, db.rs:73-76, from each merged snapshot's DELETES section in fold order),
+  // less what DB::gc popped (db.rs:82-119). Kept across cdb_merge_into chains, so that a GC after
+  // a chain pops exactly what the reference's list holds -- including stale entries of keys
+  // deleted again later, and never the entry a previous gc lost at its stop.
+  struct Garbage {
+    uint64_t kh, kf, t;
+  };
+  std::vector<Garbage> garbage;
   // replica-metadata merge, computed on first request
   bool replicas_done = false;
   std::vector<std::string> rep_str;          // addr / alias storage (stable: reserved up front)

@@ -14,6 +14,7 @@
 #include <string>
 #include <mutex>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "batch.h"
@@ -333,6 +334,67 @@ static void flatten_onto(cdb_merged* m, const cdb_merged& state, uint32_t n_new)
   (void)n_new;
 }
 
+// DB::delete (db.rs:73-76) for every Deletes entry of batch b, in stream order: the garbage list.
+static void append_garbage(cdb_merged* m, const Batch& b) {
+  for (uint64_t i = 0; i < b.n_keys(); ++i)
+    if (meta_tag(b.meta[i]) == TAG_DELETE) m->garbage.push_back({b.kh[i], b.kf[i], b.ct[i]});
+}
+
+// DB::gc(tombstone)'s pops (db.rs:82-86): from the back, every entry with t <= tombstone is
+// processed; the first with t > tombstone ends the loop, popped and lost. Returns how many
+// entries stay (the list's front); *first = the first processed entry.
+static size_t gc_stop(const cdb_merged& m, uint64_t tombstone, size_t* first) {
+  size_t i = m.garbage.size();
+  while (i > 0) {
+    --i;
+    if (m.garbage[i].t > tombstone) {
+      *first = i + 1;
+      return i;
+    }
+  }
+  *first = 0;
+  return 0;
+}
+
+// DB::gc (db.rs:82-119) on a host result: every processed entry (key, t) removes the key's Deletes
+// row when its time equals t (`deletes.get(&key) == Some(t)`; a removal is final, so the order of
+// the pops does not matter); the garbage list keeps the entries before the stop. (Field garbage is
+// never enqueued by the reference: delete_field, db.rs:78-80, is uncalled.)
+static uint64_t gc_host(cdb_merged* m, uint64_t tombstone) {
+  size_t first = 0;
+  const size_t keep = gc_stop(*m, tombstone, &first);
+  if (keep == m->garbage.size()) return 0;
+  const uint64_t nk = m->k[O_KH].size();
+  struct KeyHash {
+    size_t operator()(const std::pair<uint64_t, uint64_t>& k) const { return k.first ^ (k.second * 0x9E3779B97F4A7C15ull); }
+  };
+  std::unordered_map<std::pair<uint64_t, uint64_t>, uint64_t, KeyHash> del_row;
+  for (uint64_t r = 0; r < nk; ++r)
+    if (meta_tag(m->k[O_META][r]) == TAG_DELETE) del_row[{m->k[O_KH][r], m->k[O_KF][r]}] = r;
+  std::vector<uint8_t> drop(nk, 0);
+  uint64_t removed = 0;
+  for (size_t i = first; i < m->garbage.size(); ++i) {
+    const cdb_merged::Garbage& g = m->garbage[i];
+    auto it = del_row.find({g.kh, g.kf});
+    if (it != del_row.end() && !drop[it->second] && m->k[O_CT][it->second] == g.t) {
+      drop[it->second] = 1;
+      ++removed;
+    }
+  }
+  m->garbage.resize(keep);
+  if (removed) {
+    uint64_t w = 0;
+    for (uint64_t r = 0; r < nk; ++r) {
+      if (drop[r]) continue;
+      if (w != r)
+        for (int c = 0; c < kKeyOutCols; ++c) m->k[c][w] = m->k[c][r];
+      ++w;
+    }
+    for (int c = 0; c < kKeyOutCols; ++c) m->k[c].resize(w);
+  }
+  return removed;
+}
+
 extern "C" {
 
 cdb_status cdb_decode_snapshot(cdb_ctx* ctx, const uint8_t* buf, size_t len, uint32_t flags, cdb_batch** out,
@@ -489,6 +551,13 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n, const c
     delete m;
     return st;
   }
+  // the garbage list: this merge's Deletes entries in fold order; with DB::gc in the merge (the
+  // kernels applied its rule to the same list) the entries the pops took are gone
+  for (uint32_t i = 0; i < n; ++i) append_garbage(m, *inputs[i]->b);
+  if (opts && (opts->flags & CDB_MERGE_GC_DELETES)) {
+    size_t first = 0;
+    m->garbage.resize(gc_stop(*m, opts->gc_watermark, &first));
+  }
   if (timing) {
     const auto t3 = std::chrono::steady_clock::now();
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -571,14 +640,30 @@ cdb_status cdb_merge_into(cdb_ctx* ctx, cdb_merged* state, cdb_batch* const* inp
   if ((st = upload_state(ctx, *state, &din)) != CDB_OK) return st;
   if ((st = upload_batches(ctx, inputs, n, &din, at, 1)) != CDB_OK) return st;
   dout.compact = 1;
+  // DB::gc after a chain pops the state's garbage list, not only this merge's entries (the state's
+  // Deletes rows are its deletes map, not its list): the device merge runs without it, and the
+  // gc runs on the result over state.garbage ++ the new entries (gc_host)
+  cdb_merge_opts o;
+  std::memset(&o, 0, sizeof o);
+  if (opts) o = *opts;
+  const bool gc = (o.flags & CDB_MERGE_GC_DELETES) != 0;
+  o.flags &= ~(uint32_t)CDB_MERGE_GC_DELETES;
   cdb_merge_stats local;
-  st = merge_device_impl(ctx, &din, opts, &dout, stats ? stats : &local, ctx->stream);
+  cdb_merge_stats* ms = stats ? stats : &local;
+  st = merge_device_impl(ctx, &din, &o, &dout, ms, ctx->stream);
   if (st != CDB_OK && st != CDB_DICT_MERGE_UNIMPLEMENTED) return st;
   const cdb_status merge_st = st;
   auto m = std::make_unique<cdb_merged>();
   if ((st = download_result(ctx, dout, m.get())) != CDB_OK) return st;
   flatten_onto(m.get(), *state, n);
   for (uint32_t i = 0; i < n; ++i) m->inputs.push_back(inputs[i]->b);
+  m->garbage = state->garbage;
+  for (uint32_t i = 0; i < n; ++i) append_garbage(m.get(), *inputs[i]->b);
+  if (gc) {
+    const uint64_t removed = gc_host(m.get(), o.gc_watermark);
+    ms->deletes_gced = removed;
+    ms->key_rows_out -= removed;
+  }
   *out = m.release();
   return merge_st;
 }
@@ -610,9 +695,24 @@ cdb_status cdb_merged_from_device(cdb_ctx* ctx, cdb_merged* state, cdb_batch* co
   if (st != CDB_OK) return st;
   if (state) flatten_onto(m.get(), *state, n);
   for (uint32_t i = 0; i < n; ++i) m->inputs.push_back(inputs[i]->b);
+  // (the garbage list: state's, then the host-resident batches' entries; a batch decoded into HBM
+  // keeps its rows there, so a result over such batches starts no list -- see cdb_merged_gc)
+  if (state) m->garbage = state->garbage;
+  for (uint32_t i = 0; i < n; ++i)
+    if (!inputs[i]->b->rows_on_device) append_garbage(m.get(), *inputs[i]->b);
   *out = m.release();
   return CDB_OK;
 }
+
+cdb_status cdb_merged_gc(cdb_ctx* ctx, cdb_merged* m, uint64_t tombstone, uint64_t* removed) {
+  (void)ctx;
+  if (!m) return CDB_BAD_ARGUMENT;
+  const uint64_t r = gc_host(m, tombstone);
+  if (removed) *removed = r;
+  return CDB_OK;
+}
+
+uint64_t cdb_merged_garbage_count(const cdb_merged* m) { return m ? m->garbage.size() : 0; }
 
 cdb_status cdb_merged_canonical_dump(cdb_ctx* ctx, cdb_merged* m, char** out, size_t* len) {
   if (!m || !out || !len) return CDB_BAD_ARGUMENT;
@@ -922,6 +1022,7 @@ cdb_status cdb_apply_ops(cdb_ctx* ctx, cdb_merged* state, const cdb_ops* ops, cd
   auto m = std::make_unique<cdb_merged>();
   m->inputs = state->inputs;
   m->inputs.push_back(ops->b);
+  m->garbage = state->garbage;  // (replicated deletes tag objects; only DB::delete enqueues garbage)
   cdb_apply_stats local;
   const cdb_status st = apply_ops_impl(ctx, state->k, state->nd, state->mb, *ops->b, pos, m->k, m->nd, m->mb,
                                        stats ? stats : &local);

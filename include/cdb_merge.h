@@ -209,6 +209,20 @@ cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n,
 cdb_status cdb_merge_into(cdb_ctx* ctx, cdb_merged* state, cdb_batch* const* inputs, uint32_t n,
                           const cdb_merge_opts* opts, cdb_merged** out, cdb_merge_stats* stats);
 
+/* DB::gc(tombstone) (db.rs:82-119; Server::gc, server.rs:257-262, with ReplicaManager::min_uuid) on a
+ * merge result, in place. Every result keeps the reference's garbage list (DB::garbages, db.rs:14):
+ * the Deletes entries of every snapshot merged into it (DB::delete, db.rs:73-76), in fold order,
+ * across cdb_merge_into chains, less what earlier gcs popped. The gc pops it from the back while
+ * t <= tombstone, removes a key's Deletes row when its time equals a popped entry's, and stops at
+ * the first entry with t > tombstone, which is popped and lost (the list keeps the entries before
+ * it). *removed (may be NULL) receives the rows removed. CDB_MERGE_GC_DELETES in a cdb_merge /
+ * cdb_merge_into is this gc after the merge. A result from cdb_merged_from_device lists only the
+ * host-resident batches' entries (after its state's): a device merge's own GC flag applies the
+ * rule to that call's inputs alone. */
+cdb_status cdb_merged_gc(cdb_ctx* ctx, cdb_merged* m, uint64_t tombstone, uint64_t* removed);
+/* Entries in a result's garbage list (DB::garbages.len()). */
+uint64_t cdb_merged_garbage_count(const cdb_merged* m);
+
 /* Canonical dump of a merge result: keys sorted by bytes, members by bytes, counter nodes
  * by id, then expires and deletes (the text format of oracle/constdb_oracle.py's
  * canonical_dump). *out is released with cdb_free. */
