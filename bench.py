@@ -35,7 +35,16 @@ sys.path.insert(0, ROOT)
 # SURVEY.md §8d algorithmic row widths (bytes): compulsory read + write per row
 W_KEY, W_NODE, W_SET, W_DICT = 50, 33, 34, 42
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
+# committed measurements, newest round first (a config not yet re-measured keeps its older record)
+PROFILE_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r06", "r05")]
+
+
+def profile_file(name):
+    for d in PROFILE_DIRS:
+        f = os.path.join(d, name)
+        if os.path.exists(f):
+            return f
+    return os.path.join(PROFILE_DIRS[0], name)
 # the merge pipeline's kernels (everything cdb_merge_device launches; not the generator)
 MERGE_KERNEL_PREFIXES = ("part_", "bucket_", "compact", "scan_", "stats_reduce", "gc_lastbad", "set_dir",
                          "stamp_pos", "iota", "hot_", "sorted_", "seg_", "run_", "mat_", "radix_hist",
@@ -104,7 +113,7 @@ def pmc_traffic(config):
     """HBM bytes per merge step, from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes of
     this same bench command (scripts/gpu_round.sh -> scripts/pmc_traffic.py): every merge-pipeline
     kernel, and the bucket phase alone. None when no such measurement is committed."""
-    f = os.path.join(PROFILE_DIR, f"pmc_traffic_{config}.json")
+    f = profile_file(f"pmc_traffic_{config}.json")
     try:
         with open(f) as fh:
             d = json.load(fh)
@@ -150,7 +159,7 @@ def cpu_baseline(cdb, args, snaps, sample):
            "sample": f"{sample} ({entries} entries, decode excluded, best of {args.cpu_reps}), "
                      f"oracle/cdb_oracle.cpp std::unordered_map fold",
            **host_info()}
-    ref = os.path.join(PROFILE_DIR, f"cpu_baseline_{args.config}_10m.json")
+    ref = profile_file(f"cpu_baseline_{args.config}_10m.json")
     if os.path.exists(ref):
         with open(ref) as fh:
             out["larger_sample"] = json.load(fh)
