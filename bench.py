@@ -348,7 +348,8 @@ def run_single(cdb, args):
                   "deletes_gced": st.deletes_gced, "hot_buckets": st.hot_buckets,
                   "wide_buckets": st.wide_buckets, "mid_buckets": st.mid_buckets,
                   "orphans": st.orphan_children, "hot_slow_runs": st.hot_slow_runs,
-                  "hot_merged_children": st.hot_merged_children},
+                  "hot_merged_children": st.hot_merged_children,
+                  "wave_pipe_buckets": st.wave_pipe_buckets, "wave_pipe_units": st.wave_pipe_units},
     }
     if tr:
         res["roofline"]["traffic_per_kernel"] = tr["per_kernel"]

@@ -131,7 +131,8 @@ class MergeStats(ctypes.Structure):
         "device_ms", "partition_ms", "bucket_ms", "finish_ms")] + [("sorted_runs", ctypes.c_uint64),
                                                                   ("hot_slow_runs", ctypes.c_uint64),
                                                                   ("hot_merged_children", ctypes.c_uint64),
-                                                                  ("wave_pipe_buckets", ctypes.c_uint64)]
+                                                                  ("wave_pipe_buckets", ctypes.c_uint64),
+                                                                  ("wave_pipe_units", ctypes.c_uint64)]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -35,7 +35,7 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 enum Stat {
   ST_TYPE_CONFLICTS = 0, ST_DICT_MERGES, ST_DELETES_GCED, ST_MEMBERS_GCED, ST_DUP_ROWS,
-  ST_ORPHANS, ST_HOT, ST_WIDE, ST_HOT_SLOW, ST_HOT_MERGED, ST_PIPE, ST_COUNT
+  ST_ORPHANS, ST_HOT, ST_WIDE, ST_HOT_SLOW, ST_HOT_MERGED, ST_PIPE, ST_PIPE_UNITS, ST_COUNT
 };
 // Statistics are counted into kStatShards shards of kStatStride u64 (one 128-B line each):
 // millions of waves adding to ONE word serialise at its memory-side atomic unit.

@@ -166,11 +166,18 @@ struct WaveArgs {
   RunView V;            // sorted-run path only
   uint32_t* wide_next;  // the wide tier's next group of 64 buckets (one counter per range)
   uint32_t* pipe_next;  // the persistent wave tier's next chunk, one counter per XCD slab (8)
+  const uint32_t* units;  // the persistent wave tier's unit starts: bit b of the bitmap (pipe_units_kernel)
 };
 
 // A bucket's directory entry (row counts and first row of each family).
 struct WaveDir {
   uint32_t K = 0, N = 0, M = 0, kb = 0, nb0 = 0, mb0 = 0;
+  // Buckets of the unit: the persistent wave tier merges G consecutive buckets whose rows fit one
+  // wave as one (their rows are consecutive rows of every run, their hash span fits the sort word)
+  // and counts every output to the first: bucket b then holds the group's rows in hash order in its
+  // slots, buckets b + 1 .. b + G - 1 none -- the bucket layout's contract (cdb_dev_buckets: each
+  // bucket's rows in its slot range, in key-hash order, ascending over buckets) holds as it is.
+  uint32_t G = 1;
 };
 __device__ __forceinline__ WaveDir load_dir(const BucketArgs& A, uint32_t b) {
   WaveDir d;
@@ -262,7 +269,7 @@ __device__ __forceinline__ void load_cols(const BucketArgs& A, const WaveDir& d,
 // program point: wave_bucket's `next()`).
 template <int KE>
 struct WaveMid {
-  uint32_t K, N, M, kb, nb0, mb0, kout, nlive;  // (wave-uniform)
+  uint32_t K, N, M, kb, nb0, mb0, kout, nlive, G;  // (wave-uniform)
   uint64_t kh[KE], kf[KE], o_ct[KE], o_ut[KE], o_dt[KE], o_meta[KE], o_win[KE];
   uint32_t o_T[KE], orank[KE], fam[KE];
   bool emit[KE];
@@ -270,12 +277,12 @@ struct WaveMid {
 };
 enum { WAVE_GO = 0, WAVE_DONE = 1, WAVE_PUSH = 2 };  // first half: second half / nothing more / exact tier
 
-// Hands bucket b to the workgroup tier (no outputs until that tier's: a pipelined compaction may
-// read them first).
-__device__ __forceinline__ void wave_push(const WaveArgs& W, uint32_t b, int lane) {
-  if (lane == 0) {
-    W.A.kout[b] = W.A.nout[b] = W.A.mout[b] = 0;
-    W.big_list[atomicAdd(W.big_count, 1u)] = b;
+// Hands buckets b .. b + G - 1 to the workgroup tier (no outputs until that tier's: a pipelined
+// compaction may read them first).
+__device__ __forceinline__ void wave_push(const WaveArgs& W, uint32_t b, int lane, uint32_t G = 1) {
+  if ((uint32_t)lane < G) {
+    W.A.kout[b + lane] = W.A.nout[b + lane] = W.A.mout[b + lane] = 0;
+    W.big_list[atomicAdd(W.big_count, 1u)] = b + lane;
   }
 }
 
@@ -594,6 +601,7 @@ __device__ __forceinline__ int wave_phase_a(const WaveArgs& W, WaveLds<KE>& L, u
   mid.mb0 = mb0;
   mid.kout = kout;
   mid.nlive = nlive;
+  mid.G = in.d.G;
 #pragma unroll
   for (int e = 0; e < KE; ++e) {
     mid.kh[e] = kh[e];
@@ -662,7 +670,7 @@ __device__ __forceinline__ void wave_phase_b(const WaveArgs& W, WaveLds<KE>& L, 
     Lv[e] = __ballot(live[e]);
   }
   if (__ballot(coll2)) {  // id-hash collision or duplicate: exact tier (nothing written yet)
-    wave_push(W, b, lane);
+    wave_push(W, b, lane, mid.G);
     return;
   }
   uint64_t En[CE], Em[CE], c_v[CE], c_t[CE], c_m[CE];
@@ -755,10 +763,10 @@ __device__ __forceinline__ void wave_phase_b(const WaveArgs& W, WaveLds<KE>& L, 
       }
     }
   }
-  if (lane == 0) {
-    A.kout[b] = kout;
-    A.nout[b] = nbase;
-    A.mout[b] = mbase;
+  if ((uint32_t)lane < mid.G) {  // (a group: every output counted to its first bucket)
+    A.kout[b + lane] = lane == 0 ? kout : 0u;
+    A.nout[b + lane] = lane == 0 ? nbase : 0u;
+    A.mout[b + lane] = lane == 0 ? mbase : 0u;
   }
   unsigned long long* st = stat_shard(A.stats);
   // per-lane counts are small (<= 64 KE segment rows, <= CE children): summed by bit slices

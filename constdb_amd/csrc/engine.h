@@ -70,6 +70,7 @@ enum WsSlot {
   WS_WIDE,                                              // wide tier: group counters per range
   WS_STATE,                                             // cdb_dev_state_rows: zero bases, error word
   WS_RUNBDIR,                                           // sorted-run path: bucket-major run directory
+  WS_UNITS,                                             // persistent wave tier: unit-start bitmap
   WS_HOTMERGE,                                          // chip-wide path: list bounds, merge tiles
   WS_COUNT
 };

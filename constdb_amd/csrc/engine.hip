@@ -68,6 +68,24 @@ bool pipe_wave_wanted(uint64_t nb) {
   if (e && std::strcmp(e, "force") == 0) return true;
   return nb >= kPipeMinBuckets;
 }
+// Its units group consecutive buckets (runs.hip.h, at most kGroupMax); the plan then targets ~kPipeFineTarget key rows
+// per bucket instead of ~40. Test and A/B hooks: CDB_GROUPS=0 (one bucket per unit, round-5 buckets),
+// CDB_PIPE_TARGET (key rows per bucket), CDB_GROUP_CCAP (child rows per unit, 64 or 128).
+constexpr uint64_t kPipeFineTarget = 20;
+constexpr uint64_t kGroupMax = 16;
+bool groups_wanted() {
+  const char* e = std::getenv("CDB_GROUPS");
+  return !(e && e[0] == '0');
+}
+uint64_t pipe_fine_target() {
+  const char* e = std::getenv("CDB_PIPE_TARGET");
+  return e ? (uint64_t)std::max(8, std::min(64, std::atoi(e))) : kPipeFineTarget;
+}
+uint32_t group_ccap() {
+  const char* e = std::getenv("CDB_GROUP_CCAP");
+  const int v = e ? std::atoi(e) : 128;
+  return v >= 128 ? 128u : 64u;
+}
 // Its grid: every workgroup slot of the device (resident workgroups per CU x CUs).
 uint32_t pipe_wave_grid(cdb_ctx* ctx) {
   static uint32_t grid[64] = {0};
@@ -408,7 +426,7 @@ struct Plan {
   bool seg_final = false;  // the last level runs per row-level segment (part_final_kernel)
 };
 
-Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
+Plan make_plan(uint64_t K, uint64_t N, uint64_t M, uint64_t fine_target = 0) {
   // Test hooks (the only environment knobs of the merge): CDB_PLAN_TARGET / CDB_PLAN_CTARGET
   // override the key / child rows per bucket, so that tests can push buckets into given tiers.
   // Wave-sized buckets: ~40 key rows and at most ~80 child rows (nodes + members) on average.
@@ -422,7 +440,7 @@ Plan make_plan(uint64_t K, uint64_t N, uint64_t M) {
   // target 120 as well, 4096 8.3. C5 (2 children per key) by child target: 40 26.0, 80 24.0,
   // 160-240 24.0 (key-bound); C1 and C4 have fewer children than keys and are key-bound.
   const bool child_heavy = N + M > 8 * K;
-  uint64_t target = child_heavy ? 120 : 40;
+  uint64_t target = child_heavy ? 120 : (fine_target ? fine_target : 40);
   if (const char* e = std::getenv("CDB_PLAN_TARGET")) target = (uint64_t)std::max(8, std::min(120, std::atoi(e)));
   uint64_t ctarget = child_heavy ? 4096 : std::max<uint64_t>(target, 80);
   if (const char* e = std::getenv("CDB_PLAN_CTARGET")) ctarget = (uint64_t)std::max(8, std::min(65536, std::atoi(e)));
@@ -1148,7 +1166,15 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   const uint64_t wm = opts ? opts->gc_watermark : 0;
   InLayout lay;
   CDB_TRY(input_layout(ctx, in, &lay));
-  const Plan plan = make_plan(K, N, M);
+  Plan plan = make_plan(K, N, M);
+  // Sorted runs that the persistent wave tier will merge (at most 8 per family, enough buckets):
+  // finer buckets, which its units group back to one wave's worth of rows each (runs.hip.h), so
+  // that no bucket is beyond a wave and the waves' lanes are full. (A run found out of order sends
+  // the merge to the partition path with these buckets: the same result.)
+  if (in->n_runs && in->n_runs <= 8 && pipe_wave_wanted(plan.nb) && !std::getenv("CDB_PLAN_TARGET") && groups_wanted()) {
+    const Plan fine = make_plan(K, N, M, pipe_fine_target());
+    if (fine.nb > plan.nb) plan = fine;
+  }
   const int shift = opts ? (int)opts->key_shift : 0;
   if (shift < 0 || shift > 16) return fail(ctx, CDB_BAD_ARGUMENT, "key_shift");
   const uint64_t nb = plan.nb;
@@ -1303,12 +1329,13 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   WA.big_list = d_big_list;
   WA.big_count = d_big_count;
   WA.V = RV;
+  WA.units = nullptr;
   // counters: the wide tier's per range [0, 64), the persistent wave tier's per (range, XCD slab)
   uint32_t* d_wide = (uint32_t*)ws_get(ctx, WS_WIDE, (64 + 64 * kXcds) * sizeof(uint32_t), &st);
   if (!d_wide) return st;
   CDB_HIP(hipMemsetAsync(d_wide, 0, (64 + 64 * kXcds) * sizeof(uint32_t), s), "memset wide");
   // the persistent wave tier (runs of at most 8 per family): one resident grid
-  const bool wave_pipe = use_runs && RV.bdir != nullptr;
+  const bool wave_pipe = use_runs && RV.bdir != nullptr && nb < (1ull << 28);  // (a unit: one word)
   const uint32_t pipe_grid = wave_pipe ? pipe_wave_grid(ctx) : 0;
   CDB_HIP(hipEventRecord(ctx->ev_fork, s), "event");  // inputs of both bucket tiers are ready
   // The wave and wide tiers run over P consecutive bucket ranges. Range p is scanned and compacted
@@ -1336,6 +1363,26 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   const uint32_t P = pipe_opt ? (uint32_t)std::min<uint64_t>({pipe_opt, std::max<uint64_t>(nb, 1), 64})
                      : pipe_auto ? kPipeRanges : 1;
   const bool pipelined = P > 1;
+  if (wave_pipe) {  // the persistent tier's units (runs.hip.h): a group's hash span must fit the
+                    // sort word as one bucket's does
+    const unsigned __int128 lim = (unsigned __int128)1 << (44 + A.rel_shift);
+    uint64_t g = 1;
+    while (g < kGroupMax && (unsigned __int128)(g + 1) * A.bw + 2 * nb + 2 < lim) ++g;
+    UnitArgs ua;
+    ua.kcnt = A.kcnt;
+    ua.ncnt = A.ncnt;
+    ua.mcnt = A.mcnt;
+    ua.nb = nb;
+    ua.P = P;
+    ua.gmax = (A.force_tier || !groups_wanted()) ? 1u : (uint32_t)g;
+    ua.ccap = group_ccap();
+    const uint64_t words = (nb + 31) / 32 + 3;
+    ua.units = (uint32_t*)ws_get(ctx, WS_UNITS, words * sizeof(uint32_t), &st);
+    if (!ua.units) return st;
+    pipe_units_kernel<<<(uint32_t)std::min<uint64_t>((words + 255) / 256, 4096), 256, 0, s>>>(ua);
+    CDB_TRY(launch_check(ctx, s, "pipe_units_kernel"));
+    WA.units = ua.units;
+  }
   CompactArgs C;
   C.ks = ksp[0];
   C.ns = nsp[0];
@@ -1595,6 +1642,7 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     stats->hot_slow_runs = hs[ST_HOT_SLOW];
     stats->hot_merged_children = hs[ST_HOT_MERGED];
     stats->wave_pipe_buckets = hs[ST_PIPE];
+    stats->wave_pipe_units = hs[ST_PIPE_UNITS];
   }
   if ((flags & CDB_MERGE_STRICT_DICT_PANIC) && hs[ST_DICT_MERGES])
     return fail(ctx, CDB_DICT_MERGE_UNIMPLEMENTED, "Dict::merge reached (lwwhash.rs:180 unimplemented!())");

@@ -216,6 +216,52 @@ __global__ void __launch_bounds__(256) run_reduce3_kernel(Reduce3Args a) {
   }
 }
 
+// The persistent wave tier's units (bucket_wave_pipe_kernel): bit b of `units` is set where a unit
+// starts. Consecutive buckets are packed greedily while together they hold at most 64 key rows,
+// ccap child rows and gmax buckets (gmax: their hash span still fits the wave's sort word); a unit
+// also starts at every multiple of 32 (so a chunk's last unit ends within the next 32 bits) and at
+// every range start of a pipelined bucket phase, and a bucket beyond one wave (the wide tier's) or
+// any bucket when gmax = 1 is a unit of its own. Bits past the last bucket are set. One thread per
+// 32 buckets.
+struct UnitArgs {
+  const uint32_t *kcnt, *ncnt, *mcnt;
+  uint64_t nb;
+  uint32_t P;          // bucket-phase ranges: range p starts at bucket nb * p / P
+  uint32_t gmax, ccap;
+  uint32_t* units;     // (nb + 31) / 32 + 3 words
+};
+__global__ void __launch_bounds__(256) pipe_units_kernel(UnitArgs a) {
+  const uint64_t words = (a.nb + 31) / 32 + 3;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < words; t += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t m = 0, k = 0, c = 0, g = 0;
+    bool prev_single = true;
+    for (uint32_t i = 0; i < 32; ++i) {
+      const uint64_t b = 32 * t + i;
+      if (b >= a.nb) {  // past the last bucket: every bit
+        m |= ~0u << i;
+        break;
+      }
+      const uint32_t K = a.kcnt[b], C = a.ncnt[b] + a.mcnt[b];
+      const bool single = a.gmax <= 1 || K > (uint32_t)WaveLds<1>::KC || C > a.ccap;
+      const uint64_t p = (b * a.P + a.nb - 1) / a.nb;  // the first range starting at or after b
+      const bool rstart = a.nb * p / a.P == b;
+      if (i == 0 || prev_single || single || rstart || k + K > (uint32_t)WaveLds<1>::KC || c + C > a.ccap ||
+          g >= a.gmax) {
+        m |= 1u << i;
+        k = K;
+        c = C;
+        g = 1;
+      } else {
+        k += K;
+        c += C;
+        ++g;
+      }
+      prev_single = single;
+    }
+    a.units[t] = m;
+  }
+}
+
 // A bucket's slices of the runs, one per lane: lane j < L holds slice j of the family group --
 // keys: the nr key runs; children: the nr node runs, then the nr member runs (child slots are
 // node rows first, then member rows). incl = inclusive prefix of the slice lengths over lanes;
@@ -402,6 +448,12 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, 5) bucket_wave_runs_kernel(W
 // Work: the bucket range is cut into 8 XCD slabs; waves of XCD x claim chunks of kPipeChunk
 // consecutive buckets of slab x from its counter (the next claim is issued when a chunk starts)
 // and then help the other slabs. Results are those of bucket_wave_runs_kernel bucket for bucket.
+// Units: a wave takes a chunk's buckets in groups -- consecutive buckets packed greedily while their
+// rows fit one wave (at most 64 key rows, W.gccap child rows, W.gmax buckets; a bucket beyond one
+// wave alone stays a unit of its own, which the wide tier takes). Fixed-width hash buckets vary
+// a lot in size (C4: ~40 key rows on average, 5 % over 64), so a unit of one bucket leaves a third
+// of the lanes idle; a group of small buckets fills them, and with finer buckets (make_plan's
+// pipe target) no bucket is wide.
 #ifndef CDB_PIPE_CHUNK
 #define CDB_PIPE_CHUNK 32
 #endif
@@ -411,11 +463,12 @@ constexpr uint32_t kPipeChunk = CDB_PIPE_CHUNK;
 #endif
 constexpr uint32_t kPipeDone = 0xFFFFFFFFu;
 
-// Bucket b's slices from its bdir row (lanes 0..31) and bucket b + 1's (lanes 32..63): one
-// 256-B load, then lane j < 32 holds slice j's (first row, end row).
-__device__ __forceinline__ u32x2 pipe_pairs(const RunView& V, uint32_t b, int lane, bool valid) {
+// The slices of buckets b0 .. b1 - 1 (a group): bucket b0's bdir row (lanes 0..31) and bucket b1's
+// (lanes 32..63), two 128-B lines (one 256-B load when b1 = b0 + 1), then lane j < 32 holds slice
+// j's (first row, end row).
+__device__ __forceinline__ u32x2 pipe_pairs(const RunView& V, uint32_t b0, uint32_t b1, int lane, bool valid) {
   uint32_t v = 0;
-  if (valid) v = V.bdir[(uint64_t)b * kBdirRow + (uint32_t)lane];
+  if (valid) v = V.bdir[(uint64_t)(lane < 32 ? b0 : b1 - 1) * kBdirRow + (uint32_t)lane];
   const uint32_t e = (uint32_t)__shfl((int)v, (lane + 32) & 63, 64);
   u32x2 se = {v, e};
   if (lane >= 32) se = {0u, 0u};
@@ -497,13 +550,17 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, CDB_PIPE_MINB) bucket_wave_p
     if (lane == 0) v = atomicAdd(W.pipe_next + x, 1u);
     return v;  // (lane 0's; read once the chunk is needed)
   };
-  // the bucket stream (wave-uniform): chunk [sc, se) of slab xs, the next chunk's claim in flight
-  uint32_t xs = x0, sc = 0, se = 0, pend = claim(x0);
+  // the unit stream (wave-uniform): chunk [sc, se) of slab xs; gm = the unit starts in it not yet
+  // taken (bit i: bucket sc + i), ge = the end of its last unit; the next chunk's claim in flight
+  const __attribute__((address_space(4))) uint32_t* units =
+      (const __attribute__((address_space(4))) uint32_t*)W.units;  // (scalar loads)
+  // A unit travels as one word, first bucket << 4 | (buckets - 1) (the host keeps nb < 2^28 here).
+  uint32_t xs = x0, sc = 0, ge = 0, pend = claim(x0), gm = 0;
   bool done = false;
   auto produce = [&]() -> uint32_t {
-    if (done) return kPipeDone;
-    if (sc >= se) {
-      uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)pend, 0);
+    while (gm == 0) {
+      if (done) return kPipeDone;
+      uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)pend, 0), se = 0;
       for (;;) {
         const uint32_t lo = slab_lo(xs), hi = slab_lo(xs + 1);
         const uint64_t st = (uint64_t)lo + (uint64_t)c * kPipeChunk;
@@ -520,9 +577,23 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, CDB_PIPE_MINB) bucket_wave_p
         c = (uint32_t)__builtin_amdgcn_readlane((int)claim(xs), 0);
       }
       pend = claim(xs);
+      // bits sc .. sc + 63 of the unit bitmap (a unit starts at every multiple of 32: the chunk's
+      // last unit ends within them)
+      const uint32_t w = sc >> 5, s = sc & 31;
+      const uint64_t lo64 = (uint64_t)units[w] | ((uint64_t)units[w + 1] << 32);
+      const uint64_t win = s ? (lo64 >> s) | ((uint64_t)units[w + 2] << (64 - s)) : lo64;
+      const uint32_t n = se - sc;  // (<= kPipeChunk <= 32)
+      gm = (uint32_t)(win & ((1ull << n) - 1));
+      const uint64_t rest = win >> n;
+      ge = min(W.bhi, sc + (rest ? n + (uint32_t)__builtin_ctzll(rest) : 64u));
     }
-    return sc++;
+    const uint32_t g0 = sc + (uint32_t)__builtin_ctz(gm);
+    gm &= gm - 1;
+    const uint32_t g1 = gm ? sc + (uint32_t)__builtin_ctz(gm) : ge;
+    return (g0 << 4) | (g1 - g0 - 1);
   };
+  auto ufirst = [](uint32_t u) { return u >> 4; };
+  auto uend = [](uint32_t u) { return (u >> 4) + (u & 15) + 1; };
 
   uint32_t b = produce();
   if (b == kPipeDone) return;
@@ -530,12 +601,13 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, CDB_PIPE_MINB) bucket_wave_p
   PipeMap qc;
   {
     WaveDir d;
-    qc = pipe_map(V, pipe_pairs(V, b, lane, true), d);
+    qc = pipe_map(V, pipe_pairs(V, ufirst(b), uend(b), lane, true), d);
+    d.G = (b & 15) + 1;
     pipe_load<REC>(V, d, qc, lane, in);
   }
   uint32_t b1 = produce();
-  u32x2 pr = pipe_pairs(V, b1, lane, b1 != kPipeDone);  // (no bucket: zero pairs, an empty map)
-  uint32_t folded = 0;  // (wave-uniform) buckets this wave folded: stats.wave_pipe_buckets
+  u32x2 pr = pipe_pairs(V, ufirst(b1), uend(b1), lane, b1 != kPipeDone);  // (no unit: zero pairs, an empty map)
+  uint32_t folded = 0, nunits = 0;  // (wave-uniform) buckets / units this wave folded: stats.wave_pipe_*
   while (b != kPipeDone) {
     const uint32_t b2 = b1 != kPipeDone ? produce() : kPipeDone;
     const WaveDir d = in.d;
@@ -545,7 +617,7 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, CDB_PIPE_MINB) bucket_wave_p
     WaveMid<1> mid;
     int act;
     if (!two) {
-      act = wave_phase_a<1, 1>(W, L, b, lane, in, mid);
+      act = wave_phase_a<1, 1>(W, L, ufirst(b), lane, in, mid);
     } else {
       WaveIn<1, 2> in2;
       in2.d = d;
@@ -563,7 +635,7 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, CDB_PIPE_MINB) bucket_wave_p
       in2.ct[0] = in.ct[0];
       in2.cm[0] = in.cm[0];
       pipe_load_child<REC>(V, d, qc, lane, 1, in2);
-      act = wave_phase_a<1, 2>(W, L, b, lane, in2, mid);
+      act = wave_phase_a<1, 2>(W, L, ufirst(b), lane, in2, mid);
     }
     // bucket b's input registers are dead: bucket b + 1's rows into them and b + 2's pairs, in
     // flight while b's children fold and its outputs are written. (One program point for every
@@ -572,23 +644,28 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, CDB_PIPE_MINB) bucket_wave_p
     {
       WaveDir dn;
       qc = pipe_map(V, pr, dn);
+      dn.G = (b1 & 15) + 1;
       pipe_load<REC>(V, dn, qc, lane, in);
-      pr = pipe_pairs(V, b2, lane, b2 != kPipeDone);
+      pr = pipe_pairs(V, ufirst(b2), uend(b2), lane, b2 != kPipeDone);
     }
     if (act == WAVE_PUSH) {
-      wave_push(W, b, lane);
+      wave_push(W, ufirst(b), lane, d.G);
     } else if (act == WAVE_GO) {
       if (!two)
-        wave_phase_b<1, 1>(W, L, b, lane, mid);
+        wave_phase_b<1, 1>(W, L, ufirst(b), lane, mid);
       else
-        wave_phase_b<1, 2>(W, L, b, lane, mid);
-      ++folded;
+        wave_phase_b<1, 2>(W, L, ufirst(b), lane, mid);
+      folded += d.G;
+      ++nunits;
     }
     wave_sync();  // (the next bucket reuses this one's LDS)
     b = b1;
     b1 = b2;
   }
-  if (lane == 0 && folded) atomicAdd(&stat_shard(W.A.stats)[ST_PIPE], (unsigned long long)folded);
+  if (lane == 0 && folded) {
+    atomicAdd(&stat_shard(W.A.stats)[ST_PIPE], (unsigned long long)folded);
+    atomicAdd(&stat_shard(W.A.stats)[ST_PIPE_UNITS], (unsigned long long)nunits);
+  }
 }
 
 // The wide tier (65..128 key rows or 129..256 child rows) on the runs: as bucket_wide_kernel.
@@ -609,7 +686,7 @@ __global__ void __launch_bounds__(kWavesPerWG * 64) bucket_wide_runs_kernel(Wave
       WaveIn<2> in;
       if (W.V.bdir) {  // (wave-uniform) the bucket-major directory: one load, no directory entry
         WaveDir d;
-        const PipeMap q = pipe_map(W.V, pipe_pairs(W.V, bb, lane, true), d);
+        const PipeMap q = pipe_map(W.V, pipe_pairs(W.V, bb, bb + 1, lane, true), d);
         in.d = d;
         const uint32_t C = d.N + d.M;
 #pragma unroll

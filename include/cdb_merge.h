@@ -194,6 +194,7 @@ typedef struct cdb_merge_stats {
   uint64_t hot_merged_children; /* chip-wide path: children whose runs arrived in child order
                                 (a merge result's) and were merged instead of radix-sorted */
   uint64_t wave_pipe_buckets;   /* buckets folded by the persistent wave tier (bucket_wave_pipe_kernel) */
+  uint64_t wave_pipe_units;     /* its units: groups of consecutive buckets merged by one wave */
 } cdb_merge_stats;
 
 cdb_status cdb_merge(cdb_ctx* ctx, cdb_batch* const* inputs, uint32_t n,

@@ -25,9 +25,10 @@
 PIN_SIZE(cdb_merge_opts, 24);
 PIN_OFF(cdb_merge_opts, gc_watermark, 8);
 PIN_OFF(cdb_merge_opts, key_shift, 16);
-PIN_SIZE(cdb_merge_stats, 184);
+PIN_SIZE(cdb_merge_stats, 192);
 PIN_OFF(cdb_merge_stats, hot_merged_children, 168);
 PIN_OFF(cdb_merge_stats, wave_pipe_buckets, 176);
+PIN_OFF(cdb_merge_stats, wave_pipe_units, 184);
 PIN_OFF(cdb_merge_stats, hot_slow_runs, 160);
 PIN_OFF(cdb_merge_stats, mid_buckets, 112);
 PIN_OFF(cdb_merge_stats, device_ms, 120);

@@ -7,6 +7,11 @@ for p in (ROOT, os.path.join(ROOT, "oracle")):
         sys.path.insert(0, p)
 
 
+# torch before libcdbmerge in every session (one HIP runtime per process: torch's device init fails
+# when the library's runtime came up first, so a GPU test file run on its own would not see the GPU)
+import torch  # noqa: E402,F401
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run via gpurun)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
