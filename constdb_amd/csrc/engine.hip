@@ -71,7 +71,7 @@ bool pipe_wave_wanted(uint64_t nb) {
 // Its units group consecutive buckets (runs.hip.h, at most kGroupMax); the plan then targets ~kPipeFineTarget key rows
 // per bucket instead of ~40. Test and A/B hooks: CDB_GROUPS=0 (one bucket per unit, round-5 buckets),
 // CDB_PIPE_TARGET (key rows per bucket), CDB_GROUP_CCAP (child rows per unit, 64 or 128).
-constexpr uint64_t kPipeFineTarget = 20;
+constexpr uint64_t kPipeFineTarget = 24;  // (C4 step: 20 / 22 / 24 / 26 -> 17.96 / 17.19 / 16.98 / 17.08 ms)
 constexpr uint64_t kGroupMax = 16;
 bool groups_wanted() {
   const char* e = std::getenv("CDB_GROUPS");
@@ -1364,7 +1364,19 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
                      : pipe_auto ? kPipeRanges : 1;
   const bool pipelined = P > 1;
   if (wave_pipe) {  // the persistent tier's units (runs.hip.h): a group's hash span must fit the
-                    // sort word as one bucket's does
+                    // sort word as one bucket's does. Where fewer than 4 buckets fit (below ~2^22
+                    // buckets; below ~2^21 one bucket's span already needs a shifted word, and the
+                    // child lookup compares shifted words) the shift grows to fit kGroupMax buckets,
+                    // so that groups form at every size (an equal shifted word of two hashes goes to
+                    // the exact tier, as ever)
+    if (groups_wanted() && !A.force_tier &&
+        (unsigned __int128)4 * A.bw + 2 * nb + 2 >= (unsigned __int128)1 << (44 + A.rel_shift)) {
+      const unsigned __int128 span = (unsigned __int128)kGroupMax * A.bw + 2 * nb + 2;
+      int bits = 0;
+      while (bits < 80 && (span >> bits)) ++bits;
+      A.rel_shift = std::max(A.rel_shift, std::min(bits, 64) - 44);
+      WA.A.rel_shift = A.rel_shift;
+    }
     const unsigned __int128 lim = (unsigned __int128)1 << (44 + A.rel_shift);
     uint64_t g = 1;
     while (g < kGroupMax && (unsigned __int128)(g + 1) * A.bw + 2 * nb + 2 < lim) ++g;
@@ -1379,9 +1391,13 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     const uint64_t words = (nb + 31) / 32 + 3;
     ua.units = (uint32_t*)ws_get(ctx, WS_UNITS, words * sizeof(uint32_t), &st);
     if (!ua.units) return st;
-    pipe_units_kernel<<<(uint32_t)std::min<uint64_t>((words + 255) / 256, 4096), 256, 0, s>>>(ua);
+    pipe_units_kernel<<<(uint32_t)std::min<uint64_t>((words + 7) / 8, 4096), 256, 0, s>>>(ua);
     CDB_TRY(launch_check(ctx, s, "pipe_units_kernel"));
     WA.units = ua.units;
+    // the wide tier's side-stream launch waits for the units too, so that it is not dispatched
+    // while the persistent kernel waits behind them (it then holds CUs the persistent grid needs:
+    // +1.3 ms measured with one-bucket units)
+    CDB_HIP(hipEventRecord(ctx->ev_fork, s), "event");
   }
   CompactArgs C;
   C.ks = ksp[0];

@@ -221,8 +221,8 @@ __global__ void __launch_bounds__(256) run_reduce3_kernel(Reduce3Args a) {
 // ccap child rows and gmax buckets (gmax: their hash span still fits the wave's sort word); a unit
 // also starts at every multiple of 32 (so a chunk's last unit ends within the next 32 bits) and at
 // every range start of a pipelined bucket phase, and a bucket beyond one wave (the wide tier's) or
-// any bucket when gmax = 1 is a unit of its own. Bits past the last bucket are set. One thread per
-// 32 buckets.
+// any bucket when gmax = 1 is a unit of its own. Bits past the last bucket are set. One wave per 64
+// buckets: each lane loads one bucket's counts (coalesced), the greedy packing runs on scalars.
 struct UnitArgs {
   const uint32_t *kcnt, *ncnt, *mcnt;
   uint64_t nb;
@@ -231,34 +231,42 @@ struct UnitArgs {
   uint32_t* units;     // (nb + 31) / 32 + 3 words
 };
 __global__ void __launch_bounds__(256) pipe_units_kernel(UnitArgs a) {
-  const uint64_t words = (a.nb + 31) / 32 + 3;
-  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < words; t += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t m = 0, k = 0, c = 0, g = 0;
-    bool prev_single = true;
-    for (uint32_t i = 0; i < 32; ++i) {
-      const uint64_t b = 32 * t + i;
-      if (b >= a.nb) {  // past the last bucket: every bit
-        m |= ~0u << i;
-        break;
+  const uint64_t words = (a.nb + 31) / 32 + 3, waves = (words + 1) / 2;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < waves;
+       w += ((uint64_t)gridDim.x * blockDim.x) >> 6) {  // (wave-uniform)
+    const uint64_t b = 64 * w + lane;
+    uint32_t K = 0, C = 0;
+    bool rstart = false;
+    if (b < a.nb) {
+      K = a.kcnt[b];
+      C = a.ncnt[b] + a.mcnt[b];
+      if (a.P > 1) {  // (wave-uniform; 64-bit divisions only for a pipelined bucket phase)
+        const uint64_t p = (b * a.P + a.nb - 1) / a.nb;  // the first range starting at or after b
+        rstart = a.nb * p / a.P == b;
       }
-      const uint32_t K = a.kcnt[b], C = a.ncnt[b] + a.mcnt[b];
-      const bool single = a.gmax <= 1 || K > (uint32_t)WaveLds<1>::KC || C > a.ccap;
-      const uint64_t p = (b * a.P + a.nb - 1) / a.nb;  // the first range starting at or after b
-      const bool rstart = a.nb * p / a.P == b;
-      if (i == 0 || prev_single || single || rstart || k + K > (uint32_t)WaveLds<1>::KC || c + C > a.ccap ||
-          g >= a.gmax) {
-        m |= 1u << i;
-        k = K;
-        c = C;
+    }
+    const bool single = a.gmax <= 1 || K > (uint32_t)WaveLds<1>::KC || C > a.ccap;
+    const uint64_t past = __ballot(b >= a.nb), sgl = __ballot(single), rst = __ballot(rstart);
+    uint64_t m = past | 1ull | (1ull << 32) | sgl | rst;  // starts: past the end, each 32, ranges, singles
+    uint32_t k = 0, c = 0, g = 0;
+    for (uint32_t i = 0; i < 64; ++i) {  // (scalar)
+      const uint32_t Ki = (uint32_t)__builtin_amdgcn_readlane((int)K, (int)i);
+      const uint32_t Ci = (uint32_t)__builtin_amdgcn_readlane((int)C, (int)i);
+      const bool start = ((m >> i) & 1) || (i && ((sgl >> (i - 1)) & 1)) || k + Ki > (uint32_t)WaveLds<1>::KC ||
+                         c + Ci > a.ccap || g >= a.gmax;
+      if (start) {
+        m |= 1ull << i;
+        k = Ki;
+        c = Ci;
         g = 1;
       } else {
-        k += K;
-        c += C;
+        k += Ki;
+        c += Ci;
         ++g;
       }
-      prev_single = single;
     }
-    a.units[t] = m;
+    if (lane < 2 && 2 * w + lane < words) a.units[2 * w + lane] = (uint32_t)(m >> (32 * lane));
   }
 }
 

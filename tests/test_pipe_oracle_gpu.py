@@ -13,7 +13,10 @@ C4's keys -- type_counter.rs:59-91 with 1-8 nodes per counter, lwwhash.rs:87-128
     -- the state runs the bench times: children in child order);
   * the same with DB::gc of Deletes (db.rs:82-119);
   * C4 at a 5M-key universe (~530K buckets), where the kernel runs without the hook;
-  * small random states (type conflicts, time ties, side maps, few buckets per XCD slab), forced."""
+  * small random states (type conflicts, time ties, side maps, few buckets per XCD slab), forced.
+Round 6: the kernel's unit is a group of consecutive buckets (runs.hip.h, pipe_units_kernel); every case
+asserts that groups formed (stats.wave_pipe_units < wave_pipe_buckets), and CDB_GROUPS=0 (one bucket
+per unit, round-5 bucket sizes) is pinned to the oracle as well."""
 import ctypes
 
 import pytest
@@ -82,11 +85,15 @@ def _merge_vs_oracle(ctx, snaps, records, gc=None, upload=False):
     return st
 
 
-def _assert_pipe_folded_most(st):
+def _assert_pipe_folded_most(st, grouped=True):
     """The persistent kernel folded the bulk of the buckets (the rest: the wide tier, 65..128 key
-    rows or 129..256 children, and the workgroup tiers)."""
+    rows or 129..256 children, and the workgroup tiers), in groups of several buckets per unit."""
     assert st.wave_pipe_buckets > 0
     assert st.wave_pipe_buckets > 5 * (st.wide_buckets + st.mid_buckets + st.hot_buckets)
+    if grouped:
+        assert 0 < st.wave_pipe_units < 0.8 * st.wave_pipe_buckets
+    else:
+        assert st.wave_pipe_units == st.wave_pipe_buckets
 
 
 @pytest.fixture(scope="module")
@@ -111,6 +118,12 @@ def test_pipe_forced_c4_1m_vs_oracle(ctx, monkeypatch, c4_1m, records):
     _assert_pipe_folded_most(st)
     monkeypatch.setenv("CDB_WAVE_PIPE", "0")  # the hook really switches kernels
     assert _merge_vs_oracle(ctx, c4_1m, records).wave_pipe_buckets == 0
+
+
+def test_pipe_forced_c4_1m_one_bucket_units_vs_oracle(ctx, monkeypatch, c4_1m):
+    monkeypatch.setenv("CDB_WAVE_PIPE", "force")
+    monkeypatch.setenv("CDB_GROUPS", "0")
+    _assert_pipe_folded_most(_merge_vs_oracle(ctx, c4_1m, records=True), grouped=False)
 
 
 def test_pipe_forced_c4_1m_plain_columns_upload_vs_oracle(ctx, monkeypatch, c4_1m):
@@ -160,3 +173,4 @@ def test_pipe_forced_random_vs_oracle(ctx, monkeypatch, seed):
     snaps = [cdb.gen_snapshot(cfg, r) for r in range(cfg.n_replicas)]
     st = _merge_vs_oracle(ctx, snaps, records=bool(seed % 2))
     assert st.wave_pipe_buckets > 0
+    assert st.wave_pipe_units < st.wave_pipe_buckets
