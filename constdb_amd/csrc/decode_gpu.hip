@@ -783,14 +783,14 @@ __global__ void __launch_bounds__(256) idx_flat_walk_kernel(IdxArgs a, const uin
     }
   }
 }
-// Which walk (test and A/B hook CDB_IDX_WALK): "wave" idx_walk_kernel, "lane" idx_lane_walk_kernel,
-// "flat" (default) idx_flat_walk_kernel.
+// Which walk (test and A/B hook CDB_IDX_WALK): "wave" (default) idx_walk_kernel, "lane"
+// idx_lane_walk_kernel, "flat" idx_flat_walk_kernel.
 int idx_walk_kind() {
   static const int w = [] {
     const char* e = std::getenv("CDB_IDX_WALK");
-    if (e && std::strcmp(e, "wave") == 0) return 0;
+    if (e && std::strcmp(e, "flat") == 0) return 2;
     if (e && std::strcmp(e, "lane") == 0) return 1;
-    return 2;
+    return 0;
   }();
   return w;
 }

@@ -9,7 +9,7 @@ O=gpurun_out
 mkdir -p $O
 T=${TAG:-lw}
 if [ -z "$NO_TESTS" ]; then
-timeout -k 10 600 python -u -m pytest tests/test_decode_gpu.py tests/test_decode_device_gpu.py tests/test_decode_window_gpu.py tests/test_decode_merge_full_gpu.py -x -q --timeout 300 --timeout-method thread > $O/pytest_$T.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest_$T.log; exit 1; }
+CDB_IDX_WALK=${TEST_WALK:-flat} timeout -k 10 600 python -u -m pytest tests/test_decode_gpu.py tests/test_decode_device_gpu.py tests/test_decode_window_gpu.py tests/test_decode_merge_full_gpu.py -x -q --timeout 300 --timeout-method thread > $O/pytest_$T.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest_$T.log; exit 1; }
 tail -2 $O/pytest_$T.log
 fi
 for v in ${WALKS:-flat lane wave}; do
