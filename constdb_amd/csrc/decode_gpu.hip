@@ -397,27 +397,6 @@ struct DCur {
     return r < wlen ? lds[r] : p[i];
   }
 };
-// A lane's own cursor over the stream in global memory (the lane walk below): the 16-B aligned
-// piece holding the last byte read stays in registers, so a varint costs one load, not one per
-// byte. (A piece that starts before the end of the stream may read up to 15 bytes past it: the
-// device copy has 16 bytes of slack.)
-struct LCur {
-  const uint8_t* p;
-  uint64_t n, off;
-  uint64_t cb = ~0ull;  // the cached piece's offset
-  uint4 c = {0u, 0u, 0u, 0u};
-  __device__ __forceinline__ uint32_t at(uint64_t i) {
-    const uint64_t a = i & ~15ull;
-    if (a != cb) {
-      cb = a;
-      c = *reinterpret_cast<const uint4*>(p + a);
-    }
-    // (selects on 64-bit halves: an indexed pick of the word would become an LDS array)
-    const uint32_t r = (uint32_t)i & 15u;
-    const uint64_t h = r < 8 ? (((uint64_t)c.y << 32) | c.x) : (((uint64_t)c.w << 32) | c.z);
-    return (uint32_t)(h >> ((r & 7u) * 8u)) & 0xFFu;
-  }
-};
 template <class Cur>
 __device__ __forceinline__ bool dc_int(Cur& c, int64_t* v) {
   if (c.off >= c.n) return false;
@@ -570,238 +549,8 @@ __global__ void __launch_bounds__(256) idx_walk_kernel(IdxArgs a, const uint64_t
   }
 }
 
-// The same walk with one LANE per chunk: 64 chunks per wave walked side by side, each lane reading
-// its own bytes through a register-cached cursor (LCur). Results are idx_walk_kernel's chunk for
-// chunk: the sync point is the first of the chunk's first kIdxSyncTries offsets from which kIdxSync
-// entries of at most kIdxEntryMax bytes parse (tried in order by the lane, which idx_walk_kernel's
-// lanes do 64 at a time), then the entries from there until one starts past the chunk. There the
-// chunk's ~140 entries were one lane's serial walk and the wave's other 63 lanes waited; here every
-// lane walks. (Test and A/B hook: CDB_IDX_WAVE=1 runs idx_walk_kernel.)
-__global__ void __launch_bounds__(256) idx_lane_walk_kernel(IdxArgs a, const uint64_t* __restrict__ req,
-                                                            const uint32_t* __restrict__ list, uint32_t nlist) {
-  const uint32_t total = list ? nlist : a.T;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const uint32_t t = list ? list[i] : i;
-    const uint64_t lo = a.S + (uint64_t)t * kIdxChunk, hi = min(a.n, lo + kIdxChunk);
-    uint64_t o = list ? req[t] : lo;
-    LCur c{a.raw, a.n, lo};
-    if (!list && t > 0) {
-      uint64_t found = ~0ull;
-      for (uint32_t k = 0; k < kIdxSyncTries && lo + k < hi; ++k) {
-        c.off = lo + k;
-        uint32_t q = 0;
-        for (; q < kIdxSync && c.off < a.n; ++q) {
-          const uint64_t at = c.off;
-          if (!dc_data_entry(c, kIdxEntryMax) || c.off - at > kIdxEntryMax) break;
-        }
-        if (q == kIdxSync) {
-          found = lo + k;
-          break;
-        }
-      }
-      if (found == ~0ull) {
-        a.sync[t] = ~0ull;
-        a.count[t] = 0;
-        a.stop[t] = lo;
-        a.ok[t] = 0;
-        continue;
-      }
-      o = found;
-    }
-    c.off = o;
-    uint16_t* rel = a.rel + (uint64_t)t * kIdxRelCap;
-    uint32_t k = 0;
-    bool good = true;
-    while (c.off < hi) {
-      const uint64_t at = c.off;
-      if (k < kIdxRelCap) rel[k] = (uint16_t)(at - lo);
-      if (!dc_data_entry(c, ~0ull)) {
-        c.off = at;
-        good = false;
-        break;
-      }
-      ++k;
-    }
-    a.sync[t] = o;
-    a.count[t] = k;
-    a.stop[t] = c.off;
-    a.ok[t] = good ? 1 : 0;
-  }
-}
-// The lane walk as a state machine that parses ONE field per step (an integer, a length and the
-// bytes it spans, a count, or the tag byte), so that the 64 lanes of a wave stay converged whatever
-// entry shape each one is in (in idx_lane_walk_kernel a lane inside a counter's node loop and one in
-// a set's member loop run one after the other). Accepts exactly what dc_data_entry accepts: the same
-// checks in the same order. Sync search and walk are two modes of the same loop.
-enum : uint32_t {
-  F_KEY = 0, F_I1, F_I2, F_I3, F_TAG,  // every entry: key span, three integers, tag byte
-  F_CCNT, F_CN,                        // counter: node count, then 3 integers per node
-  F_BVAL,                              // bytes: value span
-  F_ACNT, F_AM, F_AT, F_AV,            // set / dict adds: count, then member span, time[, value span]
-  F_DCNT, F_DM, F_DT                   // set / dict dels: count, then member span, time
-};
-__global__ void __launch_bounds__(256) idx_flat_walk_kernel(IdxArgs a, const uint64_t* __restrict__ req,
-                                                            const uint32_t* __restrict__ list, uint32_t nlist) {
-  const uint32_t total = list ? nlist : a.T;
-  for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < total; i0 += gridDim.x * blockDim.x) {  // (uniform)
-    const uint32_t i = i0 + threadIdx.x;
-    const bool act = i < total;
-    const uint32_t t = act ? (list ? list[i] : i) : 0;
-    const uint64_t lo = a.S + (uint64_t)t * kIdxChunk, hi = min(a.n, lo + kIdxChunk);
-    uint16_t* rel = a.rel + (uint64_t)t * kIdxRelCap;
-    uint64_t o = act && list ? req[t] : lo;  // where the walk starts
-    LCur c{a.raw, a.n, o};
-    // mode 0: sync search (attempt at base a0, q entries parsed), 1: walk (k entries), 2: finished
-    uint32_t mode = (!act) ? 2u : (!list && t > 0) ? 0u : 1u;
-    uint64_t at = c.off, a0 = lo, rem = 0;
-    uint32_t st = F_KEY, q = 0, k = 0, sub = 0;
-    bool dict = false, good = true;
-    const uint64_t big = ~0ull;
-    if (mode == 1) {
-      if (c.off < hi) rel[0] = (uint16_t)(c.off - lo);
-      else mode = 2;
-    }
-    if (mode == 2 && act) {  // (a walk that starts past its chunk: no entries)
-      a.sync[t] = c.off;
-      a.count[t] = 0;
-      a.stop[t] = c.off;
-      a.ok[t] = 1;
-    }
-    while (__ballot(mode < 2)) {
-      if (mode < 2) {
-        const uint64_t lim = mode == 0 ? kIdxEntryMax : big;
-        bool ok;
-        int64_t v = 0;
-        if (st == F_TAG) {
-          ok = c.off < c.n;
-          if (ok) v = (int64_t)c.at(c.off++);
-        } else {
-          ok = dc_int(c, &v);
-        }
-        const bool span = st == F_KEY || st == F_BVAL || st == F_AM || st == F_AV || st == F_DM;
-        const bool cnt = st == F_CCNT || st == F_ACNT || st == F_DCNT;
-        if (ok && (span || cnt)) ok = v >= 0;
-        const uint64_t u = (uint64_t)v;
-        if (ok && span) {
-          ok = u <= c.n - c.off && u <= lim;
-          if (ok) c.off += u;
-        }
-        if (ok && cnt) {
-          const uint64_t m = min(c.n - c.off, lim);
-          ok = u <= (st == F_CCNT ? m / 3 : m / 2);
-          rem = u;
-        }
-        bool end = false;  // the entry is complete
-        if (ok) {
-          switch (st) {
-            case F_KEY: st = F_I1; break;
-            case F_I1: st = F_I2; break;
-            case F_I2: st = F_I3; break;
-            case F_I3: st = F_TAG; break;
-            case F_TAG:
-              if (v == TAG_COUNTER) st = F_CCNT;
-              else if (v == TAG_BYTES) st = F_BVAL;
-              else if (v == TAG_SET || v == TAG_DICT) {
-                st = F_ACNT;
-                dict = v == TAG_DICT;
-              } else ok = false;
-              break;
-            case F_CCNT:
-              st = F_CN;
-              sub = 0;
-              end = rem == 0;
-              break;
-            case F_CN:
-              if (++sub == 3) {
-                sub = 0;
-                end = --rem == 0;
-              }
-              break;
-            case F_BVAL: end = true; break;
-            case F_ACNT: st = rem ? F_AM : F_DCNT; break;
-            case F_AM: st = F_AT; break;
-            case F_AT:
-              if (dict) st = F_AV;
-              else st = --rem ? F_AM : F_DCNT;
-              break;
-            case F_AV: st = --rem ? F_AM : F_DCNT; break;
-            case F_DCNT:
-              st = F_DM;
-              end = rem == 0;
-              break;
-            case F_DM: st = F_DT; break;
-            default: end = --rem == 0; st = F_DM; break;  // F_DT
-          }
-        }
-        if (mode == 0) {  // sync search
-          if (ok && end) {
-            ok = c.off - at <= kIdxEntryMax;
-            if (ok && ++q == kIdxSync) {  // found: walk from the attempt's base
-              mode = 1;
-              c.off = at = o = a0;
-              st = F_KEY;
-              rel[0] = (uint16_t)(a0 - lo);
-              continue;
-            }
-            if (ok && c.off >= c.n) ok = false;  // (the stream ended before kIdxSync entries)
-            at = c.off;
-            st = F_KEY;
-          }
-          if (!ok) {  // next attempt
-            ++a0;
-            if (a0 >= lo + kIdxSyncTries || a0 >= hi) {
-              a.sync[t] = ~0ull;
-              a.count[t] = 0;
-              a.stop[t] = lo;
-              a.ok[t] = 0;
-              mode = 2;
-            } else {
-              c.off = at = a0;
-              q = 0;
-              st = F_KEY;
-            }
-          }
-        } else {  // walk
-          if (!ok) {
-            good = false;
-            c.off = at;
-          } else if (end) {
-            ++k;
-            at = c.off;
-            st = F_KEY;
-            if (c.off < hi && k < kIdxRelCap) rel[k] = (uint16_t)(c.off - lo);
-          }
-          if (!ok || (end && c.off >= hi)) {
-            a.sync[t] = o;
-            a.count[t] = k;
-            a.stop[t] = c.off;
-            a.ok[t] = good ? 1 : 0;
-            mode = 2;
-          }
-        }
-      }
-    }
-  }
-}
-// Which walk (test and A/B hook CDB_IDX_WALK): "wave" (default) idx_walk_kernel, "lane"
-// idx_lane_walk_kernel, "flat" idx_flat_walk_kernel.
-int idx_walk_kind() {
-  static const int w = [] {
-    const char* e = std::getenv("CDB_IDX_WALK");
-    if (e && std::strcmp(e, "flat") == 0) return 2;
-    if (e && std::strcmp(e, "lane") == 0) return 1;
-    return 0;
-  }();
-  return w;
-}
 void idx_walk_launch(const IdxArgs& a, const uint64_t* req, const uint32_t* list, uint32_t n, hipStream_t s) {
-  const int kind = idx_walk_kind();
-  if (kind == 0)
-    idx_walk_kernel<<<std::min<uint32_t>((n + 3) / 4, kIdxWalkBlocks), 256, 0, s>>>(a, req, list, n);
-  else if (kind == 1)
-    idx_lane_walk_kernel<<<std::min<uint32_t>((n + 255) / 256, 4096), 256, 0, s>>>(a, req, list, n);
-  else
-    idx_flat_walk_kernel<<<std::min<uint32_t>((n + 255) / 256, 4096), 256, 0, s>>>(a, req, list, n);
+  idx_walk_kernel<<<std::min<uint32_t>((n + 3) / 4, kIdxWalkBlocks), 256, 0, s>>>(a, req, list, n);
 }
 
 // Every offset of the true chain: chunk t's walk started where the chain enters it (the stitch

@@ -222,7 +222,10 @@ __global__ void __launch_bounds__(256) run_reduce3_kernel(Reduce3Args a) {
 // also starts at every multiple of 32 (so a chunk's last unit ends within the next 32 bits) and at
 // every range start of a pipelined bucket phase, and a bucket beyond one wave (the wide tier's) or
 // any bucket when gmax = 1 is a unit of its own. Bits past the last bucket are set. One wave per 64
-// buckets: each lane loads one bucket's counts (coalesced), the greedy packing runs on scalars.
+// buckets: lane i finds how far a unit starting at its bucket would extend (window prefix sums of the
+// row counts, compared up to kGroupMax buckets ahead), then the unit starts are the chain 0 ->
+// next(0) -> ... -- the greedy packing, with one scalar step per unit instead of per bucket (a scalar
+// loop over the buckets was SALU-bound: 0.46 ms per C4 step).
 struct UnitArgs {
   const uint32_t *kcnt, *ncnt, *mcnt;
   uint64_t nb;
@@ -240,32 +243,42 @@ __global__ void __launch_bounds__(256) pipe_units_kernel(UnitArgs a) {
     bool rstart = false;
     if (b < a.nb) {
       K = a.kcnt[b];
-      C = a.ncnt[b] + a.mcnt[b];
+      C = min(a.ncnt[b] + a.mcnt[b], 0x7FFFFFFFu);
       if (a.P > 1) {  // (wave-uniform; 64-bit divisions only for a pipelined bucket phase)
         const uint64_t p = (b * a.P + a.nb - 1) / a.nb;  // the first range starting at or after b
         rstart = a.nb * p / a.P == b;
       }
     }
-    const bool single = a.gmax <= 1 || K > (uint32_t)WaveLds<1>::KC || C > a.ccap;
-    const uint64_t past = __ballot(b >= a.nb), sgl = __ballot(single), rst = __ballot(rstart);
-    uint64_t m = past | 1ull | (1ull << 32) | sgl | rst;  // starts: past the end, each 32, ranges, singles
-    uint32_t k = 0, c = 0, g = 0;
-    for (uint32_t i = 0; i < 64; ++i) {  // (scalar)
-      const uint32_t Ki = (uint32_t)__builtin_amdgcn_readlane((int)K, (int)i);
-      const uint32_t Ci = (uint32_t)__builtin_amdgcn_readlane((int)C, (int)i);
-      const bool start = ((m >> i) & 1) || (i && ((sgl >> (i - 1)) & 1)) || k + Ki > (uint32_t)WaveLds<1>::KC ||
-                         c + Ci > a.ccap || g >= a.gmax;
-      if (start) {
-        m |= 1ull << i;
-        k = Ki;
-        c = Ci;
-        g = 1;
-      } else {
-        k += Ki;
-        c += Ci;
-        ++g;
+    const bool single = b >= a.nb || a.gmax <= 1 || K > (uint32_t)WaveLds<1>::KC || C > a.ccap;
+    const uint64_t sgl = __ballot(single);
+    // a unit starts here whatever precedes: the window's first bucket, each multiple of 32, a range
+    // start, a bucket beyond one wave or past the end, and the bucket after one of those
+    const uint64_t forced = 1ull | (1ull << 32) | __ballot(rstart) | sgl | (sgl << 1);
+    uint32_t ek = min(K, 0xFFFFu), ec = min(C, 0xFFFFu);  // inclusive window prefixes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t tk = (uint32_t)__shfl_up((int)ek, o, 64), tc = (uint32_t)__shfl_up((int)ec, o, 64);
+      if ((int)lane >= o) {
+        ek += tk;
+        ec += tc;
       }
     }
+    const uint32_t sk = ek - min(K, 0xFFFFu), sc = ec - min(C, 0xFFFFu);  // exclusive
+    uint32_t run = 1;  // buckets of a unit starting here
+    bool alive = !single;
+#pragma unroll
+    for (uint32_t d = 1; d < 16; ++d) {
+      const uint32_t j = lane + d;
+      const uint32_t ekj = (uint32_t)__shfl_down((int)ek, d, 64), ecj = (uint32_t)__shfl_down((int)ec, d, 64);
+      alive = alive && j < 64 && d < a.gmax && !((forced >> (j & 63)) & 1) && ekj - sk <= (uint32_t)WaveLds<1>::KC &&
+              ecj - sc <= a.ccap;
+      run += alive ? 1u : 0u;
+    }
+    const uint32_t nxt = lane + run;
+    uint64_t m = 0;
+    for (uint32_t st = 0; st < 64; st = (uint32_t)__builtin_amdgcn_readlane((int)nxt, (int)st))  // (scalar)
+      m |= 1ull << st;
+    m |= forced;  // (every forced start is on the chain already; past-the-end bits included)
     if (lane < 2 && 2 * w + lane < words) a.units[2 * w + lane] = (uint32_t)(m >> (32 * lane));
   }
 }
