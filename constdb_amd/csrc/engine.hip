@@ -71,7 +71,8 @@ bool pipe_wave_wanted(uint64_t nb) {
 // Its units group consecutive buckets (runs.hip.h, at most kGroupMax); the plan then targets ~kPipeFineTarget key rows
 // per bucket instead of ~40. Test and A/B hooks: CDB_GROUPS=0 (one bucket per unit, round-5 buckets),
 // CDB_PIPE_TARGET (key rows per bucket), CDB_GROUP_CCAP (child rows per unit, 64 or 128).
-constexpr uint64_t kPipeFineTarget = 24;  // (C4 step: 20 / 22 / 24 / 26 -> 17.96 / 17.19 / 16.98 / 17.08 ms)
+constexpr uint64_t kPipeFineTarget = 28;  // (C4 step, one box: 24 / 28 -> 16.57-16.63 / 16.32 ms; before the
+                                          // parallel unit kernel 20 / 22 / 24 / 26 / 28 -> 17.96 / 17.19 / 16.98 / 17.08 / 17.90)
 constexpr uint64_t kGroupMax = 16;
 bool groups_wanted() {
   const char* e = std::getenv("CDB_GROUPS");
