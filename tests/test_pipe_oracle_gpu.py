@@ -174,3 +174,16 @@ def test_pipe_forced_random_vs_oracle(ctx, monkeypatch, seed):
     st = _merge_vs_oracle(ctx, snaps, records=bool(seed % 2))
     assert st.wave_pipe_buckets > 0
     assert st.wave_pipe_units < st.wave_pipe_buckets
+
+
+def test_pipe_pipelined_ranges_dense_vs_oracle(ctx, monkeypatch, c4_1m):
+    """Dense output with the bucket phase in 8 ranges (cdb_merge_opts.pipe_ranges): the unit bitmap
+    starts a unit at every range start, so no group spans two ranges' compactions."""
+    from test_runs_oracle_gpu import runs_merge
+    monkeypatch.setenv("CDB_WAVE_PIPE", "force")
+    rc, want, _ = cdb_oracle.fold(c4_1m)
+    assert rc == 0
+    m = runs_merge(ctx, c4_1m, pipe_ranges=8)
+    assert m.canonical_dump() == want
+    st = m.stats
+    assert 0 < st.wave_pipe_units < 0.8 * st.wave_pipe_buckets
