@@ -631,6 +631,13 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, CDB_PIPE_MINB) bucket_wave_p
   uint32_t folded = 0, nunits = 0;  // (wave-uniform) buckets / units this wave folded: stats.wave_pipe_*
   while (b != kPipeDone) {
     const uint32_t b2 = b1 != kPipeDone ? produce() : kPipeDone;
+    // the iteration's arguments, read from the kernel-argument segment behind a barrier (as the
+    // second half's below): nothing of them is held in spilled SGPRs from one unit to the next
+    const __attribute__((address_space(4))) WaveArgs* Wa =
+        (const __attribute__((address_space(4))) WaveArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(Wa));
+    const WaveArgs Wi = *(const WaveArgs*)Wa;
+    const RunView& Vi = Wi.V;
     const WaveDir d = in.d;
     const uint32_t C = d.N + d.M;
     // 65..128 children: a second child slot per lane, loaded now (9 % of C4's buckets)
@@ -638,7 +645,7 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, CDB_PIPE_MINB) bucket_wave_p
     WaveMid<1> mid;
     int act;
     if (!two) {
-      act = wave_phase_a<1, 1>(W, L, ufirst(b), lane, in, mid);
+      act = wave_phase_a<1, 1>(Wi, L, ufirst(b), lane, in, mid);
     } else {
       WaveIn<1, 2> in2;
       in2.d = d;
@@ -655,8 +662,8 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, CDB_PIPE_MINB) bucket_wave_p
       in2.cid2[0] = in.cid2[0];
       in2.ct[0] = in.ct[0];
       in2.cm[0] = in.cm[0];
-      pipe_load_child<REC>(V, d, qc, lane, 1, in2);
-      act = wave_phase_a<1, 2>(W, L, ufirst(b), lane, in2, mid);
+      pipe_load_child<REC>(Vi, d, qc, lane, 1, in2);
+      act = wave_phase_a<1, 2>(Wi, L, ufirst(b), lane, in2, mid);
     }
     // bucket b's input registers are dead: bucket b + 1's rows into them and b + 2's pairs, in
     // flight while b's children fold and its outputs are written. (One program point for every
@@ -664,20 +671,39 @@ __global__ void __launch_bounds__(kWavesPerWG * 64, CDB_PIPE_MINB) bucket_wave_p
     // the loads land in the registers the next iteration reads: no copy that waits for them.)
     {
       WaveDir dn;
-      qc = pipe_map(V, pr, dn);
+      qc = pipe_map(Vi, pr, dn);
       dn.G = (b1 & 15) + 1;
-      pipe_load<REC>(V, dn, qc, lane, in);
-      pr = pipe_pairs(V, ufirst(b2), uend(b2), lane, b2 != kPipeDone);
+      pipe_load<REC>(Vi, dn, qc, lane, in);
+      pr = pipe_pairs(Vi, ufirst(b2), uend(b2), lane, b2 != kPipeDone);
     }
-    if (act == WAVE_PUSH) {
-      wave_push(W, ufirst(b), lane, d.G);
-    } else if (act == WAVE_GO) {
-      if (!two)
-        wave_phase_b<1, 1>(W, L, ufirst(b), lane, mid);
-      else
-        wave_phase_b<1, 2>(W, L, ufirst(b), lane, mid);
-      folded += d.G;
-      ++nunits;
+    if (act != WAVE_DONE) {
+      // The outputs' pointers are read from the kernel-argument segment here, behind a barrier the
+      // compiler cannot move loads across, so that they are not held in (spilled) SGPRs through the
+      // whole loop: the kernel needs more than the 102 SGPRs a wave has, and every reload of a
+      // spilled one is a VALU v_readlane.
+      const __attribute__((address_space(4))) WaveArgs* Wk =
+          (const __attribute__((address_space(4))) WaveArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+      asm volatile("" : "+s"(Wk));
+      WaveArgs Wb = W;
+      Wb.A.kos = Wk->A.kos;
+      Wb.A.nos = Wk->A.nos;
+      Wb.A.mos = Wk->A.mos;
+      Wb.A.kout = Wk->A.kout;
+      Wb.A.nout = Wk->A.nout;
+      Wb.A.mout = Wk->A.mout;
+      Wb.A.stats = Wk->A.stats;
+      Wb.big_list = Wk->big_list;
+      Wb.big_count = Wk->big_count;
+      if (act == WAVE_PUSH) {
+        wave_push(Wb, ufirst(b), lane, d.G);
+      } else {
+        if (!two)
+          wave_phase_b<1, 1>(Wb, L, ufirst(b), lane, mid);
+        else
+          wave_phase_b<1, 2>(Wb, L, ufirst(b), lane, mid);
+        folded += d.G;
+        ++nunits;
+      }
     }
     wave_sync();  // (the next bucket reuses this one's LDS)
     b = b1;
