@@ -187,32 +187,46 @@ struct Reduce3Args {
   uint32_t* bdir;        // (nb + 1) x kBdirRow
 };
 __global__ void __launch_bounds__(256) run_reduce3_kernel(Reduce3Args a) {
+  // the block's 256 bdir rows are staged in LDS (33-word pitch: no bank conflicts on the row writes)
+  // and stored as contiguous 16-B pieces: one lane per row wrote 8 pieces 128 B apart before
+  __shared__ uint32_t tile[256 * (kBdirRow + 1)];
   const uint64_t row = a.nb + 1, per_fam = (uint64_t)a.nr * row;
-  for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b <= a.nb; b += (uint64_t)gridDim.x * blockDim.x) {
+  for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 <= a.nb; b0 += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t b = b0 + threadIdx.x;
     uint32_t v[kBdirRow];
 #pragma unroll
     for (int j = 0; j < kBdirRow; ++j) v[j] = 0;
+    if (b <= a.nb) {
 #pragma unroll
-    for (int f = 0; f < 3; ++f) {
-      uint32_t s0 = 0, s1 = 0;
+      for (int f = 0; f < 3; ++f) {
+        uint32_t s0 = 0, s1 = 0;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        if ((uint32_t)r < a.nr) {
-          const uint32_t* d = a.rdir + f * per_fam + (uint64_t)r * row + b;
-          const uint32_t x = d[0];
-          v[f == 0 ? r : 8 + 8 * f + r] = x;
-          s0 += x;
-          if (b < a.nb) s1 += d[1];
+        for (int r = 0; r < 8; ++r) {
+          if ((uint32_t)r < a.nr) {
+            const uint32_t* d = a.rdir + f * per_fam + (uint64_t)r * row + b;
+            const uint32_t x = d[0];
+            v[f == 0 ? r : 8 + 8 * f + r] = x;
+            s0 += x;
+            if (b < a.nb) s1 += d[1];
+          }
+        }
+        if (b < a.nb) {
+          a.base[f][b] = s0 - a.rs_sum[f];
+          a.cnt[f][b] = s1 - s0;
         }
       }
-      if (b < a.nb) {
-        a.base[f][b] = s0 - a.rs_sum[f];
-        a.cnt[f][b] = s1 - s0;
-      }
     }
-    uint4* o = reinterpret_cast<uint4*>(a.bdir + b * kBdirRow);
+    __syncthreads();  // (the previous round's readers are done with the tile)
 #pragma unroll
-    for (int q = 0; q < kBdirRow / 4; ++q) o[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    for (int j = 0; j < kBdirRow; ++j) tile[threadIdx.x * (kBdirRow + 1) + j] = v[j];
+    __syncthreads();
+    const uint64_t nrow = min((uint64_t)blockDim.x, a.nb + 1 - b0);  // rows of this round
+    uint4* o = reinterpret_cast<uint4*>(a.bdir + b0 * kBdirRow);
+    for (uint32_t q = threadIdx.x; q < nrow * (kBdirRow / 4); q += blockDim.x) {
+      const uint32_t r = q / (kBdirRow / 4), c = 4 * (q % (kBdirRow / 4));
+      const uint32_t* t = tile + r * (kBdirRow + 1) + c;
+      o[q] = make_uint4(t[0], t[1], t[2], t[3]);
+    }
   }
 }
 
