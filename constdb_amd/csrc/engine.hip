@@ -1531,7 +1531,9 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   // buckets the over-capacity ones still take the copy batch (children copied by mat_copy).
   constexpr uint32_t kRunsChildMax = 0xFFFFFFFFu;
   const uint32_t runs_child_max = (use_runs && mid_wide) ? kRunsChildMax : 0;
-  if (use_runs) {
+  // (no bucket went to the workgroup tiers -- C1 and C4 -- : neither their copies nor the mid tier
+  // run; their scans and empty launches were ~0.35 ms of every C4 step)
+  if (use_runs && counts[1] > 0) {
     // the workgroup tiers' buckets: copied out of the runs into AoS rows + row indices
     MatArgs MA_;
     MA_.runs_child_max = runs_child_max;
@@ -1562,12 +1564,12 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
   }
   if (mid_wide) {
     CDB_TRY(over_capacity(ctx, A, d_big_list, counts[1], s, use_runs ? &RV : nullptr, runs_child_max, std::max(N, M)));
-  } else {
+  } else if (counts[1] > 0) {
     bucket_mid_kernel<<<std::min<uint64_t>(nb, 2048), kBktThreads, 0, s>>>(A, d_big_list, d_big_count);
     CDB_TRY(launch_check(ctx, s, "bucket_mid_kernel"));
   }
   CDB_HIP(hipEventRecord(ctx->ev_bucket, s), "event");
-  if (!mid_wide) {  // the mid tier forwards buckets over its capacity
+  if (!mid_wide && counts[1] > 0) {  // the mid tier forwards buckets over its capacity
     CDB_HIP(hipMemcpyAsync(counts, d_hot_count, sizeof(uint32_t), hipMemcpyDeviceToHost, s), "d2h");
     CDB_HIP(hipStreamSynchronize(s), "sync");
   }
@@ -1583,10 +1585,20 @@ cdb_status merge_device_impl(cdb_ctx* ctx, const cdb_dev_input* in, const cdb_me
     CDB_HIP(hipEventRecord(ctx->ev_cdone, cs), "event");
     CDB_HIP(hipStreamWaitEvent(s, ctx->ev_cdone, 0), "wait");
   }
-  if (recompact) {
-    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dk.out, nb, dk.doff, (uint32_t*)nullptr, d_totals + 0, s));
-    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dnd.out, nb, dnd.doff, (uint32_t*)nullptr, d_totals + 1, s));
-    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dm.out, nb, dm.doff, (uint32_t*)nullptr, d_totals + 2, s));
+  if (recompact) {  // the three families' dense bases side by side (each scan is a few small launches)
+    hipStream_t sn = ctx->side, sm = ctx->side2;
+    CDB_HIP(hipEventRecord(ctx->ev_pfork, s), "event");
+    CDB_HIP(hipStreamWaitEvent(sn, ctx->ev_pfork, 0), "wait");
+    CDB_HIP(hipStreamWaitEvent(sm, ctx->ev_pfork, 0), "wait");
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dk.out, nb, dk.doff, (uint32_t*)nullptr, d_totals + 0, s, WS_SCAN));
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dnd.out, nb, dnd.doff, (uint32_t*)nullptr, d_totals + 1, sn,
+                                               WS_SCAN2));
+    CDB_TRY(exclusive_scan<uint32_t, uint32_t>(ctx, dm.out, nb, dm.doff, (uint32_t*)nullptr, d_totals + 2, sm,
+                                               WS_SCAN3));
+    CDB_HIP(hipEventRecord(ctx->ev_pn, sn), "event");
+    CDB_HIP(hipEventRecord(ctx->ev_pm, sm), "event");
+    CDB_HIP(hipStreamWaitEvent(s, ctx->ev_pn, 0), "wait");
+    CDB_HIP(hipStreamWaitEvent(s, ctx->ev_pm, 0), "wait");
   }
   if (recompact && dense_out) {
     // one wave per 4096 output rows of a family (the kernel strides over any excess)
