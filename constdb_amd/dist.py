@@ -173,12 +173,19 @@ def exchange_runs(fams, plan: Plan, recv_bufs, max_piece_bytes: int = MAX_PIECE_
         # peer that never posts its half ends the step with an error instead of a hang (gloo's
         # transfers progress inside wait(), under the process group's own timeout)
         moved = sum(op.tensor.numel() * op.tensor.element_size() for op in ops)
-        deadline = time.monotonic() + 60.0 + moved / 1e9
+        # (polled every 0.1 ms for the exchange's expected length, then backing off to 5 ms: a slow
+        # or stuck peer does not keep a host core spinning for the whole deadline)
+        t0 = time.monotonic()
+        deadline = t0 + 60.0 + moved / 1e9
+        nap = 1e-4
         while dist.get_backend() == "nccl" and not all(w.is_completed() for w in works):
-            if time.monotonic() > deadline:
+            now = time.monotonic()
+            if now > deadline:
                 raise TimeoutError(f"rank {me}: row exchange not complete after {60.0 + moved / 1e9:.0f} s "
                                    f"({len(ops)} point-to-point operations, {moved} bytes)")
-            time.sleep(1e-4)
+            if now - t0 > 0.05 + moved / 50e9:
+                nap = min(2 * nap, 5e-3)
+            time.sleep(nap)
         for w in works:
             w.wait()
     return len(ops)
